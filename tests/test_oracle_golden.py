@@ -1,0 +1,161 @@
+"""Pin the CPU oracle against golden vectors produced by the real reference
+(tests/golden/make_golden.py).  CPU only."""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import centernet as O
+from oracle import targets as T
+
+
+def _pos(name, numel, k):
+    return np.random.RandomState(zlib.crc32(name.encode()) & 0xFFFFFFFF).randint(0, numel, k)
+
+
+@pytest.fixture(scope="module")
+def spec():
+    return O.model_spec(10)
+
+
+@pytest.fixture(scope="module")
+def f1_run(spec):
+    entries, topo = spec
+    P, Bf = O.split_state(O.hash_weights(entries))
+    x = T.batch_inputs(1, 2, 512)
+    with torch.no_grad():
+        out = O.forward(P, Bf, x, topo)
+    return out, Bf
+
+
+def test_param_count(spec, golden):
+    entries, _ = spec
+    n = sum(int(np.prod(s)) for k, s in entries
+            if not (k.endswith("running_mean") or k.endswith("running_var") or k.endswith("num_batches_tracked")))
+    assert n == int(golden("init")["param_count"]) == 9981383
+
+
+def test_state_keys_match_reference(spec, golden):
+    entries, _ = spec
+    g = golden("init")
+    keys = sorted({k.split("|")[0] for k in g.files if "|" in k})
+    assert keys == sorted(k for k, _ in entries)
+
+
+def test_f1_forward(f1_run, golden):
+    out, Bf = f1_run
+    g = golden("fwd")
+    for k in ("heatmap", "regr", "offset"):
+        np.testing.assert_allclose(out[k].numpy(), g[k], rtol=1e-4, atol=1e-4)
+    for k in g.files:
+        if k.startswith("rs|"):
+            np.testing.assert_allclose(Bf[k[3:]].numpy(), g[k], rtol=1e-4, atol=1e-5)
+
+
+def test_f4_decode(f1_run, golden):
+    out, _ = f1_run
+    g = golden("decode")
+    dec = O.decode({k: v.clone() for k, v in out.items()})
+    names = ["scores", "inds", "ys", "xs", "offset", "regr"]
+    np.testing.assert_allclose(dec[0].numpy(), g["f1|scores"], rtol=1e-4, atol=1e-5)
+    rs = np.random.RandomState(7)
+    syn = {"heatmap": torch.from_numpy((rs.standard_normal((2, 1, 128, 128)) * 3).astype(np.float32)),
+           "regr": torch.from_numpy(rs.standard_normal((2, 4, 128, 128)).astype(np.float32)),
+           "offset": torch.from_numpy(rs.standard_normal((2, 2, 128, 128)).astype(np.float32))}
+    dec = O.decode(syn)
+    for i, n in enumerate(names):
+        if n in ("offset", "regr", "scores"):
+            np.testing.assert_allclose(dec[i].numpy(), g["syn|" + n], rtol=0, atol=0)
+        else:
+            np.testing.assert_array_equal(dec[i].numpy(), g["syn|" + n])
+
+
+def test_f2_targets_render(golden):
+    g = golden("loss")
+    ys = T.batch_targets(2, 2, 128)
+    for i, n in enumerate(["heat", "mask", "regr", "inds"]):
+        np.testing.assert_array_equal(ys[i].numpy(), g["ys|" + n])
+
+
+@pytest.mark.parametrize("case", ["a", "b", "c", "d"])
+def test_f2_loss_and_grads(case, golden):
+    g = golden("loss")
+    f = golden("fwd")
+    ys = [torch.from_numpy(g["ys|" + n]) for n in ["heat", "mask", "regr", "inds"]]
+    preds = {k: torch.from_numpy(f[k]) for k in ("heatmap", "regr", "offset")}
+    if case == "b":
+        ys[0] = ys[0] * 0.9
+    if case == "c":
+        ys[3] = torch.from_numpy(g["c|inds"])
+    if case == "d":
+        h = preds["heatmap"]
+        preds["heatmap"] = torch.where(h > h.median(), torch.full_like(h, 20.0), torch.full_like(h, -20.0))
+    leaves = {k: v.clone().requires_grad_(True) for k, v in preds.items()}
+    loss, stats = O.centernet_loss(leaves, ys)
+    loss.mean().backward()
+    np.testing.assert_allclose(loss.detach().numpy(), g[case + "|loss"], rtol=1e-5)
+    np.testing.assert_allclose([s.item() for s in stats], g[case + "|stats"], rtol=1e-5, atol=1e-7)
+    gh = leaves["heatmap"].grad
+    if case == "a":
+        np.testing.assert_allclose(gh.numpy(), g["a|dheatmap"], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(gh.double().abs().sum().item(), g[case + "|dheatmap_abs"], rtol=1e-5)
+    for k in ("regr", "offset"):
+        np.testing.assert_allclose(O.gather_feat(leaves[k].grad, ys[3]).numpy(), g[case + "|d" + k], rtol=1e-6)
+
+
+def test_f3_train_step(spec, golden):
+    entries, topo = spec
+    g = golden("step")
+    st = O.TrainState(O.hash_weights(entries))
+    x = T.batch_inputs(3, 2, 512)
+    ys = T.batch_targets(4, 2, 128)
+    pre = {k: v.detach().clone() for k, v in st.P.items()}
+    st.opt.zero_grad()
+    outs = O.forward(st.P, st.B, x, topo)
+    loss, stats = O.centernet_loss(outs, ys)
+    loss.mean().backward()
+    grads = {k: v.grad.detach().clone() for k, v in st.P.items()}
+    st.opt.step()
+    np.testing.assert_allclose(loss.detach().numpy(), g["loss"], rtol=1e-4)
+    for k, v in st.P.items():
+        pos = _pos(k, v.numel(), 16)
+        np.testing.assert_allclose(grads[k].double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7)
+        np.testing.assert_allclose(pre[k].reshape(-1)[pos].numpy(), g["p0samp|" + k], rtol=0, atol=0)
+        np.testing.assert_allclose(v.detach().reshape(-1)[pos].numpy(), g["psamp|" + k], rtol=1e-5, atol=2e-6)
+
+
+def test_f6_layer_stats(spec, golden):
+    entries, topo = spec
+    g = golden("layers")
+    P, Bf = O.split_state(O.hash_weights(entries))
+    taps = {}
+    with torch.no_grad():
+        O.forward(P, Bf, T.batch_inputs(6, 2, 128), topo, taps=taps)
+    for name, t in taps.items():
+        if name + "|samp" not in g.files:
+            continue
+        pos = _pos(name, t.numel(), 32)
+        assert tuple(t.shape) == tuple(g[name + "|shape"])
+        np.testing.assert_allclose(t.reshape(-1)[pos].numpy(), g[name + "|samp"], rtol=1e-4, atol=1e-4)
+
+
+def test_f7_ddp_syncbn(spec, golden):
+    """Global-batch BN == SyncBN; averaging per-shard losses == DDP gradient averaging."""
+    entries, topo = spec
+    g = golden("ddp")
+    P, Bf = O.split_state(O.hash_weights(entries))
+    P = {k: v.requires_grad_(True) for k, v in P.items()}
+    x = T.batch_inputs(8, 4, 128)
+    ys = T.batch_targets(9, 4, 32)
+    outs = O.forward(P, Bf, x, topo)
+    losses = []
+    for r in range(2):
+        sl = slice(2 * r, 2 * r + 2)
+        l, _ = O.centernet_loss({k: v[sl] for k, v in outs.items()}, [y[sl] for y in ys])
+        losses.append(l.mean())
+    ((losses[0] + losses[1]) / 2).backward()
+    np.testing.assert_allclose(losses[0].item(), g["loss_r0"], rtol=1e-4)
+    np.testing.assert_allclose(losses[1].item(), g["loss_r1"], rtol=1e-4)
+    for k, v in P.items():
+        np.testing.assert_allclose(v.grad.double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7)
