@@ -1,0 +1,180 @@
+"""bench.py -- 512x512 images/s training centerOffsetRes10 (bf16) on N MI355X, one process per GPU.
+
+python bench.py --gpus N --steps K --warmup W            (N>1: launched by torch.distributed.run)
+
+A step = NetworkFactory.train on one synthetic batch of 32 tiles per GPU (zero_grad, forward,
+CenterNetLoss, backward incl. the RCCL gradient all-reduce + SyncBN statistics, Adam) with the
+inputs already resident in HBM.  Prints ONE JSON line on rank 0 with the metric, the roofline of
+the dominant kernel (HIP events on the launch stream) and the CPU-oracle baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "scd-resnet_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+TRAIN_GFLOP_PER_IMG = 147.476      # SURVEY §6 / BASELINE.md: conv+deconv fwd+dgrad+wgrad per 512^2 image
+PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--model", default="centerOffsetRes10")
+    ap.add_argument("--cpu-baseline-steps", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(steps):
+    """The CPU oracle (PyTorch fp32 restatement of the reference step) on this host's cores:
+    Res10, B=4, 512^2 -- the reference's CPU train.py configuration (BASELINE.json configs[0])."""
+    from oracle import centernet as O
+    from oracle import targets as T
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    entries, topo = O.model_spec(10)
+    st = O.TrainState(O.hash_weights(entries))
+    x = T.batch_inputs(5, 4, 512)
+    ys = T.batch_targets(6, 4, 128)
+    st.step(x, ys, topo)                       # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.step(x, ys, topo)
+    dt = time.perf_counter() - t0
+    return {"value": round(4 * steps / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": "oracle train step (fwd+loss+bwd+Adam), Res10 fp32, batch 4, 512x512, %d timed steps "
+                      "after 1 warm-up (%.1f s)" % (steps, dt)}
+
+
+def heads_gemm_roofline(model, feat_shape, dtype, reps=10):
+    """Time the dominant kernel -- the fused head conv3x3 GEMM (M=B*128*128, N=384, K=9*256) --
+    with HIP events on the stream it is launched on."""
+    from scdhip import ops
+    heads = [getattr(model, n) for n in ("heatmap", "regr", "offset")]
+    w0 = torch.cat([h[0].weight for h in heads], 0).detach()
+    b0 = torch.cat([h[0].bias for h in heads], 0).detach()
+    wp = ops.pack_weight(w0, dtype, 0)
+    feat = torch.randn(feat_shape, device="cuda").to(dtype)
+    out = torch.empty(feat_shape[0], feat_shape[1], feat_shape[2], w0.shape[0], device="cuda", dtype=dtype)
+    for _ in range(2):
+        ops.conv_fwd(feat, wp, w0.shape[0], 3, 3, 1, 1, bias=b0, relu=True, out=out)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        ops.conv_fwd(feat, wp, w0.shape[0], 3, 3, 1, 1, bias=b0, relu=True, out=out)
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    M = feat_shape[0] * feat_shape[1] * feat_shape[2]
+    flops = 2.0 * M * w0.shape[0] * (9 * feat_shape[3])
+    achieved = flops / (ms * 1e-3) / 1e12
+    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+    return {"bound": "mfma", "kernel": "conv_gemm_kernel (fused head conv3x3, fwd)", "achieved": round(achieved, 1),
+            "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+            "flop_per_launch": flops, "avg_launch_ms": round(ms, 4)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import importlib
+
+    from scdhip import ops
+    from scdhip.flat import FlatAdam, FlatDDP
+    from trainer.dataset.syntheticSCD import SCD
+    plugin = importlib.import_module("trainer.model." + args.model)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+
+    model = plugin.model(**plugin.modelParams).to(dev).set_compute_dtype(dtype).train()
+    opt = FlatAdam(filter(lambda p: p.requires_grad, model.parameters()))
+    if world > 1:
+        if torch.cuda.device_count() > 1:
+            ops.set_bn_sync(dist.group.WORLD)     # SyncBN rule of networkFactory.py:128
+        model = FlatDDP(model)
+    lossfn = plugin.loss
+
+    # synthetic batch (per-rank shard), resident in HBM before timing
+    B = args.batch
+    ds = SCD(None, True, seed=1000 + 97 * rank)
+    items = [ds[i] for i in range(B)]
+    x = torch.stack([it["xs"][0] for it in items]).to(dev)
+    ys = [torch.stack([it["ys"][k] for it in items]).to(dev) for k in range(4)]
+
+    def step():
+        opt.zero_grad()
+        loss, _ = lossfn(model(x, decode=False), ys)
+        loss = loss.mean()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    final_loss = loss.item()
+
+    if rank == 0:
+        imgs = B * world * args.steps
+        value = imgs / elapsed
+        inner = model.module if hasattr(model, "module") else model
+        roof = heads_gemm_roofline(inner, (B, 128, 128, 256), dtype)
+        step_frac = value * TRAIN_GFLOP_PER_IMG / 1e3 / (world * (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
+                                                                  else PEAK_F32_TFLOPS))
+        line = {
+            "metric": "512x512 images/sec training, centerOffsetRes10, at 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32", "data": "synthetic",
+            "config": {"workload": "centerOffsetRes10 train step (fwd+focal/L1 loss+bwd+Adam, DDP over RCCL), "
+                                   "512x512 synthetic SCD tiles", "model": args.model, "global_batch": B * world,
+                       "per_gpu_batch": B, "seq_len": None, "parallelism": "dp%d" % world,
+                       "image_size": 512},
+            "roofline": roof,
+            "step_mfma_frac": round(step_frac, 4),
+            "final_loss": round(final_loss, 5),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_baseline_steps)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,170 @@
+/*
+ * scdhip.h -- C-ABI of libscdhip.so, the MI355X (gfx950 / CDNA4) kernels behind the
+ * scd-resnet training hot path (CenterNet/CornerNet on a ResNet backbone, 512x512 SCD
+ * tiles).  Plain C: raw device pointers, sizes and a hipStream_t passed as void*.
+ *
+ * Conventions
+ *   - every entry point returns 0 on success, otherwise a hipError_t code (or SCD_ERR_*);
+ *   - no entry point allocates, synchronises or keeps state: work buffers are caller-owned
+ *     and sized with the *_workspace helpers; all work is enqueued on `stream`;
+ *   - activations are NHWC (channels innermost) in `dtype` (SCD_DT_F32 parity mode,
+ *     SCD_DT_BF16 performance mode); weights/grads/BN parameters are fp32 in the
+ *     reference (PyTorch) layout so state_dicts interchange; statistics are fp64.
+ *
+ * Each declaration names the reference interface it replaces (path:line in
+ * yang-z-03/scd-resnet @ 2024-10-22).  The reference binds these ops through
+ * torch.nn modules (cuDNN/ATen) and, for corner pooling, through pybind11 modules
+ * (models/backbones/cornerPooling/source/topPool.cpp:76-85 and siblings); the ctypes binding that
+ * replaces both lives in scd-resnet_amd/scdhip/lib.py, see INTEGRATION.md.
+ */
+#ifndef SCDHIP_H
+#define SCDHIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCD_DT_F32 0
+#define SCD_DT_BF16 1
+
+#define SCD_ERR_ARG 9001       /* invalid argument / unsupported shape */
+
+#define SCD_MAX_TAPS 16
+#define SCD_MAX_PHASES 4
+#define SCD_STAT_REPLICAS 64   /* fp64 statistics buffers are [SCD_STAT_REPLICAS][2][C] */
+
+/* One sub-pixel phase of a gather-GEMM (see DESIGN.md "Implicit GEMM").  For output
+ * pixel (n, qh, qw) of the phase grid, the GEMM row gathers input pixel
+ * (n, in_stride*qh + dh[t], in_stride*qw + dw[t]) for tap t and writes output pixel
+ * (n, out_stride*qh + rho_h, out_stride*qw + rho_w); tap t uses weight tap wt[t]. */
+typedef struct scd_gemm_phase {
+    int Qh, Qw, rho_h, rho_w, ntaps;
+    int dh[SCD_MAX_TAPS], dw[SCD_MAX_TAPS], wt[SCD_MAX_TAPS];
+} scd_gemm_phase;
+
+/* Implicit-GEMM convolution on MFMA (bf16 16x16x32 / f32 16x16x4), NHWC.
+ * y[pix, co] = sum_{t,ci} x[gather(pix,t), ci] * w[co, wt(t), ci]  (+bias, relu, +=y)
+ * Covers Conv2d forward, Conv2d dgrad (phase-decomposed for stride 2),
+ * ConvTranspose2d forward (4 phases) and ConvTranspose2d dgrad.
+ * Optionally accumulates per-channel sum/sumsq (fp64, [64][2][Co]) for training BN.
+ * Replaces: torch.nn.Conv2d in residuals.py:91,94,211,259-263 (BasicBlock/Bottleneck/stem/
+ * downsample), ConvTranspose2d residuals.py:298-307, head convs centerNetOffset.py:106-110,
+ * and their autograd input-gradients. */
+int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, const float* bias, double* stats,
+                  int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride,
+                  int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
+                  void* stream);
+
+/* Weight-gradient of the gather-GEMM (split-K over pixels on MFMA, fp32 partial slabs):
+ * ws[z, co, t*Ci+ci] = sum_{pix in split z} g[pix, co] * x[gather(pix, t), ci]
+ * with gather(pix=(n,oh,ow), t) = (n, in_stride*oh + dh[t], in_stride*ow + dw[t]).
+ * Replaces the weight-gradient half of cuDNN convolution_backward for every Conv2d /
+ * ConvTranspose2d above. */
+size_t scd_conv_wgrad_workspace(int Cg, int T, int Ci, int nsplit);
+int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws, int nsplit,
+                   int N, int Ho, int Wo, int Cg, int Hi, int Wi, int Ci, int in_stride,
+                   int T, const int* dh, const int* dw, void* stream);
+/* dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= sum_z ws[z, r, t*Ci+ci]   for r in [r0,r1), ci < cvalid */
+int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
+                     long ld_n, long ld_c, long ld_t, float* dst, int accumulate, void* stream);
+
+/* Pack an fp32 (A, B, T) weight (OIHW / IOHW flattening) into the GEMM operand layout:
+ * mode 0: out[row_off + a][t*B + b] = w[a][b][t]; mode 1: out[row_off + b][t*A + a] = w[a][b][t];
+ * rows are ldp elements long (zero padded). */
+int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp,
+                    int row_off, void* stream);
+
+/* Stem im2col: x (N,1,H,W) fp32 -> cols (N,Ho,Wo,Kpad) dtype, taps kh*kw zero-padded to Kpad.
+ * Feeds residuals.py:211 (Conv2d(1,64,7,s2,p3)) to the MFMA GEMM as a 1x1 conv. */
+int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int H, int W, int Ho, int Wo, int kh,
+                    int kw, int stride, int pad, int Kpad, void* stream);
+
+/* ---- training BatchNorm2d (residuals.py:92,95,212,262,306; momentum 0.1, eps 1e-5) ---- */
+/* sum replicas [nrep][2][C] -> [2][C] in place (replica 0); used before a SyncBN all-reduce */
+int scd_stats_collapse(double* stats, int nrep, int C, void* stream);
+/* mean/var from stats (count rows), running-stat update (unbiased var), scale/shift for apply;
+ * stats == NULL: eval mode, normalise with the running statistics (no update) */
+int scd_bn_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+                    const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
+                    float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
+                    void* stream);
+/* out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift */
+int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const float* scale,
+                 const float* shift, const void* res, const float* rscale, const float* rshift,
+                 int relu, void* stream);
+/* dz = dout * (mask ? mask>0 : 1); stats += [sum dz, sum dz*(y-mean)*invstd] */
+int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
+                      const float* invstd, int C, long total, double* stats, void* stream);
+/* dgamma (+)= sum dz*xhat, dbeta (+)= sum dz; coef[3][C] for dy = a*dz + b*y + c */
+int scd_bn_bwd_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+                        const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                        float* coef, void* stream);
+/* dy = a*dz + b*y + c (dtype); optionally also writes dz */
+int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* coef,
+                     int C, long total, void* dy, void* dz, void* stream);
+
+/* ---- stem BN-apply + ReLU + MaxPool2d(3,2,1) (residuals.py:212-214) ---- */
+int scd_stem_pool_fwd(int dtype, const void* y, const float* scale, const float* shift, void* out,
+                      uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, void* stream);
+/* dz(N,H,W,C) = relu'(y*scale+shift) * maxpool_bwd(dout) */
+int scd_stem_pool_bwd(int dtype, const void* dout, const uint8_t* argmax, const void* y,
+                      const float* scale, const float* shift, void* dz, int N, int H, int W, int C,
+                      int Ho, int Wo, void* stream);
+
+/* ---- fused CenterNet head tails: ReLU'd hidden (N,HW,nh*Hd) -> per-head 1x1 conv + bias ----
+ * Replaces the terminal Conv2d(128, {1,4,2}, 1) at centerNetOffset.py:108-110 (and its
+ * autograd).  Head h reads hidden channels [h*Hd, (h+1)*Hd); w1[h] is its fp32 (od[h], Hd)
+ * weight, b1[h] its bias; outputs are NCHW fp32 (N, od[h], HW).  nh <= 4, od[h] <= 4. */
+int scd_heads_fwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
+                  const float* const* w1, const float* const* b1, float* const* outs, void* stream);
+/* dhid = relu'(hid) * (w1^T dout) (dtype) */
+int scd_heads_bwd_data(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
+                       const float* const* w1, const float* const* douts, void* dhid, void* stream);
+/* fp64 accumulator bytes for scd_heads_bwd_weight ([SCD_STAT_REPLICAS][dW1 | db1 | db0]) */
+size_t scd_heads_bwd_weight_accsize(int nh, int Hd, const int* od);
+int scd_heads_bwd_weight(int dtype, const void* hid, const void* dhid, int N, int HW, int nh, int Hd,
+                         const int* od, const float* const* douts, double* acc, void* stream);
+/* collapse replicas; (+)= into dw1[h] (od[h],Hd), db1[h] (od[h]), db0[h] (Hd: the 3x3 conv bias) */
+int scd_heads_bwd_weight_finalize(const double* acc, int nh, int Hd, const int* od, float* const* dw1,
+                                  float* const* db1, float* const* db0, int accumulate, void* stream);
+
+/* ---- losses (focal.py:25-53, regression.py:37-44, centerNetOffset.py:182-217) ---- */
+/* per element: g = d/dlogit [pos: log(p)(1-p)^2 | neg: log(1-p) p^2 (1-gt)^4] with
+ * p = clamp(sigmoid(x),1e-4,1-1e-4); acc[0..2] (fp64, replicated [64][4]) += posL, negL, npos */
+int scd_focal_fwd(const float* logits, const float* gt, long n, float* g, double* acc, void* stream);
+/* masked L1 on gathered NCHW features: acc[0] += sum |f-t|, acc[1] += sum mask; g = sign(f-t) scattered */
+int scd_l1_gather_fwd(const float* feat, int N, int C, int HW, const int64_t* inds, const uint8_t* mask,
+                      const float* target, int K, int tstride, int toff, float* g, double* acc, void* stream);
+/* out[0..] = loss terms; factors for backward.  See centerNetOffset.py:213-217 */
+int scd_centernet_loss_finalize(const double* focal_acc, int nfocal, const double* l1_acc, int nl1,
+                                const float* l1_weights, float* out, float* factors, void* stream);
+/* g[i] *= factors[idx] * go[0]  (in place) */
+int scd_scale_by_device(float* g, long n, const float* factors, int idx, const float* go, void* stream);
+
+/* ---- decode (centerNetOffset.py:219-251, utility.py:87-118) ---- */
+size_t scd_decode_workspace(int N, int HW);
+int scd_decode_topk(const float* heat, int N, int H, int W, int K, const float* offset, int od_off,
+                    const float* regr, int od_regr, float* scores, int64_t* inds, int64_t* ys, int64_t* xs,
+                    float* off_out, float* regr_out, void* workspace, void* stream);
+
+/* ---- Adam (torch.optim.Adam defaults, networkFactory.py:79-82) over a flat fp32 buffer ---- */
+int scd_adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                  float eps, float bc1, float bc2, float gscale, void* stream);
+
+/* ---- corner pooling (cornerPooling/source/{top,bottom,left,right}Pool.cpp) ----
+ * dir: 0 top (max over k>=h), 1 bottom (k<=h), 2 left (k>=w), 3 right (k<=w); NHWC dtype.
+ * Backward routes grad to the running argmax, ties keep the first-scanned index
+ * (strict '>' update, topPool.cpp:61-65). */
+int scd_cpool_fwd(int dtype, int dir, const void* x, void* y, int N, int H, int W, int C, void* stream);
+int scd_cpool_bwd(int dtype, int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C,
+                  void* stream);
+
+/* library self-description (for the loader / tests) */
+const char* scd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,260 @@
+// Training-mode BatchNorm2d pieces for NHWC activations (residuals.py:92,95,212,262,306).
+// Statistics are accumulated in fp64 into SCD_STAT_REPLICAS replicas (spreads the atomics),
+// finalised per channel; apply / backward passes are 16-byte-vectorised elementwise kernels.
+#include "scd_common.h"
+
+namespace {
+
+__global__ void stats_collapse_kernel(double* stats, int nrep, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int r = 0; r < nrep; ++r) s += stats[(long)r * n + i];
+    stats[i] = s;
+}
+
+__global__ void bn_finalize_kernel(const double* stats, int nrep, int C, double count, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
+                                   float eps, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && nbt && stats) *nbt += 1;
+    if (c >= C) return;
+    double mean, var;
+    if (stats) {
+        double s = 0.0, q = 0.0;
+        for (int r = 0; r < nrep; ++r) {
+            s += stats[(long)r * 2 * C + c];
+            q += stats[(long)r * 2 * C + C + c];
+        }
+        mean = s / count;
+        var = q / count - mean * mean;
+        if (var < 0.0) var = 0.0;
+    } else {                       // eval mode: normalise with the running statistics
+        mean = rmean[c];
+        var = rvar[c];
+    }
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f;
+    const float b = beta ? beta[c] : 0.f;
+    const float sc = g * invstd;
+    mean_o[c] = (float)mean;
+    invstd_o[c] = invstd;
+    scale_o[c] = sc;
+    shift_o[c] = b - (float)mean * sc;
+    if (stats && rmean) {
+        const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+        rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+        rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+    }
+}
+
+template <typename T>
+__global__ void bn_apply_kernel(const T* y, T* out, int C, long nvec, const float* scale, const float* shift,
+                                const T* res, const float* rscale, const float* rshift, int relu) {
+    constexpr int E = Vec16<T>::N;
+    for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
+        const long i = v * E;
+        const int c0 = (int)(i % C);
+        float a[E], r[E];
+        Vec16<T>::load(y + i, a);
+        if (res) Vec16<T>::load(res + i, r);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            float o = a[e] * scale[c0 + e] + shift[c0 + e];
+            if (res) o += rscale ? (r[e] * rscale[c0 + e] + rshift[c0 + e]) : r[e];
+            if (relu) o = fmaxf(o, 0.f);
+            a[e] = o;
+        }
+        Vec16<T>::store(out + i, a);
+    }
+}
+
+// per-channel sums over rows: block = 256 threads handles a tile of rows x (C/E chunk) columns
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y, const float* mean,
+                                     const float* invstd, int C, long rows, int rows_per_block, double* stats) {
+    constexpr int E = Vec16<T>::N;
+    const int cpr = C / E;                     // chunks per row
+    const int lanes_per_row = min(cpr, 256);
+    const int rpi = 256 / lanes_per_row;       // rows per iteration
+    const int tid = threadIdx.x;
+    const int ch = tid % lanes_per_row;
+    const int rsub = tid / lanes_per_row;
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = min(rows, r0 + rows_per_block);
+    __shared__ float red[256 * 2 * 8];
+    for (int cc = ch; cc < cpr; cc += lanes_per_row) {
+        float s[E], q[E], mu[E], is[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) { s[e] = 0.f; q[e] = 0.f; mu[e] = mean[cc * E + e]; is[e] = invstd[cc * E + e]; }
+        if (rsub < rpi) {
+            for (long r = r0 + rsub; r < r1; r += rpi) {
+                const long i = r * C + (long)cc * E;
+                float d[E], yv[E], mk[E];
+                Vec16<T>::load(dout + i, d);
+                Vec16<T>::load(y + i, yv);
+                if (mask) Vec16<T>::load(mask + i, mk);
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    float dz = (mask && !(mk[e] > 0.f)) ? 0.f : d[e];
+                    s[e] += dz;
+                    q[e] += dz * (yv[e] - mu[e]) * is[e];
+                }
+            }
+        }
+        // reduce over the rpi row-lanes that share this chunk
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            red[(tid * E + e) * 2 + 0] = s[e];
+            red[(tid * E + e) * 2 + 1] = q[e];
+        }
+        __syncthreads();
+        if (rsub == 0) {
+            const int rep = blockIdx.x % SCD_STAT_REPLICAS;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                double ss = 0.0, qq = 0.0;
+                for (int k = 0; k < rpi; ++k) {
+                    ss += red[((k * lanes_per_row + ch) * E + e) * 2 + 0];
+                    qq += red[((k * lanes_per_row + ch) * E + e) * 2 + 1];
+                }
+                atomic_add_f64(stats + ((long)rep * 2 + 0) * C + cc * E + e, ss);
+                atomic_add_f64(stats + ((long)rep * 2 + 1) * C + cc * E + e, qq);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* stats, int nrep, int C, double count, const float* gamma,
+                                       const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                       float* coef) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < nrep; ++r) {
+        s += stats[(long)r * 2 * C + c];
+        q += stats[(long)r * 2 * C + C + c];
+    }
+    if (dgamma) dgamma[c] += (float)q;
+    if (dbeta) dbeta[c] += (float)s;
+    const float g = gamma ? gamma[c] : 1.f;
+    const float is = invstd[c];
+    const float sc = g * is;
+    const float k1 = (float)(s / count);
+    const float k2 = (float)(q / count);
+    // dy = sc*(dz - k1 - xhat*k2), xhat = (y-mean)*is
+    coef[c] = sc;
+    coef[C + c] = -sc * is * k2;
+    coef[2 * C + c] = -sc * k1 + sc * is * k2 * mean[c];
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* coef, int C, long nvec,
+                                    T* dy, T* dz_out) {
+    constexpr int E = Vec16<T>::N;
+    for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
+        const long i = v * E;
+        const int c0 = (int)(i % C);
+        float d[E], yv[E], mk[E], o[E];
+        Vec16<T>::load(dout + i, d);
+        Vec16<T>::load(y + i, yv);
+        if (mask) Vec16<T>::load(mask + i, mk);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const float dz = (mask && !(mk[e] > 0.f)) ? 0.f : d[e];
+            d[e] = dz;
+            o[e] = coef[c0 + e] * dz + coef[C + c0 + e] * yv[e] + coef[2 * C + c0 + e];
+        }
+        Vec16<T>::store(dy + i, o);
+        if (dz_out) Vec16<T>::store(dz_out + i, d);
+    }
+}
+
+inline int ew_blocks(long nvec) { return (int)std::min<long>(8192, std::max<long>(1, (nvec + 255) / 256)); }
+
+}  // namespace
+
+extern "C" int scd_stats_collapse(double* stats, int nrep, int C, void* stream) {
+    const int n = 2 * C;
+    hipLaunchKernelGGL(stats_collapse_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, stats, nrep, n);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_bn_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
+                               float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
+                               void* stream) {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
+                       count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, mean, invstd, scale,
+                       shift);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const float* scale,
+                            const float* shift, const void* res, const float* rscale, const float* rshift, int relu,
+                            void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == SCD_DT_BF16) {
+        if (C % 8) return SCD_ERR_ARG;
+        long nvec = total / 8;
+        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const __bf16*)y,
+                           (__bf16*)out, C, nvec, scale, shift, (const __bf16*)res, rscale, rshift, relu);
+    } else if (dtype == SCD_DT_F32) {
+        if (C % 4) return SCD_ERR_ARG;
+        long nvec = total / 4;
+        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)y,
+                           (float*)out, C, nvec, scale, shift, (const float*)res, rscale, rshift, relu);
+    } else {
+        return SCD_ERR_ARG;
+    }
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
+                                 const float* invstd, int C, long total, double* stats, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int E = dtype == SCD_DT_BF16 ? 8 : 4;
+    if (C % E) return SCD_ERR_ARG;
+    const long rows = total / C;
+    // aim for ~2048 blocks
+    int rpb = (int)std::max<long>(16, (rows + 2047) / 2048);
+    int blocks = cdiv(rows, rpb);
+    if (dtype == SCD_DT_BF16)
+        hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout,
+                           (const __bf16*)mask, (const __bf16*)y, mean, invstd, C, rows, rpb, stats);
+    else if (dtype == SCD_DT_F32)
+        hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dout,
+                           (const float*)mask, (const float*)y, mean, invstd, C, rows, rpb, stats);
+    else
+        return SCD_ERR_ARG;
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_bn_bwd_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+                                   const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
+                                   void* stream) {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
+                       count, gamma, mean, invstd, dgamma, dbeta, coef);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* coef, int C,
+                                long total, void* dy, void* dz, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == SCD_DT_BF16) {
+        if (C % 8) return SCD_ERR_ARG;
+        long nvec = total / 8;
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st,
+                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, coef, C, nvec, (__bf16*)dy,
+                           (__bf16*)dz);
+    } else if (dtype == SCD_DT_F32) {
+        if (C % 4) return SCD_ERR_ARG;
+        long nvec = total / 4;
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)dout,
+                           (const float*)mask, (const float*)y, coef, C, nvec, (float*)dy, (float*)dz);
+    } else {
+        return SCD_ERR_ARG;
+    }
+    SCD_RETURN_LAUNCH();
+}

@@ -1,0 +1,302 @@
+"""Block-granular autograd Functions of the CenterNet/CornerNet ResNet training path.
+
+Each Function runs one reference module group entirely on libscdhip kernels:
+  StemFn        preprocess: Conv2d(1,64,7,s2,p3)+BN+ReLU+MaxPool(3,2,1)   residuals.py:209-216
+  BasicBlockFn  BasicBlock (+downsample)                                  residuals.py:84-120, 256-271
+  BottleneckFn  Bottleneck (+downsample)                                  residuals.py:122-165
+  DeconvBNFn    ConvTranspose2d(k4,s2,p1,no bias)+BN+ReLU                 residuals.py:286-310
+  ConvBNFn      Convolution (conv+BN+ReLU) / conv+BN                      convolutions.py:25-49
+  HeadsFn       all CenterNet terminals fused: one 3x3 GEMM with N = sum of
+                hidden widths (+bias+ReLU epilogue) and the per-head 1x1s  centerNetOffset.py:103-122
+
+Parameter gradients are accumulated straight into ``param.grad`` (created on demand;
+with FlatAdam/FlatDDP they are views of one flat buffer), so the Functions return None
+for parameter inputs.  Activations between Functions are NHWC in the model's compute dtype.
+"""
+import torch
+
+from . import ops
+
+
+def _c(t):
+    return t if t is None or t.is_contiguous() else t.contiguous()
+
+
+def _conv_ld(w):
+    """dst strides of an OIHW conv weight (Co, Ci, kh, kw) for scd_wgrad_reduce: [co][ci][tap]."""
+    T = w.shape[2] * w.shape[3]
+    return (w.shape[1] * T, T, 1)
+
+
+def _train_bn_conv(x, conv, bn, stride, pad, training):
+    """conv (no bias) -> raw y + BN statistics -> BNState."""
+    C = conv.weight.shape[0]
+    kh, kw = conv.weight.shape[2], conv.weight.shape[3]
+    wp = ops.pack_weight(conv.weight, x.dtype, 0)
+    stats = ops.new_stats(C, x.device) if training else None
+    y = ops.conv_fwd(x, wp, C, kh, kw, stride, pad, stats=stats)
+    st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
+    return y, st
+
+
+class StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, conv, bn, dtype):
+        training = bn.training
+        cols = ops.im2col_stem(x, dtype, kh=conv.weight.shape[2], kw=conv.weight.shape[3],
+                               stride=conv.stride[0], pad=conv.padding[0])
+        C = conv.weight.shape[0]
+        wp = ops.pack_weight(conv.weight, dtype, 0, ldp=cols.shape[-1])
+        stats = ops.new_stats(C, x.device) if training else None
+        y = ops.conv_fwd(cols, wp, C, 1, 1, 1, 0, stats=stats)
+        st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
+        out, am = ops.stem_pool_fwd(y, st)
+        ctx.save_for_backward(cols, y, am)
+        ctx.st, ctx.conv, ctx.bn = st, conv, bn
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cols, y, am = ctx.saved_tensors
+        conv, bn, st = ctx.conv, ctx.bn, ctx.st
+        dz = ops.stem_pool_bwd(_c(dout), am, y, st)
+        dy = ops.bn_backward(bn, st, dz, y)
+        T = conv.weight.shape[2] * conv.weight.shape[3]
+        ops.conv_wgrad(dy, cols, 1, 1, 1, 0, ops.grad_of(conv.weight), (T, 1, 0), cvalid=T)
+        return None, None, None, None, None
+
+
+class BasicBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, blk):
+        tr = blk.training
+        s = blk.stride
+        y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, s, 1, tr)
+        a1 = ops.bn_apply(y1, st1, True)
+        y2, st2 = _train_bn_conv(a1, blk.conv2, blk.bn2, 1, 1, tr)
+        yd, std = None, None
+        if blk.downsample is not None:
+            yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], s, 0, tr)
+            out = ops.bn_apply(y2, st2, True, res=yd, rst=std)
+        else:
+            out = ops.bn_apply(y2, st2, True, res=x)
+        ctx.save_for_backward(x, y1, a1, y2, yd, out)
+        ctx.sts = (st1, st2, std)
+        ctx.blk = blk
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y1, a1, y2, yd, out = ctx.saved_tensors
+        st1, st2, std = ctx.sts
+        blk = ctx.blk
+        dout = _c(dout)
+        s = blk.stride
+        N, H, W, Cin = x.shape
+        C = blk.conv1.weight.shape[0]
+        if blk.downsample is not None:
+            dy2 = ops.bn_backward(blk.bn2, st2, dout, y2, mask=out)
+            dyd = ops.bn_backward(blk.downsample[1], std, dout, yd, mask=out)
+            wd = blk.downsample[0].weight
+            dx = ops.conv_dgrad(dyd, ops.pack_weight(wd, x.dtype, 1), Cin, H, W, 1, 1, s, 0)
+            ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
+        else:
+            dx = torch.empty_like(x)
+            dy2 = ops.bn_backward(blk.bn2, st2, dout, y2, mask=out, dz_out=dx)
+        w2 = blk.conv2.weight
+        ops.conv_wgrad(dy2, a1, 3, 3, 1, 1, ops.grad_of(w2), _conv_ld(w2))
+        da1 = ops.conv_dgrad(dy2, ops.pack_weight(w2, x.dtype, 1), C, a1.shape[1], a1.shape[2], 3, 3, 1, 1)
+        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, mask=a1)
+        w1 = blk.conv1.weight
+        ops.conv_wgrad(dy1, x, 3, 3, s, 1, ops.grad_of(w1), _conv_ld(w1))
+        ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 3, 3, s, 1, out=dx, accumulate=True)
+        return dx, None, None
+
+
+class BottleneckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, blk):
+        tr = blk.training
+        s = blk.stride
+        y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, 1, 0, tr)
+        a1 = ops.bn_apply(y1, st1, True)
+        y2, st2 = _train_bn_conv(a1, blk.conv2, blk.bn2, s, 1, tr)
+        a2 = ops.bn_apply(y2, st2, True)
+        y3, st3 = _train_bn_conv(a2, blk.conv3, blk.bn3, 1, 0, tr)
+        yd, std = None, None
+        if blk.downsample is not None:
+            yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], s, 0, tr)
+            out = ops.bn_apply(y3, st3, True, res=yd, rst=std)
+        else:
+            out = ops.bn_apply(y3, st3, True, res=x)
+        ctx.save_for_backward(x, y1, a1, y2, a2, y3, yd, out)
+        ctx.sts = (st1, st2, st3, std)
+        ctx.blk = blk
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y1, a1, y2, a2, y3, yd, out = ctx.saved_tensors
+        st1, st2, st3, std = ctx.sts
+        blk = ctx.blk
+        dout = _c(dout)
+        s = blk.stride
+        N, H, W, Cin = x.shape
+        P = blk.conv1.weight.shape[0]
+        if blk.downsample is not None:
+            dy3 = ops.bn_backward(blk.bn3, st3, dout, y3, mask=out)
+            dyd = ops.bn_backward(blk.downsample[1], std, dout, yd, mask=out)
+            wd = blk.downsample[0].weight
+            dx = ops.conv_dgrad(dyd, ops.pack_weight(wd, x.dtype, 1), Cin, H, W, 1, 1, s, 0)
+            ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
+        else:
+            dx = torch.empty_like(x)
+            dy3 = ops.bn_backward(blk.bn3, st3, dout, y3, mask=out, dz_out=dx)
+        w3 = blk.conv3.weight
+        ops.conv_wgrad(dy3, a2, 1, 1, 1, 0, ops.grad_of(w3), _conv_ld(w3))
+        da2 = ops.conv_dgrad(dy3, ops.pack_weight(w3, x.dtype, 1), P, a2.shape[1], a2.shape[2], 1, 1, 1, 0)
+        dy2 = ops.bn_backward(blk.bn2, st2, da2, y2, mask=a2)
+        w2 = blk.conv2.weight
+        ops.conv_wgrad(dy2, a1, 3, 3, s, 1, ops.grad_of(w2), _conv_ld(w2))
+        da1 = ops.conv_dgrad(dy2, ops.pack_weight(w2, x.dtype, 1), P, a1.shape[1], a1.shape[2], 3, 3, s, 1)
+        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, mask=a1)
+        w1 = blk.conv1.weight
+        ops.conv_wgrad(dy1, x, 1, 1, 1, 0, ops.grad_of(w1), _conv_ld(w1))
+        ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 1, 1, 1, 0, out=dx, accumulate=True)
+        return dx, None, None
+
+
+class DeconvBNFn(torch.autograd.Function):
+    """ConvTranspose2d(k, s=2, p, op=0, bias=False) -> BN -> ReLU.  The deconv forward is the
+    input-gradient of the Conv2d whose weight is W_t (4 sub-pixel phases of 2x2 taps each)."""
+
+    @staticmethod
+    def forward(ctx, x, w, deconv, bn):
+        k = w.shape[2]
+        s, p = deconv.stride[0], deconv.padding[0]
+        Cout = w.shape[1]
+        stats = ops.new_stats(Cout, x.device) if bn.training else None
+        y = ops.deconv_fwd(x, ops.pack_weight(w, x.dtype, 1), Cout, k, s, p, stats=stats)
+        st = ops.bn_finalize(bn, stats, Cout, y.numel() // Cout, bn.training)
+        out = ops.bn_apply(y, st, True)
+        ctx.save_for_backward(x, y, out)
+        ctx.st, ctx.deconv, ctx.bn = st, deconv, bn
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y, out = ctx.saved_tensors
+        deconv, bn, st = ctx.deconv, ctx.bn, ctx.st
+        w = deconv.weight
+        k = w.shape[2]
+        s, p = deconv.stride[0], deconv.padding[0]
+        dy = ops.bn_backward(bn, st, _c(dout), y, mask=out)
+        # dW_t[i][o][r][s] = sum x[i at q] * dy[o at s*q + r - p]: weight-gradient GEMM with G = x
+        T = k * k
+        ops.conv_wgrad(x, dy, k, k, s, p, ops.grad_of(w), (w.shape[1] * T, T, 1))
+        dx = ops.deconv_dgrad(dy, ops.pack_weight(w, x.dtype, 0), w.shape[0], k, s, p)
+        return dx, None, None, None
+
+
+class ConvBNFn(torch.autograd.Function):
+    """Conv2d(no bias, 'same' padding) -> BN -> [ReLU] (Convolution, convolutions.py:25-49)."""
+
+    @staticmethod
+    def forward(ctx, x, w, conv, bn, relu):
+        s, p = conv.stride[0], conv.padding[0]
+        y, st = _train_bn_conv(x, conv, bn, s, p, bn.training)
+        out = ops.bn_apply(y, st, relu)
+        ctx.save_for_backward(x, y, out)
+        ctx.st, ctx.conv, ctx.bn, ctx.relu = st, conv, bn, relu
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y, out = ctx.saved_tensors
+        conv, bn, st = ctx.conv, ctx.bn, ctx.st
+        w = conv.weight
+        kh, kw = w.shape[2], w.shape[3]
+        s, p = conv.stride[0], conv.padding[0]
+        dy = ops.bn_backward(bn, st, _c(dout), y, mask=out if ctx.relu else None)
+        ops.conv_wgrad(dy, x, kh, kw, s, p, ops.grad_of(w), _conv_ld(w))
+        dx = ops.conv_dgrad(dy, ops.pack_weight(w, x.dtype, 1), x.shape[3], x.shape[1], x.shape[2], kh, kw, s, p)
+        return dx, None, None, None, None
+
+
+class HeadsFn(torch.autograd.Function):
+    """All CenterNet terminals (Conv2d 3x3 +bias -> ReLU -> Conv2d 1x1 +bias) fused:
+    hidden = relu(conv3x3(feat, W0cat) + b0cat) with N = sum of hidden widths, then the
+    block-diagonal 1x1 tails.  Outputs are NCHW fp32, one tensor per head."""
+
+    @staticmethod
+    def forward(ctx, feat, w0_first, heads):
+        N, H, W, Cin = feat.shape
+        w0 = torch.cat([h[0].weight for h in heads], 0)
+        b0 = torch.cat([h[0].bias for h in heads], 0)
+        Hd = heads[0][0].weight.shape[0]
+        Ct = w0.shape[0]
+        hid = ops.conv_fwd(feat, ops.pack_weight(w0, feat.dtype, 0), Ct, 3, 3, 1, 1, bias=b0, relu=True)
+        od = [h[2].weight.shape[0] for h in heads]
+        outs = [torch.empty(N, o, H, W, device=feat.device, dtype=torch.float32) for o in od]
+        ops.L.call("scd_heads_fwd", ops.dt(hid), ops.ptr(hid), N, H * W, len(heads), Hd, ops.L.int_array(od),
+                   ops.L.ptr_array([h[2].weight.data_ptr() for h in heads]),
+                   ops.L.ptr_array([h[2].bias.data_ptr() for h in heads]),
+                   ops.L.ptr_array([o.data_ptr() for o in outs]), ops.stream())
+        ctx.save_for_backward(feat, hid, w0)
+        ctx.heads, ctx.od, ctx.Hd = heads, od, Hd
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        feat, hid, w0 = ctx.saved_tensors
+        heads, od, Hd = ctx.heads, ctx.od, ctx.Hd
+        N, H, W, Cin = feat.shape
+        nh = len(heads)
+        douts = [(_c(d) if d is not None else torch.zeros(N, o, H, W, device=feat.device))
+                 for d, o in zip(douts, od)]
+        dptrs = ops.L.ptr_array([d.data_ptr() for d in douts])
+        odarr = ops.L.int_array(od)
+        dhid = torch.empty_like(hid)
+        ops.L.call("scd_heads_bwd_data", ops.dt(hid), ops.ptr(hid), N, H * W, nh, Hd, odarr,
+                   ops.L.ptr_array([h[2].weight.data_ptr() for h in heads]), dptrs, ops.ptr(dhid), ops.stream())
+        accsz = ops.L.lib().scd_heads_bwd_weight_accsize(nh, Hd, odarr)
+        acc = torch.zeros(accsz // 8, dtype=torch.float64, device=feat.device)
+        ops.L.call("scd_heads_bwd_weight", ops.dt(hid), ops.ptr(hid), ops.ptr(dhid), N, H * W, nh, Hd, odarr, dptrs,
+                   ops.ptr(acc), ops.stream())
+        ops.L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), nh, Hd, odarr,
+                   ops.L.ptr_array([ops.grad_of(h[2].weight).data_ptr() for h in heads]),
+                   ops.L.ptr_array([ops.grad_of(h[2].bias).data_ptr() for h in heads]),
+                   ops.L.ptr_array([ops.grad_of(h[0].bias).data_ptr() for h in heads]), 1, ops.stream())
+        ld = (Cin * 9, 9, 1)
+        rows = [(i * Hd, (i + 1) * Hd, ops.grad_of(h[0].weight), ld) for i, h in enumerate(heads)]
+        ops.conv_wgrad(dhid, feat, 3, 3, 1, 1, None, None, rows=rows)
+        dfeat = ops.conv_dgrad(dhid, ops.pack_weight(w0, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1)
+        return dfeat, None, None
+
+
+class CPoolFn(torch.autograd.Function):
+    """Directional corner pool (TopPoolFunction etc., cornerPooling/__init__.py:8-58) on NHWC."""
+
+    @staticmethod
+    def forward(ctx, x, direction):
+        ctx.save_for_backward(x)
+        ctx.direction = direction
+        return ops.cpool_fwd(x, direction)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return ops.cpool_bwd(x, _c(dy), ctx.direction), None
+
+
+class NCHWToNHWC(torch.autograd.Function):
+    """Layout boundary for callers that hand NCHW activations to a block (tests, custom heads)."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.dtype_in = x.dtype
+        return x.permute(0, 2, 3, 1).to(dtype).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.permute(0, 3, 1, 2).to(ctx.dtype_in).contiguous(), None

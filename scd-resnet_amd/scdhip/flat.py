@@ -1,0 +1,231 @@
+"""Flat parameter / gradient buffers, the Adam step and data-parallel gradient averaging.
+
+* ``FlatParams``: all trainable fp32 parameters of a model live in one contiguous device
+  buffer and every ``param.grad`` is a view of one flat gradient buffer, so the optimizer
+  is a single kernel launch and the DDP all-reduce is one (or a few bucketed) RCCL calls.
+* ``FlatAdam``: torch.optim.Adam semantics (defaults lr=1e-3, betas (0.9,0.999), eps 1e-8,
+  as the reference builds it without an lr, networkFactory.py:79-82) on scd_adam_step;
+  ``param_groups`` keeps the reference's setLearningRate (networkFactory.py:273-276) working.
+* ``FlatDDP``: replaces DistributedDataParallel (networkFactory.py:126-136): gradients are
+  averaged across ranks with torch.distributed (RCCL over xGMI on MI355X, gloo in CPU tests)
+  from an autograd end-of-backward callback; BN buffers are broadcast from rank 0 before
+  each forward (DDP broadcast_buffers=True); state_dict keys keep the ``module.`` prefix.
+"""
+import torch
+import torch.distributed as dist
+
+_REGISTRY = {}      # id(param) -> FlatParams
+
+
+class FlatParams:
+    def __init__(self, params):
+        params = [p for p in params if p.requires_grad]
+        if not params:
+            raise ValueError("no trainable parameters")
+        dev = params[0].device
+        for p in params:
+            if p.dtype != torch.float32 or p.device != dev:
+                raise ValueError("flat buffers need fp32 parameters on one device")
+        self.params = params
+        self.numel = sum(p.numel() for p in params)
+        self.data = torch.empty(self.numel, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.offsets = []
+        o = 0
+        for p in params:
+            n = p.numel()
+            self.data[o:o + n].copy_(p.detach().reshape(-1))
+            if p.grad is not None:
+                self.grad[o:o + n].copy_(p.grad.reshape(-1))
+            p.data = self.data[o:o + n].view_as(p)
+            p.grad = self.grad[o:o + n].view_as(p)
+            self.offsets.append((o, n))
+            o += n
+        self.grad_scale = 1.0
+        for p in params:
+            _REGISTRY[id(p)] = self
+
+    def rebind_grads(self):
+        """Re-attach .grad views if something set them to None (e.g. Module.zero_grad())."""
+        for p, (o, n) in zip(self.params, self.offsets):
+            g = p.grad
+            if g is None or g.data_ptr() != self.grad[o:o + n].data_ptr():
+                if g is not None:
+                    self.grad[o:o + n].copy_(g.reshape(-1))
+                else:
+                    self.grad[o:o + n].zero_()
+                p.grad = self.grad[o:o + n].view_as(p)
+
+    def valid(self):
+        return all(p.data_ptr() == self.data[o:o + n].data_ptr() for p, (o, n) in zip(self.params, self.offsets))
+
+
+def ensure_flat(params):
+    params = [p for p in params if p.requires_grad]
+    holders = {id(_REGISTRY.get(id(p))) for p in params}
+    if len(holders) == 1 and id(params[0]) in _REGISTRY:
+        fp = _REGISTRY[id(params[0])]
+        if fp.valid() and len(fp.params) == len(params):
+            return fp
+    return FlatParams(params)
+
+
+class FlatAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if weight_decay != 0.0:
+            raise NotImplementedError("weight decay is not used by the reference Adam")
+        super(FlatAdam, self).__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._flat = None
+        self._m = self._v = None
+        self._step = 0
+
+    def _all_params(self):
+        return [p for g in self.param_groups for p in g["params"]]
+
+    def flat(self):
+        if self._flat is None or not self._flat.valid():
+            self._flat = ensure_flat(self._all_params())
+            self._m = torch.zeros_like(self._flat.data)
+            self._v = torch.zeros_like(self._flat.data)
+        return self._flat
+
+    def zero_grad(self, set_to_none=False):
+        fp = self.flat() if self._all_params()[0].is_cuda else None
+        if fp is None:
+            return super(FlatAdam, self).zero_grad(set_to_none=set_to_none)
+        fp.rebind_grads()
+        fp.grad.zero_()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from . import ops
+        fp = self.flat()
+        fp.rebind_grads()
+        g = self.param_groups[0]
+        self._step += 1
+        ops.adam_step(fp.data, fp.grad, self._m, self._v, g["lr"], g["betas"][0], g["betas"][1], g["eps"],
+                      self._step, gscale=fp.grad_scale)
+        return None
+
+    def state_dict(self):
+        return {"step": self._step, "param_groups": [{k: v for k, v in g.items() if k != "params"}
+                                                     for g in self.param_groups],
+                "exp_avg": None if self._m is None else self._m.cpu(),
+                "exp_avg_sq": None if self._v is None else self._v.cpu()}
+
+    def load_state_dict(self, sd):
+        self._step = sd["step"]
+        for g, s in zip(self.param_groups, sd["param_groups"]):
+            g.update(s)
+        if sd.get("exp_avg") is not None:
+            self.flat()
+            self._m.copy_(sd["exp_avg"])
+            self._v.copy_(sd["exp_avg_sq"])
+
+
+class _EndOfBackward(torch.autograd.Function):
+    """Identity on the model outputs whose backward queues the gradient all-reduce at the
+    end of the backward pass (the hook torch's DDP reducer also uses)."""
+
+    @staticmethod
+    def forward(ctx, ddp, *xs):
+        ctx.ddp = ddp
+        return xs if len(xs) > 1 else xs[0]
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ddp = ctx.ddp
+        if not ddp._queued:
+            ddp._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(ddp._allreduce_grads)
+        return (None,) + gs
+
+
+class FlatDDP(torch.nn.Module):
+    """DistributedDataParallel replacement: one process per GPU, grads averaged over the
+    world (bucketed RCCL all-reduce of the flat gradient buffer)."""
+
+    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_mb=25.0):
+        super(FlatDDP, self).__init__()
+        self.module = module
+        self.group = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.broadcast_buffers = broadcast_buffers
+        self.flat = ensure_flat(module.parameters())
+        self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
+        self._queued = False
+        self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        if self.world > 1:
+            # identical initial replicas (DDP broadcasts parameters from rank 0 at wrap time)
+            dist.broadcast(self.flat.data, 0, group=process_group)
+            self._sync_buffers()
+
+    def _sync_buffers(self):
+        for b in self.module.buffers():
+            dist.broadcast(b, 0, group=self.group)
+
+    def _allreduce_grads(self):
+        self._queued = False
+        if self.world == 1:
+            return
+        g = self.flat.grad
+        for o in range(0, g.numel(), self.bucket_elems):
+            bucket = g[o:o + self.bucket_elems]
+            if self._use_avg:
+                dist.all_reduce(bucket, op=dist.ReduceOp.AVG, group=self.group)
+            else:
+                dist.all_reduce(bucket, group=self.group)
+                bucket.div_(self.world)
+
+    def forward(self, *args, **kwargs):
+        if self.world > 1 and self.broadcast_buffers and self.training:
+            self._sync_buffers()
+        out = self.module(*args, **kwargs)
+        if not torch.is_grad_enabled() or self.world == 1:
+            return out
+        # route every differentiable output tensor through the end-of-backward hook
+        flat, spec = _flatten(out)
+        idx = [i for i, t in enumerate(flat) if torch.is_tensor(t) and t.requires_grad]
+        if not idx:
+            return out
+        hooked = _EndOfBackward.apply(self, *[flat[i] for i in idx])
+        if len(idx) == 1:
+            hooked = (hooked,)
+        for i, t in zip(idx, hooked):
+            flat[i] = t
+        return _unflatten(flat, spec)
+
+
+def _flatten(obj):
+    if isinstance(obj, (list, tuple)):
+        items, specs = [], []
+        for o in obj:
+            f, s = _flatten(o)
+            items.extend(f)
+            specs.append((len(f), s))
+        return items, (type(obj), specs)
+    if isinstance(obj, dict):
+        items, specs = [], []
+        for k, o in obj.items():
+            f, s = _flatten(o)
+            items.extend(f)
+            specs.append((k, len(f), s))
+        return items, (dict, specs)
+    return [obj], None
+
+
+def _unflatten(items, spec):
+    if spec is None:
+        return items[0]
+    kind, specs = spec
+    out, o = [], 0
+    if kind is dict:
+        d = {}
+        for k, n, s in specs:
+            d[k] = _unflatten(items[o:o + n], s)
+            o += n
+        return d
+    for n, s in specs:
+        out.append(_unflatten(items[o:o + n], s))
+        o += n
+    return kind(out)

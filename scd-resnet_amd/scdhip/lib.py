@@ -1,0 +1,125 @@
+"""ctypes binding of libscdhip.so (the C-ABI declared in include/scdhip.h).
+
+This is the MI355X replacement for the reference's native-op bindings: the pybind11
+``topPool/bottomPool/leftPool/rightPool`` modules (cornerPooling/source/topPool.cpp:76-85)
+and the cuDNN/ATen kernels reached through torch.nn.  No torch C++ headers: device
+pointers, sizes and the current HIP stream go through plain C.
+
+The library is required: importing this module without it, or calling it with a CPU
+tensor, raises -- there is no CPU or eager-PyTorch fallback on the product path.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported first: shares torch's libamdhip64.so.7)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SCDHIP_LIB", os.path.join(HERE, "libscdhip.so"))
+
+DT_F32 = 0
+DT_BF16 = 1
+MAX_TAPS = 16
+MAX_PHASES = 4
+STAT_REPLICAS = 64
+
+c_int, c_long, c_float, c_double, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
+                                                        ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)
+
+
+class GemmPhase(ctypes.Structure):
+    _fields_ = [("Qh", c_int), ("Qw", c_int), ("rho_h", c_int), ("rho_w", c_int), ("ntaps", c_int),
+                ("dh", c_int * MAX_TAPS), ("dw", c_int * MAX_TAPS), ("wt", c_int * MAX_TAPS)]
+
+
+P = c_void_p
+I = c_int
+L = c_long
+F = c_float
+D = c_double
+PP = ctypes.POINTER(c_void_p)
+IP = ctypes.POINTER(c_int)
+
+# name -> (restype, argtypes); mirrors include/scdhip.h one to one
+SIGNATURES = {
+    "scd_conv_gemm": (I, [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P]),
+    "scd_conv_wgrad_workspace": (c_size_t, [I, I, I, I]),
+    "scd_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, IP, IP, P]),
+    "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, P]),
+    "scd_pack_weight": (I, [I, P, P, I, I, I, I, I, I, P]),
+    "scd_im2col_stem": (I, [I, P, P, I, I, I, I, I, I, I, I, I, I, P]),
+    "scd_stats_collapse": (I, [P, I, I, P]),
+    "scd_bn_finalize": (I, [P, I, I, D, P, P, P, P, P, F, F, P, P, P, P, P]),
+    "scd_bn_apply": (I, [I, P, P, I, L, P, P, P, P, P, I, P]),
+    "scd_bn_bwd_reduce": (I, [I, P, P, P, P, P, I, L, P, P]),
+    "scd_bn_bwd_finalize": (I, [P, I, I, D, P, P, P, P, P, P, P]),
+    "scd_bn_bwd_apply": (I, [I, P, P, P, P, I, L, P, P, P]),
+    "scd_stem_pool_fwd": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
+    "scd_stem_pool_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
+    "scd_heads_fwd": (I, [I, P, I, I, I, I, IP, PP, PP, PP, P]),
+    "scd_heads_bwd_data": (I, [I, P, I, I, I, I, IP, PP, PP, P, P]),
+    "scd_heads_bwd_weight_accsize": (c_size_t, [I, I, IP]),
+    "scd_heads_bwd_weight": (I, [I, P, P, I, I, I, I, IP, PP, P, P]),
+    "scd_heads_bwd_weight_finalize": (I, [P, I, I, IP, PP, PP, PP, I, P]),
+    "scd_focal_fwd": (I, [P, P, L, P, P, P]),
+    "scd_l1_gather_fwd": (I, [P, I, I, I, P, P, P, I, I, I, P, P, P]),
+    "scd_centernet_loss_finalize": (I, [P, I, P, I, P, P, P, P]),
+    "scd_scale_by_device": (I, [P, L, P, I, P, P]),
+    "scd_decode_workspace": (c_size_t, [I, I]),
+    "scd_decode_topk": (I, [P, I, I, I, I, P, I, P, I, P, P, P, P, P, P, P, P]),
+    "scd_adam_step": (I, [P, P, P, P, L, F, F, F, F, F, F, F, P]),
+    "scd_cpool_fwd": (I, [I, I, P, P, I, I, I, I, P]),
+    "scd_cpool_bwd": (I, [I, I, P, P, P, I, I, I, I, P]),
+    "scd_version": (ctypes.c_char_p, []),
+}
+
+
+class _Lib:
+    def __init__(self, path):
+        if not os.path.exists(path):
+            raise RuntimeError("libscdhip.so not found at %s -- build it with `python -c 'import __graft_entry__ as g; "
+                               "g.build()'` (make -C scd-resnet_amd/csrc).  There is no CPU fallback." % path)
+        self.path = path
+        self.dll = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(self.dll, name)
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, name, fn)
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = _Lib(LIB_PATH)
+    return _LIB
+
+
+def check(rc, name):
+    if rc != 0:
+        raise RuntimeError("libscdhip: %s failed with status %d%s" % (
+            name, rc, " (invalid argument / unsupported shape)" if rc == 9001 else " (hipError)"))
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr_array(ptrs):
+    arr = (c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def int_array(vals):
+    arr = (c_int * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
+    return arr
+
+
+def exported_symbols():
+    return list(SIGNATURES)

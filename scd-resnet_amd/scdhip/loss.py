@@ -1,0 +1,102 @@
+"""Fused device-side CenterNet / CornerNet losses (no host syncs).
+
+CenterNetLoss.forward (centerNetOffset.py:182-217) =
+    focal(clampSigmoid(heatmap), gt)                       focal.py:25-53
+  + wr * L1LossMask(gather(regr, inds), gt[..., 2:6], mask)  regression.py:37-44
+  + wo * L1LossMask(gather(offset, inds), gt[..., 0:2], mask)
+The reference's boolean-mask indexing (a `nonzero` host sync per call) and the Python
+`#pos == 0` branch are replaced by device accumulators and a finalize kernel; the
+normalisers stay on device and scale the saved per-element gradients in backward.
+"""
+import torch
+
+from . import lib as L
+from . import ops
+
+
+class CenterNetLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, heat, regr, off, gt_heat, mask, regr_t, inds, wr, wo):
+        ops._need_gpu(heat, gt_heat)
+        heat, regr, off = heat.contiguous(), regr.contiguous(), off.contiguous()
+        N, _, H, W = heat.shape
+        HW = H * W
+        K = inds.shape[1]
+        dev = heat.device
+        mask_u8 = mask.to(torch.uint8) if mask.dtype != torch.uint8 else mask
+        mask_u8 = mask_u8.contiguous()
+        inds = inds.to(torch.int64).contiguous()
+        regr_t = regr_t.float().contiguous()
+        gt_heat = gt_heat.float().contiguous()
+        s = ops.stream()
+        g_heat = torch.empty_like(heat)
+        facc = torch.zeros(L.STAT_REPLICAS * 4, dtype=torch.float64, device=dev)
+        L.call("scd_focal_fwd", ops.ptr(heat), ops.ptr(gt_heat), heat.numel(), ops.ptr(g_heat), ops.ptr(facc), s)
+        lacc = torch.zeros(4, dtype=torch.float64, device=dev)
+        g_regr = torch.zeros_like(regr)
+        g_off = torch.zeros_like(off)
+        L.call("scd_l1_gather_fwd", ops.ptr(regr), N, regr.shape[1], HW, ops.ptr(inds), ops.ptr(mask_u8),
+               ops.ptr(regr_t), K, regr_t.shape[2], 2, ops.ptr(g_regr), ops.ptr(lacc), s)
+        L.call("scd_l1_gather_fwd", ops.ptr(off), N, off.shape[1], HW, ops.ptr(inds), ops.ptr(mask_u8),
+               ops.ptr(regr_t), K, regr_t.shape[2], 0, ops.ptr(g_off), ops.ptr(lacc[2:]), s)
+        out = torch.empty(4, device=dev)
+        factors = torch.empty(3, device=dev)
+        wts = (ctypes_float2(wr, wo))
+        L.call("scd_centernet_loss_finalize", ops.ptr(facc), 1, ops.ptr(lacc), 2, wts, ops.ptr(out),
+               ops.ptr(factors), s)
+        ctx.save_for_backward(g_heat, g_regr, g_off, factors)
+        loss = out[0:1]
+        stats = out[1:4]
+        ctx.mark_non_differentiable(stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, gl, gstats):
+        g_heat, g_regr, g_off, factors = ctx.saved_tensors
+        gl = gl.contiguous() if gl is not None else torch.ones(1, device=g_heat.device)
+        s = ops.stream()
+        for i, g in enumerate((g_heat, g_regr, g_off)):
+            L.call("scd_scale_by_device", ops.ptr(g), g.numel(), ops.ptr(factors), i, ops.ptr(gl), s)
+        return g_heat, g_regr, g_off, None, None, None, None, None, None
+
+
+class FocalOnlyLossFn(torch.autograd.Function):
+    """CornerNetLoss.forward (cornerNetCPool.py:244-272): sum of focal losses on several maps."""
+
+    @staticmethod
+    def forward(ctx, *args):
+        n = len(args) // 2
+        heats, gts = args[:n], args[n:]
+        dev = heats[0].device
+        s = ops.stream()
+        facc = torch.zeros(n * L.STAT_REPLICAS * 4, dtype=torch.float64, device=dev)
+        grads = []
+        for i, (h, g) in enumerate(zip(heats, gts)):
+            h = h.contiguous()
+            gh = torch.empty_like(h)
+            L.call("scd_focal_fwd", ops.ptr(h), ops.ptr(g.float().contiguous()), h.numel(), ops.ptr(gh),
+                   ops.ptr(facc[i * L.STAT_REPLICAS * 4:]), s)
+            grads.append(gh)
+        out = torch.empty(1 + n, device=dev)
+        factors = torch.empty(n, device=dev)
+        L.call("scd_centernet_loss_finalize", ops.ptr(facc), n, 0, 0, ctypes_float2(0.0, 0.0), ops.ptr(out),
+               ops.ptr(factors), s)
+        ctx.save_for_backward(factors, *grads)
+        stats = out[1:]
+        ctx.mark_non_differentiable(stats)
+        return out[0:1], stats
+
+    @staticmethod
+    def backward(ctx, gl, gstats):
+        factors, *grads = ctx.saved_tensors
+        gl = gl.contiguous() if gl is not None else torch.ones(1, device=factors.device)
+        s = ops.stream()
+        for i, g in enumerate(grads):
+            L.call("scd_scale_by_device", ops.ptr(g), g.numel(), ops.ptr(factors), i, ops.ptr(gl), s)
+        return tuple(grads) + (None,) * len(grads)
+
+
+def ctypes_float2(a, b):
+    import ctypes
+    arr = (ctypes.c_float * 2)(float(a), float(b))
+    return ctypes.cast(arr, ctypes.c_void_p)

@@ -1,0 +1,333 @@
+"""Tensor-level wrappers over the libscdhip C-ABI (device memory and streams come from torch).
+
+Layouts: activations NHWC (channels innermost) in the compute dtype (fp32 parity mode,
+bf16 performance mode); weights, grads, BN parameters fp32 in the reference layout.
+Every wrapper enqueues on torch's current HIP stream and never synchronises.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import lib as L
+
+_DT = {torch.float32: L.DT_F32, torch.bfloat16: L.DT_BF16}
+
+
+def dt(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise RuntimeError("libscdhip: unsupported dtype %s" % t.dtype)
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _need_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("scd-resnet_amd runs on MI355X only: got a CPU tensor (no CPU fallback; the CPU "
+                               "restatement lives in oracle/ and is test infrastructure)")
+
+
+# ------------------------------------------------------------------ SyncBN / process group
+
+class _BNSync:
+    group = None          # torch.distributed group for SyncBatchNorm semantics (None = local BN)
+    world = 1
+
+
+def set_bn_sync(group):
+    """Enable global-batch BN statistics (SyncBatchNorm, networkFactory.py:128-133)."""
+    _BNSync.group = group
+    _BNSync.world = dist.get_world_size(group) if group is not None else 1
+
+
+def bn_sync_world():
+    return _BNSync.world if _BNSync.group is not None else 1
+
+
+def _allreduce_stats(stats, C):
+    """collapse replicas and all-reduce [2][C] fp64 over the BN group; returns nrep."""
+    if _BNSync.group is None:
+        return L.STAT_REPLICAS
+    L.call("scd_stats_collapse", ptr(stats), L.STAT_REPLICAS, C, stream())
+    dist.all_reduce(stats[:2 * C], group=_BNSync.group)
+    return 1
+
+
+def new_stats(C, device):
+    return torch.zeros(L.STAT_REPLICAS * 2 * C, dtype=torch.float64, device=device)
+
+
+# ------------------------------------------------------------------ weights
+
+def pack_weight(w, dtype, mode, ldp=None, out=None, row_off=0):
+    """(A,B,kh,kw) fp32 -> GEMM operand. mode 0: [A][taps][B]; mode 1: [B][taps][A]."""
+    A, B = w.shape[0], w.shape[1]
+    T = w.shape[2] * w.shape[3]
+    rows = A if mode == 0 else B
+    ldp = ldp or T * (B if mode == 0 else A)
+    if out is None:
+        out = torch.empty(rows, ldp, dtype=dtype, device=w.device)
+    L.call("scd_pack_weight", _DT[dtype], ptr(w), ptr(out), A, B, T, mode, ldp, row_off, stream())
+    return out
+
+
+# ------------------------------------------------------------------ gather-GEMM convolution
+
+def _fwd_phase(kh, kw, pad, Ho, Wo):
+    ph = L.GemmPhase()
+    ph.Qh, ph.Qw, ph.rho_h, ph.rho_w = Ho, Wo, 0, 0
+    ph.ntaps = kh * kw
+    for r in range(kh):
+        for s in range(kw):
+            t = r * kw + s
+            ph.dh[t], ph.dw[t], ph.wt[t] = r - pad, s - pad, t
+    return [ph]
+
+
+def _dgrad_phases(kh, kw, stride, pad, Hc, Wc):
+    """Sub-pixel decomposition of the input-gradient of Conv2d(kh,kw,stride,pad) whose input is
+    (Hc,Wc): output pixel st*q+rho gathers dy at q + (rho+pad-r)/st for taps r = rho+pad (mod st)."""
+    phases = []
+    for rh in range(stride):
+        for rw in range(stride):
+            Qh = -(-(Hc - rh) // stride)
+            Qw = -(-(Wc - rw) // stride)
+            if Qh <= 0 or Qw <= 0:
+                continue
+            ph = L.GemmPhase()
+            ph.Qh, ph.Qw, ph.rho_h, ph.rho_w = Qh, Qw, rh, rw
+            taps = [(r, s) for r in range(kh) if (r - rh - pad) % stride == 0
+                    for s in range(kw) if (s - rw - pad) % stride == 0]
+            ph.ntaps = len(taps)
+            for t, (r, s) in enumerate(taps):
+                ph.dh[t] = (rh + pad - r) // stride
+                ph.dw[t] = (rw + pad - s) // stride
+                ph.wt[t] = r * kw + s
+            phases.append(ph)
+    return phases
+
+
+def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, stats=None, relu=False,
+          accumulate=False):
+    N, Hi, Wi, Ci = x.shape
+    arr = (L.GemmPhase * len(phases))(*phases)
+    L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
+           in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr, stream())
+    return y
+
+
+def conv_fwd(x, wpack, Co, kh, kw, stride, pad, bias=None, stats=None, relu=False, out=None):
+    """Conv2d forward (NHWC); wpack = pack_weight(w, mode=0)."""
+    _need_gpu(x)
+    N, H, W, _ = x.shape
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co, dtype=x.dtype, device=x.device)
+    return _gemm(x, wpack, out, Co, Ho, Wo, stride, 1, _fwd_phase(kh, kw, pad, Ho, Wo), bias, stats, relu)
+
+
+def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumulate=False, stats=None):
+    """Input-gradient of Conv2d (NHWC) as a phase-decomposed gather-GEMM; wpack_t = pack_weight(w, mode=1).
+    Also ConvTranspose2d forward (with the transposed conv's geometry)."""
+    N = dy.shape[0]
+    if out is None:
+        out = torch.empty(N, Hc, Wc, Cin, dtype=dy.dtype, device=dy.device)
+    return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, _dgrad_phases(kh, kw, stride, pad, Hc, Wc),
+                 stats=stats, accumulate=accumulate)
+
+
+def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None):
+    """ConvTranspose2d(k, stride, pad, output_padding=0) forward; wpack_t = pack_weight(W_t, mode=1)."""
+    _need_gpu(x)
+    N, H, W, _ = x.shape
+    Ho = (H - 1) * stride - 2 * pad + k
+    Wo = (W - 1) * stride - 2 * pad + k
+    return conv_dgrad(x, wpack_t, Cout, Ho, Wo, k, k, stride, pad, stats=stats)
+
+
+def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=False):
+    """ConvTranspose2d input-gradient = Conv2d forward of dy; wpack = pack_weight(W_t, mode=0)."""
+    N, H, W, _ = dy.shape
+    Ho = (H + 2 * pad - k) // stride + 1
+    Wo = (W + 2 * pad - k) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Cin, dtype=dy.dtype, device=dy.device)
+    return _gemm(dy, wpack, out, Cin, Ho, Wo, stride, 1, _fwd_phase(k, k, pad, Ho, Wo), accumulate=accumulate)
+
+
+def _nsplit(M, Cg, KK, Cg_tile, KK_tile):
+    tiles = -(-Cg // Cg_tile) * -(-KK // KK_tile)
+    ns = max(1, min(1024 // tiles, M // 1024))
+    # cap the fp32 workspace at ~256 MB
+    ns = max(1, min(ns, (256 << 20) // max(1, 4 * Cg * KK)))
+    return ns
+
+
+def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None):
+    """Weight gradient of the gather-GEMM: dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= sum_pix g[pix,r] x[gather,ci].
+
+    g: (N,Ho,Wo,Cg) NHWC output-gradient; x: (N,Hi,Wi,Ci) NHWC input; taps gather
+    x at (stride*oh + r - pad, stride*ow + s - pad).  `rows` = list of (r0, r1, dst, ld) slices.
+    """
+    N, Ho, Wo, Cg = g.shape
+    _, Hi, Wi, Ci = x.shape
+    T = kh * kw
+    dh = L.int_array([r - pad for r in range(kh) for s in range(kw)])
+    dw = L.int_array([s - pad for r in range(kh) for s in range(kw)])
+    M = N * Ho * Wo
+    narrow = Cg <= 64
+    ns = _nsplit(M, Cg, T * Ci, 64 if narrow else 128, 256 if narrow else 128)
+    ws = torch.empty(L.lib().scd_conv_wgrad_workspace(Cg, T, Ci, ns) // 4, dtype=torch.float32, device=g.device)
+    L.call("scd_conv_wgrad", dt(g), ptr(g), ptr(x), ptr(ws), ns, N, Ho, Wo, Cg, Hi, Wi, Ci, stride, T, dh, dw,
+           stream())
+    if rows is None:
+        rows = [(0, Cg, dst, ld)]
+    cv = Ci if cvalid is None else cvalid
+    for r0, r1, d, (ldn, ldc, ldt) in rows:
+        L.call("scd_wgrad_reduce", ptr(ws), ns, Cg, T, Ci, r0, r1, cv, ldn, ldc, ldt, ptr(d), int(accumulate),
+               stream())
+
+
+# ------------------------------------------------------------------ BatchNorm (training)
+
+class BNState:
+    """Per-call BN quantities kept for backward."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "count")
+
+
+def bn_finalize(bn, stats, C, count, training=True):
+    """Finalize statistics of a torch.nn.BatchNorm2d-shaped module `bn` (weight/bias/running_*)."""
+    dev = bn.weight.device
+    st = BNState()
+    st.mean = torch.empty(C, device=dev)
+    st.invstd = torch.empty(C, device=dev)
+    st.scale = torch.empty(C, device=dev)
+    st.shift = torch.empty(C, device=dev)
+    if training:
+        nrep = _allreduce_stats(stats, C)
+        count = count * bn_sync_world()
+        L.call("scd_bn_finalize", ptr(stats), nrep, C, float(count), ptr(bn.weight), ptr(bn.bias),
+               ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.num_batches_tracked), float(bn.momentum),
+               float(bn.eps), ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift), stream())
+    else:
+        L.call("scd_bn_finalize", 0, 0, C, 1.0, ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+               ptr(bn.running_var), 0, 0.0, float(bn.eps), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
+               ptr(st.shift), stream())
+    st.count = count
+    return st
+
+
+def bn_apply(y, st, relu, res=None, rst=None, out=None):
+    C = y.shape[-1]
+    if out is None:
+        out = torch.empty_like(y)
+    L.call("scd_bn_apply", dt(y), ptr(y), ptr(out), C, y.numel(), ptr(st.scale), ptr(st.shift), ptr(res),
+           ptr(rst.scale) if rst is not None else 0, ptr(rst.shift) if rst is not None else 0, int(relu), stream())
+    return out
+
+
+def bn_backward(bn, st, dout, y, mask=None, dz_out=None):
+    """Training BN backward: dgamma/dbeta accumulated into bn.weight.grad / bn.bias.grad, returns dy."""
+    C = y.shape[-1]
+    stats = new_stats(C, y.device)
+    L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), ptr(st.mean), ptr(st.invstd), C, y.numel(),
+           ptr(stats), stream())
+    nrep = _allreduce_stats(stats, C)
+    coef = torch.empty(3 * C, device=y.device)
+    L.call("scd_bn_bwd_finalize", ptr(stats), nrep, C, float(st.count), ptr(bn.weight), ptr(st.mean),
+           ptr(st.invstd), ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), ptr(coef), stream())
+    dy = torch.empty_like(y)
+    L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), ptr(coef), C, y.numel(), ptr(dy), ptr(dz_out),
+           stream())
+    return dy
+
+
+def grad_of(p):
+    """The parameter's .grad buffer (created zero if absent); kernels accumulate into it."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+# ------------------------------------------------------------------ misc layers
+
+def im2col_stem(x, dtype, kh=7, kw=7, stride=2, pad=3, Kpad=64):
+    _need_gpu(x)
+    N, _, H, W = x.shape
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    cols = torch.empty(N, Ho, Wo, Kpad, dtype=dtype, device=x.device)
+    L.call("scd_im2col_stem", _DT[dtype], ptr(x.contiguous()), ptr(cols), N, H, W, Ho, Wo, kh, kw, stride, pad, Kpad,
+           stream())
+    return cols
+
+
+def stem_pool_fwd(y, st):
+    N, H, W, C = y.shape
+    Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    out = torch.empty(N, Ho, Wo, C, dtype=y.dtype, device=y.device)
+    am = torch.empty(N, Ho, Wo, C, dtype=torch.uint8, device=y.device)
+    L.call("scd_stem_pool_fwd", dt(y), ptr(y), ptr(st.scale), ptr(st.shift), ptr(out), ptr(am), N, H, W, C, Ho, Wo,
+           stream())
+    return out, am
+
+
+def stem_pool_bwd(dout, am, y, st):
+    N, H, W, C = y.shape
+    dz = torch.empty_like(y)
+    L.call("scd_stem_pool_bwd", dt(y), ptr(dout), ptr(am), ptr(y), ptr(st.scale), ptr(st.shift), ptr(dz), N, H, W,
+           C, dout.shape[1], dout.shape[2], stream())
+    return dz
+
+
+def cpool_fwd(x, direction):
+    N, H, W, C = x.shape
+    y = torch.empty_like(x)
+    L.call("scd_cpool_fwd", dt(x), direction, ptr(x), ptr(y), N, H, W, C, stream())
+    return y
+
+
+def cpool_bwd(x, dy, direction):
+    N, H, W, C = x.shape
+    dx = torch.empty_like(x)
+    L.call("scd_cpool_bwd", dt(x), direction, ptr(x), ptr(dy), ptr(dx), N, H, W, C, stream())
+    return dx
+
+
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, gscale=1.0):
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    L.call("scd_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(beta1), float(beta2),
+           float(eps), float(bc1), float(bc2), float(gscale), stream())
+
+
+def decode_topk(heat, offset, regr, K=100):
+    """decodeCenterNet core: sigmoid -> 3x3 NMS -> top-K -> gather (centerNetOffset.py:219-251)."""
+    _need_gpu(heat)
+    N, _, H, W = heat.shape
+    K = min(K, H * W)
+    dev = heat.device
+    scores = torch.empty(N, K, device=dev)
+    inds = torch.empty(N, K, dtype=torch.int64, device=dev)
+    ys = torch.empty_like(inds)
+    xs = torch.empty_like(inds)
+    od_off = offset.shape[1] if offset is not None else 0
+    od_regr = regr.shape[1] if regr is not None else 0
+    off_out = torch.empty(N, K, max(od_off, 1), device=dev)[:, :, :od_off]
+    regr_out = torch.empty(N, K, max(od_regr, 1), device=dev)[:, :, :od_regr]
+    ws = torch.empty(L.lib().scd_decode_workspace(N, H * W) // 4, device=dev)
+    L.call("scd_decode_topk", ptr(heat.contiguous()), N, H, W, K,
+           ptr(offset.contiguous()) if offset is not None else 0, od_off,
+           ptr(regr.contiguous()) if regr is not None else 0, od_regr, ptr(scores), ptr(inds), ptr(ys), ptr(xs),
+           ptr(off_out), ptr(regr_out), ptr(ws), stream())
+    return scores, inds, ys, xs, (off_out if offset is not None else None), (regr_out if regr is not None else None)

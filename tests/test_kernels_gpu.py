@@ -1,0 +1,147 @@
+"""Per-kernel parity of libscdhip against PyTorch fp32 CPU references (floating-point ops).
+
+Tolerances: fp32 parity mode (exact-f32 MFMA) 1e-4 relative to the output scale; bf16 mode
+3e-2 relative (8-bit mantissa operands, fp32 accumulation)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    return (a - b).abs().max().item() / max(1e-6, b.abs().max().item())
+
+
+def nhwc(t, dtype):
+    return t.permute(0, 2, 3, 1).contiguous().to(DEV, dtype)
+
+
+def nchw(t):
+    return t.float().permute(0, 3, 1, 2).cpu()
+
+
+TOL = {torch.float32: 1e-4, torch.bfloat16: 3e-2}
+CONV_CASES = [  # N, Cin, H, W, Cout, k, stride, pad
+    (2, 64, 16, 16, 64, 3, 1, 1),
+    (2, 64, 16, 16, 128, 3, 2, 1),
+    (2, 64, 15, 13, 128, 1, 2, 0),
+    (1, 128, 9, 11, 256, 3, 1, 1),
+    (2, 64, 20, 20, 384, 3, 1, 1),
+    (1, 256, 8, 8, 512, 3, 2, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case, dtype):
+    from scdhip import ops
+    N, Cin, H, W, Cout, k, s, p = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    if dtype == torch.bfloat16:       # compare on bf16-representable operands
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=s, padding=p)
+    dy = torch.randn(yr.shape, generator=g)
+    if dtype == torch.bfloat16:
+        dy = dy.bfloat16().float()
+    yr.backward(dy)
+    wd = w.to(DEV)
+    xg = nhwc(x, dtype)
+    stats = ops.new_stats(Cout, DEV)
+    y = ops.conv_fwd(xg, ops.pack_weight(wd, dtype, 0), Cout, k, k, s, p, stats=stats)
+    assert rel_err(nchw(y), yr) < TOL[dtype]
+    # BN statistics from the epilogue
+    st = stats.view(-1, 2, Cout).sum(0).cpu()
+    yd = yr.detach().double()
+    np.testing.assert_allclose(st[0].numpy(), yd.sum((0, 2, 3)).numpy(), rtol=1e-3, atol=1e-2 * yd.numel() ** 0.5)
+    dyg = nhwc(dy, dtype)
+    dx = ops.conv_dgrad(dyg, ops.pack_weight(wd, dtype, 1), Cin, H, W, k, k, s, p)
+    assert rel_err(nchw(dx), xr.grad) < TOL[dtype]
+    dw = torch.zeros_like(wd)
+    ops.conv_wgrad(dyg, xg, k, k, s, p, dw, (Cin * k * k, k * k, 1), accumulate=False)
+    assert rel_err(dw, wr.grad) < TOL[dtype] * 3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 128, 5, 7, 64), (1, 256, 8, 8, 256), (2, 64, 16, 16, 128)])
+def test_deconv_fwd_dgrad_wgrad(case, dtype):
+    from scdhip import ops
+    N, Cin, H, W, Cout = case
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cin, Cout, 4, 4, generator=g) / (Cin * 4) ** 0.5
+    if dtype == torch.bfloat16:
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, wr, stride=2, padding=1)
+    dy = torch.randn(yr.shape, generator=g)
+    if dtype == torch.bfloat16:
+        dy = dy.bfloat16().float()
+    yr.backward(dy)
+    wd = w.to(DEV)
+    xg = nhwc(x, dtype)
+    y = ops.deconv_fwd(xg, ops.pack_weight(wd, dtype, 1), Cout)
+    assert y.shape == (N, 2 * H, 2 * W, Cout)
+    assert rel_err(nchw(y), yr) < TOL[dtype]
+    dyg = nhwc(dy, dtype)
+    dx = ops.deconv_dgrad(dyg, ops.pack_weight(wd, dtype, 0), Cin)
+    assert rel_err(nchw(dx), xr.grad) < TOL[dtype]
+    dw = torch.zeros_like(wd)
+    ops.conv_wgrad(xg, dyg, 4, 4, 2, 1, dw, (Cout * 16, 16, 1), accumulate=False)
+    assert rel_err(dw, wr.grad) < TOL[dtype] * 3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_stem_im2col_gemm_pool(dtype):
+    from scdhip import ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 1, 64, 48, generator=g)
+    w = torch.randn(64, 1, 7, 7, generator=g) / 7.0
+    if dtype == torch.bfloat16:
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    cols = ops.im2col_stem(x.to(DEV), dtype)
+    y = ops.conv_fwd(cols, ops.pack_weight(w.to(DEV), dtype, 0, ldp=64), 64, 1, 1, 1, 0)
+    yr = F.conv2d(x, w, stride=2, padding=3)
+    assert rel_err(nchw(y), yr) < TOL[dtype]
+
+
+def test_cpool_fwd_bwd_fp32():
+    from scdhip import ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 8, 9, 12, generator=g)
+    x[0, 0, 3, :] = x[0, 0, 5, :]          # ties along H
+    x[1, 2, :, 4] = 0.5                    # constant lines
+    dy = torch.randn(x.shape, generator=g)
+    from oracle import cpool as CP
+    for d in range(4):
+        y = ops.cpool_fwd(nhwc(x, torch.float32), d)
+        np.testing.assert_allclose(nchw(y).numpy(), CP.forward(x, d).numpy(), rtol=0, atol=0)
+        dx = ops.cpool_bwd(nhwc(x, torch.float32), nhwc(dy, torch.float32), d)
+        np.testing.assert_allclose(nchw(dx).numpy(), CP.backward(x, dy, d).numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_adam_matches_torch():
+    from scdhip import ops
+    g = torch.Generator().manual_seed(9)
+    p0 = torch.randn(10007, generator=g)
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=1e-3)
+    p = p0.clone().to(DEV)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for step in range(1, 4):
+        gr = torch.randn(10007, generator=g)
+        pt.grad = gr.clone()
+        opt.step()
+        ops.adam_step(p, gr.to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, step)
+    np.testing.assert_allclose(p.cpu().numpy(), pt.detach().numpy(), rtol=1e-6, atol=1e-7)

@@ -1,0 +1,161 @@
+"""End-to-end parity of the HIP CenterNet-Res10 path against the reference's golden vectors
+(tests/golden, produced by running the reference) and the CPU oracle.
+
+fp32 parity mode: heads within 1e-3 (north-star tolerance), losses 1e-4 relative, decode
+peak indices bit-exact wherever the oracle's scores are not tied.  bf16 mode is checked
+against fp32 with a documented looser bound."""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import centernet as O
+from oracle import targets as T
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _pos(name, numel, k):
+    return np.random.RandomState(zlib.crc32(name.encode()) & 0xFFFFFFFF).randint(0, numel, k)
+
+
+def make_model(dtype=torch.float32, name="centerOffsetRes10"):
+    import importlib
+    plugin = importlib.import_module("trainer.model." + name)
+    entries, topo = O.model_spec(plugin.modelParams["numLayers"], plugin.modelParams["dims"])
+    state = O.hash_weights(entries)
+    m = plugin.model(**plugin.modelParams)
+    m.load_state_dict(state)
+    return m.to(DEV).train().set_compute_dtype(dtype), plugin, state, topo
+
+
+@pytest.fixture(scope="module")
+def f1_outputs():
+    m, plugin, state, topo = make_model()
+    x = T.batch_inputs(1, 2, 512).to(DEV)
+    with torch.no_grad():
+        out = m(x, decode=False)[0]
+    torch.cuda.synchronize()
+    return m, {k: v.cpu() for k, v in out.items()}
+
+
+def test_f1_forward_parity(f1_outputs, golden):
+    m, out = f1_outputs
+    g = golden("fwd")
+    for k in ("heatmap", "regr", "offset"):
+        np.testing.assert_allclose(out[k].numpy(), g[k], rtol=1e-3, atol=1e-3, err_msg=k)
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith("rs|"):
+            np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    assert int(sd["layer1.0.bn1.num_batches_tracked"]) == 1
+
+
+def test_f4_decode(f1_outputs, golden):
+    from models.centerNetOffset import decodeCenterNet
+    _, out = f1_outputs
+    g = golden("decode")
+    dec = decodeCenterNet({k: v.to(DEV) for k, v in out.items()})
+    scores, inds = dec[0].cpu().numpy(), dec[1].cpu().numpy()
+    np.testing.assert_allclose(scores, g["f1|scores"], rtol=1e-5, atol=1e-6)
+    rs = np.random.RandomState(7)
+    syn = {"heatmap": torch.from_numpy((rs.standard_normal((2, 1, 128, 128)) * 3).astype(np.float32)),
+           "regr": torch.from_numpy(rs.standard_normal((2, 4, 128, 128)).astype(np.float32)),
+           "offset": torch.from_numpy(rs.standard_normal((2, 2, 128, 128)).astype(np.float32))}
+    dec = decodeCenterNet({k: v.to(DEV) for k, v in syn.items()})
+    ref_s = g["syn|scores"]
+    np.testing.assert_allclose(dec[0].cpu().numpy(), ref_s, rtol=1e-6, atol=1e-7)
+    # indices bit-exact wherever the ordering is strict (not tied within float noise)
+    for b in range(2):
+        s = ref_s[b]
+        strict = np.ones_like(s, dtype=bool)
+        gap = np.abs(np.diff(s)) > 1e-6 * np.abs(s[1:])
+        strict[1:] &= gap
+        strict[:-1] &= gap
+        np.testing.assert_array_equal(dec[1].cpu().numpy()[b][strict], g["syn|inds"][b][strict])
+        np.testing.assert_array_equal(dec[2].cpu().numpy()[b][strict], g["syn|ys"][b][strict])
+        np.testing.assert_array_equal(dec[3].cpu().numpy()[b][strict], g["syn|xs"][b][strict])
+        np.testing.assert_allclose(dec[4].cpu().numpy()[b][strict], g["syn|offset"][b][strict], rtol=0, atol=0)
+        np.testing.assert_allclose(dec[5].cpu().numpy()[b][strict], g["syn|regr"][b][strict], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("case", ["a", "b", "c", "d"])
+def test_f2_loss_and_grads(case, golden):
+    from models.centerNetOffset import CenterNetLoss
+    g = golden("loss")
+    f = golden("fwd")
+    ys = [torch.from_numpy(g["ys|" + n]) for n in ["heat", "mask", "regr", "inds"]]
+    preds = {k: torch.from_numpy(f[k]) for k in ("heatmap", "regr", "offset")}
+    if case == "b":
+        ys[0] = ys[0] * 0.9
+    if case == "c":
+        ys[3] = torch.from_numpy(g["c|inds"])
+    if case == "d":
+        h = preds["heatmap"]
+        preds["heatmap"] = torch.where(h > h.median(), torch.full_like(h, 20.0), torch.full_like(h, -20.0))
+    leaves = {k: v.to(DEV).requires_grad_(True) for k, v in preds.items()}
+    loss, stats = CenterNetLoss(0.1, 0.1)([leaves], [y.to(DEV) for y in ys])
+    loss.mean().backward()
+    np.testing.assert_allclose(loss.detach().cpu().numpy(), g[case + "|loss"], rtol=1e-4)
+    np.testing.assert_allclose([s.item() for s in stats], g[case + "|stats"], rtol=1e-4, atol=1e-6)
+    gh = leaves["heatmap"].grad.cpu()
+    if case == "a":
+        np.testing.assert_allclose(gh.numpy(), g["a|dheatmap"], rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(gh.double().abs().sum().item(), g[case + "|dheatmap_abs"], rtol=1e-4)
+    for k in ("regr", "offset"):
+        gk = leaves[k].grad.cpu()
+        np.testing.assert_allclose(O.gather_feat(gk, ys[3]).numpy(), g[case + "|d" + k], rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(gk.double().abs().sum().item(), g[case + "|d" + k + "_abs"], rtol=1e-5)
+
+
+def test_f3_train_step(golden):
+    from scdhip.flat import FlatAdam
+    g = golden("step")
+    m, plugin, state, topo = make_model()
+    opt = FlatAdam(filter(lambda p: p.requires_grad, m.parameters()))
+    x = T.batch_inputs(3, 2, 512).to(DEV)
+    ys = [y.to(DEV) for y in T.batch_targets(4, 2, 128)]
+    opt.zero_grad()
+    loss, stats = plugin.loss(m(x, decode=False), ys)
+    loss.mean().backward()
+    grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
+    opt.step()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-4)
+    for k, p in m.named_parameters():
+        np.testing.assert_allclose(grads[k].double().norm().item(), g["gnorm|" + k], rtol=1e-2, atol=1e-6,
+                                   err_msg=k)
+        pos = _pos(k, p.numel(), 16)
+        np.testing.assert_allclose(p.detach().cpu().reshape(-1)[pos].numpy(), g["psamp|" + k], rtol=1e-4,
+                                   atol=2e-5, err_msg=k)
+
+
+def test_bf16_forward_close_to_fp32(f1_outputs):
+    _, ref = f1_outputs
+    m, _, _, _ = make_model(torch.bfloat16)
+    with torch.no_grad():
+        out = m(T.batch_inputs(1, 2, 512).to(DEV), decode=False)[0]
+    for k in ("heatmap", "regr", "offset"):
+        a, b = out[k].float().cpu(), ref[k]
+        err = (a - b).abs().max().item() / b.abs().max().item()
+        assert err < 5e-2, (k, err)
+
+
+def test_full_size_bf16_steps_decrease_loss():
+    """B=32, 512^2, bf16: the benchmarked configuration trains (finite, decreasing loss)."""
+    from scdhip.flat import FlatAdam
+    m, plugin, _, _ = make_model(torch.bfloat16)
+    opt = FlatAdam(filter(lambda p: p.requires_grad, m.parameters()))
+    x = T.batch_inputs(21, 32, 512).to(DEV)
+    ys = [y.to(DEV) for y in T.batch_targets(22, 32, 128)]
+    losses = []
+    for _ in range(6):
+        opt.zero_grad()
+        loss, _ = plugin.loss(m(x, decode=False), ys)
+        loss.mean().backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(np.isfinite(losses)), losses
+    assert losses[-1] < losses[0], losses
