@@ -1,0 +1,56 @@
+"""Summarise a rocprofv3 kernel trace (sqlite .db or kernel_trace.csv) into per-kernel stats.
+
+usage: python tools/prof_summary.py <results.db|kernel_trace.csv> [out.csv]
+"""
+import csv
+import os
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    n = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", name)
+    m = re.match(r"(\w+?)I(DF16b|f)Li(\d+)ELi(\d+)E", n)
+    if m:
+        return "%s<%s,%s,%s>" % (m.group(1), "bf16" if m.group(2) == "DF16b" else "f32", m.group(3), m.group(4))
+    m = re.match(r"(\w+?)I(DF16b|f)E", n)
+    if m:
+        return "%s<%s>" % (m.group(1), "bf16" if m.group(2) == "DF16b" else "f32")
+    n = n.replace("(anonymous namespace)::", "")
+    return n.split("(")[0][:80]
+
+
+def rows_from(path):
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        for name, dur in c.execute("select name, duration from kernels"):
+            yield name, float(dur)
+    else:
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                yield r["Kernel_Name"], float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+
+
+def main():
+    src = sys.argv[1]
+    agg = defaultdict(lambda: [0, 0.0])
+    for name, dur in rows_from(src):
+        a = agg[short(name)]
+        a[0] += 1
+        a[1] += dur
+    total = sum(v[1] for v in agg.values())
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    lines = [("kernel", "calls", "total_us", "avg_us", "pct")]
+    for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        lines.append((k, n, "%.1f" % (t / 1e3), "%.2f" % (t / 1e3 / n), "%.2f" % (100 * t / total)))
+    if out:
+        with open(out, "w", newline="") as f:
+            csv.writer(f).writerows(lines)
+    for l in lines[:40]:
+        print("%-60s %6s %12s %10s %6s" % l)
+
+
+if __name__ == "__main__":
+    main()
