@@ -33,7 +33,8 @@ extern "C" {
 
 #define SCD_MAX_TAPS 16
 #define SCD_MAX_PHASES 4
-#define SCD_STAT_REPLICAS 64   /* fp64 statistics buffers are [SCD_STAT_REPLICAS][2][C] */
+#define SCD_STAT_REPLICAS 64   /* fp64 statistics buffers are [SCD_STAT_REPLICAS][2][C]; the consumer
+                                  (finalize / collapse) re-zeroes what it read, so buffers persist */
 
 /* One sub-pixel phase of a gather-GEMM (see DESIGN.md "Implicit GEMM").  For output
  * pixel (n, qh, qw) of the phase grid, the GEMM row gathers input pixel
@@ -56,6 +57,14 @@ int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, const float*
                   int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride,
                   int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
                   void* stream);
+
+/* Head convolution with the CenterNet tails fused into the epilogue: hid = relu(conv3x3(x, w) + bias)
+ * (N,H,W,nh*128) NHWC and, from the same tile, outs[h] (N,od[h],H,W) fp32 = w1[h] . hid_h + b1[h].
+ * Replaces the three terminal Sequentials (centerNetOffset.py:106-110) in one launch; w is the
+ * packed [nh*128][9][Ci] operand of the concatenated 3x3 weights. */
+int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void* hid, const float* bias, int N, int H,
+                        int W, int Ci, int nh, const int* od, const float* const* w1, const float* const* b1,
+                        float* const* outs, void* stream);
 
 /* Weight-gradient of the gather-GEMM (split-K over pixels on MFMA, fp32 partial slabs):
  * ws[z, co, t*Ci+ci] = sum_{pix in split z} g[pix, co] * x[gather(pix, t), ci]
@@ -86,7 +95,7 @@ int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int H, int W, 
 int scd_stats_collapse(double* stats, int nrep, int C, void* stream);
 /* mean/var from stats (count rows), running-stat update (unbiased var), scale/shift for apply;
  * stats == NULL: eval mode, normalise with the running statistics (no update) */
-int scd_bn_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+int scd_bn_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                     const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
                     float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
                     void* stream);
@@ -98,7 +107,7 @@ int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const f
 int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
                       const float* invstd, int C, long total, double* stats, void* stream);
 /* dgamma (+)= sum dz*xhat, dbeta (+)= sum dz; coef[3][C] for dy = a*dz + b*y + c */
-int scd_bn_bwd_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                         const float* mean, const float* invstd, float* dgamma, float* dbeta,
                         float* coef, void* stream);
 /* dy = a*dz + b*y + c (dtype); optionally also writes dz */
@@ -119,15 +128,13 @@ int scd_stem_pool_bwd(int dtype, const void* dout, const uint8_t* argmax, const 
  * weight, b1[h] its bias; outputs are NCHW fp32 (N, od[h], HW).  nh <= 4, od[h] <= 4. */
 int scd_heads_fwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
                   const float* const* w1, const float* const* b1, float* const* outs, void* stream);
-/* dhid = relu'(hid) * (w1^T dout) (dtype) */
-int scd_heads_bwd_data(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
-                       const float* const* w1, const float* const* douts, void* dhid, void* stream);
-/* fp64 accumulator bytes for scd_heads_bwd_weight ([SCD_STAT_REPLICAS][dW1 | db1 | db0]) */
-size_t scd_heads_bwd_weight_accsize(int nh, int Hd, const int* od);
-int scd_heads_bwd_weight(int dtype, const void* hid, const void* dhid, int N, int HW, int nh, int Hd,
-                         const int* od, const float* const* douts, double* acc, void* stream);
-/* collapse replicas; (+)= into dw1[h] (od[h],Hd), db1[h] (od[h]), db0[h] (Hd: the 3x3 conv bias) */
-int scd_heads_bwd_weight_finalize(const double* acc, int nh, int Hd, const int* od, float* const* dw1,
+/* fused tail backward: dhid = relu'(hid) * (w1^T dout) (dtype) and, in the same pass,
+ * acc (fp64, [SCD_STAT_REPLICAS][sum(od)*Hd | sum(od) | nh*Hd]) += [dW1 | db1 | db0] */
+size_t scd_heads_bwd_accsize(int nh, int Hd, const int* od);
+int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
+                  const float* const* w1, const float* const* douts, void* dhid, double* acc, void* stream);
+/* collapse (and re-zero) acc; (+)= into dw1[h] (od[h],Hd), db1[h] (od[h]), db0[h] (Hd: 3x3 conv bias) */
+int scd_heads_bwd_weight_finalize(double* acc, int nh, int Hd, const int* od, float* const* dw1,
                                   float* const* db1, float* const* db0, int accumulate, void* stream);
 
 /* ---- losses (focal.py:25-53, regression.py:37-44, centerNetOffset.py:182-217) ---- */

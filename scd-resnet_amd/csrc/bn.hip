@@ -5,27 +5,43 @@
 
 namespace {
 
+// sum replicas into replica 0 and zero the others (buffers are persistent: the consumer re-zeroes)
 __global__ void stats_collapse_kernel(double* stats, int nrep, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double s = 0.0;
-    for (int r = 0; r < nrep; ++r) s += stats[(long)r * n + i];
+    for (int r = 0; r < nrep; ++r) {
+        s += stats[(long)r * n + i];
+        if (r) stats[(long)r * n + i] = 0.0;
+    }
     stats[i] = s;
 }
 
-__global__ void bn_finalize_kernel(const double* stats, int nrep, int C, double count, const float* gamma,
+// one wave per channel: lane r sums replica r (and zeroes it: persistent, consumer-cleared buffers)
+__device__ __forceinline__ void wave_collect(double* stats, int nrep, int C, int c, double& s, double& q) {
+    const int lane = threadIdx.x & 63;
+    double a = 0.0, b = 0.0;
+    for (int r = lane; r < nrep; r += 64) {
+        double* p = stats + (long)r * 2 * C;
+        a += p[c];
+        b += p[C + c];
+        p[c] = 0.0;
+        p[C + c] = 0.0;
+    }
+    s = wave_sum_d(a);
+    q = wave_sum_d(b);
+}
+
+__global__ void bn_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
                                    const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
                                    float eps, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c == 0 && nbt && stats) *nbt += 1;
+    const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt && stats) *nbt += 1;
     if (c >= C) return;
     double mean, var;
     if (stats) {
-        double s = 0.0, q = 0.0;
-        for (int r = 0; r < nrep; ++r) {
-            s += stats[(long)r * 2 * C + c];
-            q += stats[(long)r * 2 * C + C + c];
-        }
+        double s, q;
+        wave_collect(stats, nrep, C, c, s, q);
         mean = s / count;
         var = q / count - mean * mean;
         if (var < 0.0) var = 0.0;
@@ -33,6 +49,7 @@ __global__ void bn_finalize_kernel(const double* stats, int nrep, int C, double 
         mean = rmean[c];
         var = rvar[c];
     }
+    if ((threadIdx.x & 63) != 0) return;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f;
     const float b = beta ? beta[c] : 0.f;
@@ -49,19 +66,29 @@ __global__ void bn_finalize_kernel(const double* stats, int nrep, int C, double 
 }
 
 template <typename T>
-__global__ void bn_apply_kernel(const T* y, T* out, int C, long nvec, const float* scale, const float* shift,
+__global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const float* scale, const float* shift,
                                 const T* res, const float* rscale, const float* rshift, int relu) {
     constexpr int E = Vec16<T>::N;
-    for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
-        const long i = v * E;
-        const int c0 = (int)(i % C);
+    extern __shared__ float prm[];          // [scale | shift | rscale | rshift] x C, staged once per block
+    const int np = rscale ? 4 : 2;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) {
+        prm[i] = scale[i];
+        prm[C + i] = shift[i];
+        if (rscale) { prm[2 * C + i] = rscale[i]; prm[3 * C + i] = rshift[i]; }
+    }
+    (void)np;
+    __syncthreads();
+    const unsigned cpr = (unsigned)C / E;
+    for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+        const size_t i = (size_t)v * E;
+        const int c0 = (int)(v % cpr) * E;
         float a[E], r[E];
         Vec16<T>::load(y + i, a);
         if (res) Vec16<T>::load(res + i, r);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            float o = a[e] * scale[c0 + e] + shift[c0 + e];
-            if (res) o += rscale ? (r[e] * rscale[c0 + e] + rshift[c0 + e]) : r[e];
+            float o = a[e] * prm[c0 + e] + prm[C + c0 + e];
+            if (res) o += rscale ? (r[e] * prm[2 * C + c0 + e] + prm[3 * C + c0 + e]) : r[e];
             if (relu) o = fmaxf(o, 0.f);
             a[e] = o;
         }
@@ -126,16 +153,14 @@ __global__ void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y, c
     }
 }
 
-__global__ void bn_bwd_finalize_kernel(const double* stats, int nrep, int C, double count, const float* gamma,
+__global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
                                        const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                        float* coef) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int r = 0; r < nrep; ++r) {
-        s += stats[(long)r * 2 * C + c];
-        q += stats[(long)r * 2 * C + C + c];
-    }
+    double s, q;
+    wave_collect(stats, nrep, C, c, s, q);
+    if ((threadIdx.x & 63) != 0) return;
     if (dgamma) dgamma[c] += (float)q;
     if (dbeta) dbeta[c] += (float)s;
     const float g = gamma ? gamma[c] : 1.f;
@@ -150,12 +175,16 @@ __global__ void bn_bwd_finalize_kernel(const double* stats, int nrep, int C, dou
 }
 
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* coef, int C, long nvec,
+__global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* coef, int C, unsigned nvec,
                                     T* dy, T* dz_out) {
     constexpr int E = Vec16<T>::N;
-    for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
-        const long i = v * E;
-        const int c0 = (int)(i % C);
+    extern __shared__ float cf[];           // coef [3][C], staged once per block
+    for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
+    __syncthreads();
+    const unsigned cpr = (unsigned)C / E;
+    for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+        const size_t i = (size_t)v * E;
+        const int c0 = (int)(v % cpr) * E;
         float d[E], yv[E], mk[E], o[E];
         Vec16<T>::load(dout + i, d);
         Vec16<T>::load(y + i, yv);
@@ -164,14 +193,15 @@ __global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, co
         for (int e = 0; e < E; ++e) {
             const float dz = (mask && !(mk[e] > 0.f)) ? 0.f : d[e];
             d[e] = dz;
-            o[e] = coef[c0 + e] * dz + coef[C + c0 + e] * yv[e] + coef[2 * C + c0 + e];
+            o[e] = cf[c0 + e] * dz + cf[C + c0 + e] * yv[e] + cf[2 * C + c0 + e];
         }
         Vec16<T>::store(dy + i, o);
         if (dz_out) Vec16<T>::store(dz_out + i, d);
     }
 }
 
-inline int ew_blocks(long nvec) { return (int)std::min<long>(8192, std::max<long>(1, (nvec + 255) / 256)); }
+inline int ew_blocks(long nvec) { return (int)std::min<long>(2048, std::max<long>(1, (nvec + 255) / 256)); }
+inline int fin_blocks(int C) { return (C + 3) / 4; }   // 4 waves (channels) per 256-thread block
 
 }  // namespace
 
@@ -181,11 +211,11 @@ extern "C" int scd_stats_collapse(double* stats, int nrep, int C, void* stream) 
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_bn_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+extern "C" int scd_bn_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                                const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
                                float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
                                void* stream) {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(fin_blocks(C)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
                        count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, mean, invstd, scale,
                        shift);
     SCD_RETURN_LAUNCH();
@@ -198,13 +228,13 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
     if (dtype == SCD_DT_BF16) {
         if (C % 8) return SCD_ERR_ARG;
         long nvec = total / 8;
-        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const __bf16*)y,
-                           (__bf16*)out, C, nvec, scale, shift, (const __bf16*)res, rscale, rshift, relu);
+        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), (rscale ? 4 : 2) * C * 4, st, (const __bf16*)y,
+                           (__bf16*)out, C, (unsigned)nvec, scale, shift, (const __bf16*)res, rscale, rshift, relu);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4) return SCD_ERR_ARG;
         long nvec = total / 4;
-        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)y,
-                           (float*)out, C, nvec, scale, shift, (const float*)res, rscale, rshift, relu);
+        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), (rscale ? 4 : 2) * C * 4, st, (const float*)y,
+                           (float*)out, C, (unsigned)nvec, scale, shift, (const float*)res, rscale, rshift, relu);
     } else {
         return SCD_ERR_ARG;
     }
@@ -231,10 +261,10 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_bn_bwd_finalize(const double* stats, int nrep, int C, double count, const float* gamma,
+extern "C" int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                                    const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
                                    void* stream) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fin_blocks(C)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
                        count, gamma, mean, invstd, dgamma, dbeta, coef);
     SCD_RETURN_LAUNCH();
 }
@@ -245,14 +275,14 @@ extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, c
     if (dtype == SCD_DT_BF16) {
         if (C % 8) return SCD_ERR_ARG;
         long nvec = total / 8;
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st,
-                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, coef, C, nvec, (__bf16*)dy,
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 3 * C * 4, st,
+                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, coef, C, (unsigned)nvec, (__bf16*)dy,
                            (__bf16*)dz);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4) return SCD_ERR_ARG;
         long nvec = total / 4;
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)dout,
-                           (const float*)mask, (const float*)y, coef, C, nvec, (float*)dy, (float*)dz);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 3 * C * 4, st, (const float*)dout,
+                           (const float*)mask, (const float*)y, coef, C, (unsigned)nvec, (float*)dy, (float*)dz);
     } else {
         return SCD_ERR_ARG;
     }

@@ -12,8 +12,6 @@
 
 namespace {
 
-constexpr int LDS_ROW = 144;   // 128 B of K + 16 B pad
-
 struct GemmParams {
     const char* x;
     const char* w;
@@ -24,7 +22,18 @@ struct GemmParams {
     int is, os, wrow, relu, accumulate, nphase, ntn;
     int tile_start[SCD_MAX_PHASES + 1];
     scd_gemm_phase ph[SCD_MAX_PHASES];
+    // optional fused CenterNet head tails (n-tile t == head t, BN == head hidden width)
+    int head_on;
+    int head_od[4];
+    const float* head_w[4];
+    const float* head_b[4];
+    float* head_out[4];
 };
+
+// LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
+// chunk c ^ (r & 7).  ds_read_b128 fragment reads (16 consecutive rows, one chunk) and the
+// ds_write_b128 staging stores (8 chunks of one row) are then bank-conflict free.
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
 template <typename T, int BM, int BN>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
@@ -34,10 +43,19 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
     constexpr int ACH = BM / 32;        // A chunks per thread
     constexpr int BCH = BN / 32;
     constexpr int WN = BN / 64;         // waves along N (each wave: 64x64)
-    __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * LDS_ROW];
+    constexpr int STAGE = (BM + BN) * 128;
+    constexpr int EROW = 64 * ESZ + 16; // epilogue staging row (64 channels + pad)
+    constexpr int EPI = 4 * 64 * EROW;
+    constexpr int SMEM = (2 * STAGE > EPI + 2048) ? 2 * STAGE : EPI + 2048;
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
     const int tid = threadIdx.x;
-    int bid = blockIdx.x;
+    // XCD-aware bijective remap: blocks that share an A (pixel) tile run on one XCD's L2
+    int bid;
+    {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+    }
     int phase = 0;
 #pragma unroll
     for (int i = 1; i < SCD_MAX_PHASES; ++i)
@@ -51,11 +69,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
 
     // ---- per-thread gather rows (fixed across the K loop)
     const int cch = tid & 7;
+    const int srow = tid >> 3;                        // staging row (mod 32)
     int a_pix[ACH], a_ih[ACH], a_iw[ACH];
     bool a_ok[ACH];
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-        int m = mt * BM + (tid >> 3) + 32 * i;
+        int m = mt * BM + srow + 32 * i;
         a_ok[i] = m < M;
         int mm = a_ok[i] ? m : 0;
         int n = mm / QQ;
@@ -70,12 +89,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
     bool b_ok[BCH];
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
-        int nn = nt * BN + (tid >> 3) + 32 * j;
+        int nn = nt * BN + srow + 32 * j;
         b_ok[j] = nn < p.Co;
         b_row[j] = b_ok[j] ? nn : 0;
     }
     const int cpt = p.Ci / BK;            // K stages per tap
     const int KT = ph.ntaps * cpt;
+    const int st_off = swz(srow, cch);    // (srow + 32i) & 7 == srow & 7
 
     uint4 ra[ACH], rb[BCH];
     auto gload = [&](int kt) {
@@ -96,19 +116,22 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
         }
     };
     auto lstore = [&](int buf) {
-        char* As = smem + buf * (BM + BN) * LDS_ROW;
-        char* Bs = As + BM * LDS_ROW;
+        char* As = smem + buf * STAGE;
+        char* Bs = As + BM * 128;
 #pragma unroll
-        for (int i = 0; i < ACH; ++i) *(uint4*)(As + ((tid >> 3) + 32 * i) * LDS_ROW + cch * 16) = ra[i];
+        for (int i = 0; i < ACH; ++i) *(uint4*)(As + st_off + 32 * 128 * i) = ra[i];
 #pragma unroll
-        for (int j = 0; j < BCH; ++j) *(uint4*)(Bs + ((tid >> 3) + 32 * j) * LDS_ROW + cch * 16) = rb[j];
+        for (int j = 0; j < BCH; ++j) *(uint4*)(Bs + st_off + 32 * 128 * j) = rb[j];
     };
 
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wm = wave / WN, wn = wave - (wave / WN) * WN;
     const int l16 = lane & 15, lg = lane >> 4;
+    const int l7 = l16 & 7;
 
+    // acc[a][b] = D[n][m] with the weight fragment as the MFMA "A" operand: lane holds pixel
+    // m = a*16 + l16 and the 4 consecutive channels n = b*16 + 4*lg + r (r = register).
     f32x4 acc[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -116,39 +139,39 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
         for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     auto compute = [&](int buf) {
-        const char* As = smem + buf * (BM + BN) * LDS_ROW;
-        const char* Bs = As + BM * LDS_ROW;
+        const char* As = smem + buf * STAGE;
+        const char* Bs = As + BM * 128;
         if constexpr (ESZ == 2) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 bf16x8 af[4], bfr[4];
+                const int co = ((s * 4 + lg) ^ l7) << 4;
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
-                    af[a] = *(const bf16x8*)(As + (wm * 64 + a * 16 + l16) * LDS_ROW + s * 64 + lg * 16);
+                for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(As + (wm * 64 + a * 16 + l16) * 128 + co);
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    bfr[b] = *(const bf16x8*)(Bs + (wn * 64 + b * 16 + l16) * LDS_ROW + s * 64 + lg * 16);
+                for (int b = 0; b < 4; ++b) bfr[b] = *(const bf16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
             }
         } else {
             // exact-f32 MFMA: lane group lg owns K elements [8lg, 8lg+8) of the 32-wide stage;
             // step j multiplies element 8lg+j of A and B (same permutation on both operands).
+            const int c0 = ((2 * lg) ^ l7) << 4, c1 = ((2 * lg + 1) ^ l7) << 4;
             float4 af[4][2], bfr[4][2];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                const char* pa = As + (wm * 64 + a * 16 + l16) * LDS_ROW + lg * 32;
-                af[a][0] = *(const float4*)pa;
-                af[a][1] = *(const float4*)(pa + 16);
+                const char* pa = As + (wm * 64 + a * 16 + l16) * 128;
+                af[a][0] = *(const float4*)(pa + c0);
+                af[a][1] = *(const float4*)(pa + c1);
             }
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const char* pb = Bs + (wn * 64 + b * 16 + l16) * LDS_ROW + lg * 32;
-                bfr[b][0] = *(const float4*)pb;
-                bfr[b][1] = *(const float4*)(pb + 16);
+                const char* pb = Bs + (wn * 64 + b * 16 + l16) * 128;
+                bfr[b][0] = *(const float4*)(pb + c0);
+                bfr[b][1] = *(const float4*)(pb + c1);
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -158,7 +181,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         float bv = (j < 4) ? bfr[b][0][j & 3] : bfr[b][1][j & 3];
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[a][b], 0, 0, 0);
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv, av, acc[a][b], 0, 0, 0);
                     }
                 }
             }
@@ -178,51 +201,85 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
         }
     }
 
-    // ---- epilogue: bias / relu / accumulate, NHWC store at the phase's output pixel
-    float csum[4], csq[4];
+    // ---- epilogue 1: bias / relu in registers, BN partial sums, stage the wave's 64x64 tile in LDS
+    char* ep = smem + wave * 64 * EROW;
+    float csum[4][4], csq[4][4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) { csum[b] = 0.f; csq[b] = 0.f; }
+    for (int b = 0; b < 4; ++b)
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
+        for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = mt * BM + wm * 64 + a * 16 + lg * 4 + r;
-            if (m >= M) continue;
+    for (int b = 0; b < 4; ++b) {
+        const int col0 = nt * BN + wn * 64 + b * 16 + lg * 4;
+        float bias[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int m = mt * BM + wm * 64 + a * 16 + l16;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[a][b][r] + bias[r];
+                if (p.relu) v[r] = fmaxf(v[r], 0.f);
+                if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+            }
+            char* dst = ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * ESZ;
+            if constexpr (ESZ == 2) {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                *(bf16x4*)dst = o;
+            } else {
+                *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+    __syncthreads();
+    // ---- epilogue 2: coalesced 16-B NHWC stores (+= for accumulate) of the staged tile
+    {
+        constexpr int CPR = 64 * ESZ / 16;        // 16-B chunks per staged row
+        constexpr int RPI = 64 / CPR;             // rows per wave instruction
+        const int ch = lane % CPR;
+        const int col = nt * BN + wn * 64 + ch * EPC;
+#pragma unroll
+        for (int j = 0; j < 64 / RPI; ++j) {
+            const int row = lane / CPR + RPI * j;
+            const int m = mt * BM + wm * 64 + row;
+            if (m >= M || col >= p.Co) continue;
             const int n = m / QQ;
             const int rem = m - n * QQ;
             const int qh = rem / ph.Qw;
             const int qw = rem - qh * ph.Qw;
             const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
-            const long obase = ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co;
+            T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+            uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
+            if (p.accumulate) {
+                float a[EPC], o[EPC];
+                Vec16<T>::load(&v, a);
+                Vec16<T>::load(dst, o);
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int col = nt * BN + wn * 64 + b * 16 + l16;
-                if (col >= p.Co) continue;
-                float v = acc[a][b][r];
-                if (p.bias) v += p.bias[col];
-                if (p.relu) v = fmaxf(v, 0.f);
-                T* dst = (T*)(p.y) + obase + col;
-                if (p.accumulate) v += to_f<T>(*dst);
-                *dst = from_f<T>(v);
-                csum[b] += v;
-                csq[b] += v * v;
+                for (int e = 0; e < EPC; ++e) a[e] += o[e];
+                Vec16<T>::store(&v, a);
             }
+            *(uint4*)dst = v;
         }
     }
     if (p.stats) {
-        // reduce over the 4 lane groups sharing a column, then over the waves sharing it
-        __syncthreads();
-        float* red = (float*)smem;   // [BM/64][BN][2]
+        // channel sums: over the 16 pixel-lanes (xor 1..8), then over the waves sharing the columns
+        float* red = (float*)(smem + EPI);   // [BM/64][BN][2] floats  (<= 2 KB)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            float s = csum[b], q = csq[b];
-            s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-            q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-            if (lg == 0) {
-                red[(wm * BN + wn * 64 + b * 16 + l16) * 2 + 0] = s;
-                red[(wm * BN + wn * 64 + b * 16 + l16) * 2 + 1] = q;
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float s = csum[b][r], q = csq[b][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                if (l16 == 0) {
+                    const int c = wn * 64 + b * 16 + lg * 4 + r;
+                    red[(wm * BN + c) * 2 + 0] = s;
+                    red[(wm * BN + c) * 2 + 1] = q;
+                }
             }
-        }
         __syncthreads();
         if (tid < BN) {
             const int col = nt * BN + tid;
@@ -233,6 +290,44 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
                 const int rep = (bid % SCD_STAT_REPLICAS);
                 atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
                 atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
+            }
+        }
+    }
+    if constexpr (BN == 128) {
+        if (p.head_on) {
+            // fused terminal 1x1 (centerNetOffset.py:108-110): head = n-tile, hidden = staged tile.
+            // thread -> (row = tid/2, half = tid&1): 64-channel partial dots, combined across the pair.
+            const int h = nt;
+            const int od = p.head_od[h];
+            float* ws = (float*)(smem + EPI);   // w1 of this head, [od][128]
+            __syncthreads();
+            for (int i = tid; i < od * 128; i += 256) ws[i] = p.head_w[h][i];
+            __syncthreads();
+            const int row = tid >> 1, half = tid & 1;
+            const int wv = (row >> 6) * WN + half;          // wave that staged this (row, half)
+            const char* src = smem + wv * 64 * EROW + (row & 63) * EROW;
+            float o4[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < 64; c += EPC) {
+                float v[EPC];
+                Vec16<T>::load(src + c * ESZ, v);
+#pragma unroll
+                for (int o = 0; o < 4; ++o)
+                    if (o < od) {
+#pragma unroll
+                        for (int e = 0; e < EPC; ++e) o4[o] += v[e] * ws[o * 128 + half * 64 + c + e];
+                    }
+            }
+#pragma unroll
+            for (int o = 0; o < 4; ++o) o4[o] += __shfl_xor(o4[o], 1, 64);
+            const int m = mt * BM + row;
+            if (half == 0 && m < M) {
+                const int n = m / QQ;
+                const int rem = m - n * QQ;
+                const int qh = rem / ph.Qw;
+                const int qw = rem - qh * ph.Qw;
+                const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
+                for (int o = 0; o < od; ++o)
+                    p.head_out[h][((long)n * od + o) * p.Ho * p.Wo + oh * p.Wo + ow] = o4[o] + p.head_b[h][o];
             }
         }
     }
@@ -407,17 +502,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 
 __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
                                     long ld_n, long ld_c, long ld_t, float* dst, int accumulate) {
-    const long KK = (long)T * Ci;
-    const long total = (long)(r1 - r0) * KK;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int r = (int)(i / KK);
-        const int k = (int)(i - r * KK);
-        const int t = k / Ci;
-        const int c = k - t * Ci;
-        if (c >= cvalid) continue;
-        float s = 0.f;
-        const float* src = ws + (long)(r0 + r) * KK + k;
-        for (int z = 0; z < nsplit; ++z) s += src[(long)z * Cg * KK];
+    const unsigned KK = (unsigned)(T * Ci);
+    const unsigned total = (unsigned)(r1 - r0) * KK;
+    const size_t zs = (size_t)Cg * KK;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const unsigned r = i / KK;
+        const unsigned k = i - r * KK;
+        const unsigned t = k / (unsigned)Ci;
+        const unsigned c = k - t * (unsigned)Ci;
+        if ((int)c >= cvalid) continue;
+        const float* src = ws + (size_t)(r0 + r) * KK + k;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int z = 0;
+        for (; z + 4 <= nsplit; z += 4) {
+            s0 += src[(size_t)z * zs];
+            s1 += src[(size_t)(z + 1) * zs];
+            s2 += src[(size_t)(z + 2) * zs];
+            s3 += src[(size_t)(z + 3) * zs];
+        }
+        for (; z < nsplit; ++z) s0 += src[(size_t)z * zs];
+        const float s = (s0 + s1) + (s2 + s3);
         float* d = dst + r * ld_n + c * ld_c + t * ld_t;
         *d = accumulate ? (*d + s) : s;
     }
@@ -431,30 +535,25 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, const float* bias, double* stats,
-                             int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride,
-                             int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
-                             void* stream) {
+static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm_phase* phases, void* stream) {
     if (nphase < 1 || nphase > SCD_MAX_PHASES) return SCD_ERR_ARG;
     const int BK = dtype == SCD_DT_BF16 ? 64 : 32;
-    if (Ci % BK != 0 || Co <= 0 || N <= 0) return SCD_ERR_ARG;
-    GemmParams p;
-    p.x = (const char*)x; p.w = (const char*)w; p.y = (char*)y; p.bias = bias; p.stats = stats;
-    p.N = N; p.Hi = Hi; p.Wi = Wi; p.Ci = Ci; p.Ho = Ho; p.Wo = Wo; p.Co = Co;
-    p.is = in_stride; p.os = out_stride; p.wrow = wrow; p.relu = relu; p.accumulate = accumulate;
+    const int EPC = dtype == SCD_DT_BF16 ? 8 : 4;
+    if (p.Ci % BK != 0 || p.Co <= 0 || p.Co % EPC != 0 || p.N <= 0) return SCD_ERR_ARG;
     p.nphase = nphase;
-    const bool narrow = Co <= 64;
+    const bool narrow = p.Co <= 64;
+    if (p.head_on && (narrow || p.Co != 128 * ((p.Co + 127) / 128))) return SCD_ERR_ARG;
     const int BM = narrow ? 256 : 128, BN = narrow ? 64 : 128;
-    p.ntn = cdiv(Co, BN);
+    p.ntn = cdiv(p.Co, BN);
     int tiles = 0;
     for (int i = 0; i < SCD_MAX_PHASES; ++i) {
         if (i < nphase) {
             p.ph[i] = phases[i];
             if (phases[i].ntaps < 0 || phases[i].ntaps > SCD_MAX_TAPS) return SCD_ERR_ARG;
             for (int t = 0; t < phases[i].ntaps; ++t)
-                if ((long)(phases[i].wt[t] + 1) * Ci > wrow) return SCD_ERR_ARG;
+                if (phases[i].wt[t] < 0 || (long)(phases[i].wt[t] + 1) * p.Ci > p.wrow) return SCD_ERR_ARG;
             p.tile_start[i] = tiles;
-            tiles += cdiv((long)N * phases[i].Qh * phases[i].Qw, BM) * p.ntn;
+            tiles += cdiv((long)p.N * phases[i].Qh * phases[i].Qw, BM) * p.ntn;
         } else {
             p.tile_start[i] = tiles;
         }
@@ -467,6 +566,42 @@ extern "C" int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, c
     if (dtype == SCD_DT_F32)
         return narrow ? launch_gemm<float, 256, 64>(p, tiles, st) : launch_gemm<float, 128, 128>(p, tiles, st);
     return SCD_ERR_ARG;
+}
+
+static void fill_params(GemmParams& p, const void* x, const void* w, void* y, const float* bias, double* stats, int N,
+                        int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride, int wrow,
+                        int relu, int accumulate) {
+    p.x = (const char*)x; p.w = (const char*)w; p.y = (char*)y; p.bias = bias; p.stats = stats;
+    p.N = N; p.Hi = Hi; p.Wi = Wi; p.Ci = Ci; p.Ho = Ho; p.Wo = Wo; p.Co = Co;
+    p.is = in_stride; p.os = out_stride; p.wrow = wrow; p.relu = relu; p.accumulate = accumulate;
+    p.head_on = 0;
+    for (int h = 0; h < 4; ++h) { p.head_od[h] = 0; p.head_w[h] = nullptr; p.head_b[h] = nullptr; p.head_out[h] = nullptr; }
+}
+
+extern "C" int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, const float* bias, double* stats,
+                             int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride,
+                             int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
+                             void* stream) {
+    GemmParams p;
+    fill_params(p, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu, accumulate);
+    return conv_gemm_launch(dtype, p, nphase, phases, stream);
+}
+
+extern "C" int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void* hid, const float* bias, int N,
+                                   int H, int W, int Ci, int nh, const int* od, const float* const* w1,
+                                   const float* const* b1, float* const* outs, void* stream) {
+    if (nh < 1 || nh > 4) return SCD_ERR_ARG;
+    GemmParams p;
+    fill_params(p, x, w, hid, bias, nullptr, N, H, W, Ci, H, W, nh * 128, 1, 1, 9 * Ci, 1, 0);
+    p.head_on = 1;
+    for (int h = 0; h < nh; ++h) {
+        if (od[h] < 1 || od[h] > 4) return SCD_ERR_ARG;
+        p.head_od[h] = od[h]; p.head_w[h] = w1[h]; p.head_b[h] = b1[h]; p.head_out[h] = outs[h];
+    }
+    scd_gemm_phase ph;
+    ph.Qh = H; ph.Qw = W; ph.rho_h = 0; ph.rho_w = 0; ph.ntaps = 9;
+    for (int t = 0; t < 9; ++t) { ph.dh[t] = t / 3 - 1; ph.dw[t] = t % 3 - 1; ph.wt[t] = t; }
+    return conv_gemm_launch(dtype, p, 1, &ph, stream);
 }
 
 extern "C" size_t scd_conv_wgrad_workspace(int Cg, int T, int Ci, int nsplit) {

@@ -11,10 +11,10 @@ namespace {
 template <typename T>
 __global__ void pack_weight_kernel(const float* w, T* out, int A, int B, int Tt, int mode, int ldp, int row_off) {
     const int rows = mode == 0 ? A : B;
-    const long total = (long)rows * ldp;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int r = (int)(i / ldp);
-        const int k = (int)(i - (long)r * ldp);
+    const unsigned total = (unsigned)rows * ldp;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const int r = (int)(i / (unsigned)ldp);
+        const int k = (int)(i - (unsigned)r * ldp);
         float v = 0.f;
         if (mode == 0) {        // out[a][t*B+b] = w[a][b][t]
             const int t = k / B, b = k - (k / B) * B;
@@ -32,13 +32,14 @@ template <typename T>
 __global__ void im2col_stem_kernel(const float* x, T* cols, int N, int H, int W, int Ho, int Wo, int kh, int kw,
                                    int stride, int pad, int Kpad) {
     constexpr int E = Vec16<T>::N;
-    const int cpp = Kpad / E;
-    const long total = (long)N * Ho * Wo * cpp;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const long pix = i / cpp;
+    const unsigned cpp = Kpad / E;
+    const unsigned total = (unsigned)N * Ho * Wo * cpp;
+    const unsigned HoWo = (unsigned)Ho * Wo;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const unsigned pix = i / cpp;
         const int ch = (int)(i - pix * cpp);
-        const int n = (int)(pix / ((long)Ho * Wo));
-        const int rem = (int)(pix - (long)n * Ho * Wo);
+        const int n = (int)(pix / HoWo);
+        const int rem = (int)(pix - (unsigned)n * HoWo);
         const int oh = rem / Wo, ow = rem - (rem / Wo) * Wo;
         float v[E];
 #pragma unroll
@@ -52,7 +53,7 @@ __global__ void im2col_stem_kernel(const float* x, T* cols, int N, int H, int W,
             }
             v[e] = val;
         }
-        Vec16<T>::store(cols + pix * Kpad + ch * E, v);
+        Vec16<T>::store(cols + (size_t)pix * Kpad + ch * E, v);
     }
 }
 
@@ -61,13 +62,14 @@ template <typename T>
 __global__ void stem_pool_fwd_kernel(const T* y, const float* scale, const float* shift, T* out, uint8_t* argmax,
                                      int N, int H, int W, int C, int Ho, int Wo) {
     constexpr int E = Vec16<T>::N;
-    const int cpp = C / E;
-    const long total = (long)N * Ho * Wo * cpp;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const long pix = i / cpp;
-        const int ch = (int)(i - pix * cpp);
-        const int n = (int)(pix / ((long)Ho * Wo));
-        const int rem = (int)(pix - (long)n * Ho * Wo);
+    const unsigned cpp = C / E;
+    const unsigned total = (unsigned)N * Ho * Wo * cpp;
+    const unsigned HoWo = (unsigned)Ho * Wo;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const size_t pix = i / cpp;
+        const int ch = (int)(i - (unsigned)pix * cpp);
+        const int n = (int)((unsigned)pix / HoWo);
+        const int rem = (int)((unsigned)pix - (unsigned)n * HoWo);
         const int oh = rem / Wo, ow = rem - (rem / Wo) * Wo;
         float best[E], sc[E], sh[E];
         int arg[E];
@@ -101,13 +103,14 @@ template <typename T>
 __global__ void stem_pool_bwd_kernel(const T* dout, const uint8_t* argmax, const T* y, const float* scale,
                                      const float* shift, T* dz, int N, int H, int W, int C, int Ho, int Wo) {
     constexpr int E = Vec16<T>::N;
-    const int cpp = C / E;
-    const long total = (long)N * H * W * cpp;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const long pix = i / cpp;
-        const int ch = (int)(i - pix * cpp);
-        const int n = (int)(pix / ((long)H * W));
-        const int rem = (int)(pix - (long)n * H * W);
+    const unsigned cpp = C / E;
+    const unsigned total = (unsigned)N * H * W * cpp;
+    const unsigned HW = (unsigned)H * W;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const size_t pix = i / cpp;
+        const int ch = (int)(i - (unsigned)pix * cpp);
+        const int n = (int)((unsigned)pix / HW);
+        const int rem = (int)((unsigned)pix - (unsigned)n * HW);
         const int h = rem / W, w = rem - (rem / W) * W;
         float acc[E];
 #pragma unroll
@@ -148,112 +151,118 @@ struct HeadsDesc {
     float* out[4];
 };
 
+// thread = (pixel, 16-B channel chunk): coalesced hidden reads; per-head partial dot products
+// reduced over the head's Hd/E chunk-lanes with xor-shuffles (aligned groups: Hd/E | 64).
 template <typename T>
 __global__ void heads_fwd_kernel(const T* hid, int N, int HW, HeadsDesc d) {
     constexpr int E = Vec16<T>::N;
-    __shared__ float w1s[8 * 512];
-    const int Ctot = d.nh * d.Hd;
-    for (int i = threadIdx.x; i < d.nout * d.Hd; i += blockDim.x) {
-        int row = i / d.Hd, c = i - (i / d.Hd) * d.Hd;
-        int h = 0;
-        while (h + 1 < d.nh && row >= d.orow[h + 1]) ++h;
-        w1s[i] = d.w1[h][(row - d.orow[h]) * d.Hd + c];
-    }
-    __syncthreads();
-    const long total = (long)N * HW;
-    for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < total; px += (long)gridDim.x * blockDim.x) {
-        const int n = (int)(px / HW);
-        const int q = (int)(px - (long)n * HW);
-        const T* hp = hid + px * Ctot;
-        for (int h = 0; h < d.nh; ++h) {
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int c = 0; c < d.Hd; c += E) {
-                float v[E];
-                Vec16<T>::load(hp + h * d.Hd + c, v);
+    const int cph = d.Hd / E;                       // chunk-lanes per head (power of two <= 64)
+    const unsigned cpp = (unsigned)(d.nh * cph);     // chunks per pixel
+    const unsigned total = (unsigned)N * HW * cpp;
+    // grid-stride loop must keep whole waves inside the range for the shuffles
+    for (unsigned base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+        const unsigned i = base + threadIdx.x;
+        const bool ok = i < total;
+        const unsigned px = ok ? i / cpp : 0;
+        const int ch = ok ? (int)(i - px * cpp) : 0;
+        const int h = ch / cph;
+        const int cl = (ch - h * cph) * E;
+        float v[E];
+        if (ok) Vec16<T>::load(hid + (size_t)i * E, v);
+        else
 #pragma unroll
-                for (int o = 0; o < 4; ++o) {
-                    if (o < d.od[h]) {
-                        const float* wr = w1s + (d.orow[h] + o) * d.Hd + c;
-#pragma unroll
-                        for (int e = 0; e < E; ++e) acc[o] += v[e] * wr[e];
-                    }
-                }
-            }
-            for (int o = 0; o < d.od[h]; ++o)
-                d.out[h][((long)n * d.od[h] + o) * HW + q] = acc[o] + d.b1[h][o];
-        }
-    }
-}
-
-template <typename T>
-__global__ void heads_bwd_data_kernel(const T* hid, int N, int HW, HeadsDesc d, T* dhid) {
-    constexpr int E = Vec16<T>::N;
-    __shared__ float w1s[8 * 512];
-    const int Ctot = d.nh * d.Hd;
-    for (int i = threadIdx.x; i < d.nout * d.Hd; i += blockDim.x) {
-        int row = i / d.Hd, c = i - (i / d.Hd) * d.Hd;
-        int h = 0;
-        while (h + 1 < d.nh && row >= d.orow[h + 1]) ++h;
-        w1s[i] = d.w1[h][(row - d.orow[h]) * d.Hd + c];
-    }
-    __syncthreads();
-    const long total = (long)N * HW;
-    for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < total; px += (long)gridDim.x * blockDim.x) {
-        const int n = (int)(px / HW);
-        const int q = (int)(px - (long)n * HW);
-        for (int h = 0; h < d.nh; ++h) {
-            float g[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int o = 0; o < d.od[h]; ++o) g[o] = d.dout[h][((long)n * d.od[h] + o) * HW + q];
-            for (int c = 0; c < d.Hd; c += E) {
-                float v[E], r[E];
-                Vec16<T>::load(hid + px * Ctot + h * d.Hd + c, v);
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int o = 0; o < 4; ++o)
-                        if (o < d.od[h]) s += g[o] * w1s[(d.orow[h] + o) * d.Hd + c + e];
-                    r[e] = v[e] > 0.f ? s : 0.f;
-                }
-                Vec16<T>::store(dhid + px * Ctot + h * d.Hd + c, r);
-            }
-        }
-    }
-}
-
-// acc layout per replica: [nout*Hd dW1][nout db1][nh*Hd db0]
-template <typename T>
-__global__ void heads_bwd_weight_kernel(const T* hid, const T* dhid, int N, int HW, HeadsDesc d, int ppb,
-                                        double* acc, int accsz) {
-    const int Ctot = d.nh * d.Hd;
-    const int c = threadIdx.x;                 // one thread per hidden channel (blockDim == Ctot)
-    const int h = c / d.Hd;
-    const int cl = c - h * d.Hd;
-    const long total = (long)N * HW;
-    const long p0 = (long)blockIdx.x * ppb;
-    const long p1 = min(total, p0 + ppb);
-    float aw[4] = {0.f, 0.f, 0.f, 0.f};
-    float ab[4] = {0.f, 0.f, 0.f, 0.f};
-    float a0 = 0.f;
-    for (long px = p0; px < p1; ++px) {
-        const int n = (int)(px / HW);
-        const int q = (int)(px - (long)n * HW);
-        const float hv = to_f<T>(hid[px * Ctot + c]);
-        a0 += to_f<T>(dhid[px * Ctot + c]);
+            for (int e = 0; e < E; ++e) v[e] = 0.f;
+        float acc[4];
 #pragma unroll
         for (int o = 0; o < 4; ++o) {
-            if (o < d.od[h]) {
-                const float g = d.dout[h][((long)n * d.od[h] + o) * HW + q];
-                aw[o] += g * hv;
-                ab[o] += g;
+            float a = 0.f;
+            if (ok && o < d.od[h]) {
+                const float* w = d.w1[h] + o * d.Hd + cl;
+#pragma unroll
+                for (int e = 0; e < E; ++e) a += v[e] * w[e];
             }
+            for (int m = cph >> 1; m > 0; m >>= 1) a += __shfl_xor(a, m, 64);
+            acc[o] = a;
+        }
+        if (ok && (ch - h * cph) == 0) {
+            const int n = (int)(px / (unsigned)HW);
+            const int q = (int)(px - (unsigned)n * HW);
+            for (int o = 0; o < d.od[h]; ++o)
+                d.out[h][((size_t)n * d.od[h] + o) * HW + q] = acc[o] + d.b1[h][o];
         }
     }
-    double* a = acc + (long)(blockIdx.x % SCD_STAT_REPLICAS) * accsz;
-    for (int o = 0; o < d.od[h]; ++o) atomic_add_f64(a + (d.orow[h] + o) * d.Hd + cl, (double)aw[o]);
+}
+
+// fused backward of the head tails: dhid = relu'(hid) * (W1^T dout) and, in the same pass,
+// dW1 = sum_px dout x hid, db1 = sum_px dout, db0 (3x3 conv bias) = sum_px dhid.
+// Block = PXB pixels; thread = (chunk c, pixel-lane g); partials reduced in LDS then fp64
+// atomics into SCD_STAT_REPLICAS replicas.
+template <typename T>
+__global__ __launch_bounds__(256) void heads_bwd_kernel(const T* hid, int N, int HW, HeadsDesc d, T* dhid,
+                                                        double* acc, int accsz, int PXB) {
+    constexpr int E = Vec16<T>::N;
+    constexpr int NA = 4 * E + E + 4;               // dW1 partials, db0 partials, db1 partials
+    const int cph = d.Hd / E;
+    const int cpp = d.nh * cph;
+    const int G = 256 / cpp;
+    const int tid = threadIdx.x;
+    const int c = tid % cpp;
+    const int g = tid / cpp;
+    const int h = c / cph;
+    const int cl = (c - h * cph) * E;
+    const int ct = h * d.Hd + cl;                   // channel of this chunk in the hidden tensor
+    float w[4][E];
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int e = 0; e < E; ++e) w[o][e] = (g < G && o < d.od[h]) ? d.w1[h][o * d.Hd + cl + e] : 0.f;
+    float a[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) a[k] = 0.f;
+    const unsigned P = (unsigned)N * HW;
+    const unsigned p0 = blockIdx.x * (unsigned)PXB;
+    const unsigned p1 = min(P, p0 + PXB);
+    const int Ctot = d.nh * d.Hd;
+    if (g < G) {
+        for (unsigned px = p0 + g; px < p1; px += G) {
+            const int n = (int)(px / (unsigned)HW);
+            const int q = (int)(px - (unsigned)n * HW);
+            float gd[4];
+#pragma unroll
+            for (int o = 0; o < 4; ++o) gd[o] = o < d.od[h] ? d.dout[h][((size_t)n * d.od[h] + o) * HW + q] : 0.f;
+            float v[E], r[E];
+            Vec16<T>::load(hid + (size_t)px * Ctot + ct, v);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float s = gd[0] * w[0][e] + gd[1] * w[1][e] + gd[2] * w[2][e] + gd[3] * w[3][e];
+                r[e] = v[e] > 0.f ? s : 0.f;
+#pragma unroll
+                for (int o = 0; o < 4; ++o) a[o * E + e] += gd[o] * v[e];
+                a[4 * E + e] += r[e];
+            }
+#pragma unroll
+            for (int o = 0; o < 4; ++o) a[5 * E + o] += gd[o];
+            Vec16<T>::store(dhid + (size_t)px * Ctot + ct, r);
+        }
+    }
+    __shared__ float red[256 * NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) red[k * 256 + tid] = a[k];
+    __syncthreads();
+    if (g != 0) return;
+    for (int k = 0; k < NA; ++k) {
+        float s = 0.f;
+        for (int j = 0; j < G; ++j) s += red[k * 256 + j * cpp + c];
+        a[k] = s;
+    }
+    double* dst = acc + (size_t)(blockIdx.x % SCD_STAT_REPLICAS) * accsz;
+    for (int o = 0; o < d.od[h]; ++o)
+#pragma unroll
+        for (int e = 0; e < E; ++e) atomic_add_f64(dst + (d.orow[h] + o) * d.Hd + cl + e, (double)a[o * E + e]);
     if (cl == 0)
-        for (int o = 0; o < d.od[h]; ++o) atomic_add_f64(a + d.nout * d.Hd + d.orow[h] + o, (double)ab[o]);
-    atomic_add_f64(a + d.nout * d.Hd + d.nout + c, (double)a0);
+        for (int o = 0; o < d.od[h]; ++o) atomic_add_f64(dst + d.nout * d.Hd + d.orow[h] + o, (double)a[5 * E + o]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) atomic_add_f64(dst + d.nout * d.Hd + d.nout + ct + e, (double)a[4 * E + e]);
 }
 
 struct HeadsGrad {
@@ -262,10 +271,13 @@ struct HeadsGrad {
     float* db0[4];
 };
 
-__global__ void heads_bwd_weight_finalize_kernel(const double* acc, int accsz, HeadsDesc d, HeadsGrad g, int accumulate) {
+__global__ void heads_bwd_weight_finalize_kernel(double* acc, int accsz, HeadsDesc d, HeadsGrad g, int accumulate) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < accsz; i += gridDim.x * blockDim.x) {
         double s = 0.0;
-        for (int r = 0; r < SCD_STAT_REPLICAS; ++r) s += acc[(long)r * accsz + i];
+        for (int r = 0; r < SCD_STAT_REPLICAS; ++r) {
+            s += acc[(long)r * accsz + i];
+            acc[(long)r * accsz + i] = 0.0;
+        }
         float* dst;
         if (i < d.nout * d.Hd) {
             const int row = i / d.Hd, cl = i - (i / d.Hd) * d.Hd;
@@ -388,10 +400,13 @@ extern "C" int scd_heads_fwd(int dtype, const void* hid, int N, int HW, int nh, 
                              const float* const* w1, const float* const* b1, float* const* outs, void* stream) {
     HeadsDesc d;
     if (!make_desc(d, nh, Hd, od)) return SCD_ERR_ARG;
+    const int E = dtype == SCD_DT_BF16 ? 8 : 4;
+    const int cph = Hd / E;
+    if (cph > 64 || (cph & (cph - 1))) return SCD_ERR_ARG;
     for (int h = 0; h < nh; ++h) { d.w1[h] = w1[h]; d.b1[h] = b1[h]; d.out[h] = outs[h]; }
     hipStream_t st = (hipStream_t)stream;
-    const long total = (long)N * HW;
-    const int blocks = (int)std::min<long>(4096, (total + 255) / 256);
+    const long total = (long)N * HW * nh * cph;
+    const int blocks = (int)std::min<long>(16384, (total + 255) / 256);
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((heads_fwd_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)hid, N, HW, d);
     else if (dtype == SCD_DT_F32)
@@ -401,55 +416,38 @@ extern "C" int scd_heads_fwd(int dtype, const void* hid, int N, int HW, int nh, 
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_heads_bwd_data(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
-                                  const float* const* w1, const float* const* douts, void* dhid, void* stream) {
-    HeadsDesc d;
-    if (!make_desc(d, nh, Hd, od)) return SCD_ERR_ARG;
-    for (int h = 0; h < nh; ++h) { d.w1[h] = w1[h]; d.dout[h] = douts[h]; }
-    hipStream_t st = (hipStream_t)stream;
-    const long total = (long)N * HW;
-    const int blocks = (int)std::min<long>(4096, (total + 255) / 256);
-    if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((heads_bwd_data_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)hid, N, HW, d,
-                           (__bf16*)dhid);
-    else if (dtype == SCD_DT_F32)
-        hipLaunchKernelGGL((heads_bwd_data_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)hid, N, HW, d,
-                           (float*)dhid);
-    else
-        return SCD_ERR_ARG;
-    SCD_RETURN_LAUNCH();
-}
-
-extern "C" size_t scd_heads_bwd_weight_accsize(int nh, int Hd, const int* od) {
+extern "C" size_t scd_heads_bwd_accsize(int nh, int Hd, const int* od) {
     int nout = 0;
     for (int h = 0; h < nh; ++h) nout += od[h];
     return (size_t)SCD_STAT_REPLICAS * (nout * Hd + nout + nh * Hd) * sizeof(double);
 }
 
-extern "C" int scd_heads_bwd_weight(int dtype, const void* hid, const void* dhid, int N, int HW, int nh, int Hd,
-                                    const int* od, const float* const* douts, double* acc, void* stream) {
+extern "C" int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
+                             const float* const* w1, const float* const* douts, void* dhid, double* acc,
+                             void* stream) {
     HeadsDesc d;
     if (!make_desc(d, nh, Hd, od)) return SCD_ERR_ARG;
-    for (int h = 0; h < nh; ++h) d.dout[h] = douts[h];
-    const int Ctot = nh * Hd;
-    if (Ctot > 1024) return SCD_ERR_ARG;
-    const int accsz = d.nout * Hd + d.nout + Ctot;
-    const long total = (long)N * HW;
-    const int ppb = 256;
-    const int blocks = cdiv(total, ppb);
+    const int E = dtype == SCD_DT_BF16 ? 8 : 4;
+    const int cpp = nh * Hd / E;
+    if (cpp > 256 || (Hd % E)) return SCD_ERR_ARG;
+    for (int h = 0; h < nh; ++h) { d.w1[h] = w1[h]; d.dout[h] = douts[h]; }
+    const int accsz = d.nout * Hd + d.nout + nh * Hd;
+    const long P = (long)N * HW;
+    const int PXB = 256;
+    const int blocks = cdiv(P, PXB);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((heads_bwd_weight_kernel<__bf16>), dim3(blocks), dim3(Ctot), 0, st, (const __bf16*)hid,
-                           (const __bf16*)dhid, N, HW, d, ppb, acc, accsz);
+        hipLaunchKernelGGL((heads_bwd_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)hid, N, HW, d,
+                           (__bf16*)dhid, acc, accsz, PXB);
     else if (dtype == SCD_DT_F32)
-        hipLaunchKernelGGL((heads_bwd_weight_kernel<float>), dim3(blocks), dim3(Ctot), 0, st, (const float*)hid,
-                           (const float*)dhid, N, HW, d, ppb, acc, accsz);
+        hipLaunchKernelGGL((heads_bwd_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)hid, N, HW, d,
+                           (float*)dhid, acc, accsz, PXB);
     else
         return SCD_ERR_ARG;
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_heads_bwd_weight_finalize(const double* acc, int nh, int Hd, const int* od, float* const* dw1,
+extern "C" int scd_heads_bwd_weight_finalize(double* acc, int nh, int Hd, const int* od, float* const* dw1,
                                              float* const* db1, float* const* db0, int accumulate, void* stream) {
     HeadsDesc d;
     if (!make_desc(d, nh, Hd, od)) return SCD_ERR_ARG;

@@ -33,7 +33,7 @@ def _train_bn_conv(x, conv, bn, stride, pad, training):
     C = conv.weight.shape[0]
     kh, kw = conv.weight.shape[2], conv.weight.shape[3]
     wp = ops.pack_weight(conv.weight, x.dtype, 0)
-    stats = ops.new_stats(C, x.device) if training else None
+    stats = ops.bn_stats(bn, "fwd") if training else None
     y = ops.conv_fwd(x, wp, C, kh, kw, stride, pad, stats=stats)
     st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
     return y, st
@@ -47,7 +47,7 @@ class StemFn(torch.autograd.Function):
                                stride=conv.stride[0], pad=conv.padding[0])
         C = conv.weight.shape[0]
         wp = ops.pack_weight(conv.weight, dtype, 0, ldp=cols.shape[-1])
-        stats = ops.new_stats(C, x.device) if training else None
+        stats = ops.bn_stats(bn, "fwd") if training else None
         y = ops.conv_fwd(cols, wp, C, 1, 1, 1, 0, stats=stats)
         st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
         out, am = ops.stem_pool_fwd(y, st)
@@ -175,7 +175,7 @@ class DeconvBNFn(torch.autograd.Function):
         k = w.shape[2]
         s, p = deconv.stride[0], deconv.padding[0]
         Cout = w.shape[1]
-        stats = ops.new_stats(Cout, x.device) if bn.training else None
+        stats = ops.bn_stats(bn, "fwd") if bn.training else None
         y = ops.deconv_fwd(x, ops.pack_weight(w, x.dtype, 1), Cout, k, s, p, stats=stats)
         st = ops.bn_finalize(bn, stats, Cout, y.numel() // Cout, bn.training)
         out = ops.bn_apply(y, st, True)
@@ -235,13 +235,22 @@ class HeadsFn(torch.autograd.Function):
         b0 = torch.cat([h[0].bias for h in heads], 0)
         Hd = heads[0][0].weight.shape[0]
         Ct = w0.shape[0]
-        hid = ops.conv_fwd(feat, ops.pack_weight(w0, feat.dtype, 0), Ct, 3, 3, 1, 1, bias=b0, relu=True)
         od = [h[2].weight.shape[0] for h in heads]
         outs = [torch.empty(N, o, H, W, device=feat.device, dtype=torch.float32) for o in od]
-        ops.L.call("scd_heads_fwd", ops.dt(hid), ops.ptr(hid), N, H * W, len(heads), Hd, ops.L.int_array(od),
-                   ops.L.ptr_array([h[2].weight.data_ptr() for h in heads]),
-                   ops.L.ptr_array([h[2].bias.data_ptr() for h in heads]),
-                   ops.L.ptr_array([o.data_ptr() for o in outs]), ops.stream())
+        wp = ops.pack_weight(w0, feat.dtype, 0)
+        w1s = ops.L.ptr_array([h[2].weight.data_ptr() for h in heads])
+        b1s = ops.L.ptr_array([h[2].bias.data_ptr() for h in heads])
+        optrs = ops.L.ptr_array([o.data_ptr() for o in outs])
+        odarr = ops.L.int_array(od)
+        if Hd == 128 and len(heads) <= 4 and max(od) <= 4:
+            # tails fused into the GEMM epilogue (one launch, hidden tensor read once)
+            hid = torch.empty(N, H, W, Ct, device=feat.device, dtype=feat.dtype)
+            ops.L.call("scd_conv_gemm_heads", ops.dt(feat), ops.ptr(feat), ops.ptr(wp), ops.ptr(hid), ops.ptr(b0),
+                       N, H, W, Cin, len(heads), odarr, w1s, b1s, optrs, ops.stream())
+        else:
+            hid = ops.conv_fwd(feat, wp, Ct, 3, 3, 1, 1, bias=b0, relu=True)
+            ops.L.call("scd_heads_fwd", ops.dt(hid), ops.ptr(hid), N, H * W, len(heads), Hd, odarr, w1s, b1s, optrs,
+                       ops.stream())
         ctx.save_for_backward(feat, hid, w0)
         ctx.heads, ctx.od, ctx.Hd = heads, od, Hd
         return tuple(outs)
@@ -257,12 +266,11 @@ class HeadsFn(torch.autograd.Function):
         dptrs = ops.L.ptr_array([d.data_ptr() for d in douts])
         odarr = ops.L.int_array(od)
         dhid = torch.empty_like(hid)
-        ops.L.call("scd_heads_bwd_data", ops.dt(hid), ops.ptr(hid), N, H * W, nh, Hd, odarr,
-                   ops.L.ptr_array([h[2].weight.data_ptr() for h in heads]), dptrs, ops.ptr(dhid), ops.stream())
-        accsz = ops.L.lib().scd_heads_bwd_weight_accsize(nh, Hd, odarr)
-        acc = torch.zeros(accsz // 8, dtype=torch.float64, device=feat.device)
-        ops.L.call("scd_heads_bwd_weight", ops.dt(hid), ops.ptr(hid), ops.ptr(dhid), N, H * W, nh, Hd, odarr, dptrs,
-                   ops.ptr(acc), ops.stream())
+        acc = ops.persistent_zeros(heads[0][2].weight, "_scd_heads_acc",
+                                   ops.L.lib().scd_heads_bwd_accsize(nh, Hd, odarr) // 8, torch.float64)
+        ops.L.call("scd_heads_bwd", ops.dt(hid), ops.ptr(hid), N, H * W, nh, Hd, odarr,
+                   ops.L.ptr_array([h[2].weight.data_ptr() for h in heads]), dptrs, ops.ptr(dhid), ops.ptr(acc),
+                   ops.stream())
         ops.L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), nh, Hd, odarr,
                    ops.L.ptr_array([ops.grad_of(h[2].weight).data_ptr() for h in heads]),
                    ops.L.ptr_array([ops.grad_of(h[2].bias).data_ptr() for h in heads]),

@@ -42,6 +42,7 @@ IP = ctypes.POINTER(c_int)
 # name -> (restype, argtypes); mirrors include/scdhip.h one to one
 SIGNATURES = {
     "scd_conv_gemm": (I, [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P]),
+    "scd_conv_gemm_heads": (I, [I, P, P, P, P, I, I, I, I, I, IP, PP, PP, PP, P]),
     "scd_conv_wgrad_workspace": (c_size_t, [I, I, I, I]),
     "scd_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, IP, IP, P]),
     "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, P]),
@@ -56,9 +57,8 @@ SIGNATURES = {
     "scd_stem_pool_fwd": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_pool_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_heads_fwd": (I, [I, P, I, I, I, I, IP, PP, PP, PP, P]),
-    "scd_heads_bwd_data": (I, [I, P, I, I, I, I, IP, PP, PP, P, P]),
-    "scd_heads_bwd_weight_accsize": (c_size_t, [I, I, IP]),
-    "scd_heads_bwd_weight": (I, [I, P, P, I, I, I, I, IP, PP, P, P]),
+    "scd_heads_bwd_accsize": (c_size_t, [I, I, IP]),
+    "scd_heads_bwd": (I, [I, P, I, I, I, I, IP, PP, PP, P, P, P]),
     "scd_heads_bwd_weight_finalize": (I, [P, I, I, IP, PP, PP, PP, I, P]),
     "scd_focal_fwd": (I, [P, P, L, P, P, P]),
     "scd_l1_gather_fwd": (I, [P, I, I, I, P, P, P, I, I, I, P, P, P]),

@@ -66,6 +66,23 @@ def new_stats(C, device):
     return torch.zeros(L.STAT_REPLICAS * 2 * C, dtype=torch.float64, device=device)
 
 
+def persistent_zeros(owner, attr, numel, dtype):
+    """A zero-initialised device buffer cached on `owner` (a module/parameter).  The kernels that
+    consume it (BN finalize, stats collapse, heads finalize, loss finalize) re-zero what they read,
+    so it is ready for the next use without a memset launch."""
+    buf = getattr(owner, attr, None)
+    dev = owner.device if torch.is_tensor(owner) else owner.weight.device
+    if buf is None or buf.numel() != numel or buf.device != dev or buf.dtype != dtype:
+        buf = torch.zeros(numel, dtype=dtype, device=dev)
+        setattr(owner, attr, buf)
+    return buf
+
+
+def bn_stats(bn, which):
+    """Persistent fp64 [replicas][2][C] statistics buffer of a BatchNorm module ('fwd' / 'bwd')."""
+    return persistent_zeros(bn, "_scd_stats_" + which, L.STAT_REPLICAS * 2 * bn.num_features, torch.float64)
+
+
 # ------------------------------------------------------------------ weights
 
 def pack_weight(w, dtype, mode, ldp=None, out=None, row_off=0):
@@ -167,7 +184,7 @@ def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=Fals
 
 def _nsplit(M, Cg, KK, Cg_tile, KK_tile):
     tiles = -(-Cg // Cg_tile) * -(-KK // KK_tile)
-    ns = max(1, min(1024 // tiles, M // 1024))
+    ns = max(1, min(1024 // tiles, M // 1024, 256))
     # cap the fp32 workspace at ~256 MB
     ns = max(1, min(ns, (256 << 20) // max(1, 4 * Cg * KK)))
     return ns
@@ -239,7 +256,7 @@ def bn_apply(y, st, relu, res=None, rst=None, out=None):
 def bn_backward(bn, st, dout, y, mask=None, dz_out=None):
     """Training BN backward: dgamma/dbeta accumulated into bn.weight.grad / bn.bias.grad, returns dy."""
     C = y.shape[-1]
-    stats = new_stats(C, y.device)
+    stats = bn_stats(bn, "bwd")
     L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), ptr(st.mean), ptr(st.invstd), C, y.numel(),
            ptr(stats), stream())
     nrep = _allreduce_stats(stats, C)
