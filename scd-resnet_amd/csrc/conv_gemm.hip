@@ -20,6 +20,7 @@ struct GemmParams {
     double* stats;
     int N, Hi, Wi, Ci, Ho, Wo, Co;
     int is, os, wrow, relu, accumulate, nphase, ntn;
+    int xbytes, wbytes;
     int tile_start[SCD_MAX_PHASES + 1];
     scd_gemm_phase ph[SCD_MAX_PHASES];
     // optional fused CenterNet head tails (n-tile t == head t, BN == head hidden width)
@@ -35,8 +36,19 @@ struct GemmParams {
 // ds_write_b128 staging stores (8 chunks of one row) are then bank-conflict free.
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
+// Buffer-load offset or an out-of-range one (the load then returns zeros).  The offset is made
+// opaque before the select so the compiler cannot sink its arithmetic into an exec-masked branch:
+// branches around loads make its waitcnt pass fall back to vmcnt(0) and drain the prefetch.
+__device__ __forceinline__ int sel_off(bool ok, int off) {
+    asm volatile("" : "+v"(off));
+    return ok ? off : -16;
+}
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 template <typename T, int BM, int BN>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;       // elements per 16-B chunk
     constexpr int BK = 128 / ESZ;       // K elements per stage
@@ -97,25 +109,29 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
     const int KT = ph.ntaps * cpt;
     const int st_off = swz(srow, cch);    // (srow + 32i) & 7 == srow & 7
 
-    uint4 ra[ACH], rb[BCH];
-    auto gload = [&](int kt) {
+    // raw buffer loads: out-of-range lanes use an offset past num_records and read zeros
+    // (no exec-mask branches around the loads, so the compiler can count vmcnt per stage)
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+    auto gload = [&](int kt_req, uint4 (&ra)[ACH], uint4 (&rb)[BCH]) {
+        // stages past the end are issued with out-of-range offsets (no traffic, no branch)
+        const bool live = kt_req < KT;
+        const int kt = min(kt_req, KT - 1);
         int tap = kt / cpt;
         int c0 = (kt - tap * cpt) * BK + cch * EPC;
         int dh = ph.dh[tap], dw = ph.dw[tap], wt = ph.wt[tap];
 #pragma unroll
         for (int i = 0; i < ACH; ++i) {
             int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
-            bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-            long off = ((long)(a_pix[i] + ih * p.Wi + iw) * p.Ci + c0) * ESZ;
-            ra[i] = ok ? *(const uint4*)(p.x + off) : make_uint4(0, 0, 0, 0);
+            bool ok = live && a_ok[i] && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+            ra[i] = bload(xrs, sel_off(ok, ((a_pix[i] + ih * p.Wi + iw) * p.Ci + c0) * ESZ));
         }
 #pragma unroll
         for (int j = 0; j < BCH; ++j) {
-            long off = ((long)b_row[j] * p.wrow + (long)wt * p.Ci + c0) * ESZ;
-            rb[j] = b_ok[j] ? *(const uint4*)(p.w + off) : make_uint4(0, 0, 0, 0);
+            rb[j] = bload(wrs, sel_off(live && b_ok[j], (b_row[j] * p.wrow + wt * p.Ci + c0) * ESZ));
         }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](int buf, const uint4 (&ra)[ACH], const uint4 (&rb)[BCH]) {
         char* As = smem + buf * STAGE;
         char* Bs = As + BM * 128;
 #pragma unroll
@@ -189,14 +205,22 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(GemmParams p) {
     };
 
     if (KT > 0) {
-        gload(0);
-        lstore(0);
+        // two stages of global loads in flight: stage k+1 lands while stage k is computed and
+        // stage k+2 is issued; LDS is double-buffered, one barrier per stage
+        uint4 ra0[ACH], rb0[BCH], ra1[ACH], rb1[BCH];
+        gload(0, ra0, rb0);
+        gload(1, ra1, rb1);
+        lstore(0, ra0, rb0);
         __syncthreads();
-        for (int kt = 0; kt < KT; ++kt) {
-            const int cur = kt & 1;
-            if (kt + 1 < KT) gload(kt + 1);
-            compute(cur);
-            if (kt + 1 < KT) lstore(cur ^ 1);
+        for (int kt = 0; kt < KT; kt += 2) {
+            gload(kt + 2, ra0, rb0);
+            compute(0);
+            lstore(1, ra1, rb1);
+            __syncthreads();
+            if (kt + 1 >= KT) break;
+            gload(kt + 3, ra1, rb1);
+            compute(1);
+            lstore(0, ra0, rb0);
             __syncthreads();
         }
     }
@@ -340,22 +364,37 @@ struct WgradParams {
     const char* x;
     float* ws;
     int N, Ho, Wo, Cg, Hi, Wi, Ci, is, T, KK, chunk, ntm, ntn;
+    int gbytes, xbytes;
     int dh[SCD_MAX_TAPS], dw[SCD_MAX_TAPS];
 };
 
+// LDS image of a [pixel][channel] stage for transposed (ds_read_b64_tr_b16) fragment reads: a row
+// stride of 8 dwords mod 64 banks (288 B for <= 256-B rows, 544 B for 512-B rows) puts rows r..r+3 on
+// disjoint 8-bank slots, and the column offset of rows with bit 3 set is XORed with 128 B, so rows
+// {0-3, 8-11} read by one 32-lane half cover all 64 banks: the transposed reads are conflict free.
+__host__ __device__ constexpr int wrow_stride(int rowbytes) { return rowbytes <= 256 ? 288 : rowbytes + 32; }
+__device__ __forceinline__ int wswz(int row, int byte, int stride) {
+    return row * stride + (byte ^ (((row >> 3) & 1) << 7));
+}
+
 template <typename T, int BM, int BN>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;
-    constexpr int KP = 32;                               // pixels per stage
-    constexpr int GROW = BM * ESZ + 16;                  // LDS row bytes (pixel rows)
-    constexpr int XROW = BN * ESZ + 16;
-    constexpr int GCPR = BM * ESZ / 16;                  // chunks per G row
-    constexpr int XCPR = BN * ESZ / 16;
+    constexpr int KP = ESZ == 2 ? 64 : 32;               // pixels per stage (2 bf16 MFMA k-steps)
+    constexpr int GROWB = BM * ESZ;                      // bytes of one G row
+    constexpr int XROWB = BN * ESZ;
+    constexpr int GROW = ESZ == 2 ? wrow_stride(GROWB) : GROWB + 16;   // LDS row stride
+    constexpr int XROW = ESZ == 2 ? wrow_stride(XROWB) : XROWB + 16;
+    constexpr int GCPR = GROWB / 16;                     // chunks per G row
+    constexpr int XCPR = XROWB / 16;
     constexpr int GCH = KP * GCPR / 256;                 // chunks per thread
     constexpr int XCH = KP * XCPR / 256;
+    constexpr int GRS = 256 / GCPR;                      // rows per load pass
+    constexpr int XRS = 256 / XCPR;
     constexpr int WN = BN / 64;
-    __shared__ __attribute__((aligned(16))) char smem[2 * KP * (GROW + XROW)];
+    constexpr int STAGE = KP * (GROW + XROW);
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int z = blockIdx.z;
@@ -364,14 +403,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     const int M = p.N * p.Ho * p.Wo;
     const int pix0 = z * p.chunk;
     const int pix1 = min(M, pix0 + p.chunk);
-    const int HoWo = p.Ho * p.Wo;
 
     // G loads: fixed channel chunk per thread
     const int gc = tid % GCPR;
     const int gr0 = tid / GCPR;
     const int gcol = mt * BM + gc * EPC;
     const bool gcol_ok = gcol < p.Cg;
-    // X loads: fixed (tap, ci) chunk per thread
+    // X loads: fixed (tap, ci) chunk per thread; pixel position advanced incrementally
     const int xc = tid % XCPR;
     const int xr0 = tid / XCPR;
     const int kk = nt * BN + xc * EPC;
@@ -379,36 +417,58 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
     const int tap = kk_ok ? kk / p.Ci : 0;
     const int ci = kk - tap * p.Ci;
     const int dh = p.dh[tap], dw = p.dw[tap];
+    int xn[XCH], xoh[XCH], xow[XCH];
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+        const int pix = pix0 + xr0 + i * XRS;
+        const int HoWo = p.Ho * p.Wo;
+        xn[i] = pix / HoWo;
+        const int rem = pix - xn[i] * HoWo;
+        xoh[i] = rem / p.Wo;
+        xow[i] = rem - xoh[i] * p.Wo;
+    }
+    auto advance = [&]() {     // every row advances by KP pixels
+#pragma unroll
+        for (int i = 0; i < XCH; ++i) {
+            xow[i] += KP;
+            while (xow[i] >= p.Wo) {
+                xow[i] -= p.Wo;
+                if (++xoh[i] >= p.Ho) { xoh[i] = 0; ++xn[i]; }
+            }
+        }
+    };
 
-    uint4 rg[GCH], rx[XCH];
-    auto gload = [&](int k0) {
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    auto gload = [&](int k0, uint4 (&rg)[GCH], uint4 (&rx)[XCH]) {
 #pragma unroll
         for (int i = 0; i < GCH; ++i) {
-            int pix = k0 + gr0 + i * (256 / GCPR);
-            bool ok = gcol_ok && pix < pix1;
-            rg[i] = ok ? *(const uint4*)(p.g + ((long)pix * p.Cg + gcol) * ESZ) : make_uint4(0, 0, 0, 0);
+            const int pix = k0 + gr0 + i * GRS;
+            rg[i] = bload(grs, sel_off(gcol_ok && pix < pix1, (pix * p.Cg + gcol) * ESZ));
         }
 #pragma unroll
         for (int i = 0; i < XCH; ++i) {
-            int pix = k0 + xr0 + i * (256 / XCPR);
-            bool ok = kk_ok && pix < pix1;
-            int n = pix / HoWo;
-            int rem = pix - n * HoWo;
-            int oh = rem / p.Wo;
-            int ow = rem - oh * p.Wo;
-            int ih = p.is * oh + dh, iw = p.is * ow + dw;
-            ok = ok && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-            long off = ((long)((n * p.Hi + ih) * p.Wi + iw) * p.Ci + ci) * ESZ;
-            rx[i] = ok ? *(const uint4*)(p.x + off) : make_uint4(0, 0, 0, 0);
+            const int pix = k0 + xr0 + i * XRS;
+            const int ih = p.is * xoh[i] + dh, iw = p.is * xow[i] + dw;
+            const bool ok = kk_ok && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+            rx[i] = bload(xrs, sel_off(ok, (((xn[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + ci) * ESZ));
         }
     };
-    auto lstore = [&](int buf) {
-        char* Gs = smem + buf * KP * (GROW + XROW);
+    auto lstore = [&](int buf, const uint4 (&rg)[GCH], const uint4 (&rx)[XCH]) {
+        char* Gs = smem + buf * STAGE;
         char* Xs = Gs + KP * GROW;
 #pragma unroll
-        for (int i = 0; i < GCH; ++i) *(uint4*)(Gs + (gr0 + i * (256 / GCPR)) * GROW + gc * 16) = rg[i];
+        for (int i = 0; i < GCH; ++i) {
+            const int row = gr0 + i * GRS;
+            char* d = ESZ == 2 ? Gs + wswz(row, gc * 16, GROW) : Gs + row * GROW + gc * 16;
+            *(uint4*)d = rg[i];
+        }
 #pragma unroll
-        for (int i = 0; i < XCH; ++i) *(uint4*)(Xs + (xr0 + i * (256 / XCPR)) * XROW + xc * 16) = rx[i];
+        for (int i = 0; i < XCH; ++i) {
+            const int row = xr0 + i * XRS;
+            char* d = ESZ == 2 ? Xs + wswz(row, xc * 16, XROW) : Xs + row * XROW + xc * 16;
+            *(uint4*)d = rx[i];
+        }
     };
 
     const int lane = tid & 63;
@@ -423,36 +483,39 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
         for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     auto compute = [&](int buf) {
-        const char* Gs = smem + buf * KP * (GROW + XROW);
+        const char* Gs = smem + buf * STAGE;
         const char* Xs = Gs + KP * GROW;
         if constexpr (ESZ == 2) {
-            // ds_read_b64_tr_b16: lane 4q+p of 16-lane group lg supplies row (8lg+q[+4]),
-            // columns c0+4p..4p+3; lane i of the group receives column c0+i, 4 rows.
+            // ds_read_b64_tr_b16: lane 4q+p of 16-lane group lg supplies row (8lg+q[+4]) of the k-step,
+            // columns c0+4p..4p+3; lane i of the group receives column c0+i of those 4 rows.
             const int q = l16 >> 2, pp = l16 & 3;
-            bf16x8 af[4], bfr[4];
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const char* base = Gs + (8 * lg + q) * GROW + (wm * 64 + a * 16 + 4 * pp) * 2;
-                s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
-                s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * GROW));
-                typedef __attribute__((ext_vector_type(8))) short s16x8;
-                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                af[a] = __builtin_bit_cast(bf16x8, v);
+            for (int s = 0; s < KP / 32; ++s) {
+                const int r0 = 32 * s + 8 * lg + q;
+                bf16x8 af[4], bfr[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    const int cb = (wm * 64 + a * 16 + 4 * pp) * 2;
+                    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + wswz(r0, cb, GROW)));
+                    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + wswz(r0 + 4, cb, GROW)));
+                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    af[a] = __builtin_bit_cast(bf16x8, v);
+                }
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int cb = (wn * 64 + b * 16 + 4 * pp) * 2;
+                    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + wswz(r0, cb, XROW)));
+                    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + wswz(r0 + 4, cb, XROW)));
+                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    bfr[b] = __builtin_bit_cast(bf16x8, v);
+                }
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
             }
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const char* base = Xs + (8 * lg + q) * XROW + (wn * 64 + b * 16 + 4 * pp) * 2;
-                s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
-                s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * XROW));
-                typedef __attribute__((ext_vector_type(8))) short s16x8;
-                s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                bfr[b] = __builtin_bit_cast(bf16x8, v);
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
         } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -473,14 +536,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 
     const int nk = (pix1 > pix0) ? (pix1 - pix0 + KP - 1) / KP : 0;
     if (nk > 0) {
-        gload(pix0);
-        lstore(0);
+        // two stages of loads in flight (see conv_gemm_kernel); stages past the end read nothing
+        uint4 rg0[GCH], rx0[XCH], rg1[GCH], rx1[XCH];
+        gload(pix0, rg0, rx0);
+        advance();
+        gload(pix0 + KP, rg1, rx1);
+        lstore(0, rg0, rx0);
         __syncthreads();
-        for (int it = 0; it < nk; ++it) {
-            const int cur = it & 1;
-            if (it + 1 < nk) gload(pix0 + (it + 1) * KP);
-            compute(cur);
-            if (it + 1 < nk) lstore(cur ^ 1);
+        for (int it = 0; it < nk; it += 2) {
+            advance();
+            gload(pix0 + (it + 2) * KP, rg0, rx0);
+            compute(0);
+            lstore(1, rg1, rx1);
+            __syncthreads();
+            if (it + 1 >= nk) break;
+            advance();
+            gload(pix0 + (it + 3) * KP, rg1, rx1);
+            compute(1);
+            lstore(0, rg0, rx0);
             __syncthreads();
         }
     }
@@ -498,6 +571,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
                 if (col < p.KK) ws[(long)row * p.KK + col] = acc[a][b][r];
             }
         }
+}
+
+// sums groups of G consecutive split slabs into the group's first slab (first pass of a wide reduce)
+__global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs) {
+    const long ngroups = (nsplit + G - 1) / G;
+    const long total = ngroups * zs;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long g = i / zs, e = i - g * zs;
+        float* base = ws + g * G * zs + e;
+        float s = 0.f;
+        const int n = (int)min((long)G, nsplit - g * G);
+        for (int k = 0; k < n; ++k) s += base[(long)k * zs];
+        base[0] = s;
+    }
 }
 
 __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
@@ -541,6 +628,9 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     const int EPC = dtype == SCD_DT_BF16 ? 8 : 4;
     if (p.Ci % BK != 0 || p.Co <= 0 || p.Co % EPC != 0 || p.N <= 0) return SCD_ERR_ARG;
     p.nphase = nphase;
+    const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
+    const long xb = (long)p.N * p.Hi * p.Wi * p.Ci * esz;
+    long wrows = 0;
     const bool narrow = p.Co <= 64;
     if (p.head_on && (narrow || p.Co != 128 * ((p.Co + 127) / 128))) return SCD_ERR_ARG;
     const int BM = narrow ? 256 : 128, BN = narrow ? 64 : 128;
@@ -560,6 +650,11 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     }
     p.tile_start[SCD_MAX_PHASES] = tiles;
     if (tiles == 0) return 0;
+    wrows = p.Co;
+    const long wb = wrows * p.wrow * esz;
+    if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;   // 32-bit buffer offsets
+    p.xbytes = (int)xb;
+    p.wbytes = (int)wb;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
         return narrow ? launch_gemm<__bf16, 256, 64>(p, tiles, st) : launch_gemm<__bf16, 128, 128>(p, tiles, st);
@@ -617,10 +712,17 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     p.g = (const char*)g; p.x = (const char*)x; p.ws = ws;
     p.N = N; p.Ho = Ho; p.Wo = Wo; p.Cg = Cg; p.Hi = Hi; p.Wi = Wi; p.Ci = Ci; p.is = in_stride; p.T = T;
     p.KK = T * Ci;
+    {
+        const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
+        const long gb = (long)N * Ho * Wo * Cg * esz, xb = (long)N * Hi * Wi * Ci * esz;
+        if (gb >= (1L << 31) - 64 || xb >= (1L << 31) - 64) return SCD_ERR_ARG;
+        p.gbytes = (int)gb;
+        p.xbytes = (int)xb;
+    }
     for (int t = 0; t < SCD_MAX_TAPS; ++t) { p.dh[t] = t < T ? dh[t] : 0; p.dw[t] = t < T ? dw[t] : 0; }
     const long M = (long)N * Ho * Wo;
     int chunk = cdiv(M, nsplit);
-    chunk = (chunk + 31) / 32 * 32;
+    chunk = (chunk + 63) / 64 * 64;
     p.chunk = chunk;
     const bool narrow = Cg <= 64;
     const int BM = narrow ? 64 : 128, BN = narrow ? 256 : 128;
@@ -643,9 +745,24 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
 extern "C" int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
                                 long ld_n, long ld_c, long ld_t, float* dst, int accumulate, void* stream) {
     if (r0 < 0 || r1 > Cg || r0 >= r1) return SCD_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const long zs = (long)Cg * T * Ci;
+    int ns = nsplit;
+    long zstride_mult = 1;
+    if (nsplit > 32) {
+        // two-pass: groups of 16 slabs summed in place (parallel over groups), then the group heads
+        const int G = 16;
+        const long total = (long)((nsplit + G - 1) / G) * zs;
+        hipLaunchKernelGGL(wgrad_presum_kernel, dim3((int)std::min<long>(8192, (total + 255) / 256)), dim3(256), 0, st,
+                           (float*)ws, nsplit, G, zs);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+        ns = (nsplit + G - 1) / G;
+        zstride_mult = G;
+    }
     const long total = (long)(r1 - r0) * T * Ci;
     const int blocks = (int)std::min<long>(4096, (total + 255) / 256);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ws, nsplit, Cg, T, Ci,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, ns, (int)(Cg * zstride_mult), T, Ci,
                        r0, r1, cvalid, ld_n, ld_c, ld_t, dst, accumulate);
     SCD_RETURN_LAUNCH();
 }

@@ -184,7 +184,7 @@ def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=Fals
 
 def _nsplit(M, Cg, KK, Cg_tile, KK_tile):
     tiles = -(-Cg // Cg_tile) * -(-KK // KK_tile)
-    ns = max(1, min(1024 // tiles, M // 1024, 256))
+    ns = max(1, min(1024 // tiles, M // 1024))
     # cap the fp32 workspace at ~256 MB
     ns = max(1, min(ns, (256 << 20) // max(1, 4 * Cg * KK)))
     return ns
