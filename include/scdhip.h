@@ -106,10 +106,12 @@ int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const f
 /* dz = dout * (mask ? mask>0 : 1); stats += [sum dz, sum dz*(y-mean)*invstd] */
 int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
                       const float* invstd, int C, long total, double* stats, void* stream);
-/* dgamma (+)= sum dz*xhat, dbeta (+)= sum dz; coef[3][C] for dy = a*dz + b*y + c */
+/* dgamma (+)= gscale * sum dz*xhat, dbeta (+)= gscale * sum dz; coef[3][C] for dy = a*dz + b*y + c.
+ * With SyncBN the sums are global; gscale = 1/world keeps the DDP-averaged dgamma/dbeta equal to the
+ * reference's (torch SyncBatchNorm returns the LOCAL weight/bias gradients, DDP then averages them). */
 int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                         const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                        float* coef, void* stream);
+                        float gscale, float* coef, void* stream);
 /* dy = a*dz + b*y + c (dtype); optionally also writes dz */
 int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* coef,
                      int C, long total, void* dy, void* dz, void* stream);

@@ -155,14 +155,14 @@ __global__ void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y, c
 
 __global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
                                        const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                                       float* coef) {
+                                       float gscale, float* coef) {
     const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (c >= C) return;
     double s, q;
     wave_collect(stats, nrep, C, c, s, q);
     if ((threadIdx.x & 63) != 0) return;
-    if (dgamma) dgamma[c] += (float)q;
-    if (dbeta) dbeta[c] += (float)s;
+    if (dgamma) dgamma[c] += gscale * (float)q;
+    if (dbeta) dbeta[c] += gscale * (float)s;
     const float g = gamma ? gamma[c] : 1.f;
     const float is = invstd[c];
     const float sc = g * is;
@@ -262,10 +262,10 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
 }
 
 extern "C" int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,
-                                   const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
-                                   void* stream) {
+                                   const float* mean, const float* invstd, float* dgamma, float* dbeta, float gscale,
+                                   float* coef, void* stream) {
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fin_blocks(C)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
-                       count, gamma, mean, invstd, dgamma, dbeta, coef);
+                       count, gamma, mean, invstd, dgamma, dbeta, gscale, coef);
     SCD_RETURN_LAUNCH();
 }
 

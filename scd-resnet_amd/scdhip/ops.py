@@ -262,7 +262,8 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None):
     nrep = _allreduce_stats(stats, C)
     coef = torch.empty(3 * C, device=y.device)
     L.call("scd_bn_bwd_finalize", ptr(stats), nrep, C, float(st.count), ptr(bn.weight), ptr(st.mean),
-           ptr(st.invstd), ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), ptr(coef), stream())
+           ptr(st.invstd), ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), 1.0 / bn_sync_world(), ptr(coef),
+           stream())
     dy = torch.empty_like(y)
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), ptr(coef), C, y.numel(), ptr(dy), ptr(dz_out),
            stream())

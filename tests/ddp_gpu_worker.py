@@ -1,0 +1,50 @@
+"""One rank of the GPU data-parallel parity test (F7): 2 ranks share cuda:0 over gloo (RCCL cannot
+put two ranks on one device; the 8-GPU RCCL path is the same code with backend "nccl").
+Checks SyncBN statistics + FlatDDP gradient averaging against the reference's golden vectors."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import trainer.model.centerOffsetRes10 as plugin
+    from oracle import centernet as O
+    from oracle import targets as T
+    from scdhip import ops
+    from scdhip.flat import FlatDDP
+
+    g = np.load(os.path.join(REPO, "tests", "golden", "ddp.npz"))
+    entries, _ = O.model_spec(10)
+    m = plugin.model(**plugin.modelParams)
+    m.load_state_dict(O.hash_weights(entries))
+    m = m.cuda().train().set_compute_dtype(torch.float32)
+    ops.set_bn_sync(dist.group.WORLD)
+    ddp = FlatDDP(m)
+    x = T.batch_inputs(8, 4, 128)[2 * rank:2 * rank + 2].cuda()
+    ys = [y[2 * rank:2 * rank + 2].cuda() for y in T.batch_targets(9, 4, 32)]
+    loss, _ = plugin.loss(ddp(x, decode=False), ys)
+    loss.mean().backward()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(loss.item(), float(g["loss_r%d" % rank]), rtol=2e-4)
+    for k, p in m.named_parameters():
+        np.testing.assert_allclose(p.grad.double().norm().item(), float(g["gnorm|" + k]), rtol=1e-2, atol=1e-6,
+                                   err_msg=k)
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith("rs|"):
+            np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    dist.barrier()
+    dist.destroy_process_group()
+    print("OK rank", rank)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

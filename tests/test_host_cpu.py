@@ -1,0 +1,156 @@
+"""CPU tests of the product's host side: C-ABI library surface, plugin/state_dict interchange,
+reference initialisation, synthetic data vs the oracle's restatement, config/CLI semantics,
+the no-CPU-fallback rule, and the data-parallel wrapper's logic (gloo, world size 2)."""
+import os
+import re
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import centernet as O
+from oracle import targets as T
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "scdhip.h")
+
+
+def header_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(scd_\w+)\(", src, re.M)))
+
+
+def test_lib_loads_and_exports_every_header_symbol():
+    import scdhip.lib as L
+    lib = L.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(lib.dll, s)]
+    assert not missing, missing
+    assert sorted(L.SIGNATURES) == syms, "ctypes signatures out of sync with include/scdhip.h"
+    assert lib.dll.scd_version().startswith(b"libscdhip")
+
+
+def test_gemm_phase_struct_matches_header():
+    import ctypes
+
+    import scdhip.lib as L
+    m = re.search(r"#define SCD_MAX_TAPS (\d+)", open(HEADER).read())
+    assert int(m.group(1)) == L.MAX_TAPS
+    assert ctypes.sizeof(L.GemmPhase) == 4 * (5 + 3 * L.MAX_TAPS)
+
+
+def test_workspace_queries():
+    import scdhip.lib as L
+    assert L.lib().scd_conv_wgrad_workspace(128, 9, 64, 4) == 4 * 128 * 9 * 64 * 4
+    assert L.lib().scd_decode_workspace(2, 16384) == 2 * 16384 * 4
+    od = L.int_array([1, 4, 2])
+    assert L.lib().scd_heads_bwd_accsize(3, 128, od) == L.STAT_REPLICAS * (7 * 128 + 7 + 384) * 8
+
+
+@pytest.mark.parametrize("name", ["centerOffsetRes10", "centerOffsetRes18", "centerOffsetRes50",
+                                  "centerOffsetRes10h"])
+def test_plugin_state_dict_matches_reference_layout(name):
+    import importlib
+    plugin = importlib.import_module("trainer.model." + name)
+    for attr in ("model", "loss", "modelParams", "evaluation", "expression"):
+        assert hasattr(plugin, attr)
+    m = plugin.model(**plugin.modelParams)
+    entries, _ = O.model_spec(plugin.modelParams["numLayers"], plugin.modelParams["dims"],
+                              head_dim=m.HEAD_DIM)
+    sd = m.state_dict()
+    assert list(sd.keys()) == [k for k, _ in entries]
+    assert all(tuple(sd[k].shape) == tuple(s) for k, s in entries)
+
+
+def test_reference_initialisation_reproduced(golden):
+    """F0: the plugin under the reference's import-order seed draws the reference's weights."""
+    import trainer.model.centerOffsetRes10 as plugin
+    g = golden("init")
+    torch.random.manual_seed(42)
+    m = plugin.model(**plugin.modelParams)
+    assert sum(p.numel() for p in m.parameters()) == int(g["param_count"])
+    for k, v in m.state_dict().items():
+        v = v.double()
+        np.testing.assert_allclose(v.sum().item(), float(g[k + "|sum"]), rtol=1e-6, atol=1e-6, err_msg=k)
+        np.testing.assert_allclose((v * v).sum().item(), float(g[k + "|sumsq"]), rtol=1e-6, atol=1e-9, err_msg=k)
+        np.testing.assert_array_equal(v.reshape(-1)[:4].float().numpy(), g[k + "|head"])
+
+
+def test_synthetic_dataset_matches_oracle_rendering():
+    from trainer.dataset.syntheticSCD import SCD, encode_targets, sample_objects
+    rs1, rs2 = np.random.RandomState(5), np.random.RandomState(5)
+    for _ in range(20):
+        locs = sample_objects(rs1)
+        ref_locs = T.random_locs(rs2)
+        np.testing.assert_array_equal(locs, ref_locs)
+        got = encode_targets(locs)
+        ref = T.render(ref_locs)
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b)
+    ds = SCD(None, True)
+    item = ds[3]
+    assert item["xs"][0].shape == (1, 512, 512) and item["xs"][0].dtype == torch.float32
+    heat, mask, regr, inds = item["ys"]
+    assert heat.shape == (1, 128, 128) and mask.dtype == torch.bool and regr.shape == (30, 6)
+    assert inds.dtype == torch.int64 and int(inds.max()) < 128 * 128
+    assert float(heat.max()) == 1.0                      # every centre is an exact positive
+    vs = ds.getValidationSet(batch=32)
+    assert len(vs) == 2 and vs[0]["ys"][3].shape == (32, 30, 8)
+
+
+def test_configuration_overlay_and_format():
+    from configuration import Configuration
+    c = Configuration()
+    c.updateConfig({"modelName": "centerOffsetRes10", "datasetName": "syntheticSCD", "trainName": "t",
+                    "notAKey": 1, "batchSize": 4})
+    assert "notAKey" not in c.config
+    assert c.batchSize == 4
+    assert c.dirModel == "trainer.model.centerOffsetRes10"
+    assert c.dirData == "trainer.dataset.syntheticSCD"
+    assert c.naming == "centerOffsetRes10.t.0.pth"
+    assert c.useGPU  # bound method, always truthy (reference quirk, configuration.py:147-148)
+
+
+def test_train_cli_accepts_both_local_rank_spellings():
+    import train
+    assert train.parseArguments(["cfg.json", "-gpu", "--local_rank", "3"]).localRank == 3
+    a = train.parseArguments(["cfg.json", "--local-rank", "2"])
+    assert a.localRank == 2 and a.useGPU is False
+
+
+def test_no_cpu_fallback():
+    import trainer.model.centerOffsetRes10 as plugin
+    m = plugin.model(**plugin.modelParams)
+    with pytest.raises(RuntimeError, match="MI355X"):
+        m(torch.zeros(1, 1, 64, 64), decode=False)
+    from models.networkFactory import NetworkFactory
+    with pytest.raises(RuntimeError, match="MI355X"):
+        NetworkFactory(False)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_flat_ddp_gloo_world2():
+    """FlatDDP semantics with 2 gloo ranks on CPU: initial broadcast, averaged gradients equal to
+    the full-batch gradient, buffer broadcast, `module.` state_dict prefix."""
+    worker = os.path.join(REPO, "tests", "ddp_cpu_worker.py")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2",
+               PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, "scd-resnet_amd")]))
+    procs = [subprocess.Popen([sys.executable, worker], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT) for r in range(2)]
+    outs = []
+    for p in procs:
+        out, _ = p.communicate(timeout=240)
+        outs.append(out.decode())
+        assert p.returncode == 0, out.decode()
+    assert all("OK" in o for o in outs), outs
