@@ -166,7 +166,8 @@ int scd_adam_step(float* p, const float* g, float* m, float* v, long n, float lr
  * dir: 0 top (max over k>=h), 1 bottom (k<=h), 2 left (k>=w), 3 right (k<=w); NHWC dtype.
  * Backward routes grad to the running argmax, ties keep the first-scanned index
  * (strict '>' update, topPool.cpp:61-65). */
-int scd_cpool_fwd(int dtype, int dir, const void* x, void* y, int N, int H, int W, int C, void* stream);
+int scd_cpool_fwd(int dtype, int dir, const void* x, const void* addend, void* y, int N, int H, int W, int C,
+                  void* stream);                     /* y = pool(x) (+ addend, nullable: the CornerPool branch sum) */
 int scd_cpool_bwd(int dtype, int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C,
                   void* stream);
 

@@ -106,3 +106,23 @@ def batch_inputs(seed, batch, size=512):
     """N(0,1) fp32 tiles, (B,1,S,S) -- the post-`normalize` distribution (argumentations.py:40-44)."""
     rs = np.random.RandomState(seed)
     return torch.from_numpy(rs.standard_normal((batch, 1, size, size)).astype(np.float32))
+
+
+def corner_targets(seed, batch, size=HEATMAPSIZE):
+    """[heat, mask, regr, tl, br] for CornerNetLoss (ys[0], ys[3], ys[4]; cornerNetCPool.py:252-254).
+    The reference has no corner target encoder; the rule used for F8 and the synthetic corner
+    dataset: corners at centre -/+ (round |major_x|, round minor), clipped, Gaussian as the centre."""
+    rs = np.random.RandomState(seed)
+    cols = []
+    for _ in range(batch):
+        locs = random_locs(rs, size=size)
+        h, m, rg, _ = render(locs, size)
+        tl, br = locs.copy(), locs.copy()
+        dx = np.round(np.abs(locs[:, 4])).astype(np.float32)
+        dy = np.round(locs[:, 6]).astype(np.float32)
+        tl[:, 0] = np.clip(locs[:, 0] - dx, 0, size - 1)
+        tl[:, 1] = np.clip(locs[:, 1] - dy, 0, size - 1)
+        br[:, 0] = np.clip(locs[:, 0] + dx, 0, size - 1)
+        br[:, 1] = np.clip(locs[:, 1] + dy, 0, size - 1)
+        cols.append((h, m, rg, render(tl, size)[0], render(br, size)[0]))
+    return [torch.from_numpy(np.stack([c[i] for c in cols])) for i in range(5)]

@@ -12,7 +12,7 @@ namespace {
 
 // dir: 0 top (scan h descending), 1 bottom (h ascending), 2 left (w descending), 3 right (w ascending)
 template <typename T>
-__global__ void cpool_fwd_kernel(int dir, const T* x, T* y, int N, int H, int W, int C) {
+__global__ void cpool_fwd_kernel(int dir, const T* x, const T* addend, T* y, int N, int H, int W, int C) {
     constexpr int E = Vec16<T>::N;
     const int cpp = C / E;
     const bool vert = dir < 2;
@@ -34,7 +34,15 @@ __global__ void cpool_fwd_kernel(int dir, const T* x, T* y, int N, int H, int W,
             Vec16<T>::load(x + base + pos * step, v);
 #pragma unroll
             for (int e = 0; e < E; ++e) m[e] = (k == 0) ? v[e] : fmaxf(m[e], v[e]);
-            Vec16<T>::store(y + base + pos * step, m);
+            if (addend) {
+                float a[E], o[E];
+                Vec16<T>::load(addend + base + pos * step, a);
+#pragma unroll
+                for (int e = 0; e < E; ++e) o[e] = m[e] + a[e];
+                Vec16<T>::store(y + base + pos * step, o);
+            } else {
+                Vec16<T>::store(y + base + pos * step, m);
+            }
         }
     }
 }
@@ -82,7 +90,8 @@ inline int ew_blocks(long n) { return (int)std::min<long>(4096, std::max<long>(1
 
 }  // namespace
 
-extern "C" int scd_cpool_fwd(int dtype, int dir, const void* x, void* y, int N, int H, int W, int C, void* stream) {
+extern "C" int scd_cpool_fwd(int dtype, int dir, const void* x, const void* addend, void* y, int N, int H, int W, int C,
+                             void* stream) {
     if (dir < 0 || dir > 3) return SCD_ERR_ARG;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
@@ -90,10 +99,10 @@ extern "C" int scd_cpool_fwd(int dtype, int dir, const void* x, void* y, int N, 
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((cpool_fwd_kernel<__bf16>), dim3(ew_blocks(lines)), dim3(256), 0, st, dir, (const __bf16*)x,
-                           (__bf16*)y, N, H, W, C);
+                           (const __bf16*)addend, (__bf16*)y, N, H, W, C);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((cpool_fwd_kernel<float>), dim3(ew_blocks(lines)), dim3(256), 0, st, dir, (const float*)x,
-                           (float*)y, N, H, W, C);
+                           (const float*)addend, (float*)y, N, H, W, C);
     else
         return SCD_ERR_ARG;
     SCD_RETURN_LAUNCH();

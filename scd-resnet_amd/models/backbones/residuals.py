@@ -74,6 +74,12 @@ def _is_plain_head(m):
             and m[0].kernel_size == (3, 3) and m[0].bias is not None and m[2].kernel_size == (1, 1))
 
 
+def _is_corner_head(m):
+    """Sequential(CornerPool, Conv2d 3x3 +bias, ReLU, Conv2d 1x1): the CornerNet TL/BR terminal."""
+    return (isinstance(m, torch.nn.Sequential) and len(m) == 4 and hasattr(m[0], "dirs")
+            and _is_plain_head(torch.nn.Sequential(m[1], m[2], m[3])))
+
+
 class ResNet(torch.nn.Module):
     """ResNet(inputDimension, block, layers, preprocess, terminals, decoder, dimensions) -- residuals.py:184-353.
 
@@ -193,6 +199,12 @@ class ResNet(torch.nn.Module):
                     ret[n] = blocks.HeadsFn.apply(feat, m[0].weight, [m])[0]
         for n, m in zip(names, mods):
             if n in ret:
+                continue
+            if _is_corner_head(m):
+                # CornerNet terminal: CornerPool -> Conv3x3+bias -> ReLU -> Conv1x1 (cornerNetCPool.py:163-199)
+                cp = m[0]
+                h = blocks.CornerPoolFn.apply(feat, cp.branch1.conv.weight, cp, cp.dirs)
+                ret[n] = blocks.HeadsFn.apply(h, m[1].weight, [(m[1], m[2], m[3])])[0]
                 continue
             if self.terminals[n].process is None:
                 Logger.err("Processor function of the terminal '{}' is not implemented.".format(n))

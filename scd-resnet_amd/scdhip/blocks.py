@@ -282,6 +282,60 @@ class HeadsFn(torch.autograd.Function):
         return dfeat, None, None
 
 
+class CornerPoolFn(torch.autograd.Function):
+    """CornerPool module (cornerNetCPool.py:83-122) on NHWC activations:
+    a_i = relu(bn(conv3x3(x)))  (branch1/2, Convolution);  s = pool1(a1) + pool2(a2)
+    r = relu(bn(conv3x3(s)) + bn(conv1x1(x)));  out = relu(bn(conv3x3(r)))  (lastConv)."""
+
+    @staticmethod
+    def forward(ctx, x, w_anchor, mod, dirs):
+        tr = mod.branchMergeBn.training
+        b1, b2, lc = mod.branch1, mod.branch2, mod.lastConv
+        y1, st1 = _train_bn_conv(x, b1.conv, b1.bn, 1, 1, tr)
+        a1 = ops.bn_apply(y1, st1, True)
+        y2, st2 = _train_bn_conv(x, b2.conv, b2.bn, 1, 1, tr)
+        a2 = ops.bn_apply(y2, st2, True)
+        p1 = ops.cpool_fwd(a1, dirs[0])
+        s = ops.cpool_fwd(a2, dirs[1], addend=p1)
+        del p1
+        ym, stm = _train_bn_conv(s, mod.branchMerge, mod.branchMergeBn, 1, 1, tr)
+        ysc, sts = _train_bn_conv(x, mod.shortcutConv, mod.shortcutBn, 1, 0, tr)
+        r = ops.bn_apply(ym, stm, True, res=ysc, rst=sts)
+        yl, stl = _train_bn_conv(r, lc.conv, lc.bn, 1, 1, tr)
+        out = ops.bn_apply(yl, stl, True)
+        ctx.save_for_backward(x, y1, a1, y2, a2, s, ym, ysc, r, yl, out)
+        ctx.sts = (st1, st2, stm, sts, stl)
+        ctx.mod, ctx.dirs = mod, dirs
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y1, a1, y2, a2, s, ym, ysc, r, yl, out = ctx.saved_tensors
+        st1, st2, stm, sts, stl = ctx.sts
+        mod, dirs = ctx.mod, ctx.dirs
+        N, H, W, C = x.shape
+        lc = mod.lastConv
+        dyl = ops.bn_backward(lc.bn, stl, _c(dout), yl, mask=out)
+        ops.conv_wgrad(dyl, r, 3, 3, 1, 1, ops.grad_of(lc.conv.weight), _conv_ld(lc.conv.weight))
+        dr = ops.conv_dgrad(dyl, ops.pack_weight(lc.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1)
+        dym = ops.bn_backward(mod.branchMergeBn, stm, dr, ym, mask=r)
+        dys = ops.bn_backward(mod.shortcutBn, sts, dr, ysc, mask=r)
+        wsc = mod.shortcutConv.weight
+        ops.conv_wgrad(dys, x, 1, 1, 1, 0, ops.grad_of(wsc), _conv_ld(wsc))
+        dx = ops.conv_dgrad(dys, ops.pack_weight(wsc, x.dtype, 1), C, H, W, 1, 1, 1, 0)
+        wm = mod.branchMerge.weight
+        ops.conv_wgrad(dym, s, 3, 3, 1, 1, ops.grad_of(wm), _conv_ld(wm))
+        Cb = wm.shape[1]
+        ds = ops.conv_dgrad(dym, ops.pack_weight(wm, x.dtype, 1), Cb, H, W, 3, 3, 1, 1)
+        for (a, y, st, br), d in zip(((a1, y1, st1, mod.branch1), (a2, y2, st2, mod.branch2)), dirs):
+            da = ops.cpool_bwd(a, ds, d)
+            dy = ops.bn_backward(br.bn, st, da, y, mask=a)
+            ops.conv_wgrad(dy, x, 3, 3, 1, 1, ops.grad_of(br.conv.weight), _conv_ld(br.conv.weight))
+            ops.conv_dgrad(dy, ops.pack_weight(br.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1, out=dx,
+                           accumulate=True)
+        return dx, None, None, None
+
+
 class CPoolFn(torch.autograd.Function):
     """Directional corner pool (TopPoolFunction etc., cornerPooling/__init__.py:8-58) on NHWC."""
 
@@ -290,6 +344,7 @@ class CPoolFn(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.direction = direction
         return ops.cpool_fwd(x, direction)
+
 
     @staticmethod
     def backward(ctx, dy):

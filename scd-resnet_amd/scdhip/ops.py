@@ -308,10 +308,11 @@ def stem_pool_bwd(dout, am, y, st):
     return dz
 
 
-def cpool_fwd(x, direction):
+def cpool_fwd(x, direction, addend=None):
+    """directional corner pool (NHWC); y = pool(x) + addend when given."""
     N, H, W, C = x.shape
     y = torch.empty_like(x)
-    L.call("scd_cpool_fwd", dt(x), direction, ptr(x), ptr(y), N, H, W, C, stream())
+    L.call("scd_cpool_fwd", dt(x), direction, ptr(x), ptr(addend), ptr(y), N, H, W, C, stream())
     return y
 
 

@@ -1,0 +1,152 @@
+"""CornerNet-with-corner-pooling path (config 4) on the HIP kernels, against the reference's
+golden vectors (F5: the reference's own C++ pools; F8: CornerNetResidual(10) forward + loss,
+both from tests/golden/make_golden_corner.py) and the CPU oracle (oracle/cornernet.py).
+
+Tolerances: pools are bit-exact (a max is exact in any dtype); fp32 model outputs 1e-3 (the
+north-star tolerance), loss 1e-4 relative; CornerPool gradients vs oracle autograd 2e-3 of the
+gradient's max magnitude (fp32 MFMA accumulation order differs from the CPU conv)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import centernet as O
+from oracle import cornernet as OC
+from oracle import cpool as OP
+from oracle import targets as T
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _nhwc(t, dtype=torch.float32):
+    return t.permute(0, 2, 3, 1).contiguous().to(DEV, dtype)
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2).float().cpu()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_f5_cpool_forward_bit_exact(golden, dtype):
+    from scdhip import ops
+    g = golden("cpool")
+    for src, pre in (("x", "y"), ("xt", "yt")):
+        x = torch.from_numpy(g[src])
+        if dtype == torch.bfloat16:                 # bf16 vectors are 8 channels wide: C=4 -> 8
+            x = torch.cat([x, -x], 1)
+        xd = _nhwc(x, dtype)
+        for d in range(4):
+            ref = OP.forward(xd.float().cpu().permute(0, 3, 1, 2), d)
+            y = _nchw(ops.cpool_fwd(xd, d))
+            np.testing.assert_array_equal(y.numpy(), ref.numpy())
+            if dtype == torch.float32:
+                np.testing.assert_array_equal(y.numpy(), g["%s%d" % (pre, d)])
+    for d in range(4):                              # bf16 ragged shapes
+        x = torch.randn(2, 7, 13, 64, device=DEV).to(torch.bfloat16)
+        ref = OP.forward(x.float().cpu().permute(0, 3, 1, 2), d).permute(0, 2, 3, 1)
+        np.testing.assert_array_equal(ops.cpool_fwd(x, d).float().cpu().numpy(), ref.numpy())
+
+
+def test_cpool_forward_addend_and_ragged_sizes():
+    from scdhip import ops
+    torch.manual_seed(0)
+    for (N, H, W, C) in [(1, 1, 1, 64), (2, 7, 13, 64), (1, 33, 5, 128), (3, 128, 128, 128)]:
+        x = torch.randn(N, H, W, C, device=DEV)
+        a = torch.randn_like(x)
+        for d in range(4):
+            ref = OP.forward(x.cpu().permute(0, 3, 1, 2), d).permute(0, 2, 3, 1) + a.cpu()
+            np.testing.assert_array_equal(ops.cpool_fwd(x, d, addend=a).cpu().numpy(), ref.numpy())
+
+
+@pytest.mark.parametrize("ties", [False, True])
+def test_cpool_backward_matches_oracle_tie_rule(ties):
+    from scdhip import ops
+    torch.manual_seed(1)
+    for (N, H, W, C) in [(2, 9, 7, 64), (1, 128, 128, 128)]:
+        x = torch.randint(0, 3, (N, H, W, C)).float() if ties else torch.randn(N, H, W, C)
+        dy = torch.randn(N, H, W, C)
+        for d in range(4):
+            ref = OP.backward(x.permute(0, 3, 1, 2).double(), dy.permute(0, 3, 1, 2).double(), d)
+            got = ops.cpool_bwd(x.to(DEV), dy.to(DEV), d).cpu().permute(0, 3, 1, 2).double()
+            np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def _model(dtype=torch.float32):
+    import trainer.model.cornerNetCPool as plugin
+    entries, topo = OC.model_spec(10)
+    state = OC.hash_weights(entries)
+    m = plugin.model(**plugin.modelParams)
+    m.load_state_dict(state)
+    return m.to(DEV).train().set_compute_dtype(dtype), plugin, state, topo
+
+
+def test_f8_cornernet_forward_and_loss(golden):
+    g = golden("corner")
+    m, plugin, _, _ = _model()
+    x = T.batch_inputs(31, 2, 128).to(DEV)
+    ys = [torch.from_numpy(g["ys|" + n]).to(DEV) for n in ["heat", "mask", "regr", "tl", "br"]]
+    outs = m(x, decode=False)
+    for k in ("heatmap", "tl", "br"):
+        np.testing.assert_allclose(outs[0][k].detach().cpu().numpy(), g[k], rtol=1e-3, atol=1e-3, err_msg=k)
+    loss, stats = plugin.loss(outs, ys)
+    assert stats == {}
+    np.testing.assert_allclose(loss.detach().cpu().numpy(), g["loss"], rtol=1e-4)
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith("rs|"):
+            np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def test_cornernet_gradients_match_oracle():
+    """Full backward (corner pools, merge/shortcut BN, tails, backbone) vs oracle autograd."""
+    m, plugin, state, topo = _model()
+    P, Bf = O.split_state(state)
+    P = {k: v.requires_grad_(True) for k, v in P.items()}
+    x = T.batch_inputs(41, 2, 128)
+    ys = T.corner_targets(42, 2, 32)
+    outs = OC.forward(P, Bf, x, topo)
+    OC.cornernet_loss(outs, ys).sum().backward()
+    m.zero_grad(set_to_none=False)
+    loss, _ = plugin.loss(m(x.to(DEV), decode=False), [y.to(DEV) for y in ys])
+    loss.sum().backward()
+    torch.cuda.synchronize()
+    names = dict(m.named_parameters())
+    bad = []
+    for k, v in P.items():
+        gr, gg = v.grad, names[k].grad.cpu()
+        scale = gr.abs().max().item() + 1e-12
+        err = (gg - gr).abs().max().item() / scale
+        if err > 2e-3:
+            bad.append((k, err))
+    assert not bad, bad[:8]
+
+
+def test_cornernet_bf16_train_steps_reduce_loss():
+    from models.networkFactory import NetworkFactory  # noqa: F401  (plugin surface import check)
+    from scdhip.flat import FlatAdam
+    m, plugin, _, _ = _model(torch.bfloat16)
+    x = T.batch_inputs(51, 4, 512).to(DEV)
+    ys = [y.to(DEV) for y in T.corner_targets(52, 4, 128)]
+    opt = FlatAdam(m.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(6):
+        opt.zero_grad()
+        loss, _ = plugin.loss(m(x, decode=False), ys)
+        loss.sum().backward()
+        opt.step()
+        losses.append(loss.item())
+    assert np.isfinite(losses).all()
+    assert losses[-1] < losses[0], losses
+
+
+def test_decode_cornernet_three_maps():
+    from models.cornerNetCPool import decodeCornerNet
+    rs = np.random.RandomState(5)
+    od = {k: torch.from_numpy((rs.standard_normal((2, 1, 128, 128)) * 3).astype(np.float32)).to(DEV)
+          for k in ("heatmap", "tl", "br")}
+    dec = decodeCornerNet(od)
+    assert len(dec) == 13 and dec[-1] is od
+    for i, k in enumerate(("heatmap", "tl", "br")):
+        ref = O.decode({"heatmap": od[k].cpu(), "regr": torch.zeros(2, 4, 128, 128),
+                        "offset": torch.zeros(2, 2, 128, 128)})
+        np.testing.assert_allclose(dec[4 * i].cpu().numpy(), ref[0].numpy(), rtol=1e-6, atol=1e-7)

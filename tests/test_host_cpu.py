@@ -102,6 +102,31 @@ def test_synthetic_dataset_matches_oracle_rendering():
     assert len(vs) == 2 and vs[0]["ys"][3].shape == (32, 30, 8)
 
 
+def test_cornernet_plugin_layout_and_dataset():
+    """config 4: the cornerNetCPool plugin's state_dict matches the reference module tree (oracle
+    spec, checked against the reference in F8) and the corner dataset renders the oracle's rule."""
+    import trainer.model.cornerNetCPool as plugin
+    from oracle import cornernet as OC
+    from trainer.dataset.syntheticCorner import corner_locs
+    from trainer.dataset.syntheticSCD import encode_targets, sample_objects
+    for attr in ("model", "loss", "modelParams", "evaluation", "expression"):
+        assert hasattr(plugin, attr)
+    sd = plugin.model(**plugin.modelParams).state_dict()
+    entries, _ = OC.model_spec(10)
+    assert list(sd.keys()) == [k for k, _ in entries]
+    assert all(tuple(sd[k].shape) == tuple(s) for k, s in entries)
+    got = []
+    rs = np.random.RandomState(32)
+    for _ in range(2):
+        locs = sample_objects(rs, 32)
+        tl, br = corner_locs(locs, 32)
+        got.append((encode_targets(tl, 32)[0], encode_targets(br, 32)[0]))
+    ref = T.corner_targets(32, 2, 32)
+    for b in range(2):
+        np.testing.assert_array_equal(got[b][0], ref[3][b].numpy())
+        np.testing.assert_array_equal(got[b][1], ref[4][b].numpy())
+
+
 def test_configuration_overlay_and_format():
     from configuration import Configuration
     c = Configuration()

@@ -159,3 +159,57 @@ def test_f7_ddp_syncbn(spec, golden):
     np.testing.assert_allclose(losses[1].item(), g["loss_r1"], rtol=1e-4)
     for k, v in P.items():
         np.testing.assert_allclose(v.grad.double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7)
+
+
+# ---------------------------------------------------------------- CornerNet (F5, F8)
+
+def test_f5_cpool_forward_matches_reference_cpp(golden):
+    from oracle import cpool
+    g = golden("cpool")
+    for d in range(4):
+        np.testing.assert_array_equal(cpool.forward(torch.from_numpy(g["x"]), d).numpy(), g["y%d" % d])
+        np.testing.assert_array_equal(cpool.forward(torch.from_numpy(g["xt"]), d).numpy(), g["yt%d" % d])
+
+
+def test_cpool_backward_restatement_matches_autograd_when_tie_free():
+    from oracle import cpool
+    x = torch.randn(2, 3, 9, 7, dtype=torch.float64)
+    dy = torch.randn_like(x)
+    for d in range(4):
+        xr = x.clone().requires_grad_(True)
+        cpool.forward(xr, d).backward(dy)
+        np.testing.assert_allclose(cpool.backward(x, dy, d).numpy(), xr.grad.numpy(), rtol=1e-12, atol=1e-12)
+
+
+def test_cpool_backward_tie_rule():
+    """ties keep the first-scanned position (strict '>' update, topPool.cpp:61-65)."""
+    from oracle import cpool
+    x = torch.tensor([[[[1.0], [2.0], [2.0], [0.0]]]])     # H=4, W=1
+    dy = torch.ones_like(x)
+    # top pool scans h = 3,2,1,0: the max 2.0 is first seen at h=2 -> h=2 collects rows 0,1,2
+    np.testing.assert_array_equal(cpool.backward(x, dy, 0).reshape(-1).numpy(), [0, 0, 3, 1])
+    # bottom pool scans h = 0,1,2,3: first seen at h=1 -> h=1 collects rows 1,2,3
+    np.testing.assert_array_equal(cpool.backward(x, dy, 1).reshape(-1).numpy(), [1, 3, 0, 0])
+
+
+def test_f8_cornernet_forward_and_loss(golden):
+    from oracle import cornernet as OC
+    g = golden("corner")
+    entries, topo = OC.model_spec(10)
+    P, Bf = O.split_state(OC.hash_weights(entries))
+    with torch.no_grad():
+        out = OC.forward(P, Bf, T.batch_inputs(31, 2, 128), topo)
+    for k in ("heatmap", "tl", "br"):
+        np.testing.assert_allclose(out[k].numpy(), g[k], rtol=1e-4, atol=1e-4, err_msg=k)
+    ys = [torch.from_numpy(g["ys|" + n]) for n in ["heat", "mask", "regr", "tl", "br"]]
+    np.testing.assert_allclose(OC.cornernet_loss(out, ys).numpy(), g["loss"], rtol=1e-4)
+    for k in g.files:
+        if k.startswith("rs|"):
+            np.testing.assert_allclose(Bf[k[3:]].numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def test_f8_corner_targets_rule(golden):
+    g = golden("corner")
+    ys = T.corner_targets(32, 2, 32)
+    for i, n in enumerate(["heat", "mask", "regr", "tl", "br"]):
+        np.testing.assert_array_equal(ys[i].numpy(), g["ys|" + n])
