@@ -97,28 +97,55 @@ def test_f8_cornernet_forward_and_loss(golden):
             np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
 
 
-def test_cornernet_gradients_match_oracle():
-    """Full backward (corner pools, merge/shortcut BN, tails, backbone) vs oracle autograd."""
-    m, plugin, state, topo = _model()
+def _oracle_grads(state, topo, x, ys, dt, eps=0.0, seed=0):
     P, Bf = O.split_state(state)
-    P = {k: v.requires_grad_(True) for k, v in P.items()}
+    g = torch.Generator().manual_seed(seed)
+    P = {k: (v * (1 + eps * torch.randn(v.shape, generator=g))).to(dt).requires_grad_(True) for k, v in P.items()}
+    Bf = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in Bf.items()}
+    ys = [y.to(dt) if y.is_floating_point() else y for y in ys]
+    OC.cornernet_loss(OC.forward(P, Bf, x.to(dt), topo), ys).sum().backward()
+    return {k: v.grad.double() for k, v in P.items()}
+
+
+def _errs(g, ref):
+    out = {}
+    for k, r in ref.items():
+        out[k] = ((g[k] - r).abs().max().item() / (r.abs().max().item() + 1e-30),
+                  ((g[k] - r).norm() / (r.norm() + 1e-30)).item())
+    return out
+
+
+def test_cornernet_gradients_match_oracle():
+    """Full backward (corner pools, merge/shortcut BN, tails, backbone) against the oracle in fp64.
+
+    The corner-pool gradient is piecewise: it follows the argmax of every scan, and after
+    top+left pooling whole regions share one value, so ulp-level changes anywhere upstream move
+    some argmaxes (tests/test_corner_gpu.py history: scaling the fp32 oracle's weights by
+    1+1e-7*N moves preprocess.0.weight's gradient by 1.1e-2 and tl.0.branch1's by 17%).  The HIP
+    path is therefore held to the spread of the reference's own fp32 computation: for every
+    parameter its error against fp64 must not exceed the worst of four fp32 oracle runs (exact
+    weights and three 1e-7-perturbed copies) by more than 3x + 2e-3 (max-abs) / 1.5x + 1e-3
+    (norm); BR and the heads, which are well conditioned here, land at ~1e-6."""
+    m, plugin, state, topo = _model()
     x = T.batch_inputs(41, 2, 128)
     ys = T.corner_targets(42, 2, 32)
-    outs = OC.forward(P, Bf, x, topo)
-    OC.cornernet_loss(outs, ys).sum().backward()
-    m.zero_grad(set_to_none=False)
+    g64 = _oracle_grads(state, topo, x, ys, torch.float64)
+    spread = [_errs(_oracle_grads(state, topo, x, ys, torch.float32, e, sd), g64)
+              for e, sd in ((0.0, 0), (1e-7, 1), (1e-7, 2), (1e-7, 3))]
     loss, _ = plugin.loss(m(x.to(DEV), decode=False), [y.to(DEV) for y in ys])
     loss.sum().backward()
     torch.cuda.synchronize()
     names = dict(m.named_parameters())
+    hip = _errs({k: names[k].grad.cpu().double() for k in g64}, g64)
     bad = []
-    for k, v in P.items():
-        gr, gg = v.grad, names[k].grad.cpu()
-        scale = gr.abs().max().item() + 1e-12
-        err = (gg - gr).abs().max().item() / scale
-        if err > 2e-3:
-            bad.append((k, err))
+    for k in g64:
+        lim_max = 3 * max(s[k][0] for s in spread) + 2e-3
+        lim_norm = 1.5 * max(s[k][1] for s in spread) + 1e-3
+        if hip[k][0] > lim_max or hip[k][1] > lim_norm:
+            bad.append((k, hip[k], lim_max, lim_norm))
     assert not bad, bad[:8]
+    for k in ("br.0.branch1.conv.weight", "br.0.lastConv.conv.weight", "br.3.weight", "heatmap.2.weight"):
+        assert hip[k][0] < 1e-3, (k, hip[k])
 
 
 def test_cornernet_bf16_train_steps_reduce_loss():

@@ -29,3 +29,21 @@ for name, cls, dirs in (("tl", M.TopLeftPool, (0, 2)), ("br", M.BottomRightPool,
     for k, v in mod.named_parameters():
         r = P[name + ".0." + k].grad
         print("  %-28s %.2e" % (k, ((v.grad.cpu() - r).abs().max() / (r.abs().max() + 1e-30)).item()))
+
+# run-to-run determinism of the full model backward
+import trainer.model.cornerNetCPool as plugin
+from oracle import targets as T
+entries, topo = OC.model_spec(10); state = OC.hash_weights(entries)
+gs = []
+for rep in range(2):
+    m = plugin.model(**plugin.modelParams); m.load_state_dict(state)
+    m = m.cuda().train().set_compute_dtype(torch.float32)
+    x = T.batch_inputs(41, 2, 128); ys = T.corner_targets(42, 2, 32)
+    loss, _ = plugin.loss(m(x.cuda(), decode=False), [y.cuda() for y in ys])
+    loss.sum().backward(); torch.cuda.synchronize()
+    gs.append({k: v.grad.cpu().clone() for k, v in m.named_parameters()})
+for k in gs[0]:
+    d = (gs[0][k] - gs[1][k]).abs().max().item()
+    if d > 0:
+        print("nondet", k, d)
+print("determinism check done")
