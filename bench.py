@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--model", default="centerOffsetRes10")
-    ap.add_argument("--cpu-baseline-steps", type=int, default=4)
+    ap.add_argument("--cpu-baseline-steps", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -59,33 +59,48 @@ def cpu_baseline(steps):
                       "after 1 warm-up (%.1f s)" % (steps, dt)}
 
 
-def heads_gemm_roofline(model, feat_shape, dtype, reps=10):
-    """Time the dominant kernel -- the fused head conv3x3 GEMM (M=B*128*128, N=384, K=9*256) --
-    with HIP events on the stream it is launched on."""
+HEADS_KERNEL = "conv_gemm_kernel<bf16,128,128,heads>"
+
+
+def pmc_traffic(kernel, batch, dtype):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/r<N>_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this same bench command), or None when none matches this workload."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")),
+                   key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
+    for f in reversed(files):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("batch") == batch and d.get("dtype") == dtype and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["hbm_bytes"], os.path.relpath(f, REPO)
+    return None, None
+
+
+def heads_gemm_roofline(B, dtype_name, cin=256, hd=128, ods=(1, 4, 2)):
+    """The dominant kernel: the fused head GEMM (conv3x3 M=B*128*128, N=3*128, K=9*256, + bias/ReLU
+    + the three 1x1 tails in the epilogue), timed live by HIP events on its launch stream around
+    every launch inside the timed steps (scdhip.ops.LaunchTimer)."""
     from scdhip import ops
-    heads = [getattr(model, n) for n in ("heatmap", "regr", "offset")]
-    w0 = torch.cat([h[0].weight for h in heads], 0).detach()
-    b0 = torch.cat([h[0].bias for h in heads], 0).detach()
-    wp = ops.pack_weight(w0, dtype, 0)
-    feat = torch.randn(feat_shape, device="cuda").to(dtype)
-    out = torch.empty(feat_shape[0], feat_shape[1], feat_shape[2], w0.shape[0], device="cuda", dtype=dtype)
-    for _ in range(2):
-        ops.conv_fwd(feat, wp, w0.shape[0], 3, 3, 1, 1, bias=b0, relu=True, out=out)
-    s = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        ops.conv_fwd(feat, wp, w0.shape[0], 3, 3, 1, 1, bias=b0, relu=True, out=out)
-    e1.record(s)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    M = feat_shape[0] * feat_shape[1] * feat_shape[2]
-    flops = 2.0 * M * w0.shape[0] * (9 * feat_shape[3])
+    r = ops.LaunchTimer.mean_ms("heads_gemm")
+    if r is None:
+        return None
+    ms, n = r
+    M = B * 128 * 128
+    ct = hd * len(ods)
+    flops = 2.0 * M * (ct * 9 * cin + hd * sum(ods))
+    esz = 2 if dtype_name == "bf16" else 4
+    algo_bytes = M * cin * esz + M * ct * esz + M * sum(ods) * 4 + ct * 9 * cin * esz
     achieved = flops / (ms * 1e-3) / 1e12
-    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
-    return {"bound": "mfma", "kernel": "conv_gemm_kernel (fused head conv3x3, fwd)", "achieved": round(achieved, 1),
-            "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
-            "flop_per_launch": flops, "avg_launch_ms": round(ms, 4)}
+    peak = PEAK_BF16_TFLOPS if dtype_name == "bf16" else PEAK_F32_TFLOPS
+    traffic, src = pmc_traffic(HEADS_KERNEL if dtype_name == "bf16" else HEADS_KERNEL.replace("bf16", "f32"),
+                               B, dtype_name)
+    return {"bound": "mfma", "kernel": HEADS_KERNEL, "achieved": round(achieved, 1), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+            "traffic": None if traffic is None else round(traffic), "traffic_source": src,
+            "algorithmic_bytes": algo_bytes, "flop_per_launch": flops, "avg_launch_ms": round(ms, 4),
+            "launches_timed": n}
 
 
 def main():
@@ -134,6 +149,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ops.LaunchTimer.arm("heads_gemm")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -150,8 +166,7 @@ def main():
     if rank == 0:
         imgs = B * world * args.steps
         value = imgs / elapsed
-        inner = model.module if hasattr(model, "module") else model
-        roof = heads_gemm_roofline(inner, (B, 128, 128, 256), dtype)
+        roof = heads_gemm_roofline(B, args.dtype)
         step_frac = value * TRAIN_GFLOP_PER_IMG / 1e3 / (world * (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
                                                                   else PEAK_F32_TFLOPS))
         line = {

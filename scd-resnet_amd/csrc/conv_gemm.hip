@@ -47,7 +47,7 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool HEADS>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;       // elements per 16-B chunk
@@ -317,8 +317,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
             }
         }
     }
-    if constexpr (BN == 128) {
-        if (p.head_on) {
+    if constexpr (HEADS && BN == 128) {
+        {
             // fused terminal 1x1 (centerNetOffset.py:108-110): head = n-tile, hidden = staged tile.
             // thread -> (row = tid/2, half = tid&1): 64-channel partial dots, combined across the pair.
             const int h = nt;
@@ -616,7 +616,12 @@ __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cg, int T, 
 
 template <typename T, int BM, int BN>
 int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st) {
-    hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN>), dim3(Mtot_tiles), dim3(256), 0, st, p);
+    if (p.head_on) {
+        if constexpr (BN == 128) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, true>), dim3(Mtot_tiles), dim3(256), 0, st, p);
+        else return SCD_ERR_ARG;
+    } else {
+        hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false>), dim3(Mtot_tiles), dim3(256), 0, st, p);
+    }
     SCD_RETURN_LAUNCH();
 }
 

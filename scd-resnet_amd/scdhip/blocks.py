@@ -245,8 +245,10 @@ class HeadsFn(torch.autograd.Function):
         if Hd == 128 and len(heads) <= 4 and max(od) <= 4:
             # tails fused into the GEMM epilogue (one launch, hidden tensor read once)
             hid = torch.empty(N, H, W, Ct, device=feat.device, dtype=feat.dtype)
+            t0 = ops.LaunchTimer.record("heads_gemm")
             ops.L.call("scd_conv_gemm_heads", ops.dt(feat), ops.ptr(feat), ops.ptr(wp), ops.ptr(hid), ops.ptr(b0),
                        N, H, W, Cin, len(heads), odarr, w1s, b1s, optrs, ops.stream())
+            ops.LaunchTimer.close("heads_gemm", t0)
         else:
             hid = ops.conv_fwd(feat, wp, Ct, 3, 3, 1, 1, bias=b0, relu=True)
             ops.L.call("scd_heads_fwd", ops.dt(hid), ops.ptr(hid), N, H * W, len(heads), Hd, odarr, w1s, b1s, optrs,

@@ -36,6 +36,42 @@ def _need_gpu(*ts):
                                "restatement lives in oracle/ and is test infrastructure)")
 
 
+# ------------------------------------------------------------------ live kernel timing
+
+class LaunchTimer:
+    """HIP-event pairs recorded around selected launches on the stream they are issued on
+    (bench.py's roofline: the dominant kernel timed inside the timed steps).  Disabled unless
+    a name is armed, so the product path records nothing."""
+    armed = set()
+    events = {}
+
+    @classmethod
+    def arm(cls, name):
+        cls.armed.add(name)
+        cls.events[name] = []
+
+    @classmethod
+    def record(cls, name):
+        if name not in cls.armed:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
+
+    @classmethod
+    def close(cls, name, start):
+        if start is not None:
+            cls.events[name].append((start, cls.record(name)))
+
+    @classmethod
+    def mean_ms(cls, name):
+        ev = cls.events.get(name, [])
+        if not ev:
+            return None
+        ev[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev), len(ev)
+
+
 # ------------------------------------------------------------------ SyncBN / process group
 
 class _BNSync:

@@ -1,0 +1,20 @@
+# Usage: bash tools/gpu_round.sh <tag>  -- GPU tests, bench (with CPU baseline), rocprofv3 kernel
+# stats of the same bench command, and two PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-run}
+mkdir -p gpurun_out
+timeout -k 10 500 python -m pytest tests -x -q -m gpu > gpurun_out/tests_$TAG.log 2>&1; rc=$?
+tail -5 gpurun_out/tests_$TAG.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$?
+cat gpurun_out/bench_$TAG.json; tail -3 gpurun_out/bench_$TAG.err
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/profbench_$TAG.json 2> gpurun_out/prof_$TAG.err; rc=$?
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcf_$TAG -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcf_$TAG.json 2> gpurun_out/pmcf_$TAG.err; rc=$?
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcw_$TAG -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcw_$TAG.json 2> gpurun_out/pmcw_$TAG.err; rc=$?
+find gpurun_out/prof_$TAG gpurun_out/pmcf_$TAG gpurun_out/pmcw_$TAG -name "*.csv" | head -20
+exit $rc

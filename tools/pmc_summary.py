@@ -1,0 +1,53 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-kernel HBM bytes per launch.
+
+usage: python tools/pmc_summary.py <fetch counter_collection.csv> <write counter_collection.csv> out.json \
+       [batch dtype command]
+
+Corrections (MI355X_MICROARCH.md, HBM section): rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
+(derived from TCC_EA0_RDREQ / _WRREQ); on gfx950 FETCH_SIZE counts half the bytes of a wide
+coalesced read, so it is doubled; WRITE_SIZE is exact for 16-B streaming stores.  The two
+counters cannot share a pass (TCC slots), hence two runs of the same command.
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from prof_summary import short  # noqa: E402
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(lambda: defaultdict(float))     # kernel -> dispatch -> value (summed over dims)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r.get("Counter_Name") != counter:
+                continue
+            acc[short(r["Kernel_Name"])][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: (len(v), sum(v.values()) / len(v)) for k, v in acc.items()}
+
+
+def main():
+    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    out = {"units": "bytes per launch (FETCH_SIZE KiB x1024 x2 gfx950 correction; WRITE_SIZE KiB x1024)",
+           "kernels": {}}
+    if len(sys.argv) > 5:
+        out.update({"batch": int(sys.argv[4]), "dtype": sys.argv[5]})
+    if len(sys.argv) > 6:
+        out["command"] = sys.argv[6]
+    for k in sorted(set(fetch) | set(write)):
+        nf, f = fetch.get(k, (0, 0.0))
+        nw, w = write.get(k, (0, 0.0))
+        out["kernels"][k] = {"launches": max(nf, nw), "fetch_bytes": f * 1024 * 2, "write_bytes": w * 1024,
+                             "hbm_bytes": f * 1024 * 2 + w * 1024}
+    with open(sys.argv[3], "w") as fo:
+        json.dump(out, fo, indent=1, sort_keys=True)
+    for k, v in sorted(out["kernels"].items(), key=lambda t: -t[1]["hbm_bytes"])[:25]:
+        print("%-50s %5d  fetch %10.1f MB  write %10.1f MB" % (k, v["launches"], v["fetch_bytes"] / 1e6,
+                                                           v["write_bytes"] / 1e6))
+
+
+if __name__ == "__main__":
+    main()
