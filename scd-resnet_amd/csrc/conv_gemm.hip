@@ -8,6 +8,8 @@
 // (32 K per stage, K permuted identically on both operands).
 // The weight gradient is a separate split-K kernel whose operands are M-contiguous, read
 // from LDS with ds_read_b64_tr_b16 (bf16) so the MFMA A/B fragments come out K-major.
+#include <stdlib.h>
+
 #include "scd_common.h"
 
 namespace {
@@ -45,6 +47,152 @@ __device__ __forceinline__ int sel_off(bool ok, int off) {
 }
 __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// Shared GEMM epilogue (NT = 2*BM threads, waves of 64x64 outputs, WN waves along N): bias / ReLU in
+// registers, the wave's tile staged in LDS, coalesced 16-B NHWC stores (+= when accumulating), BN
+// channel sums into fp64 replicas, and optionally the fused 1x1 head tails (n-tile t == head t).
+template <typename T, int BM, int BN, int WN, bool HEADS>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[4][4], char* smem, int tid, int bid,
+                                              int mt, int nt, int M, int QQ, const scd_gemm_phase& ph) {
+    constexpr int ESZ = sizeof(T);
+    constexpr int EPC = 16 / ESZ;
+    constexpr int EROW = 64 * ESZ + 16; // epilogue staging row (64 channels + pad)
+    constexpr int EPI = (BM / 64) * WN * 64 * EROW;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+    const int l16 = lane & 15, lg = lane >> 4;
+    // ---- epilogue 1: bias / relu in registers, BN partial sums, stage the wave's 64x64 tile in LDS
+    char* ep = smem + wave * 64 * EROW;
+    float csum[4][4], csq[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int col0 = nt * BN + wn * 64 + b * 16 + lg * 4;
+        float bias[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int m = mt * BM + wm * 64 + a * 16 + l16;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[a][b][r] + bias[r];
+                if (p.relu) v[r] = fmaxf(v[r], 0.f);
+                if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+            }
+            char* dst = ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * ESZ;
+            if constexpr (ESZ == 2) {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                *(bf16x4*)dst = o;
+            } else {
+                *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+    __syncthreads();
+    // ---- epilogue 2: coalesced 16-B NHWC stores (+= for accumulate) of the staged tile
+    {
+        constexpr int CPR = 64 * ESZ / 16;        // 16-B chunks per staged row
+        constexpr int RPI = 64 / CPR;             // rows per wave instruction
+        const int ch = lane % CPR;
+        const int col = nt * BN + wn * 64 + ch * EPC;
+#pragma unroll
+        for (int j = 0; j < 64 / RPI; ++j) {
+            const int row = lane / CPR + RPI * j;
+            const int m = mt * BM + wm * 64 + row;
+            if (m >= M || col >= p.Co) continue;
+            const int n = m / QQ;
+            const int rem = m - n * QQ;
+            const int qh = rem / ph.Qw;
+            const int qw = rem - qh * ph.Qw;
+            const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
+            T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+            uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
+            if (p.accumulate) {
+                float a[EPC], o[EPC];
+                Vec16<T>::load(&v, a);
+                Vec16<T>::load(dst, o);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) a[e] += o[e];
+                Vec16<T>::store(&v, a);
+            }
+            *(uint4*)dst = v;
+        }
+    }
+    if (p.stats) {
+        // channel sums: over the 16 pixel-lanes (xor 1..8), then over the waves sharing the columns
+        float* red = (float*)(smem + EPI);   // [BM/64][BN][2] floats  (<= 2 KB)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float s = csum[b][r], q = csq[b][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                if (l16 == 0) {
+                    const int c = wn * 64 + b * 16 + lg * 4 + r;
+                    red[(wm * BN + c) * 2 + 0] = s;
+                    red[(wm * BN + c) * 2 + 1] = q;
+                }
+            }
+        __syncthreads();
+        if (tid < BN) {
+            const int col = nt * BN + tid;
+            if (col < p.Co) {
+                double s = 0.0, q = 0.0;
+#pragma unroll
+                for (int w = 0; w < BM / 64; ++w) { s += red[(w * BN + tid) * 2]; q += red[(w * BN + tid) * 2 + 1]; }
+                const int rep = (bid % SCD_STAT_REPLICAS);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
+            }
+        }
+    }
+    if constexpr (HEADS && BN == 128) {
+        {
+            // fused terminal 1x1 (centerNetOffset.py:108-110): head = n-tile, hidden = staged tile.
+            // thread -> (row = tid/2, half = tid&1): 64-channel partial dots, combined across the pair.
+            const int h = nt;
+            const int od = p.head_od[h];
+            float* ws = (float*)(smem + EPI);   // w1 of this head, [od][128]
+            __syncthreads();
+            for (int i = tid; i < od * 128; i += 256) ws[i] = p.head_w[h][i];
+            __syncthreads();
+            const int row = tid >> 1, half = tid & 1;
+            const int wv = (row >> 6) * WN + half;          // wave that staged this (row, half)
+            const char* src = smem + wv * 64 * EROW + (row & 63) * EROW;
+            float o4[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < 64; c += EPC) {
+                float v[EPC];
+                Vec16<T>::load(src + c * ESZ, v);
+#pragma unroll
+                for (int o = 0; o < 4; ++o)
+                    if (o < od) {
+#pragma unroll
+                        for (int e = 0; e < EPC; ++e) o4[o] += v[e] * ws[o * 128 + half * 64 + c + e];
+                    }
+            }
+#pragma unroll
+            for (int o = 0; o < 4; ++o) o4[o] += __shfl_xor(o4[o], 1, 64);
+            const int m = mt * BM + row;
+            if (half == 0 && m < M) {
+                const int n = m / QQ;
+                const int rem = m - n * QQ;
+                const int qh = rem / ph.Qw;
+                const int qw = rem - qh * ph.Qw;
+                const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
+                for (int o = 0; o < od; ++o)
+                    p.head_out[h][((long)n * od + o) * p.Ho * p.Wo + oh * p.Wo + ow] = o4[o] + p.head_b[h][o];
+            }
+        }
+    }
 }
 
 template <typename T, int BM, int BN, bool HEADS>
@@ -225,136 +373,155 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
         }
     }
 
-    // ---- epilogue 1: bias / relu in registers, BN partial sums, stage the wave's 64x64 tile in LDS
-    char* ep = smem + wave * 64 * EROW;
-    float csum[4][4], csq[4][4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int col0 = nt * BN + wn * 64 + b * 16 + lg * 4;
-        float bias[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            const int m = mt * BM + wm * 64 + a * 16 + l16;
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = acc[a][b][r] + bias[r];
-                if (p.relu) v[r] = fmaxf(v[r], 0.f);
-                if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
-            }
-            char* dst = ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * ESZ;
-            if constexpr (ESZ == 2) {
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-                *(bf16x4*)dst = o;
-            } else {
-                *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
-            }
-        }
-    }
-    __syncthreads();
-    // ---- epilogue 2: coalesced 16-B NHWC stores (+= for accumulate) of the staged tile
+    gemm_epilogue<T, BM, BN, WN, HEADS>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
+}
+
+// -------------------------------------------------------------------------------------
+// Large-shape bf16 gather-GEMM: 256x128 tile, 8 waves (4 along M x 2 along N, 64x64 each), one
+// workgroup per CU.  Both operands are staged by LDS-DMA (buffer_load_dwordx4 ... lds) into a
+// 3-slot LDS ring: two K-stages stay in flight across the single raw s_barrier of each K-step
+// (counted vmcnt, never 0 in the loop), so the MFMAs of stage k overlap the HBM/L2 latency of
+// stages k+1 and k+2.  The 16-B chunk c of LDS row r lives in slot c ^ (r & 7): the DMA writes
+// each wave-instruction's 1 KiB lane-linearly, so the swizzle is applied to the SOURCE chunk.
+// Out-of-image taps and stages past the end use out-of-range buffer offsets (zeros, no traffic).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, int off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_wave_base, 16, off, 0, 0, 0);
+}
+
+template <bool HEADS>
+__global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
+    typedef __bf16 T;
+    constexpr int BM = 256, BN = 128, WN = 2, BK = 64, EPC = 8;
+    constexpr int STAGE = (BM + BN) * 128;          // 48 KiB
+    constexpr int NSLOT = 3;
+    __shared__ __attribute__((aligned(16))) char smem[NSLOT * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int bid;
     {
-        constexpr int CPR = 64 * ESZ / 16;        // 16-B chunks per staged row
-        constexpr int RPI = 64 / CPR;             // rows per wave instruction
-        const int ch = lane % CPR;
-        const int col = nt * BN + wn * 64 + ch * EPC;
-#pragma unroll
-        for (int j = 0; j < 64 / RPI; ++j) {
-            const int row = lane / CPR + RPI * j;
-            const int m = mt * BM + wm * 64 + row;
-            if (m >= M || col >= p.Co) continue;
-            const int n = m / QQ;
-            const int rem = m - n * QQ;
-            const int qh = rem / ph.Qw;
-            const int qw = rem - qh * ph.Qw;
-            const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
-            T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
-            uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
-            if (p.accumulate) {
-                float a[EPC], o[EPC];
-                Vec16<T>::load(&v, a);
-                Vec16<T>::load(dst, o);
-#pragma unroll
-                for (int e = 0; e < EPC; ++e) a[e] += o[e];
-                Vec16<T>::store(&v, a);
-            }
-            *(uint4*)dst = v;
-        }
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
     }
-    if (p.stats) {
-        // channel sums: over the 16 pixel-lanes (xor 1..8), then over the waves sharing the columns
-        float* red = (float*)(smem + EPI);   // [BM/64][BN][2] floats  (<= 2 KB)
+    int phase = 0;
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+    for (int i = 1; i < SCD_MAX_PHASES; ++i)
+        if (i < p.nphase && bid >= p.tile_start[i]) phase = i;
+    const scd_gemm_phase& ph = p.ph[phase];
+    const int local = bid - p.tile_start[phase];
+    const int mt = local / p.ntn;
+    const int nt = local - mt * p.ntn;
+    const int QQ = ph.Qh * ph.Qw;
+    const int M = p.N * QQ;
+
+    // DMA rows of this lane: A rows 32*wave + 8*i + lane/8 (i < 4), B rows 16*wave + 8*j + lane/8 (j < 2);
+    // the lane fetches logical chunk (lane & 7) ^ (row & 7) so that LDS slot (lane & 7) holds it.
+    const int lrow = lane >> 3;
+    const int cch = (lane & 7) ^ (lrow & 7);
+    int a_pix[4], a_ih[4], a_iw[4];
+    bool a_ok[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float s = csum[b][r], q = csq[b][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-                if (l16 == 0) {
-                    const int c = wn * 64 + b * 16 + lg * 4 + r;
-                    red[(wm * BN + c) * 2 + 0] = s;
-                    red[(wm * BN + c) * 2 + 1] = q;
-                }
-            }
-        __syncthreads();
-        if (tid < BN) {
-            const int col = nt * BN + tid;
-            if (col < p.Co) {
-                double s = 0.0, q = 0.0;
-#pragma unroll
-                for (int w = 0; w < BM / 64; ++w) { s += red[(w * BN + tid) * 2]; q += red[(w * BN + tid) * 2 + 1]; }
-                const int rep = (bid % SCD_STAT_REPLICAS);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
-            }
-        }
+    for (int i = 0; i < 4; ++i) {
+        const int m = mt * BM + 32 * wave + 8 * i + lrow;
+        a_ok[i] = m < M;
+        const int mm = a_ok[i] ? m : 0;
+        const int n = mm / QQ;
+        const int rem = mm - n * QQ;
+        const int qh = rem / ph.Qw;
+        const int qw = rem - qh * ph.Qw;
+        a_pix[i] = n * p.Hi * p.Wi;
+        a_ih[i] = p.is * qh;
+        a_iw[i] = p.is * qw;
     }
-    if constexpr (HEADS && BN == 128) {
-        {
-            // fused terminal 1x1 (centerNetOffset.py:108-110): head = n-tile, hidden = staged tile.
-            // thread -> (row = tid/2, half = tid&1): 64-channel partial dots, combined across the pair.
-            const int h = nt;
-            const int od = p.head_od[h];
-            float* ws = (float*)(smem + EPI);   // w1 of this head, [od][128]
-            __syncthreads();
-            for (int i = tid; i < od * 128; i += 256) ws[i] = p.head_w[h][i];
-            __syncthreads();
-            const int row = tid >> 1, half = tid & 1;
-            const int wv = (row >> 6) * WN + half;          // wave that staged this (row, half)
-            const char* src = smem + wv * 64 * EROW + (row & 63) * EROW;
-            float o4[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int c = 0; c < 64; c += EPC) {
-                float v[EPC];
-                Vec16<T>::load(src + c * ESZ, v);
+    int b_row[2];
+    bool b_ok[2];
 #pragma unroll
-                for (int o = 0; o < 4; ++o)
-                    if (o < od) {
-#pragma unroll
-                        for (int e = 0; e < EPC; ++e) o4[o] += v[e] * ws[o * 128 + half * 64 + c + e];
-                    }
-            }
-#pragma unroll
-            for (int o = 0; o < 4; ++o) o4[o] += __shfl_xor(o4[o], 1, 64);
-            const int m = mt * BM + row;
-            if (half == 0 && m < M) {
-                const int n = m / QQ;
-                const int rem = m - n * QQ;
-                const int qh = rem / ph.Qw;
-                const int qw = rem - qh * ph.Qw;
-                const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
-                for (int o = 0; o < od; ++o)
-                    p.head_out[h][((long)n * od + o) * p.Ho * p.Wo + oh * p.Wo + ow] = o4[o] + p.head_b[h][o];
-            }
-        }
+    for (int j = 0; j < 2; ++j) {
+        const int nn = nt * BN + 16 * wave + 8 * j + lrow;
+        b_ok[j] = nn < p.Co;
+        b_row[j] = b_ok[j] ? nn : 0;
     }
+    const int cpt = p.Ci / BK;
+    const int KT = ph.ntaps * cpt;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+
+    // per-stage tap parameters (scalar loads from the phase table), fetched one step ahead so their
+    // latency is not exposed after the barrier
+    struct StageArgs { int live, c0, dh, dw, wt; };
+    auto stage_args = [&](int kt_req) {
+        StageArgs a;
+        a.live = kt_req < KT;
+        const int kt = min(kt_req, KT - 1);
+        const int tap = kt / cpt;
+        a.c0 = (kt - tap * cpt) * BK + cch * EPC;
+        a.dh = ph.dh[tap]; a.dw = ph.dw[tap]; a.wt = ph.wt[tap];
+        return a;
+    };
+    // the 6 DMA instructions of one K-stage into ring slot `slot` (always 6: the vmcnt counts are static)
+    auto issue = [&](const StageArgs& g, int slot) {
+        char* As = smem + slot * STAGE;
+        char* Bs = As + BM * 128;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ih = a_ih[i] + g.dh, iw = a_iw[i] + g.dw;
+            const bool ok = g.live && a_ok[i] && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+            dma16(xrs, As + (32 * wave + 8 * i) * 128, sel_off(ok, ((a_pix[i] + ih * p.Wi + iw) * p.Ci + g.c0) * 2));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            dma16(wrs, Bs + (16 * wave + 8 * j) * 128,
+                  sel_off(g.live && b_ok[j], (b_row[j] * p.wrow + g.wt * p.Ci + g.c0) * 2));
+    };
+
+    const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int l7 = l16 & 7;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    issue(stage_args(0), 0);
+    issue(stage_args(1), 1);
+    int slot = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+        const StageArgs nxt = stage_args(kt + 2);
+        // this wave's DMAs of stage kt have landed (stage kt+1's 6 stay in flight); after the barrier
+        // every wave's have, and every wave is done reading the slot that stage kt+2 overwrites
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(nxt, slot == 0 ? 2 : slot - 1);
+        const char* As = smem + slot * STAGE;
+        const char* Bs = As + BM * 128;
+        bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int co = ((s * 4 + lg) ^ l7) << 4;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) af[s][a] = *(const bf16x8*)(As + (wm * 64 + a * 16 + l16) * 128 + co);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) bfr[s][b] = *(const bf16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][b], af[s][a], acc[a][b], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        slot = slot == 2 ? 0 : slot + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    gemm_epilogue<T, BM, BN, WN, HEADS>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
 }
 
 // -------------------------------------------------------------------------------------
@@ -627,6 +794,17 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st) {
 
 }  // namespace
 
+// Kernel choice: the LDS-DMA ring kernel (256x128, bf16) for large outputs, the register-staged
+// 128x128 kernel otherwise, 256x64 for narrow outputs (Co <= 64).  SCD_GEMM_RING=0/1 forces it off/on.
+static int ring_mode() {
+    static int mode = -2;
+    if (mode == -2) {
+        const char* e = getenv("SCD_GEMM_RING");
+        mode = e ? atoi(e) : -1;
+    }
+    return mode;
+}
+
 static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm_phase* phases, void* stream) {
     if (nphase < 1 || nphase > SCD_MAX_PHASES) return SCD_ERR_ARG;
     const int BK = dtype == SCD_DT_BF16 ? 64 : 32;
@@ -635,32 +813,42 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     p.nphase = nphase;
     const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
     const long xb = (long)p.N * p.Hi * p.Wi * p.Ci * esz;
-    long wrows = 0;
     const bool narrow = p.Co <= 64;
     if (p.head_on && (narrow || p.Co != 128 * ((p.Co + 127) / 128))) return SCD_ERR_ARG;
-    const int BM = narrow ? 256 : 128, BN = narrow ? 64 : 128;
+    long Mtot = 0;
+    for (int i = 0; i < nphase; ++i) {
+        if (phases[i].ntaps < 0 || phases[i].ntaps > SCD_MAX_TAPS) return SCD_ERR_ARG;
+        for (int t = 0; t < phases[i].ntaps; ++t)
+            if (phases[i].wt[t] < 0 || (long)(phases[i].wt[t] + 1) * p.Ci > p.wrow) return SCD_ERR_ARG;
+        Mtot += (long)p.N * phases[i].Qh * phases[i].Qw;
+    }
+    bool ring = false;
+    if (dtype == SCD_DT_BF16 && !narrow) {
+        const int rm = ring_mode();
+        ring = rm >= 0 ? rm != 0 : cdiv(Mtot, 256) * cdiv(p.Co, 128) >= 256;   // >= one tile per CU
+    }
+    const int BM = ring ? 256 : (narrow ? 256 : 128), BN = narrow ? 64 : 128;
     p.ntn = cdiv(p.Co, BN);
     int tiles = 0;
     for (int i = 0; i < SCD_MAX_PHASES; ++i) {
+        p.tile_start[i] = tiles;
         if (i < nphase) {
             p.ph[i] = phases[i];
-            if (phases[i].ntaps < 0 || phases[i].ntaps > SCD_MAX_TAPS) return SCD_ERR_ARG;
-            for (int t = 0; t < phases[i].ntaps; ++t)
-                if (phases[i].wt[t] < 0 || (long)(phases[i].wt[t] + 1) * p.Ci > p.wrow) return SCD_ERR_ARG;
-            p.tile_start[i] = tiles;
             tiles += cdiv((long)p.N * phases[i].Qh * phases[i].Qw, BM) * p.ntn;
-        } else {
-            p.tile_start[i] = tiles;
         }
     }
     p.tile_start[SCD_MAX_PHASES] = tiles;
     if (tiles == 0) return 0;
-    wrows = p.Co;
-    const long wb = wrows * p.wrow * esz;
+    const long wb = (long)p.Co * p.wrow * esz;
     if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;   // 32-bit buffer offsets
     p.xbytes = (int)xb;
     p.wbytes = (int)wb;
     hipStream_t st = (hipStream_t)stream;
+    if (ring) {
+        if (p.head_on) hipLaunchKernelGGL((conv_gemm_ring_kernel<true>), dim3(tiles), dim3(512), 0, st, p);
+        else hipLaunchKernelGGL((conv_gemm_ring_kernel<false>), dim3(tiles), dim3(512), 0, st, p);
+        SCD_RETURN_LAUNCH();
+    }
     if (dtype == SCD_DT_BF16)
         return narrow ? launch_gemm<__bf16, 256, 64>(p, tiles, st) : launch_gemm<__bf16, 128, 128>(p, tiles, st);
     if (dtype == SCD_DT_F32)

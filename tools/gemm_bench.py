@@ -45,12 +45,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="", help="comma-separated substrings of layer names")
     a = ap.parse_args()
+    only = [o for o in a.only.split(",") if o]
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     dev = "cuda"
     print("%-20s %-6s %10s %10s %8s" % ("layer", "pass", "GFLOP", "ms", "TF/s"))
     tot_ms = 0.0
     for name, Cin, H, W, Cout, k, s, p, kind in SHAPES:
+        if only and not any(o in name for o in only):
+            continue
         if kind == "conv":
             w = torch.randn(Cout, Cin, k, k, device=dev) / (Cin * k * k) ** 0.5
             x = torch.randn(B, H, W, Cin, device=dev).to(dt)
