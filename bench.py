@@ -59,7 +59,7 @@ def cpu_baseline(steps):
                       "after 1 warm-up (%.1f s)" % (steps, dt)}
 
 
-HEADS_KERNEL = "conv_gemm_kernel<bf16,128,128,heads>"
+HEADS_KERNEL = "conv_gemm_ring_kernel<bf16,256,128,heads>"
 
 
 def pmc_traffic(kernel, batch, dtype):
@@ -94,9 +94,9 @@ def heads_gemm_roofline(B, dtype_name, cin=256, hd=128, ods=(1, 4, 2)):
     algo_bytes = M * cin * esz + M * ct * esz + M * sum(ods) * 4 + ct * 9 * cin * esz
     achieved = flops / (ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if dtype_name == "bf16" else PEAK_F32_TFLOPS
-    traffic, src = pmc_traffic(HEADS_KERNEL if dtype_name == "bf16" else HEADS_KERNEL.replace("bf16", "f32"),
-                               B, dtype_name)
-    return {"bound": "mfma", "kernel": HEADS_KERNEL, "achieved": round(achieved, 1), "peak": peak,
+    kernel = HEADS_KERNEL if dtype_name == "bf16" else "conv_gemm_kernel<f32,128,128,heads>"
+    traffic, src = pmc_traffic(kernel, B, dtype_name)
+    return {"bound": "mfma", "kernel": kernel, "achieved": round(achieved, 1), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": None if traffic is None else round(traffic), "traffic_source": src,
             "algorithmic_bytes": algo_bytes, "flop_per_launch": flops, "avg_launch_ms": round(ms, 4),

@@ -1,6 +1,8 @@
 // Training-mode BatchNorm2d pieces for NHWC activations (residuals.py:92,95,212,262,306).
 // Statistics are accumulated in fp64 into SCD_STAT_REPLICAS replicas (spreads the atomics),
 // finalised per channel; apply / backward passes are 16-byte-vectorised elementwise kernels.
+#include <algorithm>
+
 #include "scd_common.h"
 
 namespace {
@@ -96,60 +98,72 @@ __global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const 
     }
 }
 
-// per-channel sums over rows: block = 256 threads handles a tile of rows x (C/E chunk) columns
+// Per-channel Σdz and Σdz·x̂ over rows (dz = dout masked by relu(mask) > 0).  A 256-thread block owns
+// rows [r0, r1): thread = (row lane rsub, 16-B channel chunk ch); 4 rows per step are loaded before
+// any is used (4 x 3 independent 16-B loads in flight per thread); the block's partials are folded
+// over row lanes in LDS by all threads and added to one fp64 replica slot per channel.
 template <typename T>
-__global__ void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y, const float* mean,
-                                     const float* invstd, int C, long rows, int rows_per_block, double* stats) {
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y,
+                                                            const float* mean, const float* invstd, int C,
+                                                            unsigned rows, unsigned rows_per_block, double* stats) {
     constexpr int E = Vec16<T>::N;
-    const int cpr = C / E;                     // chunks per row
-    const int lanes_per_row = min(cpr, 256);
-    const int rpi = 256 / lanes_per_row;       // rows per iteration
+    constexpr int U = 4;
+    const int cpr = C / E;                     // chunks per row (divides 256)
+    const int rpi = 256 / cpr;                 // row lanes
     const int tid = threadIdx.x;
-    const int ch = tid % lanes_per_row;
-    const int rsub = tid / lanes_per_row;
-    const long r0 = (long)blockIdx.x * rows_per_block;
-    const long r1 = min(rows, r0 + rows_per_block);
-    __shared__ float red[256 * 2 * 8];
-    for (int cc = ch; cc < cpr; cc += lanes_per_row) {
-        float s[E], q[E], mu[E], is[E];
+    const int ch = tid % cpr;
+    const int rsub = tid / cpr;
+    const unsigned r0 = blockIdx.x * rows_per_block;
+    const unsigned r1 = min(rows, r0 + rows_per_block);
+    __shared__ float red[2 * 256 * E];
+    float s[E], q[E], mu[E], is[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) { s[e] = 0.f; q[e] = 0.f; mu[e] = mean[cc * E + e]; is[e] = invstd[cc * E + e]; }
-        if (rsub < rpi) {
-            for (long r = r0 + rsub; r < r1; r += rpi) {
-                const long i = r * C + (long)cc * E;
-                float d[E], yv[E], mk[E];
-                Vec16<T>::load(dout + i, d);
-                Vec16<T>::load(y + i, yv);
-                if (mask) Vec16<T>::load(mask + i, mk);
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    float dz = (mask && !(mk[e] > 0.f)) ? 0.f : d[e];
-                    s[e] += dz;
-                    q[e] += dz * (yv[e] - mu[e]) * is[e];
-                }
-            }
-        }
-        // reduce over the rpi row-lanes that share this chunk
+    for (int e = 0; e < E; ++e) { s[e] = 0.f; q[e] = 0.f; mu[e] = mean[ch * E + e]; is[e] = invstd[ch * E + e]; }
+    auto acc = [&](const float* d, const float* yv, const float* mk) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            red[(tid * E + e) * 2 + 0] = s[e];
-            red[(tid * E + e) * 2 + 1] = q[e];
+            const float dz = (mask && !(mk[e] > 0.f)) ? 0.f : d[e];
+            s[e] += dz;
+            q[e] += dz * (yv[e] - mu[e]) * is[e];
         }
-        __syncthreads();
-        if (rsub == 0) {
-            const int rep = blockIdx.x % SCD_STAT_REPLICAS;
+    };
+    unsigned r = r0 + rsub;
+    for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+        float d[U][E], yv[U][E], mk[U][E];
 #pragma unroll
-            for (int e = 0; e < E; ++e) {
-                double ss = 0.0, qq = 0.0;
-                for (int k = 0; k < rpi; ++k) {
-                    ss += red[((k * lanes_per_row + ch) * E + e) * 2 + 0];
-                    qq += red[((k * lanes_per_row + ch) * E + e) * 2 + 1];
-                }
-                atomic_add_f64(stats + ((long)rep * 2 + 0) * C + cc * E + e, ss);
-                atomic_add_f64(stats + ((long)rep * 2 + 1) * C + cc * E + e, qq);
-            }
+        for (int u = 0; u < U; ++u) {
+            const unsigned i = (r + u * rpi) * (unsigned)C + ch * E;
+            Vec16<T>::load(dout + i, d[u]);
+            Vec16<T>::load(y + i, yv[u]);
+            if (mask) Vec16<T>::load(mask + i, mk[u]);
         }
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc(d[u], yv[u], mk[u]);
+    }
+    for (; r < r1; r += rpi) {
+        float d[E], yv[E], mk[E];
+        const unsigned i = r * (unsigned)C + ch * E;
+        Vec16<T>::load(dout + i, d);
+        Vec16<T>::load(y + i, yv);
+        if (mask) Vec16<T>::load(mask + i, mk);
+        acc(d, yv, mk);
+    }
+    // red[stat][rsub][channel]
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        red[rsub * C + ch * E + e] = s[e];
+        red[256 * E + rsub * C + ch * E + e] = q[e];
+    }
+    __syncthreads();
+    const int rep = blockIdx.x % SCD_STAT_REPLICAS;
+    for (int c = tid; c < C; c += 256) {
+        double ss = 0.0, qq = 0.0;
+        for (int k = 0; k < rpi; ++k) {
+            ss += red[k * C + c];
+            qq += red[256 * E + k * C + c];
+        }
+        atomic_add_f64(stats + ((long)rep * 2 + 0) * C + c, ss);
+        atomic_add_f64(stats + ((long)rep * 2 + 1) * C + c, qq);
     }
 }
 
@@ -247,15 +261,18 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
     const long rows = total / C;
-    // aim for ~2048 blocks
-    int rpb = (int)std::max<long>(16, (rows + 2047) / 2048);
-    int blocks = cdiv(rows, rpb);
+    const int cpr = C / E;
+    if (cpr > 256 || 256 % cpr || total >= (1L << 31)) return SCD_ERR_ARG;
+    // ~1024 blocks, at least 8 rows per row lane
+    const long rpi = 256 / cpr;
+    const long rpb = std::max<long>(8 * rpi, (rows + 1023) / 1024 + rpi - 1) / rpi * rpi;
+    const int blocks = cdiv(rows, rpb);
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout,
-                           (const __bf16*)mask, (const __bf16*)y, mean, invstd, C, rows, rpb, stats);
+                           (const __bf16*)mask, (const __bf16*)y, mean, invstd, C, (unsigned)rows, (unsigned)rpb, stats);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dout,
-                           (const float*)mask, (const float*)y, mean, invstd, C, rows, rpb, stats);
+                           (const float*)mask, (const float*)y, mean, invstd, C, (unsigned)rows, (unsigned)rpb, stats);
     else
         return SCD_ERR_ARG;
     SCD_RETURN_LAUNCH();

@@ -195,74 +195,109 @@ __global__ void heads_fwd_kernel(const T* hid, int N, int HW, HeadsDesc d) {
 
 // fused backward of the head tails: dhid = relu'(hid) * (W1^T dout) and, in the same pass,
 // dW1 = sum_px dout x hid, db1 = sum_px dout, db0 (3x3 conv bias) = sum_px dhid.
-// Block = PXB pixels; thread = (chunk c, pixel-lane g); partials reduced in LDS then fp64
-// atomics into SCD_STAT_REPLICAS replicas.
+// Block = PXB pixels, blockDim = G pixel-lanes x cpp chunk-lanes; each thread streams its chunk over
+// every G-th pixel, 4 pixels per step with all loads issued before use; block partials are folded in
+// LDS by all threads and added to fp64 replicas (SCD_STAT_REPLICAS).
 template <typename T>
-__global__ __launch_bounds__(256) void heads_bwd_kernel(const T* hid, int N, int HW, HeadsDesc d, T* dhid,
+__global__ __launch_bounds__(512) void heads_bwd_kernel(const T* hid, int N, int HW, HeadsDesc d, T* dhid,
                                                         double* acc, int accsz, int PXB) {
     constexpr int E = Vec16<T>::N;
     constexpr int NA = 4 * E + E + 4;               // dW1 partials, db0 partials, db1 partials
+    constexpr int U = 4;
     const int cph = d.Hd / E;
     const int cpp = d.nh * cph;
-    const int G = 256 / cpp;
+    const int G = blockDim.x / cpp;
     const int tid = threadIdx.x;
     const int c = tid % cpp;
     const int g = tid / cpp;
     const int h = c / cph;
     const int cl = (c - h * cph) * E;
     const int ct = h * d.Hd + cl;                   // channel of this chunk in the hidden tensor
+    const int od = d.od[h];
+    const float* dout = d.dout[h];
     float w[4][E];
 #pragma unroll
     for (int o = 0; o < 4; ++o)
 #pragma unroll
-        for (int e = 0; e < E; ++e) w[o][e] = (g < G && o < d.od[h]) ? d.w1[h][o * d.Hd + cl + e] : 0.f;
+        for (int e = 0; e < E; ++e) w[o][e] = o < od ? d.w1[h][o * d.Hd + cl + e] : 0.f;
     float a[NA];
 #pragma unroll
     for (int k = 0; k < NA; ++k) a[k] = 0.f;
     const unsigned P = (unsigned)N * HW;
     const unsigned p0 = blockIdx.x * (unsigned)PXB;
     const unsigned p1 = min(P, p0 + PXB);
-    const int Ctot = d.nh * d.Hd;
+    const unsigned Ctot = d.nh * d.Hd;
+    auto body = [&](unsigned px, const float* gd, float* v) {
+        float r[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const float s = gd[0] * w[0][e] + gd[1] * w[1][e] + gd[2] * w[2][e] + gd[3] * w[3][e];
+            r[e] = v[e] > 0.f ? s : 0.f;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) a[o * E + e] += gd[o] * v[e];
+            a[4 * E + e] += r[e];
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o) a[5 * E + o] += gd[o];
+        Vec16<T>::store(dhid + px * Ctot + ct, r);
+    };
+    auto load_gd = [&](unsigned px, float* gd) {
+        const unsigned n = px / (unsigned)HW;
+        const unsigned q = px - n * HW;
+#pragma unroll
+        for (int o = 0; o < 4; ++o) gd[o] = o < od ? dout[(n * od + o) * (unsigned)HW + q] : 0.f;
+    };
     if (g < G) {
-        for (unsigned px = p0 + g; px < p1; px += G) {
-            const int n = (int)(px / (unsigned)HW);
-            const int q = (int)(px - (unsigned)n * HW);
-            float gd[4];
+        unsigned px = p0 + g;
+        for (; px + (U - 1) * G < p1; px += U * G) {
+            float gd[U][4], v[U][E];
 #pragma unroll
-            for (int o = 0; o < 4; ++o) gd[o] = o < d.od[h] ? d.dout[h][((size_t)n * d.od[h] + o) * HW + q] : 0.f;
-            float v[E], r[E];
-            Vec16<T>::load(hid + (size_t)px * Ctot + ct, v);
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const float s = gd[0] * w[0][e] + gd[1] * w[1][e] + gd[2] * w[2][e] + gd[3] * w[3][e];
-                r[e] = v[e] > 0.f ? s : 0.f;
-#pragma unroll
-                for (int o = 0; o < 4; ++o) a[o * E + e] += gd[o] * v[e];
-                a[4 * E + e] += r[e];
+            for (int u = 0; u < U; ++u) {
+                load_gd(px + u * G, gd[u]);
+                Vec16<T>::load(hid + (px + u * G) * Ctot + ct, v[u]);
             }
 #pragma unroll
-            for (int o = 0; o < 4; ++o) a[5 * E + o] += gd[o];
-            Vec16<T>::store(dhid + (size_t)px * Ctot + ct, r);
+            for (int u = 0; u < U; ++u) body(px + u * G, gd[u], v[u]);
+        }
+        for (; px < p1; px += G) {
+            float gd[4], v[E];
+            load_gd(px, gd);
+            Vec16<T>::load(hid + px * Ctot + ct, v);
+            body(px, gd, v);
         }
     }
-    __shared__ float red[256 * NA];
-#pragma unroll
-    for (int k = 0; k < NA; ++k) red[k * 256 + tid] = a[k];
-    __syncthreads();
-    if (g != 0) return;
-    for (int k = 0; k < NA; ++k) {
-        float s = 0.f;
-        for (int j = 0; j < G; ++j) s += red[k * 256 + j * cpp + c];
-        a[k] = s;
-    }
+    // fold the G pixel-lanes in LDS, KR partials per round (red[k][g][c]), all threads busy
+    constexpr int KR = (NA + 3) / 4;
+    __shared__ float red[KR * 512];
     double* dst = acc + (size_t)(blockIdx.x % SCD_STAT_REPLICAS) * accsz;
-    for (int o = 0; o < d.od[h]; ++o)
 #pragma unroll
-        for (int e = 0; e < E; ++e) atomic_add_f64(dst + (d.orow[h] + o) * d.Hd + cl + e, (double)a[o * E + e]);
-    if (cl == 0)
-        for (int o = 0; o < d.od[h]; ++o) atomic_add_f64(dst + d.nout * d.Hd + d.orow[h] + o, (double)a[5 * E + o]);
+    for (int k0 = 0; k0 < NA; k0 += KR) {
+        if (k0) __syncthreads();
+        if (g < G)
 #pragma unroll
-    for (int e = 0; e < E; ++e) atomic_add_f64(dst + d.nout * d.Hd + d.nout + ct + e, (double)a[4 * E + e]);
+            for (int k = 0; k < KR; ++k)
+                if (k0 + k < NA) red[(k * G + g) * cpp + c] = a[k0 + k];
+        __syncthreads();
+        for (int i = tid; i < KR * cpp; i += blockDim.x) {
+            const int kk = i / cpp, cc = i - (i / cpp) * cpp;
+            const int k = k0 + kk;
+            if (k >= NA) continue;
+            float s = 0.f;
+            for (int j = 0; j < G; ++j) s += red[(kk * G + j) * cpp + cc];
+            const int hh = cc / cph;
+            const int cll = (cc - hh * cph) * E;
+            const int odh = d.od[hh];
+            if (k < 4 * E) {                        // dW1[o][cl + e]
+                const int o = k / E, e = k - (k / E) * E;
+                if (o < odh) atomic_add_f64(dst + (d.orow[hh] + o) * d.Hd + cll + e, (double)s);
+            } else if (k < 5 * E) {                 // db0[ct + e]
+                atomic_add_f64(dst + d.nout * d.Hd + d.nout + hh * d.Hd + cll + (k - 4 * E), (double)s);
+            } else {                                // db1[o]: one chunk-lane per head
+                const int o = k - 5 * E;
+                if (o < odh && cll == 0) atomic_add_f64(dst + d.nout * d.Hd + d.orow[hh] + o, (double)s);
+            }
+        }
+    }
 }
 
 struct HeadsGrad {
@@ -433,14 +468,17 @@ extern "C" int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, 
     for (int h = 0; h < nh; ++h) { d.w1[h] = w1[h]; d.dout[h] = douts[h]; }
     const int accsz = d.nout * Hd + d.nout + nh * Hd;
     const long P = (long)N * HW;
-    const int PXB = 256;
+    if (P * nh * Hd >= (1L << 31)) return SCD_ERR_ARG;     // 32-bit element offsets
+    const int G = 512 / cpp;                                // pixel lanes (cpp <= 256 -> G >= 2)
+    const int threads = G * cpp;
+    const int PXB = 1024;
     const int blocks = cdiv(P, PXB);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((heads_bwd_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)hid, N, HW, d,
-                           (__bf16*)dhid, acc, accsz, PXB);
+        hipLaunchKernelGGL((heads_bwd_kernel<__bf16>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid, N, HW,
+                           d, (__bf16*)dhid, acc, accsz, PXB);
     else if (dtype == SCD_DT_F32)
-        hipLaunchKernelGGL((heads_bwd_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)hid, N, HW, d,
+        hipLaunchKernelGGL((heads_bwd_kernel<float>), dim3(blocks), dim3(threads), 0, st, (const float*)hid, N, HW, d,
                            (float*)dhid, acc, accsz, PXB);
     else
         return SCD_ERR_ARG;

@@ -20,6 +20,9 @@ def short(name):
     if m:
         return "%s<%s>" % (m.group(1), "bf16" if m.group(2) == "DF16b" else "f32")
     n = n.replace("(anonymous namespace)::", "")
+    m = re.search(r"conv_gemm_ring_kernel(ILb([01])E|<(true|false)>)", n)
+    if m:
+        return "conv_gemm_ring_kernel<bf16,256,128%s>" % (",heads" if m.group(2) == "1" or m.group(3) == "true" else "")
     return n.split("(")[0][:80]
 
 
