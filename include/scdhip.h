@@ -72,6 +72,9 @@ int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void* hid, cons
  * Replaces the weight-gradient half of cuDNN convolution_backward for every Conv2d /
  * ConvTranspose2d above. */
 size_t scd_conv_wgrad_workspace(int Cg, int T, int Ci, int nsplit);
+/* Number of pixel splits the library picks for an M-pixel weight gradient (tile shape of the
+ * kernel it will launch, ~4 waves of workgroups, fp32 slabs capped at 256 MB). */
+int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci);
 int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws, int nsplit,
                    int N, int Ho, int Wo, int Cg, int Hi, int Wi, int Ci, int in_stride,
                    int T, const int* dh, const int* dw, void* stream);

@@ -10,6 +10,8 @@
 // from LDS with ds_read_b64_tr_b16 (bf16) so the MFMA A/B fragments come out K-major.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "scd_common.h"
 
 namespace {
@@ -27,6 +29,7 @@ struct GemmParams {
     scd_gemm_phase ph[SCD_MAX_PHASES];
     // optional fused CenterNet head tails (n-tile t == head t, BN == head hidden width)
     int head_on;
+    int debug;      // ablation (SCD_GEMM_DEBUG): 1 = no MFMA, 2 = no DMA after the prologue
     int head_od[4];
     const float* head_w[4];
     const float* head_b[4];
@@ -496,7 +499,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        issue(nxt, slot == 0 ? 2 : slot - 1);
+        if (p.debug != 2) issue(nxt, slot == 0 ? 2 : slot - 1);
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const char* As = smem + slot * STAGE;
         const char* Bs = As + BM * 128;
         bf16x8 af[2][4], bfr[2][4];
@@ -508,15 +512,22 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
 #pragma unroll
             for (int b = 0; b < 4; ++b) bfr[s][b] = *(const bf16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
         }
-        __builtin_amdgcn_s_setprio(1);
+        if (p.debug == 1) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+            for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < 4; ++a) acc[a][0][0] += (float)af[s][a][0] + (float)bfr[s][a][0];
+        } else {
+            __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][b], af[s][a], acc[a][b], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][b], af[s][a], acc[a][b], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        }
         slot = slot == 2 ? 0 : slot + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -530,10 +541,22 @@ struct WgradParams {
     const char* g;
     const char* x;
     float* ws;
-    int N, Ho, Wo, Cg, Hi, Wi, Ci, is, T, KK, chunk, ntm, ntn;
+    int N, Ho, Wo, Cg, Hi, Wi, Ci, is, T, KK, chunk, ntm, ntn, nsplit;
     int gbytes, xbytes;
     int dh[SCD_MAX_TAPS], dw[SCD_MAX_TAPS];
 };
+
+// 1-D grid of ntiles * nsplit8 blocks (nsplit8 = nsplit rounded up to 8): block b -> XCD b % 8,
+// split z = 8 * ((b / 8) / ntiles) + b % 8, tile (b / 8) % ntiles.  Returns false for padding blocks.
+__device__ __forceinline__ bool wgrad_block(const WgradParams& p, int& z, int& mt, int& nt) {
+    const int T = p.ntm * p.ntn;
+    const int j = blockIdx.x >> 3;
+    z = 8 * (j / T) + (blockIdx.x & 7);
+    const int tile = j - (j / T) * T;
+    mt = tile / p.ntn;
+    nt = tile - mt * p.ntn;
+    return z < p.nsplit;
+}
 
 // LDS image of a [pixel][channel] stage for transposed (ds_read_b64_tr_b16) fragment reads: a row
 // stride of 8 dwords mod 64 banks (288 B for <= 256-B rows, 544 B for 512-B rows) puts rows r..r+3 on
@@ -564,9 +587,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
     const int tid = threadIdx.x;
-    const int z = blockIdx.z;
-    const int mt = blockIdx.x / p.ntn;
-    const int nt = blockIdx.x - mt * p.ntn;
+    // XCD-aware split placement: every tile of split z runs on XCD z % 8 (blocks are dispatched to XCDs
+    // round-robin on blockIdx), so the tiles re-reading the split's pixel rows share one L2
+    int z, mt, nt;
+    if (!wgrad_block(p, z, mt, nt)) return;
     const int M = p.N * p.Ho * p.Wo;
     const int pix0 = z * p.chunk;
     const int pix1 = min(M, pix0 + p.chunk);
@@ -740,6 +764,190 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
         }
 }
 
+// -------------------------------------------------------------------------------------
+// Large-shape bf16 weight gradient on the LDS-DMA ring: tile 128 (Cg) x 256 (KK), 8 waves (2 x 4,
+// 64x64 each), K = pixels in stages of 64, three 48-KiB ring slots, one raw barrier per stage.
+// Both operands are [pixel][column] rows read with ds_read_b64_tr_b16; the 32-B column pair p of
+// pixel row r is stored at pair p ^ f(r), f(r) = (r & 3) | ((r >> 1) & 4): the 8 rows a half-wave's
+// transposed read touches then sit in 8 different bank groups.  The DMA writes lane-linearly, so
+// each lane fetches the chunk whose swizzled slot it writes.
+__device__ __forceinline__ int wr_f(int r) { return (r & 3) | ((r >> 1) & 4); }
+
+__global__ __launch_bounds__(512, 1) void conv_wgrad_ring_kernel(WgradParams p) {
+    constexpr int BM = 128, BN = 256, KP = 64, EPC = 8;
+    constexpr int GROWB = BM * 2, XROWB = BN * 2;          // 256 B, 512 B
+    constexpr int GST = KP * GROWB, STAGE = KP * (GROWB + XROWB);   // 16 KiB, 48 KiB
+    constexpr int NSLOT = 3;
+    __shared__ __attribute__((aligned(16))) char smem[NSLOT * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // XCD-aware split placement: every tile of split z runs on XCD z % 8 (blocks are dispatched to XCDs
+    // round-robin on blockIdx), so the tiles re-reading the split's pixel rows share one L2
+    int z, mt, nt;
+    if (!wgrad_block(p, z, mt, nt)) return;
+    const int M = p.N * p.Ho * p.Wo;
+    const int pix0 = z * p.chunk;
+    const int pix1 = min(M, pix0 + p.chunk);
+
+    // G: 16 DMA instructions per stage (4 rows of 256 B each), 2 per wave: rows 8*wave + 4*i + lane/16
+    int g_row[2], g_off[2];
+    bool g_ok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = 8 * wave + 4 * i + (lane >> 4);
+        const int slot = lane & 15;
+        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);      // chunk this slot holds
+        const int col = mt * BM + c * EPC;
+        g_row[i] = r;
+        g_ok[i] = col < p.Cg;
+        g_off[i] = col;
+    }
+    // X: 32 instructions per stage (2 rows of 512 B each), 4 per wave: rows 8*wave + 2*i + lane/32
+    int x_row[4], x_ci[4], x_dh[4], x_dw[4];
+    bool x_ok[4];
+    int xn[4], xoh[4], xow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 8 * wave + 2 * i + (lane >> 5);
+        const int slot = lane & 31;
+        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);
+        const int kk = nt * BN + c * EPC;
+        x_ok[i] = kk < p.KK;
+        const int tap = x_ok[i] ? kk / p.Ci : 0;
+        x_ci[i] = kk - tap * p.Ci;
+        x_dh[i] = p.dh[tap];
+        x_dw[i] = p.dw[tap];
+        x_row[i] = r;
+        const int pix = pix0 + r;
+        const int HoWo = p.Ho * p.Wo;
+        xn[i] = pix / HoWo;
+        const int rem = pix - xn[i] * HoWo;
+        xoh[i] = rem / p.Wo;
+        xow[i] = rem - xoh[i] * p.Wo;
+    }
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    // stage k (pixels k0 .. k0+63) into ring slot `slot`; always 6 DMA instructions per thread
+    auto issue = [&](int k0, int slot) {
+        char* Gs = smem + slot * STAGE;
+        char* Xs = Gs + GST;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int pix = k0 + g_row[i];
+            dma16(grs, Gs + (8 * wave + 4 * i) * GROWB, sel_off(g_ok[i] && pix < pix1, (pix * p.Cg + g_off[i]) * 2));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pix = k0 + x_row[i];
+            const int ih = p.is * xoh[i] + x_dh[i], iw = p.is * xow[i] + x_dw[i];
+            const bool ok = x_ok[i] && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+            dma16(xrs, Xs + (8 * wave + 2 * i) * XROWB,
+                  sel_off(ok, (((xn[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + x_ci[i]) * 2));
+        }
+    };
+    auto advance = [&]() {     // every X row advances by KP pixels
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            xow[i] += KP;
+            while (xow[i] >= p.Wo) {
+                xow[i] -= p.Wo;
+                if (++xoh[i] >= p.Ho) { xoh[i] = 0; ++xn[i]; }
+            }
+        }
+    };
+
+    const int wm = wave >> 2, wn = wave & 3;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int q = l16 >> 2, pp = l16 & 3;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (pix1 > pix0) ? (pix1 - pix0 + KP - 1) / KP : 0;
+    if (nk > 0) {
+        issue(pix0, 0);
+        advance();
+        issue(pix0 + KP, 1);
+        advance();
+        int slot = 0;
+        for (int it = 0; it < nk; ++it) {
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            issue(pix0 + (it + 2) * KP, slot == 0 ? 2 : slot - 1);
+            advance();
+            const char* Gs = smem + slot * STAGE;
+            const char* Xs = Gs + GST;
+            typedef __attribute__((ext_vector_type(8))) short s16x8;
+            bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int r0 = 32 * s + 8 * lg + q;
+                const int f0 = wr_f(r0), f1 = wr_f(r0 + 4);
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    const int cb = (wm * 64 + a * 16 + 4 * pp) * 2;         // byte column in the G row
+                    const int pr = cb >> 5, lo8 = cb & 31;
+                    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(Gs + r0 * GROWB + ((pr ^ f0) << 5) + lo8));
+                    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(Gs + (r0 + 4) * GROWB + ((pr ^ f1) << 5) + lo8));
+                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    af[s][a] = __builtin_bit_cast(bf16x8, v);
+                }
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int cb = (wn * 64 + b * 16 + 4 * pp) * 2;
+                    const int pr = cb >> 5, lo8 = cb & 31;
+                    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(Xs + r0 * XROWB + ((pr ^ f0) << 5) + lo8));
+                    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(Xs + (r0 + 4) * XROWB + ((pr ^ f1) << 5) + lo8));
+                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    bfr[s][b] = __builtin_bit_cast(bf16x8, v);
+                }
+            }
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][a], bfr[s][b], acc[a][b], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            slot = slot == 2 ? 0 : slot + 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // ---- epilogue: stage the wave's 64x64 fp32 tile in LDS, then 16-B coalesced slab stores
+    constexpr int EROW = 64 * 4 + 16;
+    float* ep = (float*)(smem + wave * 64 * EROW);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                ep[((a * 16 + lg * 4 + r) * EROW) / 4 + b * 16 + l16] = acc[a][b][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's tile is staged (wave-private)
+    float* ws = p.ws + (long)z * p.Cg * p.KK;
+    const int ch = lane & 15;              // 16-B chunk of a 64-float row
+    const int col = nt * BN + wn * 64 + ch * 4;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int rr = (lane >> 4) + 4 * j;
+        const int row = mt * BM + wm * 64 + rr;
+        if (row < p.Cg && col < p.KK)
+            *(float4*)(ws + (long)row * p.KK + col) = *(const float4*)((const char*)ep + rr * EROW + ch * 16);
+    }
+}
+
 // sums groups of G consecutive split slabs into the group's first slab (first pass of a wide reduce)
 __global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs) {
     const long ngroups = (nsplit + G - 1) / G;
@@ -863,6 +1071,11 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.N = N; p.Hi = Hi; p.Wi = Wi; p.Ci = Ci; p.Ho = Ho; p.Wo = Wo; p.Co = Co;
     p.is = in_stride; p.os = out_stride; p.wrow = wrow; p.relu = relu; p.accumulate = accumulate;
     p.head_on = 0;
+    {
+        static int dbg = -1;
+        if (dbg < 0) { const char* e = getenv("SCD_GEMM_DEBUG"); dbg = e ? atoi(e) : 0; }
+        p.debug = dbg;
+    }
     for (int h = 0; h < 4; ++h) { p.head_od[h] = 0; p.head_w[h] = nullptr; p.head_b[h] = nullptr; p.head_out[h] = nullptr; }
 }
 
@@ -896,6 +1109,36 @@ extern "C" size_t scd_conv_wgrad_workspace(int Cg, int T, int Ci, int nsplit) {
     return (size_t)nsplit * Cg * T * Ci * sizeof(float);
 }
 
+// kernel choice for the weight gradient: the ring kernel for bf16 with wide outputs and many pixels
+static bool wgrad_use_ring(int dtype, long M, int Cg) {
+    // measured slower than the register-staged kernel at every Res10 shape (staging-bound at 128x256):
+    // opt-in only (SCD_WGRAD_RING=1)
+    (void)M;
+    if (dtype != SCD_DT_BF16 || Cg <= 64) return false;
+    static int mode = -2;
+    if (mode == -2) { const char* e = getenv("SCD_WGRAD_RING"); mode = e ? atoi(e) : 0; }
+    return mode == 1;
+}
+
+static void wgrad_tile(int dtype, long M, int Cg, int& tm, int& tn) {
+    if (wgrad_use_ring(dtype, M, Cg)) { tm = 128; tn = 256; }
+    else if (Cg <= 64) { tm = 64; tn = 256; }
+    else { tm = 128; tn = 128; }
+}
+
+extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
+    int tm, tn;
+    wgrad_tile(dtype, M, Cg, tm, tn);
+    const long tiles = (long)cdiv(Cg, tm) * cdiv((long)T * Ci, tn);
+    const bool ring = wgrad_use_ring(dtype, M, Cg);
+    // ~4 (ring, one workgroup per CU) / 4 (two per CU) waves of workgroups over 256 CUs, >= 1024 pixels per split,
+    // fp32 slabs capped at 256 MB
+    long ns = std::max(1L, std::min((ring ? 1024L : 1024L) / std::max(1L, tiles), M / 1024));
+    ns = std::max(1L, std::min(ns, (256L << 20) / std::max(1L, 4L * Cg * T * Ci)));
+    if (ns >= 8) ns = ns / 8 * 8;          // whole XCD groups (see wgrad_block)
+    return (int)ns;
+}
+
 extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws, int nsplit, int N, int Ho, int Wo,
                               int Cg, int Hi, int Wi, int Ci, int in_stride, int T, const int* dh, const int* dw,
                               void* stream) {
@@ -917,17 +1160,20 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     int chunk = cdiv(M, nsplit);
     chunk = (chunk + 63) / 64 * 64;
     p.chunk = chunk;
-    const bool narrow = Cg <= 64;
-    const int BM = narrow ? 64 : 128, BN = narrow ? 256 : 128;
+    int BM, BN;
+    wgrad_tile(dtype, M, Cg, BM, BN);
     p.ntm = cdiv(Cg, BM);
     p.ntn = cdiv(p.KK, BN);
-    dim3 grid(p.ntm * p.ntn, 1, nsplit);
+    p.nsplit = nsplit;
+    dim3 grid(p.ntm * p.ntn * ((nsplit + 7) / 8 * 8));
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == SCD_DT_BF16) {
-        if (narrow) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256>), grid, dim3(256), 0, st, p);
+    if (wgrad_use_ring(dtype, M, Cg)) {
+        hipLaunchKernelGGL(conv_wgrad_ring_kernel, grid, dim3(512), 0, st, p);
+    } else if (dtype == SCD_DT_BF16) {
+        if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256>), grid, dim3(256), 0, st, p);
         else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128>), grid, dim3(256), 0, st, p);
     } else if (dtype == SCD_DT_F32) {
-        if (narrow) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256>), grid, dim3(256), 0, st, p);
+        if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256>), grid, dim3(256), 0, st, p);
         else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128>), grid, dim3(256), 0, st, p);
     } else {
         return SCD_ERR_ARG;

@@ -218,14 +218,6 @@ def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=Fals
     return _gemm(dy, wpack, out, Cin, Ho, Wo, stride, 1, _fwd_phase(k, k, pad, Ho, Wo), accumulate=accumulate)
 
 
-def _nsplit(M, Cg, KK, Cg_tile, KK_tile):
-    tiles = -(-Cg // Cg_tile) * -(-KK // KK_tile)
-    ns = max(1, min(1024 // tiles, M // 1024))
-    # cap the fp32 workspace at ~256 MB
-    ns = max(1, min(ns, (256 << 20) // max(1, 4 * Cg * KK)))
-    return ns
-
-
 def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None):
     """Weight gradient of the gather-GEMM: dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= sum_pix g[pix,r] x[gather,ci].
 
@@ -238,8 +230,7 @@ def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True,
     dh = L.int_array([r - pad for r in range(kh) for s in range(kw)])
     dw = L.int_array([s - pad for r in range(kh) for s in range(kw)])
     M = N * Ho * Wo
-    narrow = Cg <= 64
-    ns = _nsplit(M, Cg, T * Ci, 64 if narrow else 128, 256 if narrow else 128)
+    ns = L.lib().scd_conv_wgrad_nsplit(dt(g), M, Cg, T, Ci)
     ws = torch.empty(L.lib().scd_conv_wgrad_workspace(Cg, T, Ci, ns) // 4, dtype=torch.float32, device=g.device)
     L.call("scd_conv_wgrad", dt(g), ptr(g), ptr(x), ptr(ws), ns, N, Ho, Wo, Cg, Hi, Wi, Ci, stride, T, dh, dw,
            stream())

@@ -34,6 +34,8 @@ CONV_CASES = [  # N, Cin, H, W, Cout, k, stride, pad
     (1, 128, 9, 11, 256, 3, 1, 1),
     (2, 64, 20, 20, 384, 3, 1, 1),
     (1, 256, 8, 8, 512, 3, 2, 1),
+    (4, 128, 32, 32, 256, 3, 1, 1),     # large enough for the LDS-DMA ring kernels by default
+    (3, 64, 41, 37, 192, 3, 2, 1),      # ragged pixels / channels on the ring kernels
 ]
 
 

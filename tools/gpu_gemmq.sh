@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-gq}; ONLY=${2:-heads,deconv3,deconv2,layer3}
 mkdir -p gpurun_out
-SCD_GEMM_RING=1 timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -x -q -k "conv or deconv" > gpurun_out/gqk_$TAG.log 2>&1; rc=$?
+SCD_GEMM_RING=1 SCD_WGRAD_RING=1 timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -x -q -k "conv or deconv" > gpurun_out/gqk_$TAG.log 2>&1; rc=$?
 tail -3 gpurun_out/gqk_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 SCD_GEMM_RING=0 timeout -k 10 300 python tools/gemm_bench.py --only $ONLY --reps 20 > gpurun_out/gqA_$TAG.txt 2>&1 || exit 1
