@@ -29,6 +29,7 @@ struct GemmParams {
     scd_gemm_phase ph[SCD_MAX_PHASES];
     // optional fused CenterNet head tails (n-tile t == head t, BN == head hidden width)
     int head_on;
+    int tapinner;   // K order: 1 = channel chunk outer, taps inner (the chunk's halo stays in L2)
     int debug;      // ablation (SCD_GEMM_DEBUG): 1 = no MFMA, 2 = no DMA after the prologue
     int head_od[4];
     const float* head_w[4];
@@ -268,8 +269,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
         // stages past the end are issued with out-of-range offsets (no traffic, no branch)
         const bool live = kt_req < KT;
         const int kt = min(kt_req, KT - 1);
-        int tap = kt / cpt;
-        int c0 = (kt - tap * cpt) * BK + cch * EPC;
+        int tap, chunk;
+        if (p.tapinner) { chunk = kt / ph.ntaps; tap = kt - chunk * ph.ntaps; }
+        else { tap = kt / cpt; chunk = kt - tap * cpt; }
+        int c0 = chunk * BK + cch * EPC;
         int dh = ph.dh[tap], dw = ph.dw[tap], wt = ph.wt[tap];
 #pragma unroll
         for (int i = 0; i < ACH; ++i) {
@@ -459,8 +462,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
         StageArgs a;
         a.live = kt_req < KT;
         const int kt = min(kt_req, KT - 1);
-        const int tap = kt / cpt;
-        a.c0 = (kt - tap * cpt) * BK + cch * EPC;
+        int tap, chunk;
+        if (p.tapinner) { chunk = kt / ph.ntaps; tap = kt - chunk * ph.ntaps; }
+        else { tap = kt / cpt; chunk = kt - tap * cpt; }
+        a.c0 = chunk * BK + cch * EPC;
         a.dh = ph.dh[tap]; a.dw = ph.dw[tap]; a.wt = ph.wt[tap];
         return a;
     };
@@ -533,6 +538,298 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     gemm_epilogue<T, BM, BN, WN, HEADS>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
+}
+
+// -------------------------------------------------------------------------------------
+// Ping-pong bf16 gather-GEMM for the large shapes: 256 x BN tile (BN = 256 or 192), 8 waves in two
+// groups of 4 (group g owns pixel rows 128g..128g+127, wave wc of a group owns BN/4 output channels),
+// BK = 64, two LDS stage buffers.  Each K-stage runs as 4 phases (one 32-pixel quarter of the
+// group's rows each); a phase is an L part (fragment reads + 2 LDS-DMA issues for the NEXT stage)
+// and a C part (lgkmcnt(0), 4*NB MFMAs), each closed by an s_barrier.  Group 1 starts one barrier
+// late, so on every SIMD one wave's MFMAs run while its partner reads LDS and issues DMA: the matrix
+// pipe never waits for the fragment reads of the whole workgroup (the single-barrier ring kernel
+// above spends ~40% of each K-step that way).
+// DMA schedule per group and stage t (filling buffer (t+1)&1): P1 B rows part 1 (2 instr), P2 B part
+// 2 (NB2), P3 own A rows 0..63 (2), P4 own A rows 64..127 (2); counted waits: end of L4 vmcnt(4)
+// (both B parts of t+1 landed), end of C4 vmcnt(2) (A rows 0..63), end of C2 vmcnt(2+NB2) (A rows
+// 64..127 of stage t).  Every region is rewritten >= 3 phases after its last fragment read.
+template <int BN>
+__global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
+    typedef __bf16 T;
+    constexpr int BM = 256, BK = 64, EPC = 8;
+    constexpr int NB = BN / 64;                 // 16-channel blocks per wave
+    constexpr int WCOLS = BN / 4;               // channels per wave
+    constexpr int NB2 = (BN / 2 - 64) / 32;     // B part-2 DMA instructions per thread (2 or 1)
+    constexpr int STAGE = (BM + BN) * 128;
+    constexpr int EROW = WCOLS * 2 + 16;        // epilogue staging row
+    constexpr int EPI = 8 * 128 * EROW;
+    constexpr int SMEM = (2 * STAGE > EPI + 4 * BN * 4) ? 2 * STAGE : EPI + 4 * BN * 4;
+    static_assert(BN == 256 || BN == 192, "BN");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    int bid;
+    {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+    }
+    int phase = 0;
+#pragma unroll
+    for (int i = 1; i < SCD_MAX_PHASES; ++i)
+        if (i < p.nphase && bid >= p.tile_start[i]) phase = i;
+    const scd_gemm_phase& ph = p.ph[phase];
+    const int local = bid - p.tile_start[phase];
+    const int mt = local / p.ntn;
+    const int nt = local - mt * p.ntn;
+    const int QQ = ph.Qh * ph.Qw;
+    const int M = p.N * QQ;
+
+    // DMA rows of this lane (the lane fetches chunk (lane&7)^(row&7) so that LDS slot lane&7 holds it)
+    const int lrow = lane >> 3;
+    const int cch = (lane & 7) ^ lrow;
+    // A: rows 128*grp + 64*h + 16*wc + 8*j + lrow  (h, j in {0,1}); index i = 2h + j
+    int a_pix[4], a_ih[4], a_iw[4];
+    bool a_ok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = mt * BM + 128 * grp + 64 * (i >> 1) + 16 * wc + 8 * (i & 1) + lrow;
+        a_ok[i] = m < M;
+        const int mm = a_ok[i] ? m : 0;
+        const int n = mm / QQ;
+        const int rem = mm - n * QQ;
+        const int qh = rem / ph.Qw;
+        const int qw = rem - qh * ph.Qw;
+        a_pix[i] = n * p.Hi * p.Wi;
+        a_ih[i] = p.is * qh;
+        a_iw[i] = p.is * qw;
+    }
+    // B: part 1 rows (BN/2)*grp + 16*wc + 8*j + lrow (j < 2); part 2 rows (BN/2)*grp + 64 + 8*NB2*wc + 8*j + lrow
+    int b_row[2 + NB2];
+    bool b_ok[2 + NB2];
+#pragma unroll
+    for (int j = 0; j < 2 + NB2; ++j) {
+        const int r = (BN / 2) * grp + (j < 2 ? 16 * wc + 8 * j : 64 + 8 * NB2 * wc + 8 * (j - 2)) + lrow;
+        const int nn = nt * BN + r;
+        b_ok[j] = nn < p.Co;
+        b_row[j] = b_ok[j] ? nn : 0;
+    }
+    const int cpt = p.Ci / BK;
+    const int KT = ph.ntaps * cpt;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+
+    struct StageArgs { int live, c0, dh, dw, wt; };
+    auto stage_args = [&](int kt_req) {
+        StageArgs a;
+        a.live = kt_req < KT;
+        const int kt = min(kt_req, KT - 1);
+        int tap, chunk;
+        if (p.tapinner) { chunk = kt / ph.ntaps; tap = kt - chunk * ph.ntaps; }
+        else { tap = kt / cpt; chunk = kt - tap * cpt; }
+        a.c0 = chunk * BK + cch * EPC;
+        a.dh = ph.dh[tap]; a.dw = ph.dw[tap]; a.wt = ph.wt[tap];
+        return a;
+    };
+    auto issue_a = [&](const StageArgs& g, char* buf, int h) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = 2 * h + j;
+            const int ih = a_ih[i] + g.dh, iw = a_iw[i] + g.dw;
+            const bool ok = g.live && a_ok[i] && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+            dma16(xrs, buf + (128 * grp + 64 * h + 16 * wc + 8 * j) * 128,
+                  sel_off(ok, ((a_pix[i] + ih * p.Wi + iw) * p.Ci + g.c0) * 2));
+        }
+    };
+    auto issue_b = [&](const StageArgs& g, char* buf, int part) {
+        char* Bs = buf + BM * 128;
+#pragma unroll
+        for (int j = (part ? 2 : 0); j < (part ? 2 + NB2 : 2); ++j) {
+            const int r = (BN / 2) * grp + (j < 2 ? 16 * wc + 8 * j : 64 + 8 * NB2 * wc + 8 * (j - 2));
+            dma16(wrs, Bs + r * 128, sel_off(g.live && b_ok[j], (b_row[j] * p.wrow + g.wt * p.Ci + g.c0) * 2));
+        }
+    };
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int l7 = l16 & 7;
+    const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
+    f32x4 acc[8][NB];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 bfr[NB][2], afx[2][2], afy[2][2];
+
+    auto read_b = [&](const char* buf) {
+        const char* Bs = buf + BM * 128;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const char* row = Bs + (wc * WCOLS + b * 16 + l16) * 128;
+            bfr[b][0] = *(const bf16x8*)(row + co0);
+            bfr[b][1] = *(const bf16x8*)(row + co1);
+        }
+    };
+    auto read_a = [&](const char* buf, int q, bf16x8 (&af)[2][2]) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const char* row = buf + (128 * grp + 32 * q + 16 * a + l16) * 128;
+            af[a][0] = *(const bf16x8*)(row + co0);
+            af[a][1] = *(const bf16x8*)(row + co1);
+        }
+    };
+    auto mfma_q = [&](int q, const bf16x8 (&af)[2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b][s], af[a][s], acc[2 * q + a][b], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    if (KT > 0) {
+        {
+            const StageArgs g0 = stage_args(0);
+            issue_b(g0, smem, 0);
+            issue_b(g0, smem, 1);
+            issue_a(g0, smem, 0);
+            issue_a(g0, smem, 1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
+        for (int t = 0; t < KT; ++t) {
+            char* cur = smem + (t & 1) * STAGE;
+            char* nxt = smem + ((t & 1) ^ 1) * STAGE;
+            const StageArgs g = stage_args(t + 1);
+            // P1
+            read_b(cur);
+            read_a(cur, 0, afx);
+            issue_b(g, nxt, 0);
+            bar();
+            mfma_q(0, afx);
+            bar();
+            // P2
+            read_a(cur, 1, afy);
+            issue_b(g, nxt, 1);
+            bar();
+            mfma_q(1, afy);
+            if constexpr (NB2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            bar();
+            // P3
+            read_a(cur, 2, afx);
+            issue_a(g, nxt, 0);
+            bar();
+            mfma_q(2, afx);
+            bar();
+            // P4
+            read_a(cur, 3, afy);
+            issue_a(g, nxt, 1);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            bar();
+            mfma_q(3, afy);
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            bar();
+        }
+        if (grp == 0) bar();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- epilogue: bias / relu in registers, BN partial sums, stage the wave's 128 x WCOLS tile, coalesced stores
+    char* ep = smem + wave * 128 * EROW;
+    float csum[NB][4], csq[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
+        float bias[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+            const int m = mt * BM + 128 * grp + a * 16 + l16;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[a][b][r] + bias[r];
+                if (p.relu) v[r] = fmaxf(v[r], 0.f);
+                if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+            }
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+            *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the staged tile is wave-private
+    {
+        constexpr int CPR = WCOLS * 2 / 16;                  // 16-B chunks per staged row (8 or 6)
+        for (int idx = lane; idx < 128 * CPR; idx += 64) {
+            const int row = idx / CPR, ch = idx - (idx / CPR) * CPR;
+            const int m = mt * BM + 128 * grp + row;
+            const int col = nt * BN + wc * WCOLS + ch * EPC;
+            if (m >= M || col >= p.Co) continue;
+            const int n = m / QQ;
+            const int rem = m - n * QQ;
+            const int qh = rem / ph.Qw;
+            const int qw = rem - qh * ph.Qw;
+            const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
+            T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+            uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
+            if (p.accumulate) {
+                float a[EPC], o[EPC];
+                Vec16<T>::load(&v, a);
+                Vec16<T>::load(dst, o);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) a[e] += o[e];
+                Vec16<T>::store(&v, a);
+            }
+            *(uint4*)dst = v;
+        }
+    }
+    if (p.stats) {
+        float* red = (float*)(smem + EPI);    // [2 groups][BN][2]
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float s = csum[b][r], q = csq[b][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                if (l16 == 0) {
+                    const int c = wc * WCOLS + b * 16 + lg * 4 + r;
+                    red[(grp * BN + c) * 2 + 0] = s;
+                    red[(grp * BN + c) * 2 + 1] = q;
+                }
+            }
+        __syncthreads();
+        if (tid < BN) {
+            const int col = nt * BN + tid;
+            if (col < p.Co) {
+                const double s = (double)red[tid * 2] + (double)red[(BN + tid) * 2];
+                const double q = (double)red[tid * 2 + 1] + (double)red[(BN + tid) * 2 + 1];
+                const int rep = (bid % SCD_STAT_REPLICAS);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
+            }
+        }
+    }
 }
 
 // -------------------------------------------------------------------------------------
@@ -1013,6 +1310,23 @@ static int ring_mode() {
     return mode;
 }
 
+static int pp_mode() {
+    static int mode = -2;
+    if (mode == -2) {
+        const char* e = getenv("SCD_GEMM_PP");
+        mode = e ? atoi(e) : 1;
+    }
+    return mode;
+}
+
+// BN of the ping-pong kernel for this output width (0 = not applicable)
+static int pp_bn(int dtype, int Co) {
+    if (dtype != SCD_DT_BF16 || !pp_mode()) return 0;
+    if (Co % 256 == 0) return 256;
+    if (Co % 192 == 0) return 192;
+    return 0;
+}
+
 static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm_phase* phases, void* stream) {
     if (nphase < 1 || nphase > SCD_MAX_PHASES) return SCD_ERR_ARG;
     const int BK = dtype == SCD_DT_BF16 ? 64 : 32;
@@ -1029,6 +1343,35 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         for (int t = 0; t < phases[i].ntaps; ++t)
             if (phases[i].wt[t] < 0 || (long)(phases[i].wt[t] + 1) * p.Ci > p.wrow) return SCD_ERR_ARG;
         Mtot += (long)p.N * phases[i].Qh * phases[i].Qw;
+    }
+    {
+        // ping-pong 256 x BN kernel when the grid fills the chip (fused head tails are run as a separate pass)
+        const int bn = pp_bn(dtype, p.Co);
+        if (bn && (long)cdiv(Mtot, 256) * (p.Co / bn) >= 256) {
+            p.ntn = p.Co / bn;
+            int tiles = 0;
+            for (int i = 0; i < SCD_MAX_PHASES; ++i) {
+                p.tile_start[i] = tiles;
+                if (i < nphase) {
+                    p.ph[i] = phases[i];
+                    tiles += cdiv((long)p.N * phases[i].Qh * phases[i].Qw, 256) * p.ntn;
+                }
+            }
+            p.tile_start[SCD_MAX_PHASES] = tiles;
+            const long wb = (long)p.Co * p.wrow * esz;
+            if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
+            p.xbytes = (int)xb;
+            p.wbytes = (int)wb;
+            hipStream_t st = (hipStream_t)stream;
+            if (bn == 256) hipLaunchKernelGGL((conv_gemm_pp_kernel<256>), dim3(tiles), dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((conv_gemm_pp_kernel<192>), dim3(tiles), dim3(512), 0, st, p);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess || !p.head_on) return (int)e;
+            int nh = 0;
+            while (nh < 4 && p.head_out[nh]) ++nh;
+            return scd_heads_fwd(dtype, p.y, p.N, p.Ho * p.Wo, nh, 128, p.head_od, p.head_w, p.head_b,
+                                 p.head_out, stream);
+        }
     }
     bool ring = false;
     if (dtype == SCD_DT_BF16 && !narrow) {
@@ -1075,6 +1418,9 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
         static int dbg = -1;
         if (dbg < 0) { const char* e = getenv("SCD_GEMM_DEBUG"); dbg = e ? atoi(e) : 0; }
         p.debug = dbg;
+        static int ti = -1;
+        if (ti < 0) { const char* e = getenv("SCD_GEMM_TAPINNER"); ti = e ? atoi(e) : 1; }
+        p.tapinner = ti;
     }
     for (int h = 0; h < 4; ++h) { p.head_od[h] = 0; p.head_w[h] = nullptr; p.head_b[h] = nullptr; p.head_out[h] = nullptr; }
 }

@@ -73,8 +73,21 @@ def test_conv_fwd_dgrad_wgrad(case, dtype):
     assert rel_err(dw, wr.grad) < TOL[dtype] * 3
 
 
+# shapes large enough (>= 256 tiles of 256 pixels) for the bf16 ping-pong kernel (BN 256 and 192, ragged M)
+LARGE_CONV_CASES = [
+    (4, 128, 128, 128, 256, 3, 1, 1),
+    (2, 64, 181, 179, 384, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", LARGE_CONV_CASES)
+def test_conv_large_bf16(case):
+    test_conv_fwd_dgrad_wgrad(case, torch.bfloat16)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", [(2, 128, 5, 7, 64), (1, 256, 8, 8, 256), (2, 64, 16, 16, 128)])
+@pytest.mark.parametrize("case", [(2, 128, 5, 7, 64), (1, 256, 8, 8, 256), (2, 64, 16, 16, 128),
+                                  (8, 256, 64, 64, 256)])
 def test_deconv_fwd_dgrad_wgrad(case, dtype):
     from scdhip import ops
     N, Cin, H, W, Cout = case

@@ -4,10 +4,10 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 TAG=${1:-ab}; VAR=${2:-SCD_GEMM_RING}
 mkdir -p gpurun_out
-env $VAR=1 timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -x -q > gpurun_out/abk_$TAG.log 2>&1; rc=$?
+env $VAR=1 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/abk_$TAG.log 2>&1; rc=$?
 tail -5 gpurun_out/abk_$TAG.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 500 python -m pytest tests -x -q -m gpu > gpurun_out/tests_$TAG.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1; rc=$?
 tail -3 gpurun_out/tests_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 env $VAR=0 timeout -k 10 300 python tools/gemm_bench.py > gpurun_out/gemmA_$TAG.txt 2>&1 || exit 1

@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-run}
 mkdir -p gpurun_out
-timeout -k 10 500 python -m pytest tests -x -q -m gpu > gpurun_out/tests_$TAG.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1; rc=$?
 tail -15 gpurun_out/tests_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$?
