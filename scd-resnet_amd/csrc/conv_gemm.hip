@@ -14,6 +14,18 @@
 
 #include "scd_common.h"
 
+// Compile-time ablations of the LDS-DMA GEMM kernels (make ABLATE=N builds a separate library; never in the
+// product build): 1 = no MFMA, 2 = loop DMAs read nothing, 3 = no loop DMA instructions, 4 = no loop
+// fragment reads, 5 = no loop barriers; halo kernel: 6 = weight DMAs read nothing, 7 = halo DMAs read nothing,
+// 8 = no vmcnt waits in the loop.  Runtime switches would put branches in the main loop and change
+// its code (the waitcnt pass falls back to full drains around branched loads).
+#ifndef SCD_ABLATE
+#define SCD_ABLATE 0
+#endif
+#ifndef SCD_ABM
+#define SCD_ABM 0     // halo kernel ablation bitmask: 1 no MFMA, 2 no loop DMA, 4 no loop fragment reads, 8 no loop barriers
+#endif
+
 namespace {
 
 struct GemmParams {
@@ -29,7 +41,6 @@ struct GemmParams {
     scd_gemm_phase ph[SCD_MAX_PHASES];
     // optional fused CenterNet head tails (n-tile t == head t, BN == head hidden width)
     int head_on;
-    int tapinner;   // K order: 1 = channel chunk outer, taps inner (the chunk's halo stays in L2)
     int debug;      // ablation (SCD_GEMM_DEBUG): 1 = no MFMA, 2 = no DMA after the prologue
     int head_od[4];
     const float* head_w[4];
@@ -269,9 +280,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
         // stages past the end are issued with out-of-range offsets (no traffic, no branch)
         const bool live = kt_req < KT;
         const int kt = min(kt_req, KT - 1);
-        int tap, chunk;
-        if (p.tapinner) { chunk = kt / ph.ntaps; tap = kt - chunk * ph.ntaps; }
-        else { tap = kt / cpt; chunk = kt - tap * cpt; }
+        const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
         int c0 = chunk * BK + cch * EPC;
         int dh = ph.dh[tap], dw = ph.dw[tap], wt = ph.wt[tap];
 #pragma unroll
@@ -462,9 +471,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
         StageArgs a;
         a.live = kt_req < KT;
         const int kt = min(kt_req, KT - 1);
-        int tap, chunk;
-        if (p.tapinner) { chunk = kt / ph.ntaps; tap = kt - chunk * ph.ntaps; }
-        else { tap = kt / cpt; chunk = kt - tap * cpt; }
+        const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
         a.c0 = chunk * BK + cch * EPC;
         a.dh = ph.dh[tap]; a.dw = ph.dw[tap]; a.wt = ph.wt[tap];
         return a;
@@ -504,8 +511,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (p.debug != 2) issue(nxt, slot == 0 ? 2 : slot - 1);
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (SCD_ABLATE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else issue(nxt, slot == 0 ? 2 : slot - 1);
         const char* As = smem + slot * STAGE;
         const char* Bs = As + BM * 128;
         bf16x8 af[2][4], bfr[2][4];
@@ -517,7 +524,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
 #pragma unroll
             for (int b = 0; b < 4; ++b) bfr[s][b] = *(const bf16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
         }
-        if (p.debug == 1) {
+        if constexpr (SCD_ABLATE == 1) {
 #pragma unroll
             for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -626,9 +633,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         StageArgs a;
         a.live = kt_req < KT;
         const int kt = min(kt_req, KT - 1);
-        int tap, chunk;
-        if (p.tapinner) { chunk = kt / ph.ntaps; tap = kt - chunk * ph.ntaps; }
-        else { tap = kt / cpt; chunk = kt - tap * cpt; }
+        const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
         a.c0 = chunk * BK + cch * EPC;
         a.dh = ph.dh[tap]; a.dw = ph.dw[tap]; a.wt = ph.wt[tap];
         return a;
@@ -682,6 +687,16 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     auto mfma_q = [&](int q, const bf16x8 (&af)[2][2]) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SCD_ABLATE == 1) {       // ablation: fragments read, no MFMA
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+#pragma unroll
+                for (int a = 0; a < 2; ++a) asm volatile("" ::"v"(af[a][s]));
+#pragma unroll
+                for (int b = 0; b < NB; ++b) asm volatile("" ::"v"(bfr[b][s]));
+            }
+            return;
+        }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int s = 0; s < 2; ++s)
@@ -693,9 +708,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
+    // ablations (SCD_GEMM_DEBUG): 3 = no DMA instructions in the loop, 4 = no fragment reads in the loop,
+    // 5 = no barriers in the loop (timing only; 3-5 give wrong results)
+    constexpr int dbg = SCD_ABLATE;
     auto bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
+        if constexpr (dbg != 5) __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
     };
 
@@ -709,35 +727,37 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();
+        if constexpr (dbg == 4) { read_b(smem); read_a(smem, 0, afx); read_a(smem, 1, afy); }
         if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
         for (int t = 0; t < KT; ++t) {
             char* cur = smem + (t & 1) * STAGE;
             char* nxt = smem + ((t & 1) ^ 1) * STAGE;
-            const StageArgs g = stage_args(t + 1);
+            StageArgs g = stage_args(t + 1);
+            if constexpr (dbg == 2) g.live = 0;      // ablation: loop DMAs read nothing
             // P1
-            read_b(cur);
-            read_a(cur, 0, afx);
-            issue_b(g, nxt, 0);
+            if constexpr (dbg != 4) read_b(cur);
+            if constexpr (dbg != 4) read_a(cur, 0, afx);
+            if constexpr (dbg != 3) issue_b(g, nxt, 0);
             bar();
             mfma_q(0, afx);
             bar();
             // P2
-            read_a(cur, 1, afy);
-            issue_b(g, nxt, 1);
+            if constexpr (dbg != 4) read_a(cur, 1, afy);
+            if constexpr (dbg != 3) issue_b(g, nxt, 1);
             bar();
             mfma_q(1, afy);
             if constexpr (NB2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
             bar();
             // P3
-            read_a(cur, 2, afx);
-            issue_a(g, nxt, 0);
+            if constexpr (dbg != 4) read_a(cur, 2, afx);
+            if constexpr (dbg != 3) issue_a(g, nxt, 0);
             bar();
             mfma_q(2, afx);
             bar();
             // P4
-            read_a(cur, 3, afy);
-            issue_a(g, nxt, 1);
+            if constexpr (dbg != 4) read_a(cur, 3, afy);
+            if constexpr (dbg != 3) issue_a(g, nxt, 1);
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             bar();
             mfma_q(3, afy);
@@ -805,6 +825,284 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     }
     if (p.stats) {
         float* red = (float*)(smem + EPI);    // [2 groups][BN][2]
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float s = csum[b][r], q = csq[b][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                if (l16 == 0) {
+                    const int c = wc * WCOLS + b * 16 + lg * 4 + r;
+                    red[(grp * BN + c) * 2 + 0] = s;
+                    red[(grp * BN + c) * 2 + 1] = q;
+                }
+            }
+        __syncthreads();
+        if (tid < BN) {
+            const int col = nt * BN + tid;
+            if (col < p.Co) {
+                const double s = (double)red[tid * 2] + (double)red[(BN + tid) * 2];
+                const double q = (double)red[tid * 2 + 1] + (double)red[(BN + tid) * 2 + 1];
+                const int rep = (bid % SCD_STAT_REPLICAS);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
+            }
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// Halo variant of the ping-pong kernel for 3x3 stride-1 convolutions (Conv2d fwd and its dgrad, the
+// head convolution): the 256-pixel tile is a TH x TW block of one image (TW = 32 or 16, TH = 256/TW), the
+// K loop runs channel chunks of 64 (outer) x 9 taps (inner), and each chunk's (TH+2) x (TW+2) input halo is
+// staged in LDS ONCE: all 9 taps read their A fragments from it at a row offset dh*(TW+2)+dw.  Per K-stage
+// the workgroup then moves the BN x 64 weight slab plus 1/9 of a halo (<= 5 KB) instead of BN x 64 + 256 x 64.
+// Phases are N-major: a K-stage has NB phases, phase q multiplies all 8 of the wave's 16-pixel blocks by its
+// 16-channel block q (16 MFMAs), so weight block q of stage t+1 is needed only at phase q of stage t+1 and is
+// fetched at phase q of stage t: ONE weight DMA per wave per phase, a full stage ahead, on two weight buffers.
+// Halo rows of chunk c+1 go out in phase 0 of stages 1..6 of chunk c (dead slots land in a scratch KiB).
+// Waits: every wave keeps the newest NB-1 DMA instructions in flight (vmcnt(NB-1)) before the barrier that
+// opens group 0's next phase (group 0 after its C part, group 1 after its L part).
+template <int BN, int TW>
+__global__ __launch_bounds__(512, 1) void conv_gemm_halo_kernel(GemmParams p) {
+    typedef __bf16 T;
+    constexpr int BM = 256, EPC = 8;
+    constexpr int TH = BM / TW, HW2 = TW + 2;
+    constexpr int HR = (TH + 2) * HW2;               // halo rows
+    constexpr int NK = (HR + 7) / 8;                 // halo DMA wave-instructions per chunk (<= 48)
+    constexpr int HALO = NK * 1024;                  // one halo buffer
+    constexpr int NB = BN / 64, WCOLS = BN / 4;
+    constexpr int BSTAGE = BN * 128;
+    constexpr int DUMMY = 2 * HALO + 2 * BSTAGE;     // 8 x 1 KiB scratch for dead halo slots
+    constexpr int EROW = WCOLS * 2 + 16;
+    constexpr int EPI = 8 * 128 * EROW;
+    constexpr int SMEM = (DUMMY + 8192 > EPI + 4 * BN * 4) ? DUMMY + 8192 : EPI + 4 * BN * 4;
+    static_assert(NK <= 48, "halo");
+    static_assert(SMEM <= 163840, "LDS");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    int bid;
+    {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+    }
+    const scd_gemm_phase& ph = p.ph[0];
+    const int H = p.Ho, W = p.Wo;
+    const int mt = bid / p.ntn;
+    const int nt = bid - mt * p.ntn;
+    const int tw_n = W / TW, th_n = (H + TH - 1) / TH;
+    const int img = mt / (tw_n * th_n);
+    const int trem = mt - img * (tw_n * th_n);
+    const int th = trem / tw_n, tw = trem - (trem / tw_n) * tw_n;
+    const int h0 = th * TH, w0 = tw * TW;
+
+    const int lrow = lane >> 3;
+    const int cch = (lane & 7) ^ lrow;
+    // halo slot sl of this thread: instruction k = 8*sl + wave covers halo rows 8k .. 8k+7; the lane fetches
+    // row 8k+lrow (computed per use: a register array indexed by the runtime slot would live in scratch)
+    auto halo_off = [&](int sl) {
+        const int r = 8 * (8 * sl + wave) + lrow;
+        const int hi = r / HW2, hj = r - (r / HW2) * HW2;
+        const int ih = h0 - 1 + hi, iw = w0 - 1 + hj;
+        const bool ok = r < HR && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        return ok ? (((img * H + ih) * W + iw) * p.Ci + cch * EPC) * 2 : -1;
+    };
+    // weight block q (the 16 channels q of every wave) = LDS rows wc'*WCOLS + 16q + 0..15; this wave fetches
+    // rows wc*WCOLS + 16q + 8*grp + lrow
+    int b_row[NB];
+    bool b_ok[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        const int nn = nt * BN + wc * WCOLS + 16 * q + 8 * grp + lrow;
+        b_ok[q] = nn < p.Co;
+        b_row[q] = b_ok[q] ? nn : 0;
+    }
+    const int cpt = p.Ci / 64;
+    const int KT = 9 * cpt;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+    char* const Bbase = smem + 2 * HALO;
+
+    // halo slot `sl` of chunk c into halo buffer (c & 1); live == false -> the scratch KiB, no traffic
+    auto issue_halo = [&](int c, int sl, bool live) {
+        const int off = halo_off(sl);
+        const bool kl = live && (8 * sl + wave) < NK;
+        char* dst = kl ? smem + (c & 1) * HALO + (8 * sl + wave) * 1024 : smem + DUMMY + wave * 1024;
+        dma16(xrs, dst, sel_off(SCD_ABLATE != 7 && kl && off >= 0, off + c * 128));
+    };
+    auto issue_b = [&](int live, int c, int wt, char* buf, int q) {
+        dma16(wrs, buf + (wc * WCOLS + 16 * q + 8 * grp) * 128,
+              sel_off(SCD_ABLATE != 6 && live && b_ok[q], (b_row[q] * p.wrow + wt * p.Ci + c * 64 + cch * EPC) * 2));
+    };
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int l7 = l16 & 7;
+    const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
+    // centre-tap halo row of the pixel this lane feeds in 16-pixel block a
+    int hr0[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+        const int m = 128 * grp + 16 * a + l16;
+        hr0[a] = (m / TW + 1) * HW2 + (m % TW) + 1;
+    }
+    f32x4 acc[8][NB];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[8][2], bx[2], by[2];
+
+    auto read_a = [&](const char* halo, int toff) {
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+            const int hr = hr0[a] + toff;
+            const char* row = halo + hr * 128;
+            const int x7 = hr & 7;
+            af[a][0] = *(const bf16x8*)(row + (((0 * 4 + lg) ^ x7) << 4));
+            af[a][1] = *(const bf16x8*)(row + (((1 * 4 + lg) ^ x7) << 4));
+        }
+    };
+    auto read_b = [&](const char* Bs, int q, bf16x8 (&bq)[2]) {
+        const char* row = Bs + (wc * WCOLS + q * 16 + l16) * 128;
+        bq[0] = *(const bf16x8*)(row + co0);
+        bq[1] = *(const bf16x8*)(row + co1);
+    };
+    auto mfma_n = [&](int q, const bf16x8 (&bq)[2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SCD_ABLATE == 1 || (SCD_ABM & 1)) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+#pragma unroll
+                for (int a = 0; a < 8; ++a) asm volatile("" ::"v"(af[a][s]));
+                asm volatile("" ::"v"(bq[s]));
+            }
+            return;
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+                acc[a][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s], af[a][s], acc[a][q], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(SCD_ABM & 8)) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto keep_inflight = [&]() {        // all but the newest NB-1 DMA instructions have landed
+        if constexpr (SCD_ABLATE == 8) return;
+        if constexpr (NB == 4) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    };
+
+    if (cpt > 0) {
+        // prologue: the whole halo of chunk 0 and every weight block of stage 0 (tap 0)
+#pragma unroll
+        for (int sl = 0; sl < 6; ++sl) issue_halo(0, sl, true);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) issue_b(1, 0, ph.wt[0], Bbase, q);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if constexpr (SCD_ABM & 4) { read_a(smem, 0); read_b(Bbase, 0, bx); read_b(Bbase, 1, by); }
+        if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
+        int c = 0, tp = 0;
+        for (int t = 0; t < KT; ++t) {
+            const char* halo = smem + (c & 1) * HALO;
+            const char* Bcur = Bbase + (t & 1) * BSTAGE;
+            char* Bnxt = Bbase + ((t & 1) ^ 1) * BSTAGE;
+            const int toff = ph.dh[tp] * HW2 + ph.dw[tp];
+            const int ntp = tp == 8 ? 0 : tp + 1, nc = tp == 8 ? c + 1 : c;
+            const int nlive = t + 1 < KT;
+            const int nwt = ph.wt[ntp];
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                bf16x8 (&bq)[2] = (q & 1) ? by : bx;
+                // L part: fragment reads + this phase's DMA (weight block q of stage t+1; phase 0 also a halo slot)
+                if constexpr (!(SCD_ABM & 4)) {
+                    if (q == 0) read_a(halo, toff);
+                    read_b(Bcur, q, bq);
+                }
+                if constexpr (!(SCD_ABM & 2)) {
+                    issue_b(nlive, nc, nwt, Bnxt, q);
+                    if (q == 0) issue_halo(c + 1, tp - 1, tp >= 1 && tp <= 6 && c + 1 < cpt);
+                }
+                if (grp == 1) keep_inflight();
+                bar();
+                // C part
+                mfma_n(q, bq);
+                if (grp == 0) keep_inflight();
+                bar();
+            }
+            tp = ntp;
+            c = nc;
+        }
+        if (grp == 0) bar();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- epilogue (as conv_gemm_pp_kernel, pixels addressed by tile coordinates)
+    char* ep = smem + wave * 128 * EROW;
+    float csum[NB][4], csq[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
+        float bias[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+            const int m = 128 * grp + a * 16 + l16;
+            const bool valid = h0 + m / TW < H;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[a][b][r] + bias[r];
+                if (p.relu) v[r] = fmaxf(v[r], 0.f);
+                if (valid) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+            }
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+            *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    {
+        constexpr int CPR = WCOLS * 2 / 16;
+        for (int idx = lane; idx < 128 * CPR; idx += 64) {
+            const int row = idx / CPR, ch = idx - (idx / CPR) * CPR;
+            const int m = 128 * grp + row;
+            const int oh = h0 + m / TW, ow = w0 + m % TW;
+            const int col = nt * BN + wc * WCOLS + ch * EPC;
+            if (oh >= H || col >= p.Co) continue;
+            T* dst = (T*)(p.y) + ((long)(img * H + oh) * W + ow) * p.Co + col;
+            uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
+            if (p.accumulate) {
+                float a[EPC], o[EPC];
+                Vec16<T>::load(&v, a);
+                Vec16<T>::load(dst, o);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) a[e] += o[e];
+                Vec16<T>::store(&v, a);
+            }
+            *(uint4*)dst = v;
+        }
+    }
+    if (p.stats) {
+        float* red = (float*)(smem + EPI);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
 #pragma unroll
@@ -1319,6 +1617,15 @@ static int pp_mode() {
     return mode;
 }
 
+static int halo_mode() {
+    static int mode = -2;
+    if (mode == -2) {
+        const char* e = getenv("SCD_GEMM_HALO");
+        mode = e ? atoi(e) : 0;     // opt-in: measured 10% slower than the gather ping-pong kernel on the head convs
+    }
+    return mode;
+}
+
 // BN of the ping-pong kernel for this output width (0 = not applicable)
 static int pp_bn(int dtype, int Co) {
     if (dtype != SCD_DT_BF16 || !pp_mode()) return 0;
@@ -1347,6 +1654,36 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     {
         // ping-pong 256 x BN kernel when the grid fills the chip (fused head tails are run as a separate pass)
         const int bn = pp_bn(dtype, p.Co);
+        // halo variant: one 3x3 stride-1 phase over the whole image, width a multiple of 16
+        const scd_gemm_phase& f = phases[0];
+        bool halo = bn && halo_mode() && nphase == 1 && f.ntaps == 9 && p.is == 1 && p.os == 1 && f.rho_h == 0 &&
+                    f.rho_w == 0 && f.Qh == p.Ho && f.Qw == p.Wo && p.Hi == p.Ho && p.Wi == p.Wo && p.Wo % 16 == 0;
+        for (int t = 0; halo && t < 9; ++t)
+            halo = f.dh[t] >= -1 && f.dh[t] <= 1 && f.dw[t] >= -1 && f.dw[t] <= 1;
+        if (halo) {
+            const int TW = p.Wo % 32 == 0 ? 32 : 16, TH = 256 / TW;
+            const long mtiles = (long)p.N * ((p.Ho + TH - 1) / TH) * (p.Wo / TW);
+            if (mtiles * (p.Co / bn) >= 256) {
+                const long wb = (long)p.Co * p.wrow * esz;
+                if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
+                p.xbytes = (int)xb;
+                p.wbytes = (int)wb;
+                p.ntn = p.Co / bn;
+                p.ph[0] = f;
+                const int tiles = (int)(mtiles * p.ntn);
+                hipStream_t st = (hipStream_t)stream;
+                if (bn == 256 && TW == 32) hipLaunchKernelGGL((conv_gemm_halo_kernel<256, 32>), dim3(tiles), dim3(512), 0, st, p);
+                else if (bn == 256) hipLaunchKernelGGL((conv_gemm_halo_kernel<256, 16>), dim3(tiles), dim3(512), 0, st, p);
+                else if (TW == 32) hipLaunchKernelGGL((conv_gemm_halo_kernel<192, 32>), dim3(tiles), dim3(512), 0, st, p);
+                else hipLaunchKernelGGL((conv_gemm_halo_kernel<192, 16>), dim3(tiles), dim3(512), 0, st, p);
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess || !p.head_on) return (int)e;
+                int nh = 0;
+                while (nh < 4 && p.head_out[nh]) ++nh;
+                return scd_heads_fwd(dtype, p.y, p.N, p.Ho * p.Wo, nh, 128, p.head_od, p.head_w, p.head_b,
+                                     p.head_out, stream);
+            }
+        }
         if (bn && (long)cdiv(Mtot, 256) * (p.Co / bn) >= 256) {
             p.ntn = p.Co / bn;
             int tiles = 0;
@@ -1418,9 +1755,6 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
         static int dbg = -1;
         if (dbg < 0) { const char* e = getenv("SCD_GEMM_DEBUG"); dbg = e ? atoi(e) : 0; }
         p.debug = dbg;
-        static int ti = -1;
-        if (ti < 0) { const char* e = getenv("SCD_GEMM_TAPINNER"); ti = e ? atoi(e) : 1; }
-        p.tapinner = ti;
     }
     for (int h = 0; h < 4; ++h) { p.head_od[h] = 0; p.head_w[h] = nullptr; p.head_b[h] = nullptr; p.head_out[h] = nullptr; }
 }

@@ -73,10 +73,14 @@ def test_conv_fwd_dgrad_wgrad(case, dtype):
     assert rel_err(dw, wr.grad) < TOL[dtype] * 3
 
 
-# shapes large enough (>= 256 tiles of 256 pixels) for the bf16 ping-pong kernel (BN 256 and 192, ragged M)
+# shapes large enough (>= 256 tiles of 256 pixels) for the bf16 ping-pong kernels: halo variant (3x3 s1,
+# width % 16 == 0; BN 256/192, 32- and 16-wide tiles, ragged tile rows, fwd and dgrad) and gather variant
 LARGE_CONV_CASES = [
-    (4, 128, 128, 128, 256, 3, 1, 1),
-    (2, 64, 181, 179, 384, 3, 1, 1),
+    (4, 256, 128, 128, 256, 3, 1, 1),     # halo BN 256 (fwd and dgrad), 8x32 tiles
+    (12, 128, 64, 48, 384, 3, 1, 1),      # halo BN 192, 16x16 tiles
+    (10, 64, 100, 64, 192, 3, 1, 1),      # halo BN 192 fwd, last tile row ragged
+    (10, 192, 100, 64, 64, 3, 1, 1),      # halo BN 192 dgrad, ragged
+    (2, 64, 181, 179, 384, 3, 1, 1),      # gather ping-pong (odd width), ragged M
 ]
 
 
