@@ -405,6 +405,19 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_b
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds_wave_base, 16, off, 0, 0, 0);
 }
 
+// The same LDS-DMA as inline asm: hipcc does not track it, so it emits no conservative vmcnt(0) in front of
+// the ds_read_b64_tr_b16 builtins that follow (it does for its own LDS-DMA).  Completion is counted by hand
+// (s_waitcnt vmcnt(N) + barrier).  M0 is saved and restored inside the statement (it is compiler-reserved).
+__device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, const char* lds_dst, int off) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(off), "s"(lds), "s"(r)
+                 : "memory");
+}
+
 template <bool HEADS>
 __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
     typedef __bf16 T;
@@ -1543,6 +1556,209 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_ring_kernel(WgradParams p) 
     }
 }
 
+// -------------------------------------------------------------------------------------
+// Ping-pong bf16 weight gradient: tile BMG (output-gradient channels, a column slice starting at gc0) x 256
+// (taps x input channels), K = pixels in stages of 32, four LDS stage slots (stage t+2 is fetched while
+// stage t is computed).  8 waves in two staggered groups of 4 (group g owns BMG/2 channels, wave wc 64
+// columns); a stage is 2 phases (one half of the group's channel blocks each), every phase an L part
+// (ds_read_b64_tr_b16 fragment reads + LDS-DMA issue) and a C part (MFMAs), each closed by s_barrier.  Both
+// stage images are [32 pixels][row] with 32-B column pairs XOR-swizzled by f(r) (conflict-free transposed
+// reads; the DMA is lane-linear, so each lane fetches the chunk its slot holds).  Each wave issues n1 + n2
+// DMA instructions per stage (phase 1: n1, phase 2: n2) and keeps the newest n1 + n2 in flight (group 0
+// after its C2, group 1 after its L2: the barrier that opens group 0's read of the next-but-one stage).
+// The MFMA A operand is the input fragment, so each lane ends with 4 consecutive columns of one channel:
+// the fp32 slab is written with 16-B stores straight from the accumulators.
+template <int BMG>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_pp_kernel(WgradParams p, int gc0) {
+    constexpr int KP = 32, EPC = 8;
+    constexpr int GROWB = BMG * 2, XROWB = 512;
+    constexpr int GST = KP * GROWB, STAGE = GST + KP * XROWB;
+    constexpr int NSLOT = 4;
+    constexpr int MB = BMG / 32;                       // 16-channel blocks per wave (8 or 4)
+    constexpr int GI = KP * GROWB / 1024;              // G DMA instructions per stage (16 or 8)
+    constexpr int GR = 1024 / GROWB;                   // G rows per instruction (2 or 4)
+    constexpr int N1 = BMG == 256 ? 2 : 2, N2 = BMG == 256 ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) char smem[NSLOT * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    int z, mt, nt;
+    if (!wgrad_block(p, z, mt, nt)) return;
+    const int M = p.N * p.Ho * p.Wo;
+    const int pix0 = z * p.chunk;
+    const int pix1 = min(M, pix0 + p.chunk);
+    const int gbase = gc0 + mt * BMG;
+
+    // G DMA: BMG=256: instruction k = 2*wave + j (phase 1); BMG=128: k = wave (phase 2).  Row = GR*k + lane/(64/GR).
+    constexpr int NG = BMG == 256 ? 2 : 1;
+    int g_row[NG], g_col[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        const int k = NG * wave + j;
+        const int r = GR * k + lane / (64 / GR);
+        const int slot = lane % (64 / GR);
+        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);
+        g_row[j] = r;
+        g_col[j] = gbase + c * EPC;
+    }
+    // X DMA: instruction k = 2*wave + j (16 per stage), rows 2k + lane/32
+    int x_row[2], x_ci[2], x_dh[2], x_dw[2];
+    bool x_ok[2];
+    int xn[2], xoh[2], xow[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int r = 2 * (2 * wave + j) + (lane >> 5);
+        const int slot = lane & 31;
+        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);
+        const int kk = nt * 256 + c * EPC;
+        x_ok[j] = kk < p.KK;
+        const int tap = x_ok[j] ? kk / p.Ci : 0;
+        x_ci[j] = kk - tap * p.Ci;
+        x_dh[j] = p.dh[tap];
+        x_dw[j] = p.dw[tap];
+        x_row[j] = r;
+        const int pix = pix0 + r;
+        const int HoWo = p.Ho * p.Wo;
+        xn[j] = pix / HoWo;
+        const int rem = pix - xn[j] * HoWo;
+        xoh[j] = rem / p.Wo;
+        xow[j] = rem - xoh[j] * p.Wo;
+    }
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    auto issue_g = [&](int k0, char* slotp) {
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+            const int pix = k0 + g_row[j];
+            dma16_asm(grs, slotp + (GR * (NG * wave + j)) * GROWB, sel_off(pix < pix1, (pix * p.Cg + g_col[j]) * 2));
+        }
+    };
+    auto issue_x = [&](int k0, char* slotp) {
+        char* Xs = slotp + GST;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int pix = k0 + x_row[j];
+            const int ih = p.is * xoh[j] + x_dh[j], iw = p.is * xow[j] + x_dw[j];
+            const bool ok = x_ok[j] && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+            dma16_asm(xrs, Xs + 2 * (2 * wave + j) * XROWB, sel_off(ok, (((xn[j] * p.Hi + ih) * p.Wi + iw) * p.Ci + x_ci[j]) * 2));
+        }
+    };
+    auto advance = [&]() {     // every X row advances by KP pixels
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            xow[j] += KP;
+            while (xow[j] >= p.Wo) {
+                xow[j] -= p.Wo;
+                if (++xoh[j] >= p.Ho) { xoh[j] = 0; ++xn[j]; }
+            }
+        }
+    };
+    // the stage's DMA for phase ph (0/1): BMG=256: G then X; BMG=128: X then G
+    auto issue_phase = [&](int k0, char* slotp, int ph) {
+        if constexpr (BMG == 256) { if (ph == 0) issue_g(k0, slotp); else issue_x(k0, slotp); }
+        else { if (ph == 0) issue_x(k0, slotp); else issue_g(k0, slotp); }
+    };
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int q4 = l16 >> 2, pp = l16 & 3;
+    const int r0 = 8 * lg + q4;
+    const int f0 = wr_f(r0), f1 = wr_f(r0 + 4);
+    f32x4 acc[MB][4];
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    auto trfrag = [&](const char* img, int rowb, int colbyte) {
+        const int pr = colbyte >> 5, lo8 = colbyte & 31;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r0 * rowb + ((pr ^ f0) << 5) + lo8));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (r0 + 4) * rowb + ((pr ^ f1) << 5) + lo8));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    bf16x8 xf[4], gfa[MB / 2], gfb[MB / 2];
+    auto read_x = [&](const char* slotp) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) xf[b] = trfrag(slotp + GST, XROWB, (wc * 64 + b * 16 + 4 * pp) * 2);
+    };
+    auto read_g = [&](const char* slotp, int h, bf16x8 (&gf)[MB / 2]) {
+#pragma unroll
+        for (int a = 0; a < MB / 2; ++a)
+            gf[a] = trfrag(slotp, GROWB, (grp * (BMG / 2) + (h * (MB / 2) + a) * 16 + 4 * pp) * 2);
+    };
+    auto mfma_h = [&](int h, const bf16x8 (&gf)[MB / 2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int a = 0; a < MB / 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                acc[h * (MB / 2) + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[b], gf[a], acc[h * (MB / 2) + a][b], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto keep_inflight = [&]() {
+        if constexpr (N1 + N2 == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    };
+
+    const int nk = (pix1 > pix0) ? (pix1 - pix0 + KP - 1) / KP : 0;
+    if (nk > 0) {
+        // prologue: stages 0 and 1, stage 0 landed
+        issue_phase(pix0, smem, 0);
+        issue_phase(pix0, smem, 1);
+        advance();
+        issue_phase(pix0 + KP, smem + STAGE, 0);
+        issue_phase(pix0 + KP, smem + STAGE, 1);
+        advance();
+        keep_inflight();
+        bar();
+        if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
+        for (int it = 0; it < nk; ++it) {
+            const char* cur = smem + (it & 3) * STAGE;
+            char* nx2 = smem + ((it + 2) & 3) * STAGE;
+            const int k2 = pix0 + (it + 2) * KP;
+            // phase 1
+            read_x(cur);
+            read_g(cur, 0, gfa);
+            issue_phase(k2, nx2, 0);
+            bar();
+            mfma_h(0, gfa);
+            bar();
+            // phase 2
+            read_g(cur, 1, gfb);
+            issue_phase(k2, nx2, 1);
+            advance();
+            if (grp == 1) keep_inflight();
+            bar();
+            mfma_h(1, gfb);
+            if (grp == 0) keep_inflight();
+            bar();
+        }
+        if (grp == 0) bar();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // ---- fp32 partial slab: lane holds columns kk..kk+3 of channel row cg for every (a, b) block
+    float* ws = p.ws + (long)z * p.Cg * p.KK;
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+        const int row = gbase + grp * (BMG / 2) + a * 16 + l16;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int col = nt * 256 + wc * 64 + b * 16 + lg * 4;
+            if (col < p.KK) *(f32x4*)(ws + (long)row * p.KK + col) = acc[a][b];
+        }
+    }
+}
+
 // sums groups of G consecutive split slabs into the group's first slab (first pass of a wide reduce)
 __global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs) {
     const long ngroups = (nsplit + G - 1) / G;
@@ -1800,6 +2016,15 @@ static bool wgrad_use_ring(int dtype, long M, int Cg) {
     return mode == 1;
 }
 
+// ping-pong weight gradient (bf16, output-gradient channels a multiple of 128, enough pixels): column
+// slices of 256 (+ one of 128), 256-wide column tiles of taps x channels
+static bool wgrad_use_pp(int dtype, long M, int Cg, int KK) {
+    static int mode = -2;
+    // opt-in (SCD_WGRAD_PP=1): correct, but measured 10-40% slower than conv_wgrad_kernel at every Res10 shape
+    if (mode == -2) { const char* e = getenv("SCD_WGRAD_PP"); mode = e ? atoi(e) : 0; }
+    return mode && dtype == SCD_DT_BF16 && Cg >= 128 && Cg % 128 == 0 && KK >= 128 && M >= 8 * 1024;
+}
+
 static void wgrad_tile(int dtype, long M, int Cg, int& tm, int& tn) {
     if (wgrad_use_ring(dtype, M, Cg)) { tm = 128; tn = 256; }
     else if (Cg <= 64) { tm = 64; tn = 256; }
@@ -1807,6 +2032,15 @@ static void wgrad_tile(int dtype, long M, int Cg, int& tm, int& tn) {
 }
 
 extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
+    if (wgrad_use_pp(dtype, M, Cg, T * Ci)) {
+        // about three rounds of one-per-CU workgroups, whole XCD groups of splits, >= 1024 pixels per split,
+        // fp32 slabs capped at 192 MB
+        const long tiles = (long)cdiv(Cg, 256) * cdiv((long)T * Ci, 256);
+        long ns = std::max(8L, (768L / tiles) / 8 * 8);
+        ns = std::min(ns, std::max(8L, M / 1024 / 8 * 8));
+        ns = std::min(ns, std::max(8L, (192L << 20) / std::max(1L, 4L * Cg * T * Ci) / 8 * 8));
+        return (int)ns;
+    }
     int tm, tn;
     wgrad_tile(dtype, M, Cg, tm, tn);
     const long tiles = (long)cdiv(Cg, tm) * cdiv((long)T * Ci, tn);
@@ -1840,6 +2074,24 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     int chunk = cdiv(M, nsplit);
     chunk = (chunk + 63) / 64 * 64;
     p.chunk = chunk;
+    if (wgrad_use_pp(dtype, M, Cg, p.KK)) {
+        hipStream_t st = (hipStream_t)stream;
+        p.ntn = cdiv(p.KK, 256);
+        p.nsplit = nsplit;
+        const int n8 = (nsplit + 7) / 8 * 8;
+        const int nfull = Cg / 256;
+        if (nfull > 0) {
+            p.ntm = nfull;
+            hipLaunchKernelGGL((conv_wgrad_pp_kernel<256>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p, 0);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return (int)e;
+        }
+        if (Cg % 256) {
+            p.ntm = 1;
+            hipLaunchKernelGGL((conv_wgrad_pp_kernel<128>), dim3(p.ntn * n8), dim3(512), 0, st, p, Cg - 128);
+        }
+        SCD_RETURN_LAUNCH();
+    }
     int BM, BN;
     wgrad_tile(dtype, M, Cg, BM, BN);
     p.ntm = cdiv(Cg, BM);
