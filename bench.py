@@ -59,7 +59,7 @@ def cpu_baseline(steps):
                       "after 1 warm-up (%.1f s)" % (steps, dt)}
 
 
-HEADS_KERNEL = "conv_gemm_ring_kernel<bf16,256,128,heads>"
+HEADS_KERNEL = "conv_gemm_pp_kernel<bf16,256,192,heads>"
 
 
 def pmc_traffic(kernel, batch, dtype):

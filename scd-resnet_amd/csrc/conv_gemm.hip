@@ -573,7 +573,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
 // 2 (NB2), P3 own A rows 0..63 (2), P4 own A rows 64..127 (2); counted waits: end of L4 vmcnt(4)
 // (both B parts of t+1 landed), end of C4 vmcnt(2) (A rows 0..63), end of C2 vmcnt(2+NB2) (A rows
 // 64..127 of stage t).  Every region is rewritten >= 3 phases after its last fragment read.
-template <int BN>
+template <int BN, bool HEADS>
 __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     typedef __bf16 T;
     constexpr int BM = 256, BK = 64, EPC = 8;
@@ -860,6 +860,63 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                 const int rep = (bid % SCD_STAT_REPLICAS);
                 atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
                 atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
+            }
+        }
+    }
+    if constexpr (HEADS) {
+        // fused CenterNet tails (centerNetOffset.py:108-110): out_h[o] = b1_h[o] + sum_j w1_h[o][j] * hid[128h + j]
+        // from the staged tile.  Thread pair (2r, 2r+1) takes pixel r, each half BN/2 of the tile's channels; a
+        // head split between two column tiles gets two partial sums, added onto its zeroed output (two
+        // commutative fp32 adds onto 0: the same bits in either order).
+        __syncthreads();
+        const int r = tid >> 1, half = tid & 1;
+        const int g = r >> 7, row = r & 127;
+        const int hbase = (nt * BN) >> 7;
+        const float* wA = p.head_w[hbase];
+        const float* wB = hbase + 1 < 4 ? p.head_w[hbase + 1] : nullptr;
+        float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cc = 0; cc < BN / 2; cc += EPC) {
+            const int c = half * (BN / 2) + cc;                // tile channel
+            const int wv = c / WCOLS, cl = c - (c / WCOLS) * WCOLS;
+            float v[EPC];
+            Vec16<T>::load(smem + (4 * g + wv) * 128 * EROW + row * EROW + cl * 2, v);
+            const int gc = nt * BN + c;
+            const int hs = (gc >> 7) - hbase, j = gc & 127;
+            const int od = p.head_od[hbase + hs];
+            const float* w = hs ? wB : wA;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (o < od) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) a += v[e] * w[o * 128 + j + e];
+                    if (hs) a1[o] += a; else a0[o] += a;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o) { a0[o] += __shfl_xor(a0[o], 1, 64); a1[o] += __shfl_xor(a1[o], 1, 64); }
+        const int m = mt * BM + r;
+        if (half == 0 && m < M) {
+            const int n = m / QQ;
+            const int rem = m - n * QQ;
+            const int oh = rem / ph.Qw, ow = rem - (rem / ph.Qw) * ph.Qw;
+            const long HWo = (long)p.Ho * p.Wo;
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs) {
+                const int h = hbase + hs;
+                if (h >= 4 || !p.head_out[h] || h * 128 >= nt * BN + BN) continue;
+                const int od = p.head_od[h];
+                const bool first = h * 128 >= nt * BN, full = first && h * 128 + 128 <= nt * BN + BN;
+#pragma unroll
+                for (int o = 0; o < 4; ++o) {
+                    if (o >= od) continue;
+                    const float val = (hs ? a1[o] : a0[o]) + (first ? p.head_b[h][o] : 0.f);
+                    float* dst = p.head_out[h] + ((long)n * od + o) * HWo + (long)oh * p.Wo + ow;
+                    if (full) *dst = val;
+                    else atomic_add_f32(dst, val);
+                }
             }
         }
     }
@@ -1444,14 +1501,14 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_ring_kernel(WgradParams p) 
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int pix = k0 + g_row[i];
-            dma16(grs, Gs + (8 * wave + 4 * i) * GROWB, sel_off(g_ok[i] && pix < pix1, (pix * p.Cg + g_off[i]) * 2));
+            dma16_asm(grs, Gs + (8 * wave + 4 * i) * GROWB, sel_off(g_ok[i] && pix < pix1, (pix * p.Cg + g_off[i]) * 2));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int pix = k0 + x_row[i];
             const int ih = p.is * xoh[i] + x_dh[i], iw = p.is * xow[i] + x_dw[i];
             const bool ok = x_ok[i] && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-            dma16(xrs, Xs + (8 * wave + 2 * i) * XROWB,
+            dma16_asm(xrs, Xs + (8 * wave + 2 * i) * XROWB,
                   sel_off(ok, (((xn[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + x_ci[i]) * 2));
         }
     };
@@ -1916,14 +1973,20 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
             p.xbytes = (int)xb;
             p.wbytes = (int)wb;
             hipStream_t st = (hipStream_t)stream;
-            if (bn == 256) hipLaunchKernelGGL((conv_gemm_pp_kernel<256>), dim3(tiles), dim3(512), 0, st, p);
-            else hipLaunchKernelGGL((conv_gemm_pp_kernel<192>), dim3(tiles), dim3(512), 0, st, p);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess || !p.head_on) return (int)e;
-            int nh = 0;
-            while (nh < 4 && p.head_out[nh]) ++nh;
-            return scd_heads_fwd(dtype, p.y, p.N, p.Ho * p.Wo, nh, 128, p.head_od, p.head_w, p.head_b,
-                                 p.head_out, stream);
+            if (p.head_on) {
+                // heads split between two column tiles accumulate two partial sums: zero them first
+                for (int h = 0; h < 4 && p.head_out[h]; ++h)
+                    if ((h * 128) / bn != (h * 128 + 127) / bn) {
+                        hipError_t e = hipMemsetAsync(p.head_out[h], 0, sizeof(float) * p.head_od[h] * (size_t)p.N * p.Ho * p.Wo, st);
+                        if (e != hipSuccess) return (int)e;
+                    }
+                if (bn == 256) hipLaunchKernelGGL((conv_gemm_pp_kernel<256, true>), dim3(tiles), dim3(512), 0, st, p);
+                else hipLaunchKernelGGL((conv_gemm_pp_kernel<192, true>), dim3(tiles), dim3(512), 0, st, p);
+            } else {
+                if (bn == 256) hipLaunchKernelGGL((conv_gemm_pp_kernel<256, false>), dim3(tiles), dim3(512), 0, st, p);
+                else hipLaunchKernelGGL((conv_gemm_pp_kernel<192, false>), dim3(tiles), dim3(512), 0, st, p);
+            }
+            SCD_RETURN_LAUNCH();
         }
     }
     bool ring = false;

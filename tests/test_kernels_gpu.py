@@ -121,6 +121,42 @@ def test_deconv_fwd_dgrad_wgrad(case, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N", [1, 2])
+def test_heads_fused_gemm(N, dtype):
+    """scd_conv_gemm_heads (3x3 conv + bias + ReLU with the three 1x1 tails in the epilogue) against
+    torch fp32; N=2 runs the bf16 ping-pong kernel, whose 192-wide column tiles split head 1 (two partial
+    sums added onto its zeroed output)."""
+    from scdhip import ops
+    L = ops.L
+    g = torch.Generator().manual_seed(31 + N)
+    Cin, H, W, od = 256, 128, 128, [1, 4, 2]
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w0 = [torch.randn(128, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5 for _ in od]
+    b0 = [0.1 * torch.randn(128, generator=g) for _ in od]
+    w1 = [torch.randn(o, 128, 1, 1, generator=g) / 128 ** 0.5 for o in od]
+    b1 = [0.1 * torch.randn(o, generator=g) for o in od]
+    if dtype == torch.bfloat16:
+        x = x.bfloat16().float()
+        w0 = [w.bfloat16().float() for w in w0]
+    refs = [F.conv2d(F.relu(F.conv2d(x, a, b, padding=1)), c, d) for a, b, c, d in zip(w0, b0, w1, b1)]
+    xg = nhwc(x, dtype)
+    w0c = torch.cat(w0, 0).to(DEV)
+    wp = ops.pack_weight(w0c, dtype, 0)
+    b0c = torch.cat(b0, 0).to(DEV)
+    w1d = [w.to(DEV).contiguous() for w in w1]
+    b1d = [b.to(DEV) for b in b1]
+    outs = [torch.full((N, o, H, W), float("nan"), device=DEV) for o in od]
+    hid = torch.empty(N, H, W, 128 * len(od), device=DEV, dtype=dtype)
+    L.call("scd_conv_gemm_heads", ops.dt(xg), ops.ptr(xg), ops.ptr(wp), ops.ptr(hid), ops.ptr(b0c), N, H, W, Cin,
+           len(od), L.int_array(od), L.ptr_array([w.data_ptr() for w in w1d]),
+           L.ptr_array([b.data_ptr() for b in b1d]), L.ptr_array([o.data_ptr() for o in outs]), ops.stream())
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.isfinite(o).all()
+        assert rel_err(o, r) < TOL[dtype] * (3 if dtype == torch.bfloat16 else 10)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_stem_im2col_gemm_pool(dtype):
     from scdhip import ops
     g = torch.Generator().manual_seed(3)

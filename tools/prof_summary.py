@@ -20,6 +20,12 @@ def short(name):
     if m:
         return "%s<%s>" % (m.group(1), "bf16" if m.group(2) == "DF16b" else "f32")
     n = n.replace("(anonymous namespace)::", "")
+    m = re.search(r"conv_gemm_pp_kernel<(\d+)(, (true|false))?>", n)
+    if m:
+        return "conv_gemm_pp_kernel<bf16,256,%s%s>" % (m.group(1), ",heads" if m.group(3) == "true" else "")
+    m = re.search(r"(conv_gemm_halo_kernel|conv_wgrad_pp_kernel)<([\d, ]+)>", n)
+    if m:
+        return "%s<%s>" % (m.group(1), m.group(2).replace(" ", ""))
     m = re.search(r"conv_gemm_ring_kernel(ILb([01])E|<(true|false)>)", n)
     if m:
         return "conv_gemm_ring_kernel<bf16,256,128%s>" % (",heads" if m.group(2) == "1" or m.group(3) == "true" else "")
