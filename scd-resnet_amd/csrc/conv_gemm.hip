@@ -1232,7 +1232,12 @@ __device__ __forceinline__ int wswz(int row, int byte, int stride) {
     return row * stride + (byte ^ (((row >> 3) & 1) << 7));
 }
 
-template <typename T, int BM, int BN>
+// FASTX: a KP-pixel stage never straddles an image and covers either part of one output row (Wo % KP == 0)
+// or whole rows (KP % Wo == 0).  The stage position (n, oh, ow) is then workgroup-uniform (scalar registers)
+// and every X slot's gather offset is that stage base plus a per-lane constant: a few VALU per load instead
+// of the per-row decomposition (the generic path is VALU-issue-bound: ~250 address instructions per stage
+// against 32 MFMAs per wave).
+template <typename T, int BM, int BN, bool FASTX>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;
@@ -1276,6 +1281,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     int xn[XCH], xoh[XCH], xow[XCH];
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
+        xn[i] = xoh[i] = xow[i] = 0;
+        if constexpr (FASTX) continue;
         const int pix = pix0 + xr0 + i * XRS;
         const int HoWo = p.Ho * p.Wo;
         xn[i] = pix / HoWo;
@@ -1283,13 +1290,49 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
         xoh[i] = rem / p.Wo;
         xow[i] = rem - xoh[i] * p.Wo;
     }
-    auto advance = [&]() {     // every row advances by KP pixels
+    // FASTX: stage cursor (uniform) and per-slot constants
+    int sn = 0, soh = 0, sow = 0;
+    int xA[XCH], xB[XCH], xL[XCH];
+    if constexpr (FASTX) {
+        const int HoWo = p.Ho * p.Wo;
+        sn = __builtin_amdgcn_readfirstlane(pix0 / HoWo);
+        const int rem = pix0 - sn * HoWo;
+        soh = __builtin_amdgcn_readfirstlane(rem / p.Wo);
+        sow = __builtin_amdgcn_readfirstlane(rem - soh * p.Wo);
 #pragma unroll
         for (int i = 0; i < XCH; ++i) {
-            xow[i] += KP;
-            while (xow[i] >= p.Wo) {
-                xow[i] -= p.Wo;
-                if (++xoh[i] >= p.Ho) { xoh[i] = 0; ++xn[i]; }
+            const int rr = xr0 + i * XRS;
+            const int doh = p.Wo >= KP ? 0 : rr / p.Wo, dow = p.Wo >= KP ? rr : rr - (rr / p.Wo) * p.Wo;
+            xA[i] = p.is * doh + dh;
+            xB[i] = p.is * dow + dw;
+            xL[i] = (xA[i] * p.Wi + xB[i]) * p.Ci + ci;
+        }
+    }
+    auto advance = [&]() {     // every row advances by KP pixels
+        if constexpr (FASTX) {
+            if (p.Wo >= KP) {
+                sow += KP;
+                const bool wrap = sow >= p.Wo;
+                sow = wrap ? 0 : sow;
+                soh += wrap ? 1 : 0;
+            } else {
+                soh += KP / p.Wo;
+            }
+            const bool wrap2 = soh >= p.Ho;
+            soh = wrap2 ? 0 : soh;
+            sn += wrap2 ? 1 : 0;
+            // workgroup-uniform: keep the cursor in scalar registers
+            sn = __builtin_amdgcn_readfirstlane(sn);
+            soh = __builtin_amdgcn_readfirstlane(soh);
+            sow = __builtin_amdgcn_readfirstlane(sow);
+        } else {
+#pragma unroll
+            for (int i = 0; i < XCH; ++i) {
+                xow[i] += KP;
+                while (xow[i] >= p.Wo) {
+                    xow[i] -= p.Wo;
+                    if (++xoh[i] >= p.Ho) { xoh[i] = 0; ++xn[i]; }
+                }
             }
         }
     };
@@ -1297,16 +1340,35 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
     auto gload = [&](int k0, uint4 (&rg)[GCH], uint4 (&rx)[XCH]) {
+        if constexpr (FASTX) {
+            const int S = __builtin_amdgcn_readfirstlane(((sn * p.Hi + p.is * soh) * p.Wi + p.is * sow) * p.Ci);
+            const int ihs = __builtin_amdgcn_readfirstlane(p.is * soh), iws = __builtin_amdgcn_readfirstlane(p.is * sow);
+            const int kr = pix1 - k0;        // rows of this stage inside the split
+            const int gS = __builtin_amdgcn_readfirstlane(k0 * p.Cg);
+#pragma unroll
+            for (int i = 0; i < GCH; ++i) {
+                const int r = gr0 + i * GRS;
+                rg[i] = bload(grs, sel_off(gcol_ok & (r < kr), (gS + r * p.Cg + gcol) * ESZ));
+            }
+#pragma unroll
+            for (int i = 0; i < XCH; ++i) {
+                // non-short-circuit &: straight-line selects, no exec-masked branches around the loads
+                const bool ok = kk_ok & (xr0 + i * XRS < kr) & ((unsigned)(ihs + xA[i]) < (unsigned)p.Hi) &
+                                ((unsigned)(iws + xB[i]) < (unsigned)p.Wi);
+                rx[i] = bload(xrs, sel_off(ok, (S + xL[i]) * ESZ));
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < GCH; ++i) {
             const int pix = k0 + gr0 + i * GRS;
-            rg[i] = bload(grs, sel_off(gcol_ok && pix < pix1, (pix * p.Cg + gcol) * ESZ));
+            rg[i] = bload(grs, sel_off(SCD_ABLATE != 22 && gcol_ok && pix < pix1, (pix * p.Cg + gcol) * ESZ));
         }
 #pragma unroll
         for (int i = 0; i < XCH; ++i) {
             const int pix = k0 + xr0 + i * XRS;
             const int ih = p.is * xoh[i] + dh, iw = p.is * xow[i] + dw;
-            const bool ok = kk_ok && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+            const bool ok = SCD_ABLATE != 22 && kk_ok && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
             rx[i] = bload(xrs, sel_off(ok, (((xn[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + ci) * ESZ));
         }
     };
@@ -1339,6 +1401,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
         for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     auto compute = [&](int buf) {
+        if constexpr (SCD_ABLATE == 23) return;      // ablation: no fragment reads, no MFMA
         const char* Gs = smem + buf * STAGE;
         const char* Xs = Gs + KP * GROW;
         if constexpr (ESZ == 2) {
@@ -1366,11 +1429,19 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
                     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                     bfr[b] = __builtin_bit_cast(bf16x8, v);
                 }
+                if constexpr (SCD_ABLATE == 21) {
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) { asm volatile("" ::"v"(af[a])); asm volatile("" ::"v"(bfr[a])); }
+                } else {
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 4; ++b)
                         acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+                }
+                // FASTX frees the address registers the hoisted fragment reads of the next k-step would take:
+                // keep one k-step of fragments live at a time (256-VGPR budget at two workgroups per CU)
+                if constexpr (FASTX) __builtin_amdgcn_sched_barrier(0);
             }
         } else {
 #pragma unroll
@@ -2088,6 +2159,12 @@ static bool wgrad_use_pp(int dtype, long M, int Cg, int KK) {
     return mode && dtype == SCD_DT_BF16 && Cg >= 128 && Cg % 128 == 0 && KK >= 128 && M >= 8 * 1024;
 }
 
+static bool wgrad_fastx() {
+    static int mode = -2;
+    if (mode == -2) { const char* e = getenv("SCD_WGRAD_FASTX"); mode = e ? atoi(e) : 1; }
+    return mode != 0;
+}
+
 static void wgrad_tile(int dtype, long M, int Cg, int& tm, int& tn) {
     if (wgrad_use_ring(dtype, M, Cg)) { tm = 128; tn = 256; }
     else if (Cg <= 64) { tm = 64; tn = 256; }
@@ -2164,12 +2241,26 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     hipStream_t st = (hipStream_t)stream;
     if (wgrad_use_ring(dtype, M, Cg)) {
         hipLaunchKernelGGL(conv_wgrad_ring_kernel, grid, dim3(512), 0, st, p);
-    } else if (dtype == SCD_DT_BF16) {
-        if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128>), grid, dim3(256), 0, st, p);
-    } else if (dtype == SCD_DT_F32) {
-        if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128>), grid, dim3(256), 0, st, p);
+    } else if (dtype == SCD_DT_BF16 || dtype == SCD_DT_F32) {
+        // fast addressing when a stage of KP pixels stays inside one image and one row block
+        const int KP = dtype == SCD_DT_BF16 ? 64 : 32;
+        const bool fast = wgrad_fastx() && (Wo % KP == 0 || KP % Wo == 0) && ((long)Ho * Wo) % KP == 0 && chunk % KP == 0;
+        if (dtype == SCD_DT_BF16) {
+            // (the 128 x 128 tile spills at 256 VGPRs with FASTX: generic addressing there)
+            if (fast && Cg <= 64) {
+                hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, true>), grid, dim3(256), 0, st, p);
+            } else {
+                if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, false>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, false>), grid, dim3(256), 0, st, p);
+            }
+        } else {
+            if (fast && Cg <= 64) {
+                hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, true>), grid, dim3(256), 0, st, p);
+            } else {
+                if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, false>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, false>), grid, dim3(256), 0, st, p);
+            }
+        }
     } else {
         return SCD_ERR_ARG;
     }
