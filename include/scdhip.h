@@ -93,6 +93,19 @@ int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, i
 int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int H, int W, int Ho, int Wo, int kh,
                     int kw, int stride, int pad, int Kpad, void* stream);
 
+/* Direct stem convolution (bf16): Conv2d(1,64,7,stride 2,pad 3,no bias) of residuals.py:211 with the
+ * [pixel][tap] tile built in LDS from the input patch (no column tensor in HBM); wpk = the [64][64] packed
+ * weight (pack_weight mode 0, ldp 64); y (N,Ho,Wo,64) NHWC; stats as scd_conv_gemm (may be NULL).
+ * Requires Wo % 128 == 0 and Ho % 2 == 0. */
+int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H, int W,
+                      int Ho, int Wo, void* stream);
+/* Its weight gradient: ws[z][co][k] (fp32, nsplit x 64 x 64) = sum over split z's pixels of
+ * dy[pix][co] * col[pix][k]; reduce with scd_wgrad_reduce(ws, nsplit, 64, 1, 64, ..., cvalid = 49).
+ * Requires Wo % 64 == 0. */
+int scd_stem_conv_wgrad_nsplit(long M);
+int scd_stem_conv_wgrad(int dtype, const void* dy, const float* x, float* ws, int nsplit, int N, int H, int W,
+                        int Ho, int Wo, void* stream);
+
 /* ---- training BatchNorm2d (residuals.py:92,95,212,262,306; momentum 0.1, eps 1e-5) ---- */
 /* sum replicas [nrep][2][C] -> [2][C] in place (replica 0); used before a SyncBN all-reduce */
 int scd_stats_collapse(double* stats, int nrep, int C, void* stream);

@@ -43,16 +43,24 @@ class StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, conv, bn, dtype):
         training = bn.training
-        cols = ops.im2col_stem(x, dtype, kh=conv.weight.shape[2], kw=conv.weight.shape[3],
-                               stride=conv.stride[0], pad=conv.padding[0])
         C = conv.weight.shape[0]
-        wp = ops.pack_weight(conv.weight, dtype, 0, ldp=cols.shape[-1])
         stats = ops.bn_stats(bn, "fwd") if training else None
-        y = ops.conv_fwd(cols, wp, C, 1, 1, 1, 0, stats=stats)
+        direct = (ops.stem_direct_ok(x, dtype) and tuple(conv.weight.shape) == (64, 1, 7, 7)
+                  and conv.stride[0] == 2 and conv.padding[0] == 3)
+        if direct:
+            # direct 7x7/s2 conv: the tap tile is built in LDS from the input patch (no column tensor)
+            x = _c(x)
+            y = ops.stem_conv_fwd(x, ops.pack_weight(conv.weight, dtype, 0, ldp=64), stats=stats)
+            cols = x
+        else:
+            cols = ops.im2col_stem(x, dtype, kh=conv.weight.shape[2], kw=conv.weight.shape[3],
+                                   stride=conv.stride[0], pad=conv.padding[0])
+            wp = ops.pack_weight(conv.weight, dtype, 0, ldp=cols.shape[-1])
+            y = ops.conv_fwd(cols, wp, C, 1, 1, 1, 0, stats=stats)
         st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
         out, am = ops.stem_pool_fwd(y, st)
         ctx.save_for_backward(cols, y, am)
-        ctx.st, ctx.conv, ctx.bn = st, conv, bn
+        ctx.st, ctx.conv, ctx.bn, ctx.direct = st, conv, bn, direct
         return out
 
     @staticmethod
@@ -61,8 +69,11 @@ class StemFn(torch.autograd.Function):
         conv, bn, st = ctx.conv, ctx.bn, ctx.st
         dz = ops.stem_pool_bwd(_c(dout), am, y, st)
         dy = ops.bn_backward(bn, st, dz, y)
-        T = conv.weight.shape[2] * conv.weight.shape[3]
-        ops.conv_wgrad(dy, cols, 1, 1, 1, 0, ops.grad_of(conv.weight), (T, 1, 0), cvalid=T)
+        if ctx.direct:
+            ops.stem_conv_wgrad(dy, cols, ops.grad_of(conv.weight))
+        else:
+            T = conv.weight.shape[2] * conv.weight.shape[3]
+            ops.conv_wgrad(dy, cols, 1, 1, 1, 0, ops.grad_of(conv.weight), (T, 1, 0), cvalid=T)
         return None, None, None, None, None
 
 

@@ -49,6 +49,9 @@ SIGNATURES = {
     "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, P]),
     "scd_pack_weight": (I, [I, P, P, I, I, I, I, I, I, P]),
     "scd_im2col_stem": (I, [I, P, P, I, I, I, I, I, I, I, I, I, I, P]),
+    "scd_stem_conv_fwd": (I, [I, P, P, P, P, I, I, I, I, I, P]),
+    "scd_stem_conv_wgrad_nsplit": (I, [L]),
+    "scd_stem_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, P]),
     "scd_stats_collapse": (I, [P, I, I, P]),
     "scd_bn_finalize": (I, [P, I, I, D, P, P, P, P, P, F, F, P, P, P, P, P]),
     "scd_bn_apply": (I, [I, P, P, I, L, P, P, P, P, P, I, P]),

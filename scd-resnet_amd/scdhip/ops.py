@@ -317,6 +317,34 @@ def im2col_stem(x, dtype, kh=7, kw=7, stride=2, pad=3, Kpad=64):
     return cols
 
 
+def stem_direct_ok(x, dtype):
+    """The direct stem kernels (bf16; Conv2d(1,64,7,s2,p3) with an output width that is a multiple of 128)."""
+    N, _, H, W = x.shape
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    return dtype == torch.bfloat16 and Wo % 128 == 0 and Ho % 2 == 0
+
+
+def stem_conv_fwd(x, wpk, stats=None):
+    """Conv2d(1,64,7,s2,p3) of NCHW fp32 x -> (N,Ho,Wo,64) bf16 NHWC (+BN sums); wpk = pack_weight(w, bf16, 0, ldp=64)."""
+    _need_gpu(x)
+    N, _, H, W = x.shape
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    y = torch.empty(N, Ho, Wo, 64, dtype=torch.bfloat16, device=x.device)
+    L.call("scd_stem_conv_fwd", L.DT_BF16, ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo, stream())
+    return y
+
+
+def stem_conv_wgrad(dy, x, dst, accumulate=True):
+    """dst (64,1,7,7) fp32 (+)= weight gradient of the stem conv from dy (N,Ho,Wo,64) bf16 and the input x."""
+    N, _, H, W = x.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    M = N * Ho * Wo
+    ns = L.lib().scd_stem_conv_wgrad_nsplit(M)
+    ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=dy.device)
+    L.call("scd_stem_conv_wgrad", L.DT_BF16, ptr(dy), ptr(x), ptr(ws), ns, N, H, W, Ho, Wo, stream())
+    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 49, 49, 1, 0, ptr(dst), int(accumulate), stream())
+
+
 def stem_pool_fwd(y, st):
     N, H, W, C = y.shape
     Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1

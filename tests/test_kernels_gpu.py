@@ -170,6 +170,32 @@ def test_stem_im2col_gemm_pool(dtype):
     assert rel_err(nchw(y), yr) < TOL[dtype]
 
 
+@pytest.mark.parametrize("shape", [(2, 512, 512), (1, 260, 256)])
+def test_stem_direct_bf16(shape):
+    """Direct stem conv (tap tile built in LDS) forward + BN sums and its weight gradient vs torch fp32."""
+    from scdhip import ops
+    N, H, W = shape
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, 1, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).bfloat16().float()
+    xr = x.clone()
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=2, padding=3)
+    dy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    yr.backward(dy)
+    xd = x.to(DEV)
+    assert ops.stem_direct_ok(xd, torch.bfloat16)
+    stats = ops.new_stats(64, DEV)
+    y = ops.stem_conv_fwd(xd, ops.pack_weight(w.to(DEV), torch.bfloat16, 0, ldp=64), stats=stats)
+    assert rel_err(nchw(y), yr) < TOL[torch.bfloat16]
+    st = stats.view(-1, 2, 64).sum(0).cpu()
+    yd = yr.detach().double()
+    np.testing.assert_allclose(st[0].numpy(), yd.sum((0, 2, 3)).numpy(), rtol=1e-3, atol=1e-2 * yd.numel() ** 0.5)
+    dw = torch.full((64, 1, 7, 7), 0.25, device=DEV)
+    ops.stem_conv_wgrad(nhwc(dy, torch.bfloat16), xd, dw, accumulate=True)
+    assert rel_err(dw - 0.25, wr.grad) < TOL[torch.bfloat16] * 3
+
+
 def test_cpool_fwd_bwd_fp32():
     from scdhip import ops
     g = torch.Generator().manual_seed(5)

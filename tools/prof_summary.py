@@ -14,7 +14,9 @@ def short(name):
     n = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", name)
     m = re.match(r"(\w+?)I(DF16b|f)Li(\d+)ELi(\d+)E(Lb([01])E)?", n)
     if m:
-        tail = ",heads" if m.group(6) == "1" else ""
+        tail = ""
+        if m.group(6) == "1":
+            tail = ",fastx" if m.group(1).startswith("conv_wgrad") else ",heads"
         return "%s<%s,%s,%s%s>" % (m.group(1), "bf16" if m.group(2) == "DF16b" else "f32", m.group(3), m.group(4), tail)
     m = re.match(r"(\w+?)I(DF16b|f)E", n)
     if m:
