@@ -88,6 +88,20 @@ int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0,
 int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp,
                     int row_off, void* stream);
 
+/* Batched weight packing: all operand layouts of one training step in one launch.  descs (device memory)
+ * are sorted by start; descriptor d covers elements [start, start + count) of the concatenated index space:
+ * mode 0: out[row_off + a][t*B + b] = w[a][b][t], count = A * ldp (k >= T*B zero-filled);
+ * mode 1: out[b][t*a_tot + a_off + a] = w[a][b][t], count = B * T * A (a slice of a concatenated
+ * operand when a_tot > A).  Every start (and total) is a multiple of 4096 elements.  Replaces one
+ * scd_pack_weight launch per conv and direction. */
+typedef struct scd_pack_desc {
+    const float* w;
+    void* out;
+    long start;
+    int A, B, T, mode, ldp, row_off, a_off, a_tot;
+} scd_pack_desc;
+int scd_pack_weights_batched(int dtype, const scd_pack_desc* descs, int n, long total, void* stream);
+
 /* Stem im2col: x (N,1,H,W) fp32 -> cols (N,Ho,Wo,Kpad) dtype, taps kh*kw zero-padded to Kpad.
  * Feeds residuals.py:211 (Conv2d(1,64,7,s2,p3)) to the MFMA GEMM as a 1x1 conv. */
 int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int H, int W, int Ho, int Wo, int kh,

@@ -1237,7 +1237,7 @@ __device__ __forceinline__ int wswz(int row, int byte, int stride) {
 // and every X slot's gather offset is that stage base plus a per-lane constant: a few VALU per load instead
 // of the per-row decomposition (the generic path is VALU-issue-bound: ~250 address instructions per stage
 // against 32 MFMAs per wave).
-template <typename T, int BM, int BN, bool FASTX>
+template <typename T, int BM, int BN, int FASTX>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;
@@ -1282,7 +1282,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
         xn[i] = xoh[i] = xow[i] = 0;
-        if constexpr (FASTX) continue;
+        if constexpr (FASTX != 0) continue;
         const int pix = pix0 + xr0 + i * XRS;
         const int HoWo = p.Ho * p.Wo;
         xn[i] = pix / HoWo;
@@ -1292,25 +1292,28 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     }
     // FASTX: stage cursor (uniform) and per-slot constants
     int sn = 0, soh = 0, sow = 0;
-    int xA[XCH], xB[XCH], xL[XCH];
-    if constexpr (FASTX) {
+    // FASTX 1 (Wo % KP == 0): a stage is part of one output row, slot i sits XRS*i pixels right of slot 0, so one
+    // base value per quantity suffices (3 VGPRs); FASTX 2 (KP % Wo == 0): whole rows, per-slot constants
+    constexpr int NXS = FASTX == 2 ? XCH : 1;
+    int xA[NXS], xB[NXS], xL[NXS];
+    if constexpr (FASTX != 0) {
         const int HoWo = p.Ho * p.Wo;
         sn = __builtin_amdgcn_readfirstlane(pix0 / HoWo);
         const int rem = pix0 - sn * HoWo;
         soh = __builtin_amdgcn_readfirstlane(rem / p.Wo);
         sow = __builtin_amdgcn_readfirstlane(rem - soh * p.Wo);
 #pragma unroll
-        for (int i = 0; i < XCH; ++i) {
+        for (int i = 0; i < NXS; ++i) {
             const int rr = xr0 + i * XRS;
-            const int doh = p.Wo >= KP ? 0 : rr / p.Wo, dow = p.Wo >= KP ? rr : rr - (rr / p.Wo) * p.Wo;
+            const int doh = FASTX == 1 ? 0 : rr / p.Wo, dow = FASTX == 1 ? rr : rr - (rr / p.Wo) * p.Wo;
             xA[i] = p.is * doh + dh;
             xB[i] = p.is * dow + dw;
             xL[i] = (xA[i] * p.Wi + xB[i]) * p.Ci + ci;
         }
     }
     auto advance = [&]() {     // every row advances by KP pixels
-        if constexpr (FASTX) {
-            if (p.Wo >= KP) {
+        if constexpr (FASTX != 0) {
+            if (FASTX == 1) {
                 sow += KP;
                 const bool wrap = sow >= p.Wo;
                 sow = wrap ? 0 : sow;
@@ -1340,7 +1343,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
     auto gload = [&](int k0, uint4 (&rg)[GCH], uint4 (&rx)[XCH]) {
-        if constexpr (FASTX) {
+        if constexpr (FASTX != 0) {
             const int S = __builtin_amdgcn_readfirstlane(((sn * p.Hi + p.is * soh) * p.Wi + p.is * sow) * p.Ci);
             const int ihs = __builtin_amdgcn_readfirstlane(p.is * soh), iws = __builtin_amdgcn_readfirstlane(p.is * sow);
             const int kr = pix1 - k0;        // rows of this stage inside the split
@@ -1352,10 +1355,13 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
             }
 #pragma unroll
             for (int i = 0; i < XCH; ++i) {
+                const int j = FASTX == 2 ? i : 0;
+                const int xb = xB[j] + (FASTX == 1 ? p.is * XRS * i : 0);
+                const int xl = xL[j] + (FASTX == 1 ? p.is * XRS * i * p.Ci : 0);
                 // non-short-circuit &: straight-line selects, no exec-masked branches around the loads
-                const bool ok = kk_ok & (xr0 + i * XRS < kr) & ((unsigned)(ihs + xA[i]) < (unsigned)p.Hi) &
-                                ((unsigned)(iws + xB[i]) < (unsigned)p.Wi);
-                rx[i] = bload(xrs, sel_off(ok, (S + xL[i]) * ESZ));
+                const bool ok = kk_ok & (xr0 + i * XRS < kr) & ((unsigned)(ihs + xA[j]) < (unsigned)p.Hi) &
+                                ((unsigned)(iws + xb) < (unsigned)p.Wi);
+                rx[i] = bload(xrs, sel_off(ok, (S + xl) * ESZ));
             }
             return;
         }
@@ -1441,7 +1447,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
                 }
                 // FASTX frees the address registers the hoisted fragment reads of the next k-step would take:
                 // keep one k-step of fragments live at a time (256-VGPR budget at two workgroups per CU)
-                if constexpr (FASTX) __builtin_amdgcn_sched_barrier(0);
+                if constexpr (FASTX == 2) __builtin_amdgcn_sched_barrier(0);
             }
         } else {
 #pragma unroll
@@ -2244,21 +2250,26 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     } else if (dtype == SCD_DT_BF16 || dtype == SCD_DT_F32) {
         // fast addressing when a stage of KP pixels stays inside one image and one row block
         const int KP = dtype == SCD_DT_BF16 ? 64 : 32;
-        const bool fast = wgrad_fastx() && (Wo % KP == 0 || KP % Wo == 0) && ((long)Ho * Wo) % KP == 0 && chunk % KP == 0;
+        const bool fastok = wgrad_fastx() && ((long)Ho * Wo) % KP == 0 && chunk % KP == 0;
+        const int fx = !fastok ? 0 : (Wo % KP == 0 ? 1 : (KP % Wo == 0 ? 2 : 0));
+        // (the 128 x 128 tile has registers for FASTX 1 only)
         if (dtype == SCD_DT_BF16) {
-            // (the 128 x 128 tile spills at 256 VGPRs with FASTX: generic addressing there)
-            if (fast && Cg <= 64) {
-                hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, true>), grid, dim3(256), 0, st, p);
+            if (Cg <= 64) {
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
+                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), 0, st, p);
             } else {
-                if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, false>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, false>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), 0, st, p);
             }
         } else {
-            if (fast && Cg <= 64) {
-                hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, true>), grid, dim3(256), 0, st, p);
+            if (Cg <= 64) {
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 1>), grid, dim3(256), 0, st, p);
+                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 2>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 0>), grid, dim3(256), 0, st, p);
             } else {
-                if (Cg <= 64) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, false>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, false>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 1>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 0>), grid, dim3(256), 0, st, p);
             }
         }
     } else {

@@ -27,6 +27,51 @@ __global__ void pack_weight_kernel(const float* w, T* out, int A, int B, int Tt,
     }
 }
 
+// ---------------------------------------------------------------- batched pack (one launch per step)
+// Every conv/deconv weight operand of a training step in one launch.  Descriptor starts are multiples of
+// PACK_UNIT elements (host side), so each workgroup handles one unit of ONE descriptor, found by a
+// workgroup-uniform binary search (scalar loads).
+constexpr int PACK_UNIT = 4096;
+
+__global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pack_desc* __restrict__ d, int n, int bf16) {
+    const long e0 = (long)blockIdx.x * PACK_UNIT;
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (d[mid].start <= e0) lo = mid; else hi = mid - 1;
+    }
+    const scd_pack_desc q = d[lo];
+    const long count = q.mode == 0 ? (long)q.A * q.ldp : (long)q.B * q.T * q.A;
+#pragma unroll 4
+    for (int j = 0; j < PACK_UNIT / 256; ++j) {
+        const long i = e0 - q.start + threadIdx.x + 256 * j;
+        if (i >= count) break;
+        float v;
+        long o;
+        if (q.mode == 0) {            // out[row_off + a][t*B + b] = w[a][b][t]   (A x ldp elements, padding zeroed)
+            const int r = (int)(i / q.ldp), k = (int)(i - (long)r * q.ldp);
+            const int t = k / q.B, b = k - (k / q.B) * q.B;
+            v = t < q.T ? q.w[((long)r * q.B + b) * q.T + t] : 0.f;
+            o = (long)(q.row_off + r) * q.ldp + k;
+        } else {                      // out[b][t*a_tot + a_off + a] = w[a][b][t]  (B x T x A elements)
+            const int TA = q.T * q.A;
+            const int r = (int)(i / TA), rem = (int)(i - (long)r * TA);
+            const int t = rem / q.A, a = rem - (rem / q.A) * q.A;
+            v = q.w[((long)a * q.B + r) * q.T + t];
+            o = (long)r * q.ldp + (long)t * q.a_tot + q.a_off + a;
+        }
+        if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
+        else ((float*)q.out)[o] = v;
+    }
+}
+
+extern "C" int scd_pack_weights_batched(int dtype, const scd_pack_desc* descs, int n, long total, void* stream) {
+    if (n < 1 || total < 1 || total % PACK_UNIT || (dtype != SCD_DT_BF16 && dtype != SCD_DT_F32)) return SCD_ERR_ARG;
+    hipLaunchKernelGGL(pack_weights_batched_kernel, dim3((unsigned)(total / PACK_UNIT)), dim3(256), 0, (hipStream_t)stream,
+                       descs, n, dtype == SCD_DT_BF16 ? 1 : 0);
+    SCD_RETURN_LAUNCH();
+}
+
 // ---------------------------------------------------------------- stem im2col
 template <typename T>
 __global__ void im2col_stem_kernel(const float* x, T* cols, int N, int H, int W, int Ho, int Wo, int kh, int kw,

@@ -14,7 +14,7 @@ import torch
 from logger import Logger
 from models.backbones.terminal import BackboneTerminal
 from models.backbones.utility import convolution3x3
-from scdhip import blocks
+from scdhip import blocks, ops
 
 BNMOMENTUM = 0.1
 
@@ -214,6 +214,11 @@ class ResNet(torch.nn.Module):
 
     def forward(self, *x, **kwargs):
         decode = kwargs.get("decode", False)
+        # all packed weight operands of this step in one launch (scdhip.ops.PackPlan)
+        plan = self.__dict__.get("_scd_packplan")
+        if plan is None:
+            plan = self.__dict__["_scd_packplan"] = ops.PackPlan()
+        ops.pack_begin(plan)
         feat = self.backbone_forward(x[0])
         ret = self.heads_forward(feat, *x, **kwargs)
         return [ret] if not decode else self.decoder(ret)

@@ -242,13 +242,13 @@ class HeadsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feat, w0_first, heads):
         N, H, W, Cin = feat.shape
-        w0 = torch.cat([h[0].weight for h in heads], 0)
+        w0s = [h[0].weight for h in heads]
         b0 = torch.cat([h[0].bias for h in heads], 0)
         Hd = heads[0][0].weight.shape[0]
-        Ct = w0.shape[0]
+        Ct = sum(w.shape[0] for w in w0s)
         od = [h[2].weight.shape[0] for h in heads]
         outs = [torch.empty(N, o, H, W, device=feat.device, dtype=torch.float32) for o in od]
-        wp = ops.pack_weight(w0, feat.dtype, 0)
+        wp = ops.pack_concat(w0s, feat.dtype, 0)
         w1s = ops.L.ptr_array([h[2].weight.data_ptr() for h in heads])
         b1s = ops.L.ptr_array([h[2].bias.data_ptr() for h in heads])
         optrs = ops.L.ptr_array([o.data_ptr() for o in outs])
@@ -264,13 +264,15 @@ class HeadsFn(torch.autograd.Function):
             hid = ops.conv_fwd(feat, wp, Ct, 3, 3, 1, 1, bias=b0, relu=True)
             ops.L.call("scd_heads_fwd", ops.dt(hid), ops.ptr(hid), N, H * W, len(heads), Hd, odarr, w1s, b1s, optrs,
                        ops.stream())
-        ctx.save_for_backward(feat, hid, w0)
+        ctx.save_for_backward(feat, hid)
+        ctx.w0s = w0s
         ctx.heads, ctx.od, ctx.Hd = heads, od, Hd
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *douts):
-        feat, hid, w0 = ctx.saved_tensors
+        feat, hid = ctx.saved_tensors
+        w0s = ctx.w0s
         heads, od, Hd = ctx.heads, ctx.od, ctx.Hd
         N, H, W, Cin = feat.shape
         nh = len(heads)
@@ -291,7 +293,7 @@ class HeadsFn(torch.autograd.Function):
         ld = (Cin * 9, 9, 1)
         rows = [(i * Hd, (i + 1) * Hd, ops.grad_of(h[0].weight), ld) for i, h in enumerate(heads)]
         ops.conv_wgrad(dhid, feat, 3, 3, 1, 1, None, None, rows=rows)
-        dfeat = ops.conv_dgrad(dhid, ops.pack_weight(w0, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1)
+        dfeat = ops.conv_dgrad(dhid, ops.pack_concat(w0s, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1)
         return dfeat, None, None
 
 

@@ -99,6 +99,7 @@ class FlatAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         from . import ops
+        ops.pack_end()          # the packed operands of this step go stale now
         fp = self.flat()
         fp.rebind_grads()
         g = self.param_groups[0]

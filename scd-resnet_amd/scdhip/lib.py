@@ -31,6 +31,11 @@ class GemmPhase(ctypes.Structure):
                 ("dh", c_int * MAX_TAPS), ("dw", c_int * MAX_TAPS), ("wt", c_int * MAX_TAPS)]
 
 
+class PackDesc(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("out", c_void_p), ("start", c_long), ("A", c_int), ("B", c_int), ("T", c_int),
+                ("mode", c_int), ("ldp", c_int), ("row_off", c_int), ("a_off", c_int), ("a_tot", c_int)]
+
+
 P = c_void_p
 I = c_int
 L = c_long
@@ -48,6 +53,7 @@ SIGNATURES = {
     "scd_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, IP, IP, P]),
     "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, P]),
     "scd_pack_weight": (I, [I, P, P, I, I, I, I, I, I, P]),
+    "scd_pack_weights_batched": (I, [I, P, I, L, P]),
     "scd_im2col_stem": (I, [I, P, P, I, I, I, I, I, I, I, I, I, I, P]),
     "scd_stem_conv_fwd": (I, [I, P, P, P, P, I, I, I, I, I, P]),
     "scd_stem_conv_wgrad_nsplit": (I, [L]),

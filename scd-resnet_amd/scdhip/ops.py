@@ -121,8 +121,120 @@ def bn_stats(bn, which):
 
 # ------------------------------------------------------------------ weights
 
-def pack_weight(w, dtype, mode, ldp=None, out=None, row_off=0):
-    """(A,B,kh,kw) fp32 -> GEMM operand. mode 0: [A][taps][B]; mode 1: [B][taps][A]."""
+class PackPlan:
+    """Per-model cache of the packed weight operands of one training step.
+
+    The first step records every (parameter, layout) a block asks for and packs it on demand; from then on
+    ``pack_begin`` repacks all of them in ONE ``scd_pack_weights_batched`` launch at the start of the model's
+    forward (the parameters change every optimizer step), and ``pack_weight`` / ``pack_concat`` return the
+    packed views.  Only nn.Parameter arguments are cached (keyed by the Parameter object); the plan is active
+    from the model's forward until the next optimizer step (``pack_end``)."""
+
+    def __init__(self):
+        self.entries = {}           # key -> [out tensor, parts, dtype, used]
+        self._sig = None
+        self._dev = {}              # dtype -> (device descriptor tensor, n, total)
+
+    def lookup(self, key):
+        e = self.entries.get(key)
+        if e is None:
+            return None
+        e[3] = True
+        return e[0]
+
+    def add(self, key, out, parts, dtype):
+        self.entries[key] = [out, parts, dtype, True]
+
+    def refresh(self):
+        # drop entries the previous step did not use, then repack the rest (one launch per dtype)
+        self.entries = {k: e for k, e in self.entries.items() if e[3]}
+        if not self.entries:
+            return
+        sig = tuple((k, e[0].data_ptr(), tuple(p[0].data_ptr() for p in e[1])) for k, e in self.entries.items())
+        if sig != self._sig:
+            self._sig = sig
+            self._dev = {}
+            per = {}
+            for e in self.entries.values():
+                per.setdefault(e[2], []).append(e)
+            for dtype, es in per.items():
+                descs, start = [], 0
+                for out, parts, _, _ in es:
+                    for (w, mode, ldp, row_off, a_off, a_tot) in parts:
+                        A, B, T = w.shape[0], w.shape[1], w.shape[2] * w.shape[3]
+                        d = L.PackDesc(w.data_ptr(), out.data_ptr(), start, A, B, T, mode, ldp, row_off, a_off, a_tot)
+                        descs.append(d)
+                        start += A * ldp if mode == 0 else B * T * A
+                        start = (start + 4095) // 4096 * 4096      # whole workgroup units per descriptor
+                arr = (L.PackDesc * len(descs))(*descs)
+                host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+                self._dev[dtype] = (host.to(es[0][0].device), len(descs), start)
+        for dtype, (dev, n, total) in self._dev.items():
+            L.call("scd_pack_weights_batched", _DT[dtype], dev.data_ptr(), n, total, stream())
+        for e in self.entries.values():
+            e[3] = False
+
+
+_ACTIVE_PLAN = None
+
+
+def pack_begin(plan):
+    """Start of a model forward: repack every recorded operand (one launch) and activate the plan."""
+    global _ACTIVE_PLAN
+    _ACTIVE_PLAN = None
+    plan.refresh()
+    _ACTIVE_PLAN = plan
+
+
+def pack_end():
+    """Parameters are about to change (optimizer step): stop serving cached operands."""
+    global _ACTIVE_PLAN
+    _ACTIVE_PLAN = None
+
+
+def pack_concat(ws, dtype, mode):
+    """Pack the row-concatenation of the conv weights `ws` (same (B,kh,kw)) without materialising the
+    concatenation: mode 0 stacks their output rows, mode 1 interleaves their columns per tap."""
+    A_tot = sum(w.shape[0] for w in ws)
+    B, T = ws[0].shape[1], ws[0].shape[2] * ws[0].shape[3]
+    plan = _ACTIVE_PLAN
+    key = (tuple(id(w) for w in ws), dtype, mode)
+    if plan is not None and all(isinstance(w, torch.nn.Parameter) for w in ws):
+        hit = plan.lookup(key)
+        if hit is not None:
+            return hit
+    if mode == 0:
+        out = torch.empty(A_tot, T * B, dtype=dtype, device=ws[0].device)
+        parts, off = [], 0
+        for w in ws:
+            parts.append((w, 0, T * B, off, 0, 0))
+            pack_weight(w, dtype, 0, out=out, row_off=off, _cache=False)
+            off += w.shape[0]
+    else:
+        cat = torch.cat(list(ws), 0)
+        out = pack_weight(cat, dtype, 1, _cache=False)
+        parts, off = [], 0
+        for w in ws:
+            parts.append((w, 1, T * A_tot, 0, off, A_tot))
+            off += w.shape[0]
+    if plan is not None and all(isinstance(w, torch.nn.Parameter) for w in ws):
+        plan.add(key, out, parts, dtype)
+    return out
+
+
+def pack_weight(w, dtype, mode, ldp=None, out=None, row_off=0, _cache=True):
+    """(A,B,kh,kw) fp32 -> GEMM operand. mode 0: [A][taps][B]; mode 1: [B][taps][A].
+    During a model step (PackPlan active) a Parameter's operand comes from the step's batched pack."""
+    plan = _ACTIVE_PLAN
+    if _cache and out is None and row_off == 0 and plan is not None and isinstance(w, torch.nn.Parameter):
+        key = (id(w), dtype, mode, ldp)
+        hit = plan.lookup(key)
+        if hit is not None:
+            return hit
+        res = pack_weight(w, dtype, mode, ldp, _cache=False)
+        T = w.shape[2] * w.shape[3]
+        plan.add(key, res, [(w, mode, res.shape[1], 0, 0, w.shape[0])], dtype)
+        return res
     A, B = w.shape[0], w.shape[1]
     T = w.shape[2] * w.shape[3]
     rows = A if mode == 0 else B
