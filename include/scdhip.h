@@ -115,10 +115,12 @@ int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, doubl
                       int Ho, int Wo, void* stream);
 /* Its weight gradient: ws[z][co][k] (fp32, nsplit x 64 x 64) = sum over split z's pixels of
  * dy[pix][co] * col[pix][k]; reduce with scd_wgrad_reduce(ws, nsplit, 64, 1, 64, ..., cvalid = 49).
+ * coef != NULL fuses the stem BN backward apply: dy is then the masked dz, ybn the BN input, and the
+ * operand is bf16(coef[0][c]*dz + coef[1][c]*ybn + coef[2][c]) (scd_bn_bwd_finalize's coefficients).
  * Requires Wo % 64 == 0. */
 int scd_stem_conv_wgrad_nsplit(long M);
-int scd_stem_conv_wgrad(int dtype, const void* dy, const float* x, float* ws, int nsplit, int N, int H, int W,
-                        int Ho, int Wo, void* stream);
+int scd_stem_conv_wgrad(int dtype, const void* dy, const void* ybn, const float* coef, const float* x, float* ws,
+                        int nsplit, int N, int H, int W, int Ho, int Wo, void* stream);
 
 /* ---- training BatchNorm2d (residuals.py:92,95,212,262,306; momentum 0.1, eps 1e-5) ---- */
 /* sum replicas [nrep][2][C] -> [2][C] in place (replica 0); used before a SyncBN all-reduce */
@@ -133,20 +135,29 @@ int scd_bn_finalize(double* stats, int nrep, int C, double count, const float* g
 int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const float* scale,
                  const float* shift, const void* res, const float* rscale, const float* rshift,
                  int relu, void* stream);
-/* dz = dout * (mask ? mask>0 : 1); stats += [sum dz, sum dz*(y-mean)*invstd] */
-int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
-                      const float* invstd, int C, long total, double* stats, void* stream);
+/* dz = dout * relu'(.) ; stats += [sum dz, sum dz*(y-mean)*invstd].  relu' from the stored activation
+ * (mask > 0) or, for a plain BN+ReLU (mask == NULL, relu_scale != NULL), from the forward's own
+ * y*relu_scale + relu_shift > 0 (no activation read); both NULL: no ReLU. */
+int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
+                      const float* relu_shift, const float* mean, const float* invstd, int C, long total,
+                      double* stats, void* stream);
 /* dgamma (+)= gscale * sum dz*xhat, dbeta (+)= gscale * sum dz; coef[3][C] for dy = a*dz + b*y + c.
  * With SyncBN the sums are global; gscale = 1/world keeps the DDP-averaged dgamma/dbeta equal to the
  * reference's (torch SyncBatchNorm returns the LOCAL weight/bias gradients, DDP then averages them). */
 int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                         const float* mean, const float* invstd, float* dgamma, float* dbeta,
                         float gscale, float* coef, void* stream);
-/* dy = a*dz + b*y + c (dtype); optionally also writes dz */
-int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* coef,
-                     int C, long total, void* dy, void* dz, void* stream);
+/* dy = a*dz + b*y + c (dtype), dz masked as in scd_bn_bwd_reduce; optionally also writes dz */
+int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
+                     const float* relu_shift, const float* coef, int C, long total, void* dy, void* dz,
+                     void* stream);
 
 /* ---- stem BN-apply + ReLU + MaxPool2d(3,2,1) (residuals.py:212-214) ---- */
+/* MaxPool backward + ReLU mask (as scd_stem_pool_bwd) fused with the stem BN backward reduction:
+ * also stats[rep][2][C] += [sum dz, sum dz*(y-mean)*invstd] over the rounded dz it writes. */
+int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
+                         const float* shift, const float* mean, const float* invstd, void* dz, double* stats, int N,
+                         int H, int W, int C, int Ho, int Wo, void* stream);
 int scd_stem_pool_fwd(int dtype, const void* y, const float* scale, const float* shift, void* out,
                       uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, void* stream);
 /* dz(N,H,W,C) = relu'(y*scale+shift) * maxpool_bwd(dout) */

@@ -71,26 +71,26 @@ template <typename T>
 __global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const float* scale, const float* shift,
                                 const T* res, const float* rscale, const float* rshift, int relu) {
     constexpr int E = Vec16<T>::N;
-    extern __shared__ float prm[];          // [scale | shift | rscale | rshift] x C, staged once per block
-    const int np = rscale ? 4 : 2;
-    for (int i = threadIdx.x; i < C; i += blockDim.x) {
-        prm[i] = scale[i];
-        prm[C + i] = shift[i];
-        if (rscale) { prm[2 * C + i] = rscale[i]; prm[3 * C + i] = rshift[i]; }
-    }
-    (void)np;
-    __syncthreads();
+    // the grid stride is a multiple of the chunks per row (C/E divides 256): a thread always owns the same
+    // E channels, so the per-channel parameters live in registers (no LDS, no bank conflicts)
     const unsigned cpr = (unsigned)C / E;
-    for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c0 = (int)(v0 % cpr) * E;
+    float sc[E], sh[E], rs[E], rh[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e];
+        rs[e] = rscale ? rscale[c0 + e] : 0.f; rh[e] = rscale ? rshift[c0 + e] : 0.f;
+    }
+    for (unsigned v = v0; v < nvec; v += gridDim.x * blockDim.x) {
         const size_t i = (size_t)v * E;
-        const int c0 = (int)(v % cpr) * E;
         float a[E], r[E];
         Vec16<T>::load(y + i, a);
         if (res) Vec16<T>::load(res + i, r);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            float o = a[e] * prm[c0 + e] + prm[C + c0 + e];
-            if (res) o += rscale ? (r[e] * prm[2 * C + c0 + e] + prm[3 * C + c0 + e]) : r[e];
+            float o = a[e] * sc[e] + sh[e];
+            if (res) o += rscale ? (r[e] * rs[e] + rh[e]) : r[e];
             if (relu) o = fmaxf(o, 0.f);
             a[e] = o;
         }
@@ -104,6 +104,7 @@ __global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const 
 // over row lanes in LDS by all threads and added to one fp64 replica slot per channel.
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y,
+                                                            const float* rsc, const float* rsh,
                                                             const float* mean, const float* invstd, int C,
                                                             unsigned rows, unsigned rows_per_block, double* stats) {
     constexpr int E = Vec16<T>::N;
@@ -116,13 +117,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const
     const unsigned r0 = blockIdx.x * rows_per_block;
     const unsigned r1 = min(rows, r0 + rows_per_block);
     __shared__ float red[2 * 256 * E];
-    float s[E], q[E], mu[E], is[E];
+    float s[E], q[E], mu[E], is[E], ka[E], kb[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) { s[e] = 0.f; q[e] = 0.f; mu[e] = mean[ch * E + e]; is[e] = invstd[ch * E + e]; }
+    for (int e = 0; e < E; ++e) {
+        s[e] = 0.f; q[e] = 0.f; mu[e] = mean[ch * E + e]; is[e] = invstd[ch * E + e];
+        ka[e] = rsc ? rsc[ch * E + e] : 0.f;
+        kb[e] = rsc ? rsh[ch * E + e] : 0.f;
+    }
     auto acc = [&](const float* d, const float* yv, const float* mk) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const float dz = (mask && !(mk[e] > 0.f)) ? 0.f : d[e];
+            // relu mask: the stored activation (mask) or, for BN+ReLU, the forward's own y*scale+shift > 0
+            const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
+            const float dz = off ? 0.f : d[e];
             s[e] += dz;
             q[e] += dz * (yv[e] - mu[e]) * is[e];
         }
@@ -189,25 +196,31 @@ __global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double co
 }
 
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* coef, int C, unsigned nvec,
-                                    T* dy, T* dz_out) {
+__global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* rsc, const float* rsh,
+                                    const float* coef, int C, unsigned nvec, T* dy, T* dz_out) {
     constexpr int E = Vec16<T>::N;
-    extern __shared__ float cf[];           // coef [3][C], staged once per block
-    for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
-    __syncthreads();
+    // fixed channel chunk per thread (see bn_apply_kernel): coefficients in registers
     const unsigned cpr = (unsigned)C / E;
-    for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c0 = (int)(v0 % cpr) * E;
+    float ca[E], cb[E], cc[E], ka[E], kb[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        ca[e] = coef[c0 + e]; cb[e] = coef[C + c0 + e]; cc[e] = coef[2 * C + c0 + e];
+        ka[e] = rsc ? rsc[c0 + e] : 0.f; kb[e] = rsc ? rsh[c0 + e] : 0.f;
+    }
+    for (unsigned v = v0; v < nvec; v += gridDim.x * blockDim.x) {
         const size_t i = (size_t)v * E;
-        const int c0 = (int)(v % cpr) * E;
         float d[E], yv[E], mk[E], o[E];
         Vec16<T>::load(dout + i, d);
         Vec16<T>::load(y + i, yv);
         if (mask) Vec16<T>::load(mask + i, mk);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            const float dz = (mask && !(mk[e] > 0.f)) ? 0.f : d[e];
+            const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
+            const float dz = off ? 0.f : d[e];
             d[e] = dz;
-            o[e] = cf[c0 + e] * dz + cf[C + c0 + e] * yv[e] + cf[2 * C + c0 + e];
+            o[e] = ca[e] * dz + cb[e] * yv[e] + cc[e];
         }
         Vec16<T>::store(dy + i, o);
         if (dz_out) Vec16<T>::store(dz_out + i, d);
@@ -240,14 +253,14 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
                             void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16) {
-        if (C % 8) return SCD_ERR_ARG;
+        if (C % 8 || 256 % (C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
-        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), (rscale ? 4 : 2) * C * 4, st, (const __bf16*)y,
+        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const __bf16*)y,
                            (__bf16*)out, C, (unsigned)nvec, scale, shift, (const __bf16*)res, rscale, rshift, relu);
     } else if (dtype == SCD_DT_F32) {
-        if (C % 4) return SCD_ERR_ARG;
+        if (C % 4 || 256 % (C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
-        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), (rscale ? 4 : 2) * C * 4, st, (const float*)y,
+        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)y,
                            (float*)out, C, (unsigned)nvec, scale, shift, (const float*)res, rscale, rshift, relu);
     } else {
         return SCD_ERR_ARG;
@@ -255,7 +268,8 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* mean,
+extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
+                                 const float* relu_shift, const float* mean,
                                  const float* invstd, int C, long total, double* stats, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
@@ -269,10 +283,12 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
     const int blocks = cdiv(rows, rpb);
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout,
-                           (const __bf16*)mask, (const __bf16*)y, mean, invstd, C, (unsigned)rows, (unsigned)rpb, stats);
+                           (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, mean, invstd, C, (unsigned)rows,
+                           (unsigned)rpb, stats);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dout,
-                           (const float*)mask, (const float*)y, mean, invstd, C, (unsigned)rows, (unsigned)rpb, stats);
+                           (const float*)mask, (const float*)y, relu_scale, relu_shift, mean, invstd, C, (unsigned)rows,
+                           (unsigned)rpb, stats);
     else
         return SCD_ERR_ARG;
     SCD_RETURN_LAUNCH();
@@ -286,20 +302,22 @@ extern "C" int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count,
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* coef, int C,
-                                long total, void* dy, void* dz, void* stream) {
+extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
+                                const float* relu_shift, const float* coef, int C, long total, void* dy, void* dz,
+                                void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16) {
-        if (C % 8) return SCD_ERR_ARG;
+        if (C % 8 || 256 % (C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 3 * C * 4, st,
-                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, coef, C, (unsigned)nvec, (__bf16*)dy,
-                           (__bf16*)dz);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st,
+                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, coef, C,
+                           (unsigned)nvec, (__bf16*)dy, (__bf16*)dz);
     } else if (dtype == SCD_DT_F32) {
-        if (C % 4) return SCD_ERR_ARG;
+        if (C % 4 || 256 % (C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 3 * C * 4, st, (const float*)dout,
-                           (const float*)mask, (const float*)y, coef, C, (unsigned)nvec, (float*)dy, (float*)dz);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)dout,
+                           (const float*)mask, (const float*)y, relu_scale, relu_shift, coef, C, (unsigned)nvec, (float*)dy,
+                           (float*)dz);
     } else {
         return SCD_ERR_ARG;
     }

@@ -187,6 +187,86 @@ __global__ void stem_pool_bwd_kernel(const T* dout, const uint8_t* argmax, const
     }
 }
 
+// Stem MaxPool backward + ReLU mask (as stem_pool_bwd_kernel) fused with the stem BN backward reduction:
+// the same pass accumulates sum dz and sum dz*(y-mean)*invstd per channel (fp64 replica slots), so the
+// separate reduce pass over dz and y is gone.  The grid stride is a multiple of the chunks per pixel, so a
+// thread always owns the same 8 (bf16) channels.
+template <typename T>
+__global__ __launch_bounds__(256) void stem_pool_bwd_bn_kernel(const T* dout, const uint8_t* argmax, const T* y,
+                                                               const float* scale, const float* shift, const float* mean,
+                                                               const float* invstd, T* dz, double* stats, int N, int H,
+                                                               int W, int C, int Ho, int Wo) {
+    constexpr int E = Vec16<T>::N;
+    const unsigned cpp = C / E;
+    const unsigned total = (unsigned)N * H * W * cpp;
+    const unsigned HW = (unsigned)H * W;
+    const int ch = (int)(threadIdx.x % cpp);
+    float sc[E], sh[E], mu[E], is[E], s1[E], s2[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        sc[e] = scale[ch * E + e]; sh[e] = shift[ch * E + e]; mu[e] = mean[ch * E + e]; is[e] = invstd[ch * E + e];
+        s1[e] = 0.f; s2[e] = 0.f;
+    }
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const size_t pix = i / cpp;
+        const int n = (int)((unsigned)pix / HW);
+        const int rem = (int)((unsigned)pix - (unsigned)n * HW);
+        const int h = rem / W, w = rem - (rem / W) * W;
+        float acc[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.f;
+        const int oh0 = h / 2, oh1 = min(Ho - 1, (h + 1) / 2);
+        const int ow0 = w / 2, ow1 = min(Wo - 1, (w + 1) / 2);
+        for (int oh = oh0; oh <= oh1; ++oh) {
+            const int di = h - (2 * oh - 1);
+            if (di < 0 || di > 2) continue;
+            for (int ow = ow0; ow <= ow1; ++ow) {
+                const int dj = w - (2 * ow - 1);
+                if (dj < 0 || dj > 2) continue;
+                const long o = (((long)n * Ho + oh) * Wo + ow) * C + ch * E;
+                float d[E];
+                Vec16<T>::load(dout + o, d);
+                uint8_t am[E];
+                if constexpr (E == 8) *(uint2*)am = *(const uint2*)(argmax + o);
+                else *(uint32_t*)am = *(const uint32_t*)(argmax + o);
+                const int sel = di * 3 + dj;
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (am[e] == sel) acc[e] += d[e];
+            }
+        }
+        float v[E];
+        Vec16<T>::load(y + pix * C + ch * E, v);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const float z = v[e] * sc[e] + sh[e];
+            acc[e] = z > 0.f ? acc[e] : 0.f;
+        }
+        Vec16<T>::store(dz + pix * C + ch * E, acc);
+        // BN backward sums of the value the apply pass will see (the stored, rounded dz)
+        float r[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) r[e] = to_f<T>(from_f<T>(acc[e]));
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            s1[e] += r[e];
+            s2[e] += r[e] * (v[e] - mu[e]) * is[e];
+        }
+    }
+    __shared__ float red[2][256][E + 1];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { red[0][threadIdx.x][e] = s1[e]; red[1][threadIdx.x][e] = s2[e]; }
+    __syncthreads();
+    // channel c = ch*E + e is held by threads t with t % cpp == ch
+    for (int k = threadIdx.x; k < 2 * C; k += blockDim.x) {
+        const int stat = k / C, c = k - (k / C) * C;
+        const int cc = c / E, e = c - (c / E) * E;
+        double a = 0.0;
+        for (int t = cc; t < (int)blockDim.x; t += cpp) a += red[stat][t][e];
+        atomic_add_f64(stats + ((long)(blockIdx.x % SCD_STAT_REPLICAS) * 2 + stat) * C + c, a);
+    }
+}
+
 // ---------------------------------------------------------------- CenterNet head tails
 struct HeadsDesc {
     int nh, Hd, od[4], orow[4], nout;
@@ -471,6 +551,25 @@ extern "C" int scd_stem_pool_bwd(int dtype, const void* dout, const uint8_t* arg
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((stem_pool_bwd_kernel<float>), dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)dout,
                            argmax, (const float*)y, scale, shift, (float*)dz, N, H, W, C, Ho, Wo);
+    else
+        return SCD_ERR_ARG;
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
+                                    const float* shift, const float* mean, const float* invstd, void* dz, double* stats,
+                                    int N, int H, int W, int C, int Ho, int Wo, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int E = dtype == SCD_DT_BF16 ? 8 : 4;
+    if (C % E || 256 % (C / E)) return SCD_ERR_ARG;
+    const long total = (long)N * H * W * (C / E);
+    const int blocks = (int)std::min<long>(2048, (total + 255) / 256);
+    if (dtype == SCD_DT_BF16)
+        hipLaunchKernelGGL((stem_pool_bwd_bn_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout, argmax,
+                           (const __bf16*)y, scale, shift, mean, invstd, (__bf16*)dz, stats, N, H, W, C, Ho, Wo);
+    else if (dtype == SCD_DT_F32)
+        hipLaunchKernelGGL((stem_pool_bwd_bn_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dout, argmax,
+                           (const float*)y, scale, shift, mean, invstd, (float*)dz, stats, N, H, W, C, Ho, Wo);
     else
         return SCD_ERR_ARG;
     SCD_RETURN_LAUNCH();

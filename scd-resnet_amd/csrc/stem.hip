@@ -163,7 +163,8 @@ constexpr int DROW = 288;                           // dy stage row stride (128 
 
 __device__ __forceinline__ int dswz(int row, int byte) { return row * DROW + (byte ^ (((row >> 3) & 1) << 7)); }
 
-__global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __restrict__ dy, const float* __restrict__ x,
+__global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ ybn,
+                                                              const float* __restrict__ coef, const float* __restrict__ x,
                                                               float* __restrict__ ws, int H, int W, int Ho, int Wo,
                                                               long M, int chunk) {
     constexpr int DT = WPX * DROW;                  // dy stage
@@ -197,12 +198,25 @@ __global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __re
         const int ih0 = oh * SP - PD, iw0 = ow0 * SP - PD;
         const float* xn = x + (size_t)n * H * W;
         __syncthreads();                              // previous stage's reads are done
-        // dy stage: 64 px x 128 B = 512 chunks of 16 B
+        // dy stage: 64 px x 128 B = 512 chunks of 16 B.  With coef (fused BN backward apply): dy is the masked
+        // dz and the BN input y of the stem, and the stage holds a*dz + b*y + c rounded to bf16 (as the apply pass)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int idx = tid + 256 * j;
             const int r = idx >> 3, c = idx & 7;
-            *(uint4*)(Ds + dswz(r, c * 16)) = *(const uint4*)(dy + (ps + r) * CO + c * 8);
+            uint4 v = *(const uint4*)(dy + (ps + r) * CO + c * 8);
+            if (coef) {
+                const uint4 yv = *(const uint4*)(ybn + (ps + r) * CO + c * 8);
+                const bf16x8 d8 = __builtin_bit_cast(bf16x8, v), y8 = __builtin_bit_cast(bf16x8, yv);
+                bf16x8 o8;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int ch = c * 8 + e;
+                    o8[e] = (__bf16)(coef[ch] * (float)d8[e] + coef[CO + ch] * (float)y8[e] + coef[2 * CO + ch]);
+                }
+                v = __builtin_bit_cast(uint4, o8);
+            }
+            *(uint4*)(Ds + dswz(r, c * 16)) = v;
         }
         for (int i = tid; i < KS * WPCOLS; i += 256) {
             const int r = i / WPCOLS, c = i - (i / WPCOLS) * WPCOLS;
@@ -277,8 +291,8 @@ extern "C" int scd_stem_conv_wgrad_nsplit(long M) {
     return (int)ns;
 }
 
-extern "C" int scd_stem_conv_wgrad(int dtype, const void* dy, const float* x, float* ws, int nsplit, int N, int H,
-                                   int W, int Ho, int Wo, void* stream) {
+extern "C" int scd_stem_conv_wgrad(int dtype, const void* dy, const void* ybn, const float* coef, const float* x,
+                                   float* ws, int nsplit, int N, int H, int W, int Ho, int Wo, void* stream) {
     if (dtype != SCD_DT_BF16 || nsplit < 1 || Wo % WPX || Ho != (H + 2 * PD - KS) / SP + 1 ||
         Wo != (W + 2 * PD - KS) / SP + 1)
         return SCD_ERR_ARG;
@@ -286,7 +300,8 @@ extern "C" int scd_stem_conv_wgrad(int dtype, const void* dy, const float* x, fl
     long chunk = (M + nsplit - 1) / nsplit;
     chunk = (chunk + WPX - 1) / WPX * WPX;
     if (chunk >= (1L << 31)) return SCD_ERR_ARG;
-    hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(nsplit), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dy, x, ws,
-                       H, W, Ho, Wo, M, (int)chunk);
+    if (coef && !ybn) return SCD_ERR_ARG;
+    hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(nsplit), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dy,
+                       (const __bf16*)ybn, coef, x, ws, H, W, Ho, Wo, M, (int)chunk);
     SCD_RETURN_LAUNCH();
 }

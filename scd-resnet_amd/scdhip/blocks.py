@@ -67,11 +67,13 @@ class StemFn(torch.autograd.Function):
     def backward(ctx, dout):
         cols, y, am = ctx.saved_tensors
         conv, bn, st = ctx.conv, ctx.bn, ctx.st
-        dz = ops.stem_pool_bwd(_c(dout), am, y, st)
-        dy = ops.bn_backward(bn, st, dz, y)
         if ctx.direct:
-            ops.stem_conv_wgrad(dy, cols, ops.grad_of(conv.weight))
+            # pool/ReLU backward + BN reduction in one pass; the BN apply runs inside the weight gradient
+            dz, coef = ops.stem_pool_bwd_bn(bn, _c(dout), am, y, st)
+            ops.stem_conv_wgrad(dz, cols, ops.grad_of(conv.weight), ybn=y, coef=coef)
         else:
+            dz = ops.stem_pool_bwd(_c(dout), am, y, st)
+            dy = ops.bn_backward(bn, st, dz, y)
             T = conv.weight.shape[2] * conv.weight.shape[3]
             ops.conv_wgrad(dy, cols, 1, 1, 1, 0, ops.grad_of(conv.weight), (T, 1, 0), cvalid=T)
         return None, None, None, None, None
@@ -117,7 +119,7 @@ class BasicBlockFn(torch.autograd.Function):
         w2 = blk.conv2.weight
         ops.conv_wgrad(dy2, a1, 3, 3, 1, 1, ops.grad_of(w2), _conv_ld(w2))
         da1 = ops.conv_dgrad(dy2, ops.pack_weight(w2, x.dtype, 1), C, a1.shape[1], a1.shape[2], 3, 3, 1, 1)
-        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, mask=a1)
+        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, relu=True)
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 3, 3, s, 1, ops.grad_of(w1), _conv_ld(w1))
         ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 3, 3, s, 1, out=dx, accumulate=True)
@@ -166,11 +168,11 @@ class BottleneckFn(torch.autograd.Function):
         w3 = blk.conv3.weight
         ops.conv_wgrad(dy3, a2, 1, 1, 1, 0, ops.grad_of(w3), _conv_ld(w3))
         da2 = ops.conv_dgrad(dy3, ops.pack_weight(w3, x.dtype, 1), P, a2.shape[1], a2.shape[2], 1, 1, 1, 0)
-        dy2 = ops.bn_backward(blk.bn2, st2, da2, y2, mask=a2)
+        dy2 = ops.bn_backward(blk.bn2, st2, da2, y2, relu=True)
         w2 = blk.conv2.weight
         ops.conv_wgrad(dy2, a1, 3, 3, s, 1, ops.grad_of(w2), _conv_ld(w2))
         da1 = ops.conv_dgrad(dy2, ops.pack_weight(w2, x.dtype, 1), P, a1.shape[1], a1.shape[2], 3, 3, s, 1)
-        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, mask=a1)
+        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, relu=True)
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 1, 1, 1, 0, ops.grad_of(w1), _conv_ld(w1))
         ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 1, 1, 1, 0, out=dx, accumulate=True)
@@ -201,7 +203,7 @@ class DeconvBNFn(torch.autograd.Function):
         w = deconv.weight
         k = w.shape[2]
         s, p = deconv.stride[0], deconv.padding[0]
-        dy = ops.bn_backward(bn, st, _c(dout), y, mask=out)
+        dy = ops.bn_backward(bn, st, _c(dout), y, relu=True)
         # dW_t[i][o][r][s] = sum x[i at q] * dy[o at s*q + r - p]: weight-gradient GEMM with G = x
         T = k * k
         ops.conv_wgrad(x, dy, k, k, s, p, ops.grad_of(w), (w.shape[1] * T, T, 1))
@@ -228,7 +230,7 @@ class ConvBNFn(torch.autograd.Function):
         w = conv.weight
         kh, kw = w.shape[2], w.shape[3]
         s, p = conv.stride[0], conv.padding[0]
-        dy = ops.bn_backward(bn, st, _c(dout), y, mask=out if ctx.relu else None)
+        dy = ops.bn_backward(bn, st, _c(dout), y, relu=ctx.relu)
         ops.conv_wgrad(dy, x, kh, kw, s, p, ops.grad_of(w), _conv_ld(w))
         dx = ops.conv_dgrad(dy, ops.pack_weight(w, x.dtype, 1), x.shape[3], x.shape[1], x.shape[2], kh, kw, s, p)
         return dx, None, None, None, None
@@ -330,7 +332,7 @@ class CornerPoolFn(torch.autograd.Function):
         mod, dirs = ctx.mod, ctx.dirs
         N, H, W, C = x.shape
         lc = mod.lastConv
-        dyl = ops.bn_backward(lc.bn, stl, _c(dout), yl, mask=out)
+        dyl = ops.bn_backward(lc.bn, stl, _c(dout), yl, relu=True)
         ops.conv_wgrad(dyl, r, 3, 3, 1, 1, ops.grad_of(lc.conv.weight), _conv_ld(lc.conv.weight))
         dr = ops.conv_dgrad(dyl, ops.pack_weight(lc.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1)
         dym = ops.bn_backward(mod.branchMergeBn, stm, dr, ym, mask=r)
@@ -344,7 +346,7 @@ class CornerPoolFn(torch.autograd.Function):
         ds = ops.conv_dgrad(dym, ops.pack_weight(wm, x.dtype, 1), Cb, H, W, 3, 3, 1, 1)
         for (a, y, st, br), d in zip(((a1, y1, st1, mod.branch1), (a2, y2, st2, mod.branch2)), dirs):
             da = ops.cpool_bwd(a, ds, d)
-            dy = ops.bn_backward(br.bn, st, da, y, mask=a)
+            dy = ops.bn_backward(br.bn, st, da, y, relu=True)
             ops.conv_wgrad(dy, x, 3, 3, 1, 1, ops.grad_of(br.conv.weight), _conv_ld(br.conv.weight))
             ops.conv_dgrad(dy, ops.pack_weight(br.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1, out=dx,
                            accumulate=True)

@@ -57,13 +57,14 @@ SIGNATURES = {
     "scd_im2col_stem": (I, [I, P, P, I, I, I, I, I, I, I, I, I, I, P]),
     "scd_stem_conv_fwd": (I, [I, P, P, P, P, I, I, I, I, I, P]),
     "scd_stem_conv_wgrad_nsplit": (I, [L]),
-    "scd_stem_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, P]),
+    "scd_stem_conv_wgrad": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
+    "scd_stem_pool_bwd_bn": (I, [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stats_collapse": (I, [P, I, I, P]),
     "scd_bn_finalize": (I, [P, I, I, D, P, P, P, P, P, F, F, P, P, P, P, P]),
     "scd_bn_apply": (I, [I, P, P, I, L, P, P, P, P, P, I, P]),
-    "scd_bn_bwd_reduce": (I, [I, P, P, P, P, P, I, L, P, P]),
+    "scd_bn_bwd_reduce": (I, [I, P, P, P, P, P, P, P, I, L, P, P]),
     "scd_bn_bwd_finalize": (I, [P, I, I, D, P, P, P, P, P, F, P, P]),
-    "scd_bn_bwd_apply": (I, [I, P, P, P, P, I, L, P, P, P]),
+    "scd_bn_bwd_apply": (I, [I, P, P, P, P, P, P, I, L, P, P, P]),
     "scd_stem_pool_fwd": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_pool_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_heads_fwd": (I, [I, P, I, I, I, I, IP, PP, PP, PP, P]),

@@ -392,21 +392,30 @@ def bn_apply(y, st, relu, res=None, rst=None, out=None):
     return out
 
 
-def bn_backward(bn, st, dout, y, mask=None, dz_out=None):
-    """Training BN backward: dgamma/dbeta accumulated into bn.weight.grad / bn.bias.grad, returns dy."""
+def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False):
+    """Training BN backward: dgamma/dbeta accumulated into bn.weight.grad / bn.bias.grad, returns dy.
+    relu=True: the layer is BN+ReLU and its ReLU mask is recomputed from y (no activation read);
+    mask: the stored activation whose > 0 pattern is the ReLU mask (residual joins)."""
     C = y.shape[-1]
     stats = bn_stats(bn, "bwd")
-    L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), ptr(st.mean), ptr(st.invstd), C, y.numel(),
-           ptr(stats), stream())
+    rsc, rsh = (ptr(st.scale), ptr(st.shift)) if (relu and mask is None) else (0, 0)
+    L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd), C,
+           y.numel(), ptr(stats), stream())
+    coef = bn_backward_coef(bn, st, stats, C)
+    dy = torch.empty_like(y)
+    L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),
+           ptr(dz_out), stream())
+    return dy
+
+
+def bn_backward_coef(bn, st, stats, C):
+    """SyncBN all-reduce of the backward sums, dgamma/dbeta accumulation and the apply coefficients."""
     nrep = _allreduce_stats(stats, C)
-    coef = torch.empty(3 * C, device=y.device)
+    coef = torch.empty(3 * C, device=stats.device)
     L.call("scd_bn_bwd_finalize", ptr(stats), nrep, C, float(st.count), ptr(bn.weight), ptr(st.mean),
            ptr(st.invstd), ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), 1.0 / bn_sync_world(), ptr(coef),
            stream())
-    dy = torch.empty_like(y)
-    L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), ptr(coef), C, y.numel(), ptr(dy), ptr(dz_out),
-           stream())
-    return dy
+    return coef
 
 
 def grad_of(p):
@@ -446,14 +455,16 @@ def stem_conv_fwd(x, wpk, stats=None):
     return y
 
 
-def stem_conv_wgrad(dy, x, dst, accumulate=True):
-    """dst (64,1,7,7) fp32 (+)= weight gradient of the stem conv from dy (N,Ho,Wo,64) bf16 and the input x."""
+def stem_conv_wgrad(dy, x, dst, accumulate=True, ybn=None, coef=None):
+    """dst (64,1,7,7) fp32 (+)= weight gradient of the stem conv from dy (N,Ho,Wo,64) bf16 and the input x.
+    With coef (scd_bn_bwd_finalize coefficients) dy is the masked dz and the BN backward apply runs fused."""
     N, _, H, W = x.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
     M = N * Ho * Wo
     ns = L.lib().scd_stem_conv_wgrad_nsplit(M)
     ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=dy.device)
-    L.call("scd_stem_conv_wgrad", L.DT_BF16, ptr(dy), ptr(x), ptr(ws), ns, N, H, W, Ho, Wo, stream())
+    L.call("scd_stem_conv_wgrad", L.DT_BF16, ptr(dy), ptr(ybn), ptr(coef), ptr(x), ptr(ws), ns, N, H, W, Ho, Wo,
+           stream())
     L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 49, 49, 1, 0, ptr(dst), int(accumulate), stream())
 
 
@@ -465,6 +476,17 @@ def stem_pool_fwd(y, st):
     L.call("scd_stem_pool_fwd", dt(y), ptr(y), ptr(st.scale), ptr(st.shift), ptr(out), ptr(am), N, H, W, C, Ho, Wo,
            stream())
     return out, am
+
+
+def stem_pool_bwd_bn(bn, dout, am, y, st):
+    """MaxPool/ReLU backward of the stem fused with its BN backward reduction; returns (dz, coef):
+    dgamma/dbeta are accumulated, coef = the apply coefficients for dy = a*dz + b*y + c."""
+    N, H, W, C = y.shape
+    dz = torch.empty_like(y)
+    stats = bn_stats(bn, "bwd")
+    L.call("scd_stem_pool_bwd_bn", dt(y), ptr(dout), ptr(am), ptr(y), ptr(st.scale), ptr(st.shift), ptr(st.mean),
+           ptr(st.invstd), ptr(dz), ptr(stats), N, H, W, C, dout.shape[1], dout.shape[2], stream())
+    return dz, bn_backward_coef(bn, st, stats, C)
 
 
 def stem_pool_bwd(dout, am, y, st):

@@ -196,6 +196,39 @@ def test_stem_direct_bf16(shape):
     assert rel_err(dw - 0.25, wr.grad) < TOL[torch.bfloat16] * 3
 
 
+def test_stem_fused_backward_matches_unfused():
+    """Stem backward: pool/ReLU backward fused with the BN reduction and the BN apply fused into the weight
+    gradient give the unfused chain's dz (bit-exact), BN parameter gradients and conv weight gradient."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 1, 512, 512, generator=g).to(DEV)
+    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).to(DEV)
+    bns = [torch.nn.BatchNorm2d(64).to(DEV) for _ in range(2)]
+    for b in bns:
+        with torch.no_grad():
+            b.weight.uniform_(0.5, 1.5, generator=None)
+            b.bias.normal_()
+        b.bias.data.copy_(bns[0].bias.data)
+        b.weight.data.copy_(bns[0].weight.data)
+    stats = ops.new_stats(64, DEV)
+    y = ops.stem_conv_fwd(x, ops.pack_weight(w, torch.bfloat16, 0, ldp=64), stats=stats)
+    st = ops.bn_finalize(bns[0], stats, 64, y.numel() // 64)
+    out, am = ops.stem_pool_fwd(y, st)
+    dout = torch.randn(out.shape, generator=g).to(DEV, torch.bfloat16)
+    dz = ops.stem_pool_bwd(dout, am, y, st)
+    dy = ops.bn_backward(bns[0], st, dz, y)
+    dwa = torch.zeros_like(w)
+    ops.stem_conv_wgrad(dy, x, dwa)
+    dz2, coef = ops.stem_pool_bwd_bn(bns[1], dout, am, y, st)
+    dwb = torch.zeros_like(w)
+    ops.stem_conv_wgrad(dz2, x, dwb, ybn=y, coef=coef)
+    torch.cuda.synchronize()
+    assert torch.equal(dz, dz2)
+    for a, b in ((bns[0].weight.grad, bns[1].weight.grad), (bns[0].bias.grad, bns[1].bias.grad)):
+        assert rel_err(b, a) < 1e-5
+    assert rel_err(dwb, dwa) < 2e-2
+
+
 def test_cpool_fwd_bwd_fp32():
     from scdhip import ops
     g = torch.Generator().manual_seed(5)
