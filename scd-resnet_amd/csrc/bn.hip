@@ -67,6 +67,16 @@ __global__ void bn_finalize_kernel(double* stats, int nrep, int C, double count,
     }
 }
 
+// E consecutive per-channel floats (E = 4 or 8, 16-B aligned) as float4 loads
+template <int E>
+__device__ __forceinline__ void load_params(const float* p, float* v) {
+#pragma unroll
+    for (int k = 0; k < E / 4; ++k) {
+        const float4 f = *(const float4*)(p + 4 * k);
+        v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+    }
+}
+
 template <typename T>
 __global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const float* scale, const float* shift,
                                 const T* res, const float* rscale, const float* rshift, int relu) {
@@ -77,10 +87,12 @@ __global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const 
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
     const int c0 = (int)(v0 % cpr) * E;
     float sc[E], sh[E], rs[E], rh[E];
+    load_params<E>(scale + c0, sc);
+    load_params<E>(shift + c0, sh);
+    if (rscale) { load_params<E>(rscale + c0, rs); load_params<E>(rshift + c0, rh); }
+    else {
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        sc[e] = scale[c0 + e]; sh[e] = shift[c0 + e];
-        rs[e] = rscale ? rscale[c0 + e] : 0.f; rh[e] = rscale ? rshift[c0 + e] : 0.f;
+        for (int e = 0; e < E; ++e) { rs[e] = 0.f; rh[e] = 0.f; }
     }
     for (unsigned v = v0; v < nvec; v += gridDim.x * blockDim.x) {
         const size_t i = (size_t)v * E;
@@ -204,10 +216,13 @@ __global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, co
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
     const int c0 = (int)(v0 % cpr) * E;
     float ca[E], cb[E], cc[E], ka[E], kb[E];
+    load_params<E>(coef + c0, ca);
+    load_params<E>(coef + C + c0, cb);
+    load_params<E>(coef + 2 * C + c0, cc);
+    if (rsc) { load_params<E>(rsc + c0, ka); load_params<E>(rsh + c0, kb); }
+    else {
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        ca[e] = coef[c0 + e]; cb[e] = coef[C + c0 + e]; cc[e] = coef[2 * C + c0 + e];
-        ka[e] = rsc ? rsc[c0 + e] : 0.f; kb[e] = rsc ? rsh[c0 + e] : 0.f;
+        for (int e = 0; e < E; ++e) { ka[e] = 0.f; kb[e] = 0.f; }
     }
     for (unsigned v = v0; v < nvec; v += gridDim.x * blockDim.x) {
         const size_t i = (size_t)v * E;
