@@ -75,6 +75,8 @@ size_t scd_conv_wgrad_workspace(int Cg, int T, int Ci, int nsplit);
 /* Number of pixel splits the library picks for an M-pixel weight gradient (tile shape of the
  * kernel it will launch, ~4 waves of workgroups, fp32 slabs capped at 256 MB). */
 int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci);
+/* the same knowing the output geometry (selects the 64-pixel ping-pong kernel when Wo % 64 == 0) */
+int scd_conv_wgrad_nsplit2(int dtype, long M, int Ho, int Wo, int Cg, int T, int Ci);
 int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws, int nsplit,
                    int N, int Ho, int Wo, int Cg, int Hi, int Wi, int Ci, int in_stride,
                    int T, const int* dh, const int* dw, void* stream);

@@ -1207,6 +1207,7 @@ struct WgradParams {
     const char* x;
     float* ws;
     int N, Ho, Wo, Cg, Hi, Wi, Ci, is, T, KK, chunk, ntm, ntn, nsplit;
+    int cg0, cgn;       // output-gradient channel window of this launch: [cg0, cg0 + cgn) of Cg
     int gbytes, xbytes;
     int dh[SCD_MAX_TAPS], dw[SCD_MAX_TAPS];
 };
@@ -1268,8 +1269,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     // G loads: fixed channel chunk per thread
     const int gc = tid % GCPR;
     const int gr0 = tid / GCPR;
-    const int gcol = mt * BM + gc * EPC;
-    const bool gcol_ok = gcol < p.Cg;
+    const int gcol = p.cg0 + mt * BM + gc * EPC;
+    const bool gcol_ok = gcol < p.cg0 + p.cgn;
     // X loads: fixed (tap, ci) chunk per thread; pixel position advanced incrementally
     const int xc = tid % XCPR;
     const int xr0 = tid / XCPR;
@@ -1496,8 +1497,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int row = mt * BM + wm * 64 + a * 16 + lg * 4 + r;
-            if (row >= p.Cg) continue;
+            const int row = p.cg0 + mt * BM + wm * 64 + a * 16 + lg * 4 + r;
+            if (row >= p.cg0 + p.cgn) continue;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const int col = nt * BN + wn * 64 + b * 16 + l16;
@@ -1893,6 +1894,225 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp_kernel(WgradParams p, in
     }
 }
 
+// -------------------------------------------------------------------------------------
+// Ping-pong bf16 weight gradient, 64-pixel stages (the conv_gemm_pp_kernel schedule applied to the
+// weight gradient): tile 256 output-gradient channels (window cg0 + 256*mt) x 256 columns of taps x input
+// channels, two LDS stage buffers of 64 KB, 8 waves in two staggered groups (group g: 128 channels = 8
+// blocks, wave wc: 64 columns = 4 blocks), 4 phases per stage (phase q: channel blocks 2q, 2q+1 = 16
+// MFMAs).  Each group's G operand is stored as four [64 px][64 B] quarter images (the 32 channels of
+// one phase), so quarter q of stage t+1 is needed only at phase q of stage t+1 and is fetched at phase
+// 3/4 of stage t, like the A rows of the forward kernel; X ([64 px][512 B], read whole in phase 1) is
+// fetched in phases 1/2.  Counted waits as conv_gemm_pp_kernel (NB2 = 2).  Requires Wo % 64 == 0 and
+// (Ho*Wo) % 64 == 0: a stage is part of one output row, addressed by a scalar cursor (see FASTX 1).
+__global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
+    constexpr int KP = 64, EPC = 8;
+    constexpr int QIMG = KP * 64;                     // one G quarter image: 64 px x 64 B
+    constexpr int GBYTES = 8 * QIMG;                  // 2 groups x 4 quarters
+    constexpr int STAGE = GBYTES + KP * 512;          // + X image
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    int z, mt, nt;
+    if (!wgrad_block(p, z, mt, nt)) return;
+    const int M = p.N * p.Ho * p.Wo;
+    const int pix0 = z * p.chunk;
+    const int pix1 = min(M, pix0 + p.chunk);
+    const int cbase = p.cg0 + mt * 256 + grp * 128;   // this group's first channel
+
+    // G DMA: quarter q, rows 16*wc + lane/4; the lane's 16-B slot (lane & 3) holds logical chunk c
+    const int g_r = 16 * wc + (lane >> 2);
+    int g_off;
+    {
+        const int slot = lane & 3;
+        const int c = 2 * ((slot >> 1) ^ ((g_r >> 3) & 1)) + (slot & 1);
+        g_off = cbase + c * EPC;
+    }
+    // X DMA: instruction k = 4*wave + j covers rows 2k, 2k+1; per slot constants (FASTX 1 addressing)
+    int x_r[4], xA[4], xB[4], xL[4];
+    bool x_ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = 2 * (4 * wave + j) + (lane >> 5);
+        const int slot = lane & 31;
+        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);
+        const int kk = nt * 256 + c * EPC;
+        x_ok[j] = kk < p.KK;
+        const int tap = x_ok[j] ? kk / p.Ci : 0;
+        const int ci = kk - tap * p.Ci;
+        x_r[j] = r;
+        xA[j] = p.dh[tap];
+        xB[j] = p.is * r + p.dw[tap];
+        xL[j] = (xA[j] * p.Wi + xB[j]) * p.Ci + ci;
+    }
+    int sn, soh, sow;
+    {
+        const int HoWo = p.Ho * p.Wo;
+        sn = __builtin_amdgcn_readfirstlane(pix0 / HoWo);
+        const int rem = pix0 - sn * HoWo;
+        soh = __builtin_amdgcn_readfirstlane(rem / p.Wo);
+        sow = __builtin_amdgcn_readfirstlane(rem - soh * p.Wo);
+    }
+    auto advance = [&]() {
+        sow += KP;
+        const bool wrap = sow >= p.Wo;
+        sow = wrap ? 0 : sow;
+        soh += wrap ? 1 : 0;
+        const bool wrap2 = soh >= p.Ho;
+        soh = wrap2 ? 0 : soh;
+        sn += wrap2 ? 1 : 0;
+        sn = __builtin_amdgcn_readfirstlane(sn);
+        soh = __builtin_amdgcn_readfirstlane(soh);
+        sow = __builtin_amdgcn_readfirstlane(sow);
+    };
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    // stage whose first pixel is k0 (cursor = its position)
+    auto issue_x = [&](int k0, char* stg, int half) {
+        const int S = __builtin_amdgcn_readfirstlane(((sn * p.Hi + p.is * soh) * p.Wi + p.is * sow) * p.Ci);
+        const int ihs = __builtin_amdgcn_readfirstlane(p.is * soh), iws = __builtin_amdgcn_readfirstlane(p.is * sow);
+        const int kr = pix1 - k0;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * half + jj;
+            const bool ok = x_ok[j] & (x_r[j] < kr) & ((unsigned)(ihs + xA[j]) < (unsigned)p.Hi) &
+                            ((unsigned)(iws + xB[j]) < (unsigned)p.Wi);
+            dma16_asm(xrs, stg + GBYTES + 2 * (4 * wave + j) * 512, sel_off(ok, (S + xL[j]) * 2));
+        }
+    };
+    auto issue_g = [&](int k0, char* stg, int half) {
+        const int kr = pix1 - k0;
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+            const int q = 2 * half + qq;
+            dma16_asm(grs, stg + (grp * 4 + q) * QIMG + 16 * wc * 64,
+                      sel_off(g_r < kr, ((k0 + g_r) * p.Cg + g_off + q * 32) * 2));
+        }
+    };
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int q4 = l16 >> 2, pp = l16 & 3;
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    auto trf = [&](const char* lo_addr, const char* hi_addr) {
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo_addr);
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)hi_addr);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 xf[4][2], gfx[2][2], gfy[2][2];
+    auto read_x = [&](const char* stg) {
+        const char* X = stg + GBYTES;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int r0 = 32 * s + 8 * lg + q4;
+            const int f0 = wr_f(r0), f1 = wr_f(r0 + 4);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int cb = (wc * 64 + b * 16 + 4 * pp) * 2;
+                const int pr = cb >> 5, lo8 = cb & 31;
+                xf[b][s] = trf(X + r0 * 512 + ((pr ^ f0) << 5) + lo8, X + (r0 + 4) * 512 + ((pr ^ f1) << 5) + lo8);
+            }
+        }
+    };
+    auto read_g = [&](const char* stg, int q, bf16x8 (&gf)[2][2]) {
+        const char* G = stg + (grp * 4 + q) * QIMG;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int r0 = 32 * s + 8 * lg + q4;
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const int plo = a ^ ((r0 >> 3) & 1), phi = a ^ (((r0 + 4) >> 3) & 1);
+                gf[a][s] = trf(G + r0 * 64 + plo * 32 + 8 * pp, G + (r0 + 4) * 64 + phi * 32 + 8 * pp);
+            }
+        }
+    };
+    auto mfma_q = [&](int q, const bf16x8 (&gf)[2][2]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[b][s], gf[a][s], acc[2 * q + a][b], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    const int nk = (pix1 > pix0) ? (pix1 - pix0 + KP - 1) / KP : 0;
+    if (nk > 0) {
+        issue_x(pix0, smem, 0);
+        issue_x(pix0, smem, 1);
+        issue_g(pix0, smem, 0);
+        issue_g(pix0, smem, 1);
+        advance();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if (grp == 1) bar();
+        for (int t = 0; t < nk; ++t) {
+            char* cur = smem + (t & 1) * STAGE;
+            char* nxt = smem + ((t & 1) ^ 1) * STAGE;
+            const int k1 = pix0 + (t + 1) * KP;      // >= pix1 on the last stage: the DMAs read nothing
+            // P1
+            read_x(cur);
+            read_g(cur, 0, gfx);
+            issue_x(k1, nxt, 0);
+            bar();
+            mfma_q(0, gfx);
+            bar();
+            // P2
+            read_g(cur, 1, gfy);
+            issue_x(k1, nxt, 1);
+            bar();
+            mfma_q(1, gfy);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            bar();
+            // P3
+            read_g(cur, 2, gfx);
+            issue_g(k1, nxt, 0);
+            bar();
+            mfma_q(2, gfx);
+            bar();
+            // P4
+            read_g(cur, 3, gfy);
+            issue_g(k1, nxt, 1);
+            advance();
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            bar();
+            mfma_q(3, gfy);
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            bar();
+        }
+        if (grp == 0) bar();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // fp32 slab: lane holds columns kk..kk+3 of channel row cg for every (m, b) block
+    float* ws = p.ws + (long)z * p.Cg * p.KK;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int row = cbase + m * 16 + l16;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int col = nt * 256 + wc * 64 + b * 16 + lg * 4;
+            if (col < p.KK) *(f32x4*)(ws + (long)row * p.KK + col) = acc[m][b];
+        }
+    }
+}
+
 // sums groups of G consecutive split slabs into the group's first slab (first pass of a wide reduce)
 __global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs) {
     const long ngroups = (nsplit + G - 1) / G;
@@ -2177,6 +2397,28 @@ static void wgrad_tile(int dtype, long M, int Cg, int& tm, int& tn) {
     else { tm = 128; tn = 128; }
 }
 
+// the 64-pixel ping-pong weight gradient: bf16, a stage inside one output row, at least one 256-channel window
+static bool wgrad_use_pp2(int dtype, long M, int Ho, int Wo, int Cg) {
+    static int mode = -2;
+    if (mode == -2) { const char* e = getenv("SCD_WGRAD_PP2"); mode = e ? atoi(e) : 1; }
+    return mode && dtype == SCD_DT_BF16 && Cg >= 256 && Wo % 64 == 0 && ((long)Ho * Wo) % 64 == 0 && M >= 64 * 256;
+}
+
+static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
+    // about two rounds of one-per-CU workgroups over the 256-channel windows, whole XCD groups, >= 2048 pixels
+    // per split, fp32 slabs capped at 256 MB
+    const long tiles = (long)(Cg / 256) * cdiv(KK, 256);
+    long ns = std::max(8L, (512L / tiles + 4) / 8 * 8);
+    ns = std::min(ns, std::max(8L, M / 2048 / 8 * 8));
+    ns = std::min(ns, std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * KK) / 8 * 8));
+    return (int)ns;
+}
+
+extern "C" int scd_conv_wgrad_nsplit2(int dtype, long M, int Ho, int Wo, int Cg, int T, int Ci) {
+    if (wgrad_use_pp2(dtype, M, Ho, Wo, Cg)) return wgrad_pp2_nsplit(M, Cg, T * Ci);
+    return scd_conv_wgrad_nsplit(dtype, M, Cg, T, Ci);
+}
+
 extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
     if (wgrad_use_pp(dtype, M, Cg, T * Ci)) {
         // about three rounds of one-per-CU workgroups, whole XCD groups of splits, >= 1024 pixels per split,
@@ -2207,6 +2449,7 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     WgradParams p;
     p.g = (const char*)g; p.x = (const char*)x; p.ws = ws;
     p.N = N; p.Ho = Ho; p.Wo = Wo; p.Cg = Cg; p.Hi = Hi; p.Wi = Wi; p.Ci = Ci; p.is = in_stride; p.T = T;
+    p.cg0 = 0; p.cgn = Cg;
     p.KK = T * Ci;
     {
         const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
@@ -2220,6 +2463,35 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     int chunk = cdiv(M, nsplit);
     chunk = (chunk + 63) / 64 * 64;
     p.chunk = chunk;
+    if (wgrad_use_pp2(dtype, M, Ho, Wo, Cg) && chunk % 64 == 0) {
+        // 256-channel windows on the ping-pong kernel, a remainder on the register-staged one
+        hipStream_t st = (hipStream_t)stream;
+        p.ntn = cdiv(p.KK, 256);
+        p.nsplit = nsplit;
+        const int n8 = (nsplit + 7) / 8 * 8;
+        p.cg0 = 0;
+        p.cgn = Cg / 256 * 256;
+        p.ntm = Cg / 256;
+        hipLaunchKernelGGL(conv_wgrad_pp2_kernel, dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess || Cg % 256 == 0) return (int)e;
+        p.cg0 = Cg / 256 * 256;
+        p.cgn = Cg % 256;
+        int BM, BN;
+        wgrad_tile(dtype, M, p.cgn, BM, BN);
+        p.ntm = cdiv(p.cgn, BM);
+        p.ntn = cdiv(p.KK, BN);
+        const bool fastok = wgrad_fastx() && ((long)Ho * Wo) % 64 == 0;
+        dim3 grid(p.ntm * p.ntn * n8);
+        if (BM == 64) {
+            if (fastok) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
+            else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), 0, st, p);
+        } else {
+            if (fastok) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
+            else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), 0, st, p);
+        }
+        SCD_RETURN_LAUNCH();
+    }
     if (wgrad_use_pp(dtype, M, Cg, p.KK)) {
         hipStream_t st = (hipStream_t)stream;
         p.ntn = cdiv(p.KK, 256);

@@ -50,6 +50,7 @@ SIGNATURES = {
     "scd_conv_gemm_heads": (I, [I, P, P, P, P, I, I, I, I, I, IP, PP, PP, PP, P]),
     "scd_conv_wgrad_workspace": (c_size_t, [I, I, I, I]),
     "scd_conv_wgrad_nsplit": (I, [I, L, I, I, I]),
+    "scd_conv_wgrad_nsplit2": (I, [I, L, I, I, I, I, I]),
     "scd_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, IP, IP, P]),
     "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, P]),
     "scd_pack_weight": (I, [I, P, P, I, I, I, I, I, I, P]),

@@ -342,7 +342,7 @@ def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True,
     dh = L.int_array([r - pad for r in range(kh) for s in range(kw)])
     dw = L.int_array([s - pad for r in range(kh) for s in range(kw)])
     M = N * Ho * Wo
-    ns = L.lib().scd_conv_wgrad_nsplit(dt(g), M, Cg, T, Ci)
+    ns = L.lib().scd_conv_wgrad_nsplit2(dt(g), M, Ho, Wo, Cg, T, Ci)
     ws = torch.empty(L.lib().scd_conv_wgrad_workspace(Cg, T, Ci, ns) // 4, dtype=torch.float32, device=g.device)
     L.call("scd_conv_wgrad", dt(g), ptr(g), ptr(x), ptr(ws), ns, N, Ho, Wo, Cg, Hi, Wi, Ci, stride, T, dh, dw,
            stream())

@@ -81,6 +81,7 @@ LARGE_CONV_CASES = [
     (10, 64, 100, 64, 192, 3, 1, 1),      # halo BN 192 fwd, last tile row ragged
     (10, 192, 100, 64, 64, 3, 1, 1),      # halo BN 192 dgrad, ragged
     (2, 64, 181, 179, 384, 3, 1, 1),      # gather ping-pong (odd width), ragged M
+    (2, 64, 128, 128, 384, 3, 1, 1),      # weight gradient: 256-channel ping-pong window + 128-channel remainder
 ]
 
 
