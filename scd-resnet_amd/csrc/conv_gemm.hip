@@ -1904,10 +1904,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp_kernel(WgradParams p, in
 // 3/4 of stage t, like the A rows of the forward kernel; X ([64 px][512 B], read whole in phase 1) is
 // fetched in phases 1/2.  Counted waits as conv_gemm_pp_kernel (NB2 = 2).  Requires Wo % 64 == 0 and
 // (Ho*Wo) % 64 == 0: a stage is part of one output row, addressed by a scalar cursor (see FASTX 1).
+template <int NQ>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     constexpr int KP = 64, EPC = 8;
     constexpr int QIMG = KP * 64;                     // one G quarter image: 64 px x 64 B
-    constexpr int GBYTES = 8 * QIMG;                  // 2 groups x 4 quarters
+    constexpr int GBYTES = 2 * NQ * QIMG;             // 2 groups x NQ quarters
+    constexpr int WIN = 64 * NQ;                      // channels per window (256 or 192)
+    static_assert(NQ == 3 || NQ == 4, "NQ");
     constexpr int STAGE = GBYTES + KP * 512;          // + X image
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
@@ -1920,7 +1923,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     const int M = p.N * p.Ho * p.Wo;
     const int pix0 = z * p.chunk;
     const int pix1 = min(M, pix0 + p.chunk);
-    const int cbase = p.cg0 + mt * 256 + grp * 128;   // this group's first channel
+    const int cbase = p.cg0 + mt * WIN + grp * 32 * NQ;   // this group's first channel
 
     // G DMA: quarter q, rows 16*wc + lane/4; the lane's 16-B slot (lane & 3) holds logical chunk c
     const int g_r = 16 * wc + (lane >> 2);
@@ -1982,14 +1985,10 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
             dma16_asm(xrs, stg + GBYTES + 2 * (4 * wave + j) * 512, sel_off(ok, (S + xL[j]) * 2));
         }
     };
-    auto issue_g = [&](int k0, char* stg, int half) {
+    auto issue_g = [&](int k0, char* stg, int q) {
         const int kr = pix1 - k0;
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            const int q = 2 * half + qq;
-            dma16_asm(grs, stg + (grp * 4 + q) * QIMG + 16 * wc * 64,
-                      sel_off(g_r < kr, ((k0 + g_r) * p.Cg + g_off + q * 32) * 2));
-        }
+        dma16_asm(grs, stg + (grp * NQ + q) * QIMG + 16 * wc * 64,
+                  sel_off(g_r < kr, ((k0 + g_r) * p.Cg + g_off + q * 32) * 2));
     };
 
     const int l16 = lane & 15, lg = lane >> 4;
@@ -2001,9 +2000,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(bf16x8, v);
     };
-    f32x4 acc[8][4];
+    f32x4 acc[2 * NQ][4];
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < 2 * NQ; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
     bf16x8 xf[4][2], gfx[2][2], gfy[2][2];
@@ -2022,7 +2021,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         }
     };
     auto read_g = [&](const char* stg, int q, bf16x8 (&gf)[2][2]) {
-        const char* G = stg + (grp * 4 + q) * QIMG;
+        const char* G = stg + (grp * NQ + q) * QIMG;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int r0 = 32 * s + 8 * lg + q4;
@@ -2057,45 +2056,43 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     if (nk > 0) {
         issue_x(pix0, smem, 0);
         issue_x(pix0, smem, 1);
-        issue_g(pix0, smem, 0);
-        issue_g(pix0, smem, 1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) issue_g(pix0, smem, q);
         advance();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();
         if (grp == 1) bar();
+        // schedule (stage t fetches stage t+1 into the other buffer): phase 1: X half 0, phase 2: X half 1,
+        // phases 3(-4): the G quarters.  NQ 4: C2 vmcnt(4), L4 vmcnt(4), C4 vmcnt(2);
+        // NQ 3: C1 vmcnt(3), C2 vmcnt(4), L3 vmcnt(3), C3 vmcnt(2)
         for (int t = 0; t < nk; ++t) {
             char* cur = smem + (t & 1) * STAGE;
             char* nxt = smem + ((t & 1) ^ 1) * STAGE;
             const int k1 = pix0 + (t + 1) * KP;      // >= pix1 on the last stage: the DMAs read nothing
-            // P1
-            read_x(cur);
-            read_g(cur, 0, gfx);
-            issue_x(k1, nxt, 0);
-            bar();
-            mfma_q(0, gfx);
-            bar();
-            // P2
-            read_g(cur, 1, gfy);
-            issue_x(k1, nxt, 1);
-            bar();
-            mfma_q(1, gfy);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            bar();
-            // P3
-            read_g(cur, 2, gfx);
-            issue_g(k1, nxt, 0);
-            bar();
-            mfma_q(2, gfx);
-            bar();
-            // P4
-            read_g(cur, 3, gfy);
-            issue_g(k1, nxt, 1);
-            advance();
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            bar();
-            mfma_q(3, gfy);
-            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            bar();
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                bf16x8 (&gf)[2][2] = (q & 1) ? gfy : gfx;
+                if (q == 0) read_x(cur);
+                read_g(cur, q, gf);
+                if (q < 2) issue_x(k1, nxt, q);
+                if constexpr (NQ == 4) {
+                    if (q == 2) { issue_g(k1, nxt, 0); issue_g(k1, nxt, 1); }
+                    if (q == 3) { issue_g(k1, nxt, 2); issue_g(k1, nxt, 3); advance(); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+                } else {
+                    if (q == 2) { issue_g(k1, nxt, 0); issue_g(k1, nxt, 1); issue_g(k1, nxt, 2); advance(); asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); }
+                }
+                bar();
+                mfma_q(q, gf);
+                if constexpr (NQ == 4) {
+                    if (q == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    if (q == 3) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                } else {
+                    if (q == 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                    if (q == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    if (q == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                }
+                bar();
+            }
         }
         if (grp == 0) bar();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2103,7 +2100,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     // fp32 slab: lane holds columns kk..kk+3 of channel row cg for every (m, b) block
     float* ws = p.ws + (long)z * p.Cg * p.KK;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    for (int m = 0; m < 2 * NQ; ++m) {
         const int row = cbase + m * 16 + l16;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -2114,12 +2111,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
 }
 
 // sums groups of G consecutive split slabs into the group's first slab (first pass of a wide reduce)
-__global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs) {
+// (elements [e0, e0 + n) of each slab only: the rows one reduce call consumes)
+__global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs, long e0, long n) {
     const long ngroups = (nsplit + G - 1) / G;
-    const long total = ngroups * zs;
+    const long total = ngroups * n;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const long g = i / zs, e = i - g * zs;
-        float* base = ws + g * G * zs + e;
+        const long g = i / n, e = i - g * n;
+        float* base = ws + g * G * zs + e0 + e;
         float s = 0.f;
         const int n = (int)min((long)G, nsplit - g * G);
         for (int k = 0; k < n; ++k) s += base[(long)k * zs];
@@ -2404,10 +2402,13 @@ static bool wgrad_use_pp2(int dtype, long M, int Ho, int Wo, int Cg) {
     return mode && dtype == SCD_DT_BF16 && Cg >= 256 && Wo % 64 == 0 && ((long)Ho * Wo) % 64 == 0 && M >= 64 * 256;
 }
 
+// channel window of the ping-pong weight gradient: 256 (NQ 4) or, for widths that are multiples of 192 only, 192
+static int wgrad_pp2_win(int Cg) { return (Cg % 256 != 0 && Cg % 192 == 0) ? 192 : 256; }
+
 static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
-    // about two rounds of one-per-CU workgroups over the 256-channel windows, whole XCD groups, >= 2048 pixels
+    // about two rounds of one-per-CU workgroups over the channel windows, whole XCD groups, >= 2048 pixels
     // per split, fp32 slabs capped at 256 MB
-    const long tiles = (long)(Cg / 256) * cdiv(KK, 256);
+    const long tiles = (long)(Cg / wgrad_pp2_win(Cg)) * cdiv(KK, 256);
     long ns = std::max(8L, (512L / tiles + 4) / 8 * 8);
     ns = std::min(ns, std::max(8L, M / 2048 / 8 * 8));
     ns = std::min(ns, std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * KK) / 8 * 8));
@@ -2469,14 +2470,16 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
         p.ntn = cdiv(p.KK, 256);
         p.nsplit = nsplit;
         const int n8 = (nsplit + 7) / 8 * 8;
+        const int win = wgrad_pp2_win(Cg);
         p.cg0 = 0;
-        p.cgn = Cg / 256 * 256;
-        p.ntm = Cg / 256;
-        hipLaunchKernelGGL(conv_wgrad_pp2_kernel, dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
+        p.cgn = Cg / win * win;
+        p.ntm = Cg / win;
+        if (win == 256) hipLaunchKernelGGL((conv_wgrad_pp2_kernel<4>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
+        else hipLaunchKernelGGL((conv_wgrad_pp2_kernel<3>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
         hipError_t e = hipGetLastError();
-        if (e != hipSuccess || Cg % 256 == 0) return (int)e;
-        p.cg0 = Cg / 256 * 256;
-        p.cgn = Cg % 256;
+        if (e != hipSuccess || Cg % win == 0) return (int)e;
+        p.cg0 = Cg / win * win;
+        p.cgn = Cg % win;
         int BM, BN;
         wgrad_tile(dtype, M, p.cgn, BM, BN);
         p.ntm = cdiv(p.cgn, BM);
@@ -2560,9 +2563,10 @@ extern "C" int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int 
     if (nsplit > 32) {
         // two-pass: groups of 16 slabs summed in place (parallel over groups), then the group heads
         const int G = 16;
-        const long total = (long)((nsplit + G - 1) / G) * zs;
+        const long e0 = (long)r0 * T * Ci, n = (long)(r1 - r0) * T * Ci;
+        const long total = (long)((nsplit + G - 1) / G) * n;
         hipLaunchKernelGGL(wgrad_presum_kernel, dim3((int)std::min<long>(8192, (total + 255) / 256)), dim3(256), 0, st,
-                           (float*)ws, nsplit, G, zs);
+                           (float*)ws, nsplit, G, zs, e0, n);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
         ns = (nsplit + G - 1) / G;
