@@ -78,13 +78,17 @@ __device__ __forceinline__ void load_params(const float* p, float* v) {
 }
 
 template <typename T>
-__global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const float* scale, const float* shift,
-                                const T* res, const float* rscale, const float* rshift, int relu) {
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const float* scale,
+                                                       const float* shift, const T* res, const float* rscale,
+                                                       const float* rshift, int relu) {
     constexpr int E = Vec16<T>::N;
+    constexpr int U = 4;
     // the grid stride is a multiple of the chunks per row (C/E divides 256): a thread always owns the same
-    // E channels, so the per-channel parameters live in registers (no LDS, no bank conflicts)
+    // E channels, so the per-channel parameters live in registers (no LDS, no bank conflicts).  U vectors
+    // per thread are loaded before any is used (U x 16 B, x2 with a residual, in flight per thread).
     const unsigned cpr = (unsigned)C / E;
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned stride = gridDim.x * blockDim.x;
     const int c0 = (int)(v0 % cpr) * E;
     float sc[E], sh[E], rs[E], rh[E];
     load_params<E>(scale + c0, sc);
@@ -94,11 +98,7 @@ __global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const 
 #pragma unroll
         for (int e = 0; e < E; ++e) { rs[e] = 0.f; rh[e] = 0.f; }
     }
-    for (unsigned v = v0; v < nvec; v += gridDim.x * blockDim.x) {
-        const size_t i = (size_t)v * E;
-        float a[E], r[E];
-        Vec16<T>::load(y + i, a);
-        if (res) Vec16<T>::load(res + i, r);
+    auto body = [&](float* a, const float* r) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             float o = a[e] * sc[e] + sh[e];
@@ -106,7 +106,27 @@ __global__ void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const 
             if (relu) o = fmaxf(o, 0.f);
             a[e] = o;
         }
-        Vec16<T>::store(out + i, a);
+    };
+    unsigned v = v0;
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+        float a[U][E], r[U][E];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            Vec16<T>::load(y + (size_t)(v + u * stride) * E, a[u]);
+            if (res) Vec16<T>::load(res + (size_t)(v + u * stride) * E, r[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            body(a[u], r[u]);
+            Vec16<T>::store(out + (size_t)(v + u * stride) * E, a[u]);
+        }
+    }
+    for (; v < nvec; v += stride) {
+        float a[E], r[E];
+        Vec16<T>::load(y + (size_t)v * E, a);
+        if (res) Vec16<T>::load(res + (size_t)v * E, r);
+        body(a, r);
+        Vec16<T>::store(out + (size_t)v * E, a);
     }
 }
 
@@ -208,12 +228,15 @@ __global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double co
 }
 
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* rsc, const float* rsh,
-                                    const float* coef, int C, unsigned nvec, T* dy, T* dz_out) {
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* rsc,
+                                                           const float* rsh, const float* coef, int C, unsigned nvec,
+                                                           T* dy, T* dz_out) {
     constexpr int E = Vec16<T>::N;
-    // fixed channel chunk per thread (see bn_apply_kernel): coefficients in registers
+    constexpr int U = 4;
+    // fixed channel chunk per thread (see bn_apply_kernel): coefficients in registers; U vectors in flight
     const unsigned cpr = (unsigned)C / E;
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned stride = gridDim.x * blockDim.x;
     const int c0 = (int)(v0 % cpr) * E;
     float ca[E], cb[E], cc[E], ka[E], kb[E];
     load_params<E>(coef + c0, ca);
@@ -224,25 +247,46 @@ __global__ void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, co
 #pragma unroll
         for (int e = 0; e < E; ++e) { ka[e] = 0.f; kb[e] = 0.f; }
     }
-    for (unsigned v = v0; v < nvec; v += gridDim.x * blockDim.x) {
-        const size_t i = (size_t)v * E;
-        float d[E], yv[E], mk[E], o[E];
-        Vec16<T>::load(dout + i, d);
-        Vec16<T>::load(y + i, yv);
-        if (mask) Vec16<T>::load(mask + i, mk);
+    // d <- dz (masked gradient), yv <- dy
+    auto body = [&](float* d, float* yv, const float* mk) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
             const float dz = off ? 0.f : d[e];
             d[e] = dz;
-            o[e] = ca[e] * dz + cb[e] * yv[e] + cc[e];
+            yv[e] = ca[e] * dz + cb[e] * yv[e] + cc[e];
         }
-        Vec16<T>::store(dy + i, o);
+    };
+    unsigned v = v0;
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+        float d[U][E], yv[U][E], mk[U][E];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = (size_t)(v + u * stride) * E;
+            Vec16<T>::load(dout + i, d[u]);
+            Vec16<T>::load(y + i, yv[u]);
+            if (mask) Vec16<T>::load(mask + i, mk[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = (size_t)(v + u * stride) * E;
+            body(d[u], yv[u], mk[u]);
+            Vec16<T>::store(dy + i, yv[u]);
+            if (dz_out) Vec16<T>::store(dz_out + i, d[u]);
+        }
+    }
+    for (; v < nvec; v += stride) {
+        const size_t i = (size_t)v * E;
+        float d[E], yv[E], mk[E];
+        Vec16<T>::load(dout + i, d);
+        Vec16<T>::load(y + i, yv);
+        if (mask) Vec16<T>::load(mask + i, mk);
+        body(d, yv, mk);
+        Vec16<T>::store(dy + i, yv);
         if (dz_out) Vec16<T>::store(dz_out + i, d);
     }
 }
 
-inline int ew_blocks(long nvec) { return (int)std::min<long>(2048, std::max<long>(1, (nvec + 255) / 256)); }
 inline int fin_blocks(int C) { return (C + 3) / 4; }   // 4 waves (channels) per 256-thread block
 
 }  // namespace
@@ -270,12 +314,14 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
     if (dtype == SCD_DT_BF16) {
         if (C % 8 || 256 % (C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
-        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const __bf16*)y,
+        static const int g = resident_grid((const void*)bn_apply_kernel<__bf16>, 256);
+        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st, (const __bf16*)y,
                            (__bf16*)out, C, (unsigned)nvec, scale, shift, (const __bf16*)res, rscale, rshift, relu);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4 || 256 % (C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
-        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)y,
+        static const int g = resident_grid((const void*)bn_apply_kernel<float>, 256);
+        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st, (const float*)y,
                            (float*)out, C, (unsigned)nvec, scale, shift, (const float*)res, rscale, rshift, relu);
     } else {
         return SCD_ERR_ARG;
@@ -292,9 +338,12 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
     const long rows = total / C;
     const int cpr = C / E;
     if (cpr > 256 || 256 % cpr || total >= (1L << 31)) return SCD_ERR_ARG;
-    // ~1024 blocks, at least 8 rows per row lane
+    // one round of resident blocks (at most), at least 8 rows per row lane
+    static const int gb = resident_grid((const void*)bn_bwd_reduce_kernel<__bf16>, 256);
+    static const int gf = resident_grid((const void*)bn_bwd_reduce_kernel<float>, 256);
+    const long nb = dtype == SCD_DT_BF16 ? gb : gf;
     const long rpi = 256 / cpr;
-    const long rpb = std::max<long>(8 * rpi, (rows + 1023) / 1024 + rpi - 1) / rpi * rpi;
+    const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
     const int blocks = cdiv(rows, rpb);
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout,
@@ -324,13 +373,15 @@ extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, c
     if (dtype == SCD_DT_BF16) {
         if (C % 8 || 256 % (C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_blocks(nvec)), dim3(256), 0, st,
+        static const int g = resident_grid((const void*)bn_bwd_apply_kernel<__bf16>, 256);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st,
                            (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, coef, C,
                            (unsigned)nvec, (__bf16*)dy, (__bf16*)dz);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4 || 256 % (C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const float*)dout,
+        static const int g = resident_grid((const void*)bn_bwd_apply_kernel<float>, 256);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st, (const float*)dout,
                            (const float*)mask, (const float*)y, relu_scale, relu_shift, coef, C, (unsigned)nvec, (float*)dy,
                            (float*)dz);
     } else {

@@ -2405,13 +2405,45 @@ static bool wgrad_use_pp2(int dtype, long M, int Ho, int Wo, int Cg) {
 // channel window of the ping-pong weight gradient: 256 (NQ 4) or, for widths that are multiples of 192 only, 192
 static int wgrad_pp2_win(int Cg) { return (Cg % 256 != 0 && Cg % 192 == 0) ? 192 : 256; }
 
+// split count from a wave-quantisation cost model (SCD_WGRAD_NSMODEL=0: the fixed rules below it).  A launch of
+// tiles x ns workgroups runs in ceil(tiles*ns / slots) rounds; a round costs its K stages (stage_us each) plus the
+// workgroup's fp32 slab store (epi_us), and every split adds one slab to the reduce (read at ~3.5 TB/s).  Candidates
+// are whole XCD groups (multiples of 8) within the pixel and slab-memory caps.
+static bool wgrad_nsmodel() {
+    static int mode = -2;
+    if (mode == -2) { const char* e = getenv("SCD_WGRAD_NSMODEL"); mode = e ? atoi(e) : 1; }
+    return mode != 0;
+}
+
+static long wgrad_ns_model(long M, long tiles, int slots, int kp, double stage_us, double epi_us, double slab_bytes,
+                           long ns_max) {
+    long best = 8;
+    double bt = 1e30;
+    for (long ns = 8; ns <= std::max(8L, ns_max); ns += 8) {
+        const long stages = cdiv(cdiv(M, ns), (long)kp);
+        const long rounds = cdiv(tiles * ns, (long)slots);
+        const double t = rounds * (stages * stage_us + epi_us) + ns * slab_bytes / 3.5e6;
+        if (t < bt * 0.995) { bt = t; best = ns; }
+    }
+    return best;
+}
+
 static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
+    const int win = wgrad_pp2_win(Cg);
+    const long tiles = (long)(Cg / win) * cdiv(KK, 256);
+    const long cap_px = std::max(8L, M / 2048 / 8 * 8);
+    const long cap_mem = std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * KK) / 8 * 8);
+    if (wgrad_nsmodel()) {
+        // one workgroup per CU; a 64-pixel stage ~ 2*win*256*64 flop at ~4.3 TF/s per CU; slab win x 256 fp32
+        const double stage_us = 2.0 * win * 256 * 64 / 4.3e6;
+        const double epi_us = 4.0 * win * 256 / (5.0e6 / 256);
+        return (int)wgrad_ns_model(M, tiles, 256, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem));
+    }
     // about two rounds of one-per-CU workgroups over the channel windows, whole XCD groups, >= 2048 pixels
     // per split, fp32 slabs capped at 256 MB
-    const long tiles = (long)(Cg / wgrad_pp2_win(Cg)) * cdiv(KK, 256);
     long ns = std::max(8L, (512L / tiles + 4) / 8 * 8);
-    ns = std::min(ns, std::max(8L, M / 2048 / 8 * 8));
-    ns = std::min(ns, std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * KK) / 8 * 8));
+    ns = std::min(ns, cap_px);
+    ns = std::min(ns, cap_mem);
     return (int)ns;
 }
 
@@ -2436,6 +2468,17 @@ extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
     const bool ring = wgrad_use_ring(dtype, M, Cg);
     // ~4 (ring, one workgroup per CU) / 4 (two per CU) waves of workgroups over 256 CUs, >= 1024 pixels per split,
     // fp32 slabs capped at 256 MB
+    if (!ring && wgrad_nsmodel() && M >= 8 * 1024) {
+        // 128x128: two workgroups per CU, 64x256: one (register-bound); a stage of KP pixels ~ 2*tm*tn*KP flop
+        // at ~2.4 TF/s per CU; slab tm x tn fp32
+        const int KP = dtype == SCD_DT_BF16 ? 64 : 32;
+        const int slots = tm == 64 ? 256 : 512;
+        const double stage_us = 2.0 * tm * tn * KP / (2.4e6 * 256 / slots);
+        const double epi_us = 4.0 * tm * tn / (5.0e6 / slots);
+        const long cap_px = std::max(8L, M / 1024 / 8 * 8);
+        const long cap_mem = std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * T * Ci) / 8 * 8);
+        return (int)wgrad_ns_model(M, tiles, slots, KP, stage_us, epi_us, 4.0 * Cg * T * Ci, std::min(cap_px, cap_mem));
+    }
     long ns = std::max(1L, std::min((ring ? 1024L : 1024L) / std::max(1L, tiles), M / 1024));
     ns = std::max(1L, std::min(ns, (256L << 20) / std::max(1L, 4L * Cg * T * Ci)));
     if (ns >= 8) ns = ns / 8 * 8;          // whole XCD groups (see wgrad_block)

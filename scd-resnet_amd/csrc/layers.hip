@@ -41,24 +41,26 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
         if (d[mid].start <= e0) lo = mid; else hi = mid - 1;
     }
     const scd_pack_desc q = d[lo];
-    const long count = q.mode == 0 ? (long)q.A * q.ldp : (long)q.B * q.T * q.A;
+    // 32-bit index math (a descriptor holds < 2^31 elements; 64-bit divides dominated this kernel)
+    const unsigned count = q.mode == 0 ? (unsigned)q.A * q.ldp : (unsigned)q.B * q.T * q.A;
+    const unsigned base = (unsigned)(e0 - q.start);
+    const unsigned ldp = q.ldp, B = q.B, Tt = q.T, A = q.A, TA = Tt * A;
 #pragma unroll 4
     for (int j = 0; j < PACK_UNIT / 256; ++j) {
-        const long i = e0 - q.start + threadIdx.x + 256 * j;
+        const unsigned i = base + threadIdx.x + 256 * j;
         if (i >= count) break;
         float v;
-        long o;
+        unsigned o;
         if (q.mode == 0) {            // out[row_off + a][t*B + b] = w[a][b][t]   (A x ldp elements, padding zeroed)
-            const int r = (int)(i / q.ldp), k = (int)(i - (long)r * q.ldp);
-            const int t = k / q.B, b = k - (k / q.B) * q.B;
-            v = t < q.T ? q.w[((long)r * q.B + b) * q.T + t] : 0.f;
-            o = (long)(q.row_off + r) * q.ldp + k;
+            const unsigned r = i / ldp, k = i - r * ldp;
+            const unsigned t = k / B, b = k - t * B;
+            v = t < Tt ? q.w[(r * B + b) * Tt + t] : 0.f;
+            o = (q.row_off + r) * ldp + k;
         } else {                      // out[b][t*a_tot + a_off + a] = w[a][b][t]  (B x T x A elements)
-            const int TA = q.T * q.A;
-            const int r = (int)(i / TA), rem = (int)(i - (long)r * TA);
-            const int t = rem / q.A, a = rem - (rem / q.A) * q.A;
-            v = q.w[((long)a * q.B + r) * q.T + t];
-            o = (long)r * q.ldp + (long)t * q.a_tot + q.a_off + a;
+            const unsigned r = i / TA, rem = i - r * TA;
+            const unsigned t = rem / A, a = rem - t * A;
+            v = q.w[(a * B + r) * Tt + t];
+            o = r * ldp + t * q.a_tot + q.a_off + a;
         }
         if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
         else ((float*)q.out)[o] = v;
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
 }
 
 extern "C" int scd_pack_weights_batched(int dtype, const scd_pack_desc* descs, int n, long total, void* stream) {
-    if (n < 1 || total < 1 || total % PACK_UNIT || (dtype != SCD_DT_BF16 && dtype != SCD_DT_F32)) return SCD_ERR_ARG;
+    if (n < 1 || total < 1 || total >= (1L << 31) || total % PACK_UNIT || (dtype != SCD_DT_BF16 && dtype != SCD_DT_F32)) return SCD_ERR_ARG;
     hipLaunchKernelGGL(pack_weights_batched_kernel, dim3((unsigned)(total / PACK_UNIT)), dim3(256), 0, (hipStream_t)stream,
                        descs, n, dtype == SCD_DT_BF16 ? 1 : 0);
     SCD_RETURN_LAUNCH();
@@ -563,7 +565,9 @@ extern "C" int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* 
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E || 256 % (C / E)) return SCD_ERR_ARG;
     const long total = (long)N * H * W * (C / E);
-    const int blocks = (int)std::min<long>(2048, (total + 255) / 256);
+    static const int gb = resident_grid((const void*)stem_pool_bwd_bn_kernel<__bf16>, 256);
+    static const int gf = resident_grid((const void*)stem_pool_bwd_bn_kernel<float>, 256);
+    const int blocks = (int)std::min<long>(dtype == SCD_DT_BF16 ? gb : gf, (total + 255) / 256);
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((stem_pool_bwd_bn_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout, argmax,
                            (const __bf16*)y, scale, shift, mean, invstd, (__bf16*)dz, stats, N, H, W, C, Ho, Wo);
@@ -615,7 +619,9 @@ extern "C" int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, 
     if (P * nh * Hd >= (1L << 31)) return SCD_ERR_ARG;     // 32-bit element offsets
     const int G = 512 / cpp;                                // pixel lanes (cpp <= 256 -> G >= 2)
     const int threads = G * cpp;
-    const int PXB = 1024;
+    static int pxb_env = -1;
+    if (pxb_env < 0) { const char* e = getenv("SCD_HEADS_PXB"); pxb_env = e ? atoi(e) : 0; }
+    const int PXB = pxb_env > 0 ? pxb_env : 1024;
     const int blocks = cdiv(P, PXB);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
