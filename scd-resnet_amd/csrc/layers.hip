@@ -269,6 +269,101 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_bn_kernel(const T* dout, co
     }
 }
 
+// The same pass for even inputs (H = 2 Ho, W = 2 Wo), one thread per 2x2 input block and 16-B channel chunk:
+// input rows {2oh, 2oh+1} x cols {2ow, 2ow+1} are covered only by pooled outputs (oh..oh+1, ow..ow+1), so the
+// thread issues its 4 gradient vectors, 4 argmax words and 4 activation vectors together (no data-dependent
+// branches around loads) and each pooled gradient is read ~once per 4 inputs.  Window position of input
+// (2oh+a, 2ow+b) in output (oh+i, ow+j): di = a - 2i + 1, dj = b - 2j + 1; sums run over outputs in
+// (oh, ow) order as the generic kernel's loops do.
+template <typename T>
+__global__ __launch_bounds__(256) void stem_pool_bwd_bn_2x2_kernel(const T* dout, const uint8_t* argmax, const T* y,
+                                                                   const float* scale, const float* shift,
+                                                                   const float* mean, const float* invstd, T* dz,
+                                                                   double* stats, int N, int C, int Ho, int Wo) {
+    constexpr int E = Vec16<T>::N;
+    const unsigned cpp = C / E;
+    const unsigned total = (unsigned)N * Ho * Wo * cpp;
+    const unsigned HWo = (unsigned)Ho * Wo;
+    const int W = 2 * Wo;
+    const int ch = (int)(threadIdx.x % cpp);
+    float sc[E], sh[E], mu[E], is[E], s1[E], s2[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        sc[e] = scale[ch * E + e]; sh[e] = shift[ch * E + e]; mu[e] = mean[ch * E + e]; is[e] = invstd[ch * E + e];
+        s1[e] = 0.f; s2[e] = 0.f;
+    }
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const unsigned blk = i / cpp;
+        const unsigned n = blk / HWo;
+        const unsigned rem = blk - n * HWo;
+        const int oh = (int)(rem / Wo), ow = (int)(rem - (rem / Wo) * Wo);
+        const bool okh = oh + 1 < Ho, okw = ow + 1 < Wo;
+        // pooled outputs O[i][j] = (oh+i, ow+j); out-of-range ones read O[0][0] and are ignored
+        float d[2][2][E];
+        uint8_t am[2][2][E];
+        float v[2][2][E];
+#pragma unroll
+        for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+            for (int oj = 0; oj < 2; ++oj) {
+                const bool ok = (oi == 0 || okh) && (oj == 0 || okw);
+                const unsigned o = ((n * Ho + oh + (ok ? oi : 0)) * Wo + ow + (ok ? oj : 0)) * C + ch * E;
+                Vec16<T>::load(dout + o, d[oi][oj]);
+                if constexpr (E == 8) *(uint2*)am[oi][oj] = *(const uint2*)(argmax + o);
+                else *(uint32_t*)am[oi][oj] = *(const uint32_t*)(argmax + o);
+                if (!ok)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) am[oi][oj][e] = 0xff;
+            }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                Vec16<T>::load(y + ((n * (2 * Ho) + 2 * oh + a) * W + 2 * ow + b) * (unsigned)C + ch * E, v[a][b]);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                float acc[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) acc[e] = 0.f;
+#pragma unroll
+                for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+                    for (int oj = 0; oj < 2; ++oj) {
+                        if (oi > a || oj > b) continue;                // (a=0 -> only i=0; a=1 -> i=0,1)
+                        const int sel = (a - 2 * oi + 1) * 3 + (b - 2 * oj + 1);
+#pragma unroll
+                        for (int e = 0; e < E; ++e)
+                            if (am[oi][oj][e] == sel) acc[e] += d[oi][oj][e];
+                    }
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const float z = v[a][b][e] * sc[e] + sh[e];
+                    acc[e] = z > 0.f ? acc[e] : 0.f;
+                }
+                Vec16<T>::store(dz + ((n * (2 * Ho) + 2 * oh + a) * W + 2 * ow + b) * (unsigned)C + ch * E, acc);
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const float r = to_f<T>(from_f<T>(acc[e]));
+                    s1[e] += r;
+                    s2[e] += r * (v[a][b][e] - mu[e]) * is[e];
+                }
+            }
+    }
+    __shared__ float red[2][256][E + 1];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { red[0][threadIdx.x][e] = s1[e]; red[1][threadIdx.x][e] = s2[e]; }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 2 * C; k += blockDim.x) {
+        const int stat = k / C, c = k - (k / C) * C;
+        const int cc = c / E, e = c - (c / E) * E;
+        double a = 0.0;
+        for (int t = cc; t < (int)blockDim.x; t += cpp) a += red[stat][t][e];
+        atomic_add_f64(stats + ((long)(blockIdx.x % SCD_STAT_REPLICAS) * 2 + stat) * C + c, a);
+    }
+}
+
 // ---------------------------------------------------------------- CenterNet head tails
 struct HeadsDesc {
     int nh, Hd, od[4], orow[4], nout;
@@ -325,12 +420,11 @@ __global__ void heads_fwd_kernel(const T* hid, int N, int HW, HeadsDesc d) {
 // Block = PXB pixels, blockDim = G pixel-lanes x cpp chunk-lanes; each thread streams its chunk over
 // every G-th pixel, 4 pixels per step with all loads issued before use; block partials are folded in
 // LDS by all threads and added to fp64 replicas (SCD_STAT_REPLICAS).
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(512) void heads_bwd_kernel(const T* hid, int N, int HW, HeadsDesc d, T* dhid,
                                                         double* acc, int accsz, int PXB) {
     constexpr int E = Vec16<T>::N;
     constexpr int NA = 4 * E + E + 4;               // dW1 partials, db0 partials, db1 partials
-    constexpr int U = 4;
     const int cph = d.Hd / E;
     const int cpp = d.nh * cph;
     const int G = blockDim.x / cpp;
@@ -565,6 +659,23 @@ extern "C" int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* 
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E || 256 % (C / E)) return SCD_ERR_ARG;
     const long total = (long)N * H * W * (C / E);
+    static int mode = -1;
+    if (mode < 0) { const char* e = getenv("SCD_POOL_2X2"); mode = e ? atoi(e) : 1; }
+    if (mode && H == 2 * Ho && W == 2 * Wo && (long)N * H * W * C < (1L << 31)) {
+        static const int g2b = resident_grid((const void*)stem_pool_bwd_bn_2x2_kernel<__bf16>, 256);
+        static const int g2f = resident_grid((const void*)stem_pool_bwd_bn_2x2_kernel<float>, 256);
+        const long blocks2 = (long)N * Ho * Wo * (C / E);
+        const int grid = (int)std::min<long>(dtype == SCD_DT_BF16 ? g2b : g2f, (blocks2 + 255) / 256);
+        if (dtype == SCD_DT_BF16)
+            hipLaunchKernelGGL((stem_pool_bwd_bn_2x2_kernel<__bf16>), dim3(grid), dim3(256), 0, st, (const __bf16*)dout,
+                               argmax, (const __bf16*)y, scale, shift, mean, invstd, (__bf16*)dz, stats, N, C, Ho, Wo);
+        else if (dtype == SCD_DT_F32)
+            hipLaunchKernelGGL((stem_pool_bwd_bn_2x2_kernel<float>), dim3(grid), dim3(256), 0, st, (const float*)dout,
+                               argmax, (const float*)y, scale, shift, mean, invstd, (float*)dz, stats, N, C, Ho, Wo);
+        else
+            return SCD_ERR_ARG;
+        SCD_RETURN_LAUNCH();
+    }
     static const int gb = resident_grid((const void*)stem_pool_bwd_bn_kernel<__bf16>, 256);
     static const int gf = resident_grid((const void*)stem_pool_bwd_bn_kernel<float>, 256);
     const int blocks = (int)std::min<long>(dtype == SCD_DT_BF16 ? gb : gf, (total + 255) / 256);
@@ -621,15 +732,20 @@ extern "C" int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, 
     const int threads = G * cpp;
     static int pxb_env = -1;
     if (pxb_env < 0) { const char* e = getenv("SCD_HEADS_PXB"); pxb_env = e ? atoi(e) : 0; }
-    const int PXB = pxb_env > 0 ? pxb_env : 1024;
+    const int PXB = pxb_env > 0 ? pxb_env : 2048;      // one 1-per-CU round at B=32, 128x128
     const int blocks = cdiv(P, PXB);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((heads_bwd_kernel<__bf16>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid, N, HW,
-                           d, (__bf16*)dhid, acc, accsz, PXB);
+    static int u_env = -1;
+    if (u_env < 0) { const char* e = getenv("SCD_HEADS_U"); u_env = e ? atoi(e) : 8; }
+    if (dtype == SCD_DT_BF16 && u_env == 8)
+        hipLaunchKernelGGL((heads_bwd_kernel<__bf16, 8>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid, N,
+                           HW, d, (__bf16*)dhid, acc, accsz, PXB);
+    else if (dtype == SCD_DT_BF16)
+        hipLaunchKernelGGL((heads_bwd_kernel<__bf16, 4>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid, N,
+                           HW, d, (__bf16*)dhid, acc, accsz, PXB);
     else if (dtype == SCD_DT_F32)
-        hipLaunchKernelGGL((heads_bwd_kernel<float>), dim3(blocks), dim3(threads), 0, st, (const float*)hid, N, HW, d,
-                           (float*)dhid, acc, accsz, PXB);
+        hipLaunchKernelGGL((heads_bwd_kernel<float, 4>), dim3(blocks), dim3(threads), 0, st, (const float*)hid, N, HW,
+                           d, (float*)dhid, acc, accsz, PXB);
     else
         return SCD_ERR_ARG;
     SCD_RETURN_LAUNCH();

@@ -158,6 +158,51 @@ def test_heads_fused_gemm(N, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("HW", [(128, 128), (9, 11)])
+def test_heads_tail_backward(HW, dtype):
+    """scd_heads_bwd + finalize (CenterNet tails, centerNetOffset.py:108-110): dhid = relu'(hid) * W1^T dout,
+    dW1 = sum dout x hid, db1 = sum dout, db0 = sum dhid against torch fp32 on the same hidden tensor
+    (128x128: whole 4-pixel unrolled steps; 9x11: ragged tail)."""
+    from scdhip import ops
+    L = ops.L
+    g = torch.Generator().manual_seed(77)
+    N, (H, W), Hd, od = 2, HW, 128, [1, 4, 2]
+    P = N * H * W
+    hid = F.relu(torch.randn(N, H, W, Hd * 3, generator=g))
+    if dtype == torch.bfloat16:
+        hid = hid.bfloat16().float()
+    w1 = [torch.randn(o, Hd, generator=g) / Hd ** 0.5 for o in od]
+    douts = [torch.randn(N, o, H, W, generator=g) for o in od]
+    hd = hid.to(DEV, dtype).contiguous()
+    dhid = torch.empty_like(hd)
+    odarr = L.int_array(od)
+    acc = torch.zeros(L.lib().scd_heads_bwd_accsize(3, Hd, odarr) // 8, dtype=torch.float64, device=DEV)
+    w1d = [w.to(DEV).contiguous() for w in w1]
+    dd = [d.to(DEV).contiguous() for d in douts]
+    dw1 = [torch.zeros(o, Hd, device=DEV) for o in od]
+    db1 = [torch.zeros(o, device=DEV) for o in od]
+    db0 = [torch.zeros(Hd, device=DEV) for o in od]
+    L.call("scd_heads_bwd", ops.dt(hd), ops.ptr(hd), N, H * W, 3, Hd, odarr,
+           L.ptr_array([w.data_ptr() for w in w1d]), L.ptr_array([d.data_ptr() for d in dd]), ops.ptr(dhid),
+           ops.ptr(acc), ops.stream())
+    L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), 3, Hd, odarr, L.ptr_array([t.data_ptr() for t in dw1]),
+           L.ptr_array([t.data_ptr() for t in db1]), L.ptr_array([t.data_ptr() for t in db0]), 0, ops.stream())
+    torch.cuda.synchronize()
+    hp = hid.reshape(P, 3 * Hd)
+    tol = TOL[dtype] if dtype == torch.bfloat16 else 1e-5
+    for h, o in enumerate(od):
+        hh = hp[:, h * Hd:(h + 1) * Hd]
+        dh = douts[h].permute(0, 2, 3, 1).reshape(P, o)
+        ref = (dh @ w1[h]) * (hh > 0)
+        got = dhid.float().cpu().reshape(P, 3 * Hd)[:, h * Hd:(h + 1) * Hd]
+        assert rel_err(got, ref) < tol
+        assert rel_err(dw1[h], dh.t() @ hh) < 1e-5
+        assert rel_err(db1[h], dh.sum(0)) < 1e-5
+        assert rel_err(db0[h], ref.sum(0)) < 1e-5
+    assert torch.count_nonzero(acc) == 0          # the finalize re-zeroes the persistent accumulators
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_stem_im2col_gemm_pool(dtype):
     from scdhip import ops
     g = torch.Generator().manual_seed(3)
