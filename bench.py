@@ -108,10 +108,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob for a one-GPU box: SCD_BENCH_SHARE_GPU=1 puts every rank on cuda:0 over gloo (RCCL needs
+    # one GPU per rank); the driver's multi-GPU runs use the default, one GPU per rank over RCCL
+    share = os.environ.get("SCD_BENCH_SHARE_GPU", "0") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import importlib
 
@@ -124,7 +132,7 @@ def main():
     model = plugin.model(**plugin.modelParams).to(dev).set_compute_dtype(dtype).train()
     opt = FlatAdam(filter(lambda p: p.requires_grad, model.parameters()))
     if world > 1:
-        if torch.cuda.device_count() > 1:
+        if torch.cuda.device_count() > 1 or share:
             ops.set_bn_sync(dist.group.WORLD)     # SyncBN rule of networkFactory.py:128
         model = FlatDDP(model)
     lossfn = plugin.loss

@@ -8,8 +8,11 @@
   ``param_groups`` keeps the reference's setLearningRate (networkFactory.py:273-276) working.
 * ``FlatDDP``: replaces DistributedDataParallel (networkFactory.py:126-136): gradients are
   averaged across ranks with torch.distributed (RCCL over xGMI on MI355X, gloo in CPU tests)
-  from an autograd end-of-backward callback; BN buffers are broadcast from rank 0 before
-  each forward (DDP broadcast_buffers=True); state_dict keys keep the ``module.`` prefix.
+  in ~25 MB buckets of the flat gradient, each launched asynchronously as soon as the backward
+  pass has written all of its parameters' gradients (so RCCL runs on its own stream while the
+  remaining backward kernels run), the rest from an autograd end-of-backward callback that then
+  joins every bucket; BN buffers are broadcast from rank 0 before each forward (DDP
+  broadcast_buffers=True, coalesced per dtype); state_dict keys keep the ``module.`` prefix.
 """
 import torch
 import torch.distributed as dist
@@ -144,7 +147,21 @@ class _EndOfBackward(torch.autograd.Function):
 
 class FlatDDP(torch.nn.Module):
     """DistributedDataParallel replacement: one process per GPU, grads averaged over the
-    world (bucketed RCCL all-reduce of the flat gradient buffer)."""
+    world (bucketed RCCL all-reduce of the flat gradient buffer, overlapped with backward).
+
+    Gradient readiness: the model's blocks write parameter gradients straight into the flat buffer
+    (no AccumulateGrad hooks fire), so readiness is observed one level up -- every submodule that
+    holds parameters gets a forward pre-hook that hooks its first grad-requiring input; the gradient
+    w.r.t. a module's input is complete only after that module's backward has run, so the hook marks
+    all of the module's parameters ready.  Buckets are contiguous flat ranges of the parameters in
+    reverse registration order (the order backward produces them, as torch DDP buckets them); a bucket
+    whose parameters are all ready is all-reduced asynchronously (RCCL queues it behind the kernels
+    already on the compute stream).  Parameters whose module input needs no gradient (the stem) are
+    covered by the end-of-backward callback, which launches what is left in order and joins all
+    buckets before the optimizer can run.  Parameters whose gradients torch's own AccumulateGrad
+    writes (plain torch modules) may be accumulated after their module's input gradient exists:
+    the first backward only learns which they are (post-accumulate hooks) and launches every bucket
+    at the end; from then on those parameters are marked by their post-accumulate hook instead."""
 
     def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_mb=25.0):
         super(FlatDDP, self).__init__()
@@ -156,31 +173,122 @@ class FlatDDP(torch.nn.Module):
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
         self._queued = False
         self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        self._engine = set()                  # ids of parameters written by torch's AccumulateGrad
+        self._learned = False                 # one backward seen: early launches allowed
+        self._build_buckets()
+        self._hooks = []
         if self.world > 1:
+            for m in module.modules():
+                if any(True for _ in m.parameters(recurse=False)):
+                    self._hooks.append(m.register_forward_pre_hook(self._pre_hook))
+            for p in self.flat.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._acc_hook))
             # identical initial replicas (DDP broadcasts parameters from rank 0 at wrap time)
             dist.broadcast(self.flat.data, 0, group=process_group)
             self._sync_buffers()
 
+    # ---- buckets
+    def _build_buckets(self):
+        fp = self.flat
+        self._bucket_of = {}
+        self._buckets = []                    # [lo, hi) flat ranges, in launch (reverse-parameter) order
+        self._bucket_params = []
+        lo = hi = None
+        members = []
+        for p, (o, n) in reversed(list(zip(fp.params, fp.offsets))):
+            if hi is None:
+                lo, hi = o, o + n
+            elif o + n == lo and hi - o <= self.bucket_elems:
+                lo = o
+            else:
+                self._buckets.append((lo, hi))
+                self._bucket_params.append(members)
+                lo, hi, members = o, o + n, []
+            members.append(id(p))
+        self._buckets.append((lo, hi))
+        self._bucket_params.append(members)
+        for b, ms in enumerate(self._bucket_params):
+            for pid in ms:
+                self._bucket_of[pid] = b
+        self._reset_step()
+
+    def _reset_step(self):
+        self._ready = set()
+        self._pending = [len(ms) for ms in self._bucket_params]
+        self._works = [None] * len(self._buckets)
+        self._next = 0                        # buckets are launched in order: RCCL needs one order on all ranks
+
+    def _launch_ready(self, final=False):
+        while self._next < len(self._buckets) and (final or self._pending[self._next] == 0):
+            b = self._next
+            lo, hi = self._buckets[b]
+            bucket = self.flat.grad[lo:hi]
+            if self._use_avg:
+                self._works[b] = dist.all_reduce(bucket, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+            else:
+                self._works[b] = dist.all_reduce(bucket, group=self.group, async_op=True)
+            self._next += 1
+
+    def _mark(self, pid):
+        b = self._bucket_of.get(pid)
+        if b is None or pid in self._ready:
+            return
+        self._ready.add(pid)
+        self._pending[b] -= 1
+
+    def _mark_ready(self, module):
+        if not self._learned:
+            return
+        for p in module.parameters():
+            if id(p) not in self._engine:
+                self._mark(id(p))
+        self._launch_ready()
+
+    def _acc_hook(self, p):
+        self._engine.add(id(p))
+        if self._learned:
+            self._mark(id(p))
+            self._launch_ready()
+
+    def _pre_hook(self, module, args):
+        if not (self.training and torch.is_grad_enabled()):
+            return None
+        for a in args:
+            if torch.is_tensor(a) and a.requires_grad:
+                a.register_hook(lambda g, m=module: self._mark_ready(m))
+                break
+        return None
+
     def _sync_buffers(self):
-        for b in self.module.buffers():
-            dist.broadcast(b, 0, group=self.group)
+        bufs = list(self.module.buffers())
+        if not bufs:
+            return
+        pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
+        coalesced = getattr(dist, "_broadcast_coalesced", None)
+        if coalesced is not None:
+            coalesced(pg, bufs, 256 << 20, 0)         # one broadcast per dtype (as torch DDP does)
+        else:
+            for b in bufs:
+                dist.broadcast(b, 0, group=self.group)
 
     def _allreduce_grads(self):
         self._queued = False
         if self.world == 1:
             return
-        g = self.flat.grad
-        for o in range(0, g.numel(), self.bucket_elems):
-            bucket = g[o:o + self.bucket_elems]
-            if self._use_avg:
-                dist.all_reduce(bucket, op=dist.ReduceOp.AVG, group=self.group)
-            else:
-                dist.all_reduce(bucket, group=self.group)
-                bucket.div_(self.world)
+        self._launch_ready(final=True)
+        for b, w in enumerate(self._works):
+            w.wait()                                # NCCL: the compute stream waits; gloo: blocks
+            if not self._use_avg:
+                lo, hi = self._buckets[b]
+                self.flat.grad[lo:hi].div_(self.world)
+        self._learned = True
+        self._reset_step()
 
     def forward(self, *args, **kwargs):
         if self.world > 1 and self.broadcast_buffers and self.training:
             self._sync_buffers()
+        if self.world > 1:
+            self._reset_step()
         out = self.module(*args, **kwargs)
         if not torch.is_grad_enabled() or self.world == 1:
             return out

@@ -17,12 +17,12 @@ class Toy(torch.nn.Module):
         return {"y": self.bn(self.fc(x)), "aux": [self.fc.weight.sum()]}
 
 
-def main():
-    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def check(rank, world, bucket_mb):
     torch.manual_seed(100 + rank)                      # different init per rank: the wrap must broadcast
     m = Toy()
-    ddp = FlatDDP(m)
+    ddp = FlatDDP(m, bucket_mb=bucket_mb)
+    if bucket_mb < 1:
+        assert len(ddp._buckets) == 4
     ref = Toy()
     ref.load_state_dict({k[len("module."):]: v.clone() for k, v in ddp.state_dict().items()})
     assert all(k.startswith("module.") for k in ddp.state_dict())
@@ -39,8 +39,10 @@ def main():
         o = ref(xfull[4 * r:4 * r + 4])
         (o["y"].square().mean()).backward()
         grads.append({k: p.grad.clone() for k, p in ref.named_parameters()})
+    expected = {}
     for k, p in m.named_parameters():
         exp = sum(gr[k] for gr in grads) / world
+        expected[k] = exp
         assert torch.allclose(p.grad, exp, atol=1e-6), (k, p.grad, exp)
     # flat buffer views
     assert ddp.flat.grad.numel() == sum(p.numel() for p in m.parameters())
@@ -49,6 +51,20 @@ def main():
     w = m.fc.weight.detach().clone()
     dist.all_reduce(w)
     assert torch.allclose(w / world, m.fc.weight.detach())
+    # later steps launch buckets during backward (after the first backward learned the hook kinds)
+    for _ in range(2):
+        ddp.flat.grad.zero_()
+        out = ddp(x)
+        (out["y"].square().mean() + 0 * out["aux"][0]).backward()
+        for k, p in m.named_parameters():
+            assert torch.allclose(p.grad, expected[k], atol=1e-6), (k, p.grad, expected[k])
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    for bucket_mb in (25.0, 1e-5):                     # one bucket / one bucket per parameter
+        check(rank, world, bucket_mb)
     dist.barrier()
     dist.destroy_process_group()
     print("OK rank", rank)

@@ -37,7 +37,16 @@ def main():
     for k, p in m.named_parameters():
         np.testing.assert_allclose(p.grad.double().norm().item(), float(g["gnorm|" + k]), rtol=1e-2, atol=1e-6,
                                    err_msg=k)
-    sd = m.state_dict()
+    # a second backward on the same batch launches gradient buckets during backward (FlatDDP learned the
+    # hook kinds on the first one): the averaged gradients must not change
+    first = {k: p.grad.double().norm().item() for k, p in m.named_parameters()}
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    ddp.flat.grad.zero_()
+    loss2, _ = plugin.loss(ddp(x, decode=False), ys)
+    loss2.mean().backward()
+    torch.cuda.synchronize()
+    for k, p in m.named_parameters():
+        np.testing.assert_allclose(p.grad.double().norm().item(), first[k], rtol=1e-5, atol=1e-9, err_msg=k)
     for k in g.files:
         if k.startswith("rs|"):
             np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
