@@ -93,9 +93,10 @@ int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, i
 /* Batched weight packing: all operand layouts of one training step in one launch.  descs (device memory)
  * are sorted by start; descriptor d covers elements [start, start + count) of the concatenated index space:
  * mode 0: out[row_off + a][t*B + b] = w[a][b][t], count = A * ldp (k >= T*B zero-filled);
- * mode 1: out[b][t*a_tot + a_off + a] = w[a][b][t], count = B * T * A (a slice of a concatenated
- * operand when a_tot > A).  Every start (and total) is a multiple of 4096 elements.  Replaces one
- * scd_pack_weight launch per conv and direction. */
+ * mode 1: out[b][t*a_tot + a_off + a] = w[a][b][t] (a slice of a concatenated operand when a_tot > A),
+ * transposed through LDS in tiles of 64 a x max(1, 64/T) b (T <= 64), one 4096-element unit per tile:
+ * count = 4096 * ceil(A/64) * ceil(B / max(1, 64/T)).  Every start (and total) is a multiple of 4096.
+ * Replaces one scd_pack_weight launch per conv and direction. */
 typedef struct scd_pack_desc {
     const float* w;
     void* out;

@@ -583,7 +583,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     constexpr int STAGE = (BM + BN) * 128;
     constexpr int EROW = WCOLS * 2 + 16;        // epilogue staging row
     constexpr int EPI = 8 * 128 * EROW;
-    constexpr int SMEM = (2 * STAGE > EPI + 4 * BN * 4) ? 2 * STAGE : EPI + 4 * BN * 4;
+    constexpr int EPX = EPI + 4 * BN * 4 + (HEADS ? 256 * 8 * 4 : 0);    // + the heads' partial exchange
+    constexpr int SMEM = (2 * STAGE > EPX) ? 2 * STAGE : EPX;
     static_assert(BN == 256 || BN == 192, "BN");
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -865,11 +866,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     }
     if constexpr (HEADS) {
         // fused CenterNet tails (centerNetOffset.py:108-110): out_h[o] = b1_h[o] + sum_j w1_h[o][j] * hid[128h + j]
-        // from the staged tile.  Thread pair (2r, 2r+1) takes pixel r, each half BN/2 of the tile's channels; a
-        // head split between two column tiles gets two partial sums, added onto its zeroed output (two
-        // commutative fp32 adds onto 0: the same bits in either order).
+        // from the staged tile.  Waves 0-3 take the first BN/2 tile channels of pixels 64*wave + lane, waves 4-7
+        // the second half of the same pixels: the half (hence every weight address) is wave-uniform, so the
+        // 1x1 weights come in through the scalar cache, and the lanes' staged rows (EROW apart) are read without
+        // bank conflicts.  The second-half partials meet the first half's through LDS; a head split between two
+        // column tiles gets two partial sums, added onto its zeroed output (two commutative fp32 adds onto 0:
+        // the same bits in either order).
         __syncthreads();
-        const int r = tid >> 1, half = tid & 1;
+        const int half = wave >> 2;                            // wave-uniform
+        const int r = (wave & 3) * 64 + lane;                  // tile pixel
         const int g = r >> 7, row = r & 127;
         const int hbase = (nt * BN) >> 7;
         const float* wA = p.head_w[hbase];
@@ -877,7 +882,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int cc = 0; cc < BN / 2; cc += EPC) {
-            const int c = half * (BN / 2) + cc;                // tile channel
+            const int c = half * (BN / 2) + cc;                // tile channel (wave-uniform)
             const int wv = c / WCOLS, cl = c - (c / WCOLS) * WCOLS;
             float v[EPC];
             Vec16<T>::load(smem + (4 * g + wv) * 128 * EROW + row * EROW + cl * 2, v);
@@ -895,10 +900,16 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                 }
             }
         }
+        float* xch = (float*)(smem + EPI + 4 * BN * 4);        // [256 px][8]: second-half partials
+        if (half) {
 #pragma unroll
-        for (int o = 0; o < 4; ++o) { a0[o] += __shfl_xor(a0[o], 1, 64); a1[o] += __shfl_xor(a1[o], 1, 64); }
+            for (int o = 0; o < 4; ++o) { xch[r * 8 + o] = a0[o]; xch[r * 8 + 4 + o] = a1[o]; }
+        }
+        __syncthreads();
         const int m = mt * BM + r;
         if (half == 0 && m < M) {
+#pragma unroll
+            for (int o = 0; o < 4; ++o) { a0[o] += xch[r * 8 + o]; a1[o] += xch[r * 8 + 4 + o]; }
             const int n = m / QQ;
             const int rem = m - n * QQ;
             const int oh = rem / ph.Qw, ow = rem - (rem / ph.Qw) * ph.Qw;

@@ -41,6 +41,34 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
         if (d[mid].start <= e0) lo = mid; else hi = mid - 1;
     }
     const scd_pack_desc q = d[lo];
+    if (q.mode == 1) {
+        // [B][taps][A] (input-gradient operand): a transpose of every tap's A x B plane.  Unit u of the
+        // descriptor is one tile of 64 a x BB b (BB*T <= 64 elements of a contiguous input row segment): the
+        // tile's rows are read coalesced into LDS and written as runs of <= 64 consecutive a per (b, tap).
+        __shared__ float tile[64 * 65];
+        const int T = q.T, BB = max(1, 64 / T);
+        const int nbb = (q.B + BB - 1) / BB;
+        const int u = (int)((e0 - q.start) / PACK_UNIT);
+        const int ta = u / nbb, tb = u - (u / nbb) * nbb;
+        const int a0 = ta * 64, b0 = tb * BB;
+        if (a0 >= q.A) return;
+        const int na = min(64, q.A - a0), nb = min(BB, q.B - b0);
+        const int rowl = nb * T, pitch = rowl + 1;
+        for (int i = threadIdx.x; i < na * rowl; i += 256) {
+            const int a = i / rowl, k = i - a * rowl;
+            tile[a * pitch + k] = q.w[((unsigned)(a0 + a) * q.B + b0) * T + k];
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < na * rowl; i += 256) {
+            const int bt = i / na, a = i - bt * na;
+            const int b = bt / T, t = bt - b * T;
+            const float v = tile[a * pitch + b * T + t];
+            const unsigned o = (unsigned)(b0 + b) * q.ldp + t * q.a_tot + q.a_off + a0 + a;
+            if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
+            else ((float*)q.out)[o] = v;
+        }
+        return;
+    }
     // 32-bit index math (a descriptor holds < 2^31 elements; 64-bit divides dominated this kernel)
     const unsigned count = q.mode == 0 ? (unsigned)q.A * q.ldp : (unsigned)q.B * q.T * q.A;
     const unsigned base = (unsigned)(e0 - q.start);

@@ -164,8 +164,12 @@ class PackPlan:
                         A, B, T = w.shape[0], w.shape[1], w.shape[2] * w.shape[3]
                         d = L.PackDesc(w.data_ptr(), out.data_ptr(), start, A, B, T, mode, ldp, row_off, a_off, a_tot)
                         descs.append(d)
-                        start += A * ldp if mode == 0 else B * T * A
-                        start = (start + 4095) // 4096 * 4096      # whole workgroup units per descriptor
+                        if mode == 0:
+                            start += (A * ldp + 4095) // 4096 * 4096      # whole workgroup units per descriptor
+                        else:
+                            # one 4096-element unit per 64 x max(1, 64 // T) transpose tile (scd_pack_desc)
+                            bb = max(1, 64 // T)
+                            start += ((A + 63) // 64) * ((B + bb - 1) // bb) * 4096
                 arr = (L.PackDesc * len(descs))(*descs)
                 host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
                 self._dev[dtype] = (host.to(es[0][0].device), len(descs), start)

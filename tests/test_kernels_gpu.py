@@ -305,3 +305,31 @@ def test_adam_matches_torch():
         opt.step()
         ops.adam_step(p, gr.to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, step)
     np.testing.assert_allclose(p.cpu().numpy(), pt.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_batched_pack_matches_single(dtype):
+    """PackPlan's one-launch batched packing (mode 0 rows, mode 1 LDS-tiled transposes, concatenated head
+    operands) reproduces the per-weight scd_pack_weight layouts bit for bit."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(12)
+    shapes = [(64, 64, 3, 3), (128, 64, 3, 3), (128, 64, 1, 1), (512, 256, 3, 3), (256, 256, 4, 4), (64, 1, 7, 7),
+              (96, 40, 3, 3), (200, 72, 4, 4)]
+    ws = [torch.nn.Parameter((torch.randn(*s, generator=g)).to(DEV)) for s in shapes]
+    heads = [torch.nn.Parameter(torch.randn(128, 256, 3, 3, generator=g).to(DEV)) for _ in range(3)]
+    plan = ops.PackPlan()
+    ops.pack_begin(plan)                       # first step: records and packs on demand
+    first = [ops.pack_weight(w, dtype, m) for w in ws for m in (0, 1)]
+    first += [ops.pack_concat(heads, dtype, m) for m in (0, 1)]
+    first = [f.clone() for f in first]
+    ops.pack_end()
+    # scribble over the cached operands, then repack everything in one batched launch
+    for e in plan.entries.values():
+        e[0].fill_(float("nan"))
+    ops.pack_begin(plan)
+    again = [ops.pack_weight(w, dtype, m) for w in ws for m in (0, 1)]
+    again += [ops.pack_concat(heads, dtype, m) for m in (0, 1)]
+    torch.cuda.synchronize()
+    ops.pack_end()
+    for a, b in zip(first, again):
+        assert torch.equal(a, b)
