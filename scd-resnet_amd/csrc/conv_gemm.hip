@@ -611,55 +611,62 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     // DMA rows of this lane (the lane fetches chunk (lane&7)^(row&7) so that LDS slot lane&7 holds it)
     const int lrow = lane >> 3;
     const int cch = (lane & 7) ^ lrow;
-    // A: rows 128*grp + 64*h + 16*wc + 8*j + lrow  (h, j in {0,1}); index i = 2h + j
-    int a_pix[4], a_ih[4], a_iw[4];
-    bool a_ok[4];
+    // A: rows 128*grp + 64*h + 16*wc + 8*j + lrow  (h, j in {0,1}); index i = 2h + j.  Per row the lane keeps
+    // its byte offset at tap (0,0) of channel chunk 0 and a bit mask of the phase's taps that land inside
+    // the image; a stage then costs one scalar delta ((dh*Wi + dw)*Ci + chunk*BK)*2, one add and one bit
+    // test per DMA (no multiplies or bounds compares in the K loop)
+    int a_base[4];
+    unsigned a_mask[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = mt * BM + 128 * grp + 64 * (i >> 1) + 16 * wc + 8 * (i & 1) + lrow;
-        a_ok[i] = m < M;
-        const int mm = a_ok[i] ? m : 0;
+        const bool ok = m < M;
+        const int mm = ok ? m : 0;
         const int n = mm / QQ;
         const int rem = mm - n * QQ;
         const int qh = rem / ph.Qw;
         const int qw = rem - qh * ph.Qw;
-        a_pix[i] = n * p.Hi * p.Wi;
-        a_ih[i] = p.is * qh;
-        a_iw[i] = p.is * qw;
+        const int ih0 = p.is * qh, iw0 = p.is * qw;
+        a_base[i] = ((n * p.Hi + ih0) * p.Wi + iw0) * p.Ci * 2 + cch * EPC * 2;
+        unsigned msk = 0;
+        for (int t = 0; t < ph.ntaps; ++t) {
+            const int ih = ih0 + ph.dh[t], iw = iw0 + ph.dw[t];
+            if (ok && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) msk |= 1u << t;
+        }
+        a_mask[i] = msk;
     }
-    // B: part 1 rows (BN/2)*grp + 16*wc + 8*j + lrow (j < 2); part 2 rows (BN/2)*grp + 64 + 8*NB2*wc + 8*j + lrow
-    int b_row[2 + NB2];
+    // B: part 1 rows (BN/2)*grp + 16*wc + 8*j + lrow (j < 2); part 2 rows (BN/2)*grp + 64 + 8*NB2*wc + 8*(j-2) + lrow
+    int b_base[2 + NB2];
     bool b_ok[2 + NB2];
 #pragma unroll
     for (int j = 0; j < 2 + NB2; ++j) {
         const int r = (BN / 2) * grp + (j < 2 ? 16 * wc + 8 * j : 64 + 8 * NB2 * wc + 8 * (j - 2)) + lrow;
         const int nn = nt * BN + r;
         b_ok[j] = nn < p.Co;
-        b_row[j] = b_ok[j] ? nn : 0;
+        b_base[j] = ((b_ok[j] ? nn : 0) * p.wrow + cch * EPC) * 2;
     }
     const int cpt = p.Ci / BK;
     const int KT = ph.ntaps * cpt;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
 
-    struct StageArgs { int live, c0, dh, dw, wt; };
+    struct StageArgs { int live, tap, adelta, bdelta; };
     auto stage_args = [&](int kt_req) {
         StageArgs a;
         a.live = kt_req < KT;
         const int kt = min(kt_req, KT - 1);
         const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
-        a.c0 = chunk * BK + cch * EPC;
-        a.dh = ph.dh[tap]; a.dw = ph.dw[tap]; a.wt = ph.wt[tap];
+        a.tap = tap;
+        a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * BK) * 2;
+        a.bdelta = (ph.wt[tap] * p.Ci + chunk * BK) * 2;
         return a;
     };
     auto issue_a = [&](const StageArgs& g, char* buf, int h) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int i = 2 * h + j;
-            const int ih = a_ih[i] + g.dh, iw = a_iw[i] + g.dw;
-            const bool ok = g.live && a_ok[i] && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-            dma16(xrs, buf + (128 * grp + 64 * h + 16 * wc + 8 * j) * 128,
-                  sel_off(ok, ((a_pix[i] + ih * p.Wi + iw) * p.Ci + g.c0) * 2));
+            const bool ok = g.live && ((a_mask[i] >> g.tap) & 1u);
+            dma16(xrs, buf + (128 * grp + 64 * h + 16 * wc + 8 * j) * 128, sel_off(ok, a_base[i] + g.adelta));
         }
     };
     auto issue_b = [&](const StageArgs& g, char* buf, int part) {
@@ -667,7 +674,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
 #pragma unroll
         for (int j = (part ? 2 : 0); j < (part ? 2 + NB2 : 2); ++j) {
             const int r = (BN / 2) * grp + (j < 2 ? 16 * wc + 8 * j : 64 + 8 * NB2 * wc + 8 * (j - 2));
-            dma16(wrs, Bs + r * 128, sel_off(g.live && b_ok[j], (b_row[j] * p.wrow + g.wt * p.Ci + g.c0) * 2));
+            dma16(wrs, Bs + r * 128, sel_off(g.live && b_ok[j], b_base[j] + g.bdelta));
         }
     };
 
