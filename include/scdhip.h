@@ -190,8 +190,9 @@ int scd_focal_fwd(const float* logits, const float* gt, long n, float* g, double
 /* masked L1 on gathered NCHW features: acc[0] += sum |f-t|, acc[1] += sum mask; g = sign(f-t) scattered */
 int scd_l1_gather_fwd(const float* feat, int N, int C, int HW, const int64_t* inds, const uint8_t* mask,
                       const float* target, int K, int tstride, int toff, float* g, double* acc, void* stream);
-/* out[0..] = loss terms; factors for backward.  See centerNetOffset.py:213-217 */
-int scd_centernet_loss_finalize(const double* focal_acc, int nfocal, const double* l1_acc, int nl1,
+/* out[0..] = loss terms; factors for backward.  See centerNetOffset.py:213-217.  Re-zeroes focal_acc and
+ * l1_acc after reading them (persistent accumulators: no memset before the next loss). */
+int scd_centernet_loss_finalize(double* focal_acc, int nfocal, double* l1_acc, int nl1,
                                 const float* l1_weights, float* out, float* factors, void* stream);
 /* g[i] *= factors[idx] * go[0]  (in place) */
 int scd_scale_by_device(float* g, long n, const float* factors, int idx, const float* go, void* stream);

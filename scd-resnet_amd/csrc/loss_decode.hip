@@ -82,31 +82,39 @@ struct LossFin {
     float l1w[8];
 };
 
-__global__ void loss_finalize_kernel(const double* facc, int nfocal, const double* lacc, int nl1, LossFin w, float* out,
+// one block of 64 threads: thread 0 forms the loss terms, then the block re-zeroes both accumulators
+// (persistent, consumer-cleared buffers: no memset launch before the next step's loss)
+__global__ void loss_finalize_kernel(double* facc, int nfocal, double* lacc, int nl1, LossFin w, float* out,
                                      float* factors) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double total = 0.0;
-    for (int f = 0; f < nfocal; ++f) {
-        double pl = 0, nl = 0, np = 0;
-        for (int r = 0; r < SCD_STAT_REPLICAS; ++r) {
-            const double* a = facc + ((long)f * SCD_STAT_REPLICAS + r) * FOCAL_ACC;
-            pl += a[0]; nl += a[1]; np += a[2];
+    if (blockIdx.x != 0) return;
+    if (threadIdx.x == 0) {
+        double total = 0.0;
+        for (int f = 0; f < nfocal; ++f) {
+            double pl = 0, nl = 0, np = 0;
+            for (int r = 0; r < SCD_STAT_REPLICAS; ++r) {
+                const double* a = facc + ((long)f * SCD_STAT_REPLICAS + r) * FOCAL_ACC;
+                pl += a[0]; nl += a[1]; np += a[2];
+            }
+            // focal.py:47-51: no positives -> -negL ; else -(posL+negL)/#pos
+            const float posl = (float)pl, negl = (float)nl, npos = (float)np;
+            const float v = np == 0.0 ? -negl : -(posl + negl) / npos;
+            out[1 + f] = v;
+            factors[f] = np == 0.0 ? -1.f : -1.f / npos;
+            total += v;
         }
-        // focal.py:47-51: no positives -> -negL ; else -(posL+negL)/#pos
-        const float posl = (float)pl, negl = (float)nl, npos = (float)np;
-        const float v = np == 0.0 ? -negl : -(posl + negl) / npos;
-        out[1 + f] = v;
-        factors[f] = np == 0.0 ? -1.f : -1.f / npos;
-        total += v;
+        for (int l = 0; l < nl1; ++l) {
+            const double s = lacc[2 * l], cnt = lacc[2 * l + 1];
+            const float v = w.l1w[l] * ((float)s / ((float)cnt + 1e-4f));
+            out[1 + nfocal + l] = v;
+            factors[nfocal + l] = w.l1w[l] / ((float)cnt + 1e-4f);
+            total += v;
+        }
+        out[0] = (float)total;
     }
-    for (int l = 0; l < nl1; ++l) {
-        const double s = lacc[2 * l], cnt = lacc[2 * l + 1];
-        const float v = w.l1w[l] * ((float)s / ((float)cnt + 1e-4f));
-        out[1 + nfocal + l] = v;
-        factors[nfocal + l] = w.l1w[l] / ((float)cnt + 1e-4f);
-        total += v;
-    }
-    out[0] = (float)total;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nfocal * SCD_STAT_REPLICAS * FOCAL_ACC; i += blockDim.x) facc[i] = 0.0;
+    if (lacc)
+        for (int i = threadIdx.x; i < 2 * nl1; i += blockDim.x) lacc[i] = 0.0;
 }
 
 __global__ void scale_by_device_kernel(float* g, long n, const float* factors, int idx, const float* go) {
@@ -265,7 +273,7 @@ extern "C" int scd_l1_gather_fwd(const float* feat, int N, int C, int HW, const 
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_centernet_loss_finalize(const double* focal_acc, int nfocal, const double* l1_acc, int nl1,
+extern "C" int scd_centernet_loss_finalize(double* focal_acc, int nfocal, double* l1_acc, int nl1,
                                            const float* l1_weights, float* out, float* factors, void* stream) {
     if (nl1 > 8) return SCD_ERR_ARG;
     LossFin w;

@@ -223,10 +223,17 @@ class FlatDDP(torch.nn.Module):
             b = self._next
             lo, hi = self._buckets[b]
             bucket = self.flat.grad[lo:hi]
-            if self._use_avg:
-                self._works[b] = dist.all_reduce(bucket, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-            else:
-                self._works[b] = dist.all_reduce(bucket, group=self.group, async_op=True)
+            # weight gradients may be written on scdhip's side stream (ops.conv_wgrad): issue the collective
+            # from that stream, ordered after both
+            side = None
+            if bucket.is_cuda:
+                from . import ops
+                side = ops.side_stream_for_comm(bucket.device)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                if self._use_avg:
+                    self._works[b] = dist.all_reduce(bucket, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+                else:
+                    self._works[b] = dist.all_reduce(bucket, group=self.group, async_op=True)
             self._next += 1
 
     def _mark(self, pid):
@@ -276,6 +283,9 @@ class FlatDDP(torch.nn.Module):
         if self.world == 1:
             return
         self._launch_ready(final=True)
+        if self.flat.grad.is_cuda:
+            from . import ops
+            ops.join_side_streams()
         for b, w in enumerate(self._works):
             w.wait()                                # NCCL: the compute stream waits; gloo: blocks
             if not self._use_avg:
@@ -303,6 +313,14 @@ class FlatDDP(torch.nn.Module):
         for i, t in zip(idx, hooked):
             flat[i] = t
         return _unflatten(flat, spec)
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 def _flatten(obj):

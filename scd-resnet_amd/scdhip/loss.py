@@ -23,18 +23,20 @@ class CenterNetLossFn(torch.autograd.Function):
         HW = H * W
         K = inds.shape[1]
         dev = heat.device
-        mask_u8 = mask.to(torch.uint8) if mask.dtype != torch.uint8 else mask
-        mask_u8 = mask_u8.contiguous()
+        mask_u8 = mask.contiguous()
+        mask_u8 = mask_u8.view(torch.uint8) if mask_u8.dtype == torch.bool else mask_u8.to(torch.uint8)
         inds = inds.to(torch.int64).contiguous()
         regr_t = regr_t.float().contiguous()
         gt_heat = gt_heat.float().contiguous()
         s = ops.stream()
         g_heat = torch.empty_like(heat)
-        facc = torch.zeros(L.STAT_REPLICAS * 4, dtype=torch.float64, device=dev)
+        facc = _acc_buffer(dev, "focal", L.STAT_REPLICAS * 4)
         L.call("scd_focal_fwd", ops.ptr(heat), ops.ptr(gt_heat), heat.numel(), ops.ptr(g_heat), ops.ptr(facc), s)
-        lacc = torch.zeros(4, dtype=torch.float64, device=dev)
-        g_regr = torch.zeros_like(regr)
-        g_off = torch.zeros_like(off)
+        lacc = _acc_buffer(dev, "l1", 4)
+        # one zero fill for both scattered L1 gradients
+        g_both = torch.zeros(regr.numel() + off.numel(), dtype=regr.dtype, device=dev)
+        g_regr = g_both[:regr.numel()].view(regr.shape)
+        g_off = g_both[regr.numel():].view(off.shape)
         L.call("scd_l1_gather_fwd", ops.ptr(regr), N, regr.shape[1], HW, ops.ptr(inds), ops.ptr(mask_u8),
                ops.ptr(regr_t), K, regr_t.shape[2], 2, ops.ptr(g_regr), ops.ptr(lacc), s)
         L.call("scd_l1_gather_fwd", ops.ptr(off), N, off.shape[1], HW, ops.ptr(inds), ops.ptr(mask_u8),
@@ -69,7 +71,7 @@ class FocalOnlyLossFn(torch.autograd.Function):
         heats, gts = args[:n], args[n:]
         dev = heats[0].device
         s = ops.stream()
-        facc = torch.zeros(n * L.STAT_REPLICAS * 4, dtype=torch.float64, device=dev)
+        facc = _acc_buffer(dev, "focal%d" % n, n * L.STAT_REPLICAS * 4)
         grads = []
         for i, (h, g) in enumerate(zip(heats, gts)):
             h = h.contiguous()
@@ -94,6 +96,20 @@ class FocalOnlyLossFn(torch.autograd.Function):
         for i, g in enumerate(grads):
             L.call("scd_scale_by_device", ops.ptr(g), g.numel(), ops.ptr(factors), i, ops.ptr(gl), s)
         return tuple(grads) + (None,) * len(grads)
+
+
+_ACC = {}
+
+
+def _acc_buffer(dev, kind, numel):
+    """Persistent fp64 loss accumulators per device: zero when created, re-zeroed by the finalize kernel
+    that consumes them (scd_centernet_loss_finalize), so the loss needs no memset launches."""
+    key = (str(dev), kind, numel)
+    buf = _ACC.get(key)
+    if buf is None:
+        buf = torch.zeros(numel, dtype=torch.float64, device=dev)
+        _ACC[key] = buf
+    return buf
 
 
 def ctypes_float2(a, b):

@@ -5,6 +5,7 @@ bf16 performance mode); weights, grads, BN parameters fp32 in the reference layo
 Every wrapper enqueues on torch's current HIP stream and never synchronises.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -334,7 +335,75 @@ def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=Fals
     return _gemm(dy, wpack, out, Cin, Ho, Wo, stride, 1, _fwd_phase(k, k, pad, Ho, Wo), accumulate=accumulate)
 
 
+# ------------------------------------------------------------------ weight gradients on a side stream
+#
+# Inside a backward pass the weight-gradient GEMMs (+ their split reductions) only feed the optimizer (and
+# the DDP buckets), while the input-gradient chain (dgrad GEMM -> BN backward -> next dgrad ...) is the
+# critical path.  They go to one side HIP stream per device, ordered after everything the compute stream
+# has queued so far, so they fill the gaps the chain leaves (small BN / finalize launches, GEMM tails).
+# Their operands are recorded on the side stream (the caching allocator keeps them alive until it is
+# done); an end-of-backward callback makes the compute stream wait for the side stream, before Adam,
+# zero_grad or anything else can touch the gradients.  SCD_WGRAD_STREAM=0 keeps everything on one stream.
+
+class _Side:
+    enabled = os.environ.get("SCD_WGRAD_STREAM", "1") != "0"
+    streams = {}          # device index -> side stream
+    joined_task = {}      # device index -> graph task whose end-of-backward join is queued
+
+
+def _graph_task():
+    try:
+        return torch._C._current_graph_task_id()
+    except Exception:
+        return -1
+
+
+def side_stream(dev):
+    """The device's side stream, ordered after the current stream, if called inside a backward pass."""
+    task = _graph_task()
+    if not _Side.enabled or task == -1:
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _Side.streams.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _Side.streams[idx] = s
+    s.wait_stream(torch.cuda.current_stream(idx))
+    if _Side.joined_task.get(idx) != task:
+        _Side.joined_task[idx] = task
+        torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
+    return s
+
+
+def join_side_streams():
+    """Make every device's compute stream wait for its side stream (end of backward)."""
+    for idx, s in _Side.streams.items():
+        torch.cuda.current_stream(idx).wait_stream(s)
+    _Side.joined_task.clear()
+
+
+def side_stream_for_comm(dev):
+    """For a collective launched during backward: the side stream (if any), first ordered after the compute
+    stream, so that a collective issued from it sees every gradient written on either stream so far."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _Side.streams.get(idx)
+    if s is None or _graph_task() == -1:
+        return None
+    s.wait_stream(torch.cuda.current_stream(idx))
+    return s
+
+
 def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None):
+    side = side_stream(g.device) if g.is_cuda else None
+    if side is None:
+        return _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows)
+    with torch.cuda.stream(side):
+        _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows)
+    g.record_stream(side)
+    x.record_stream(side)
+
+
+def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None):
     """Weight gradient of the gather-GEMM: dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= sum_pix g[pix,r] x[gather,ci].
 
     g: (N,Ho,Wo,Cg) NHWC output-gradient; x: (N,Hi,Wi,Ci) NHWC input; taps gather
