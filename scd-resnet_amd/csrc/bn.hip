@@ -137,18 +137,19 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* y, T* out, int C
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y,
                                                             const float* rsc, const float* rsh,
-                                                            const float* mean, const float* invstd, int C,
+                                                            const float* mean, const float* invstd, int C, int ld,
                                                             unsigned rows, unsigned rows_per_block, double* stats) {
     constexpr int E = Vec16<T>::N;
     constexpr int U = 4;
-    const int cpr = C / E;                     // chunks per row (divides 256)
-    const int rpi = 256 / cpr;                 // row lanes
+    constexpr int nt = 256;
+    const int cpr = C / E;                     // chunks per row of this channel slice (divides 256)
+    const int rpi = nt / cpr;                  // row lanes
     const int tid = threadIdx.x;
     const int ch = tid % cpr;
     const int rsub = tid / cpr;
     const unsigned r0 = blockIdx.x * rows_per_block;
     const unsigned r1 = min(rows, r0 + rows_per_block);
-    __shared__ float red[2 * 256 * E];
+    __shared__ float red[2 * nt * E];
     float s[E], q[E], mu[E], is[E], ka[E], kb[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const
         float d[U][E], yv[U][E], mk[U][E];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const unsigned i = (r + u * rpi) * (unsigned)C + ch * E;
+            const unsigned i = (r + u * rpi) * (unsigned)ld + ch * E;
             Vec16<T>::load(dout + i, d[u]);
             Vec16<T>::load(y + i, yv[u]);
             if (mask) Vec16<T>::load(mask + i, mk[u]);
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const
     }
     for (; r < r1; r += rpi) {
         float d[E], yv[E], mk[E];
-        const unsigned i = r * (unsigned)C + ch * E;
+        const unsigned i = r * (unsigned)ld + ch * E;
         Vec16<T>::load(dout + i, d);
         Vec16<T>::load(y + i, yv);
         if (mask) Vec16<T>::load(mask + i, mk);
@@ -191,18 +192,18 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         red[rsub * C + ch * E + e] = s[e];
-        red[256 * E + rsub * C + ch * E + e] = q[e];
+        red[nt * E + rsub * C + ch * E + e] = q[e];
     }
     __syncthreads();
     const int rep = blockIdx.x % SCD_STAT_REPLICAS;
-    for (int c = tid; c < C; c += 256) {
+    for (int c = tid; c < C; c += nt) {
         double ss = 0.0, qq = 0.0;
         for (int k = 0; k < rpi; ++k) {
             ss += red[k * C + c];
-            qq += red[256 * E + k * C + c];
+            qq += red[nt * E + k * C + c];
         }
-        atomic_add_f64(stats + ((long)rep * 2 + 0) * C + c, ss);
-        atomic_add_f64(stats + ((long)rep * 2 + 1) * C + c, qq);
+        atomic_add_f64(stats + ((long)rep * 2 + 0) * ld + c, ss);
+        atomic_add_f64(stats + ((long)rep * 2 + 1) * ld + c, qq);
     }
 }
 
@@ -287,6 +288,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const 
     }
 }
 
+// elementwise BN kernels keep one channel chunk per thread: the grid stride (grid * 256 threads) must be a
+// multiple of the chunks per row cpr, i.e. cpr divides 256 or is a multiple of it (grid a multiple of cpr/256)
+inline bool ew_rows_ok(int cpr) { return cpr > 0 && (256 % cpr == 0 || cpr % 256 == 0); }
+inline int ew_grid(int resident, long nvec, int cpr) {
+    const long m = cpr > 256 ? cpr / 256 : 1;
+    long g = std::min<long>(resident, (nvec + 255) / 256);
+    g = std::max<long>(m, g / m * m);
+    return (int)g;
+}
 inline int fin_blocks(int C) { return (C + 3) / 4; }   // 4 waves (channels) per 256-thread block
 
 }  // namespace
@@ -312,16 +322,16 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
                             void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16) {
-        if (C % 8 || 256 % (C / 8)) return SCD_ERR_ARG;
+        if (C % 8 || !ew_rows_ok(C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
         static const int g = resident_grid((const void*)bn_apply_kernel<__bf16>, 256);
-        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st, (const __bf16*)y,
+        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 0, st, (const __bf16*)y,
                            (__bf16*)out, C, (unsigned)nvec, scale, shift, (const __bf16*)res, rscale, rshift, relu);
     } else if (dtype == SCD_DT_F32) {
-        if (C % 4 || 256 % (C / 4)) return SCD_ERR_ARG;
+        if (C % 4 || !ew_rows_ok(C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
         static const int g = resident_grid((const void*)bn_apply_kernel<float>, 256);
-        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st, (const float*)y,
+        hipLaunchKernelGGL((bn_apply_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 0, st, (const float*)y,
                            (float*)out, C, (unsigned)nvec, scale, shift, (const float*)res, rscale, rshift, relu);
     } else {
         return SCD_ERR_ARG;
@@ -337,25 +347,37 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
     if (C % E) return SCD_ERR_ARG;
     const long rows = total / C;
     const int cpr = C / E;
-    if (cpr > 256 || 256 % cpr || total >= (1L << 31)) return SCD_ERR_ARG;
+    // rows wider than 256 chunks run as channel slices of 256 chunks (ld = the full row)
+    if (!ew_rows_ok(cpr) || total >= (1L << 31)) return SCD_ERR_ARG;
+    const int scpr = std::min(cpr, 256), sC = scpr * E;
     // one round of resident blocks (at most), at least 8 rows per row lane
     static const int gb = resident_grid((const void*)bn_bwd_reduce_kernel<__bf16>, 256);
     static const int gf = resident_grid((const void*)bn_bwd_reduce_kernel<float>, 256);
     const long nb = dtype == SCD_DT_BF16 ? gb : gf;
-    const long rpi = 256 / cpr;
+    const long rpi = 256 / scpr;
     const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
     const int blocks = cdiv(rows, rpb);
-    if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout,
-                           (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, mean, invstd, C, (unsigned)rows,
-                           (unsigned)rpb, stats);
-    else if (dtype == SCD_DT_F32)
-        hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dout,
-                           (const float*)mask, (const float*)y, relu_scale, relu_shift, mean, invstd, C, (unsigned)rows,
-                           (unsigned)rpb, stats);
-    else
-        return SCD_ERR_ARG;
-    SCD_RETURN_LAUNCH();
+    const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
+    for (int c0 = 0; c0 < C; c0 += sC) {
+        const char* dz = (const char*)dout + (size_t)c0 * esz;
+        const char* mk = mask ? (const char*)mask + (size_t)c0 * esz : nullptr;
+        const char* yy = (const char*)y + (size_t)c0 * esz;
+        const float* rs = relu_scale ? relu_scale + c0 : nullptr;
+        const float* rh = relu_shift ? relu_shift + c0 : nullptr;
+        if (dtype == SCD_DT_BF16)
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dz,
+                               (const __bf16*)mk, (const __bf16*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
+                               (unsigned)rows, (unsigned)rpb, stats + c0);
+        else if (dtype == SCD_DT_F32)
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dz,
+                               (const float*)mk, (const float*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
+                               (unsigned)rows, (unsigned)rpb, stats + c0);
+        else
+            return SCD_ERR_ARG;
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
 }
 
 extern "C" int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,
@@ -371,17 +393,17 @@ extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, c
                                 void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16) {
-        if (C % 8 || 256 % (C / 8)) return SCD_ERR_ARG;
+        if (C % 8 || !ew_rows_ok(C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
         static const int g = resident_grid((const void*)bn_bwd_apply_kernel<__bf16>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 0, st,
                            (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, coef, C,
                            (unsigned)nvec, (__bf16*)dy, (__bf16*)dz);
     } else if (dtype == SCD_DT_F32) {
-        if (C % 4 || 256 % (C / 4)) return SCD_ERR_ARG;
+        if (C % 4 || !ew_rows_ok(C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
         static const int g = resident_grid((const void*)bn_bwd_apply_kernel<float>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(std::min<long>(g, (nvec + 255) / 256)), dim3(256), 0, st, (const float*)dout,
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 0, st, (const float*)dout,
                            (const float*)mask, (const float*)y, relu_scale, relu_shift, coef, C, (unsigned)nvec, (float*)dy,
                            (float*)dz);
     } else {

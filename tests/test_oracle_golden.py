@@ -213,3 +213,25 @@ def test_f8_corner_targets_rule(golden):
     ys = T.corner_targets(32, 2, 32)
     for i, n in enumerate(["heat", "mask", "regr", "tl", "br"]):
         np.testing.assert_array_equal(ys[i].numpy(), g["ys|" + n])
+
+
+def test_f9_res50_bottleneck_step(golden):
+    """Oracle Bottleneck path (residuals.py:122-165, ResNetSpec[50]) against the reference's Res50 forward,
+    CenterNetLoss and gradients (F9, make_golden_res50.py): pins the oracle for the a3 row."""
+    g = golden("res50")
+    entries, topo = O.model_spec(50, [64, 64, 128, 256, 512, 256, 256, 256])
+    st = O.TrainState(O.hash_weights(entries))
+    x = T.batch_inputs(9, 2, 128)
+    ys = T.batch_targets(10, 2, 32)
+    outs = O.forward(st.P, st.B, x, topo)
+    for k in ("heatmap", "regr", "offset"):
+        np.testing.assert_allclose(outs[k].detach().numpy(), g[k], rtol=1e-4, atol=1e-4, err_msg=k)
+    loss, stats = O.centernet_loss(outs, ys)
+    loss.mean().backward()
+    np.testing.assert_allclose(loss.detach().numpy(), g["loss"], rtol=1e-4)
+    np.testing.assert_allclose([s.item() for s in stats], g["stats"], rtol=1e-4, atol=1e-6)
+    for k, v in st.P.items():
+        np.testing.assert_allclose(v.grad.double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7, err_msg=k)
+    for k in g.files:
+        if k.startswith("rs|"):
+            np.testing.assert_allclose(st.B[k[3:]].numpy(), g[k], rtol=1e-4, atol=1e-6, err_msg=k)
