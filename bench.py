@@ -20,7 +20,7 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-TRAIN_GFLOP_PER_IMG = 147.476      # SURVEY §6 / BASELINE.md: conv+deconv fwd+dgrad+wgrad per 512^2 image
+TRAIN_GFLOP_PER_IMG = 147.476      # SURVEY §6 / BASELINE.md: conv+deconv fwd+dgrad+wgrad per 512^2 Res10 image
 PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 
@@ -33,6 +33,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--model", default="centerOffsetRes10")
+    ap.add_argument("--image-size", type=int, default=512,
+                    help="tile size; 512 uses the synthetic SCD dataset plugin, other sizes N(0,1) tiles with "
+                         "random sparse targets of the same layout (e.g. BASELINE configs[4]: Res50 at 1024)")
     ap.add_argument("--cpu-baseline-steps", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -62,6 +65,34 @@ def cpu_baseline(steps):
 HEADS_KERNEL = "conv_gemm_pp_kernel<bf16,256,192,heads>"
 
 
+def train_gflop_per_img(model, S):
+    """Conv + transposed-conv MACs x 2 x 3 (fwd, dgrad, wgrad) per SxS image, from the model's layer shapes
+    (residuals.py layout: stem /2, layerK at /4 / 2^(K-1), deconvs x2 each from /32, heads at /4);
+    147.48 GFLOP for Res10 at 512."""
+    import re
+    tot = 0.0
+    ndec = 0
+    for n, m in model.named_modules():
+        if isinstance(m, torch.nn.ConvTranspose2d):
+            ndec += 1
+            hin = S // 32 * 2 ** (ndec - 1)
+            ci, co, kh, kw = m.weight.shape
+            tot += 2.0 * ci * co * kh * kw * hin * hin
+        elif isinstance(m, torch.nn.Conv2d):
+            co, ci, kh, kw = m.weight.shape
+            if n.startswith("preprocess"):
+                ho = S // 2
+            elif n.startswith("layer"):
+                k = int(re.match(r"layer(\d+)", n).group(1))
+                ho = S // 4 // 2 ** (k - 1)
+                if k > 1 and n.endswith(".0.conv1") and kh == 1:     # Bottleneck: stride on conv2, conv1 at input res
+                    ho *= 2
+            else:
+                ho = S // 4
+            tot += 2.0 * co * ci * kh * kw * ho * ho
+    return 3.0 * tot / 1e9
+
+
 def pmc_traffic(kernel, batch, dtype):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/r<N>_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
@@ -78,8 +109,8 @@ def pmc_traffic(kernel, batch, dtype):
     return None, None
 
 
-def heads_gemm_roofline(B, dtype_name, cin=256, hd=128, ods=(1, 4, 2)):
-    """The dominant kernel: the fused head GEMM (conv3x3 M=B*128*128, N=3*128, K=9*256, + bias/ReLU
+def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2)):
+    """The dominant kernel: the fused head GEMM (conv3x3 M=B*(S/4)^2, N=3*128, K=9*256, + bias/ReLU
     + the three 1x1 tails in the epilogue), timed live by HIP events on its launch stream around
     every launch inside the timed steps (scdhip.ops.LaunchTimer)."""
     from scdhip import ops
@@ -87,7 +118,7 @@ def heads_gemm_roofline(B, dtype_name, cin=256, hd=128, ods=(1, 4, 2)):
     if r is None:
         return None
     ms, n = r
-    M = B * 128 * 128
+    M = B * (S // 4) ** 2
     ct = hd * len(ods)
     flops = 2.0 * M * (ct * 9 * cin + hd * sum(ods))
     esz = 2 if dtype_name == "bf16" else 4
@@ -95,7 +126,7 @@ def heads_gemm_roofline(B, dtype_name, cin=256, hd=128, ods=(1, 4, 2)):
     achieved = flops / (ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if dtype_name == "bf16" else PEAK_F32_TFLOPS
     kernel = HEADS_KERNEL if dtype_name == "bf16" else "conv_gemm_kernel<f32,128,128,heads>"
-    traffic, src = pmc_traffic(kernel, B, dtype_name)
+    traffic, src = pmc_traffic(kernel, B, dtype_name) if S == 512 else (None, None)
     return {"bound": "mfma", "kernel": kernel, "achieved": round(achieved, 1), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": None if traffic is None else round(traffic), "traffic_source": src,
@@ -139,10 +170,22 @@ def main():
 
     # synthetic batch (per-rank shard), resident in HBM before timing
     B = args.batch
-    ds = SCD(None, True, seed=1000 + 97 * rank)
-    items = [ds[i] for i in range(B)]
-    x = torch.stack([it["xs"][0] for it in items]).to(dev)
-    ys = [torch.stack([it["ys"][k] for it in items]).to(dev) for k in range(4)]
+    S = args.image_size
+    if S == 512:
+        ds = SCD(None, True, seed=1000 + 97 * rank)
+        items = [ds[i] for i in range(B)]
+        x = torch.stack([it["xs"][0] for it in items]).to(dev)
+        ys = [torch.stack([it["ys"][k] for it in items]).to(dev) for k in range(4)]
+    else:
+        # same layout as the dataset plugin at another tile size: N(0,1) tiles, sparse heatmaps, 30 slots
+        g = torch.Generator().manual_seed(1000 + 97 * rank)
+        H = S // 4
+        x = torch.randn(B, 1, S, S, generator=g).to(dev)
+        heat = (torch.rand(B, 1, H, H, generator=g) > 0.999).float()
+        mask = torch.arange(30)[None, :] < torch.randint(5, 21, (B, 1), generator=g)
+        regr = torch.rand(B, 30, 6, generator=g) * 4
+        inds = torch.randint(0, H * H, (B, 30), generator=g) * mask
+        ys = [heat.to(dev), mask.to(dev), regr.to(dev), inds.to(dev)]
 
     def step():
         opt.zero_grad()
@@ -174,19 +217,23 @@ def main():
     if rank == 0:
         imgs = B * world * args.steps
         value = imgs / elapsed
-        roof = heads_gemm_roofline(B, args.dtype)
-        step_frac = value * TRAIN_GFLOP_PER_IMG / 1e3 / (world * (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
-                                                                  else PEAK_F32_TFLOPS))
+        roof = heads_gemm_roofline(B, args.dtype, S)
+        core = model.module if hasattr(model, "module") else model
+        gflop = TRAIN_GFLOP_PER_IMG if (args.model == "centerOffsetRes10" and S == 512) else \
+            train_gflop_per_img(core, S)
+        step_frac = value * gflop / 1e3 / (world * (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
+                                                    else PEAK_F32_TFLOPS))
         line = {
-            "metric": "512x512 images/sec training, centerOffsetRes10, at 1/2/4/8 MI355X",
+            "metric": "512x512 images/sec training, centerOffsetRes10, at 1/2/4/8 MI355X" if (
+                args.model == "centerOffsetRes10" and S == 512) else "%dx%d images/sec training, %s" % (S, S, args.model),
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if dtype == torch.bfloat16 else "fp32", "data": "synthetic",
-            "config": {"workload": "centerOffsetRes10 train step (fwd+focal/L1 loss+bwd+Adam, DDP over RCCL), "
-                                   "512x512 synthetic SCD tiles", "model": args.model, "global_batch": B * world,
+            "config": {"workload": "%s train step (fwd+focal/L1 loss+bwd+Adam, DDP over RCCL), %dx%d synthetic "
+                                   "SCD tiles" % (args.model, S, S), "model": args.model, "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "parallelism": "dp%d" % world,
-                       "image_size": 512},
+                       "image_size": S, "train_gflop_per_img": round(gflop, 3)},
             "roofline": roof,
             "step_mfma_frac": round(step_frac, 4),
             "final_loss": round(final_loss, 5),
