@@ -172,10 +172,14 @@ def main():
     B = args.batch
     S = args.image_size
     if S == 512:
-        ds = SCD(None, True, seed=1000 + 97 * rank)
+        if args.model.startswith("cornerNet"):
+            from trainer.dataset.syntheticCorner import CornerSCD
+            ds = CornerSCD(None, True, seed=1000 + 97 * rank)       # ys: heat, mask, regr, tl, br
+        else:
+            ds = SCD(None, True, seed=1000 + 97 * rank)
         items = [ds[i] for i in range(B)]
         x = torch.stack([it["xs"][0] for it in items]).to(dev)
-        ys = [torch.stack([it["ys"][k] for it in items]).to(dev) for k in range(4)]
+        ys = [torch.stack([it["ys"][k] for it in items]).to(dev) for k in range(len(items[0]["ys"]))]
     else:
         # same layout as the dataset plugin at another tile size: N(0,1) tiles, sparse heatmaps, 30 slots
         g = torch.Generator().manual_seed(1000 + 97 * rank)
@@ -217,7 +221,8 @@ def main():
     if rank == 0:
         imgs = B * world * args.steps
         value = imgs / elapsed
-        roof = heads_gemm_roofline(B, args.dtype, S)
+        # the fused CenterNet head GEMM (HeadsFn) is the dominant kernel of the centerOffset* plugins only
+        roof = heads_gemm_roofline(B, args.dtype, S) if args.model.startswith("centerOffset") else None
         core = model.module if hasattr(model, "module") else model
         gflop = TRAIN_GFLOP_PER_IMG if (args.model == "centerOffsetRes10" and S == 512) else \
             train_gflop_per_img(core, S)
