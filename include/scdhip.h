@@ -197,6 +197,14 @@ int scd_centernet_loss_finalize(double* focal_acc, int nfocal, double* l1_acc, i
 /* g[i] *= factors[idx] * go[0]  (in place) */
 int scd_scale_by_device(float* g, long n, const float* factors, int idx, const float* go, void* stream);
 
+/* CenterNet training targets on the GPU (datasets/scds/scdx16p100.py:514-531, :575-591,
+ * datasets/utility.py:11-16, evaluations/intersection.py:46-63): locs (B,K,8) fp32 object rows
+ * [ctx, cty, offx, offy, majx, majy, minl, halo], counts (B) int32 objects per tile (<= K <= 64) ->
+ * heat (B,1,H,H) fp32 (Gaussian splats in object order, each added in float64 and clipped at 1),
+ * mask (B,K) u8, regr (B,K,6) fp32 = locs[..., 2:8], inds (B,K) int64 = floor(cty)*H + floor(ctx)
+ * (0 where the centre is outside the map). threshold = the IoU threshold of the radius rule (0.5). */
+int scd_render_center_targets(const float* locs, const int* counts, int B, int K, int H, float threshold,
+                              float* heat, uint8_t* mask, float* regr, int64_t* inds, void* stream);
 /* ---- decode (centerNetOffset.py:219-251, utility.py:87-118) ---- */
 size_t scd_decode_workspace(int N, int HW);
 int scd_decode_topk(const float* heat, int N, int H, int W, int K, const float* offset, int od_off,

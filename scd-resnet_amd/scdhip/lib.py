@@ -79,6 +79,7 @@ SIGNATURES = {
     "scd_decode_workspace": (c_size_t, [I, I]),
     "scd_decode_topk": (I, [P, I, I, I, I, P, I, P, I, P, P, P, P, P, P, P, P]),
     "scd_adam_step": (I, [P, P, P, P, L, F, F, F, F, F, F, F, P]),
+    "scd_render_center_targets": (I, [P, P, I, I, I, F, P, P, P, P, P]),
     "scd_cpool_fwd": (I, [I, I, P, P, P, I, I, I, I, P]),
     "scd_cpool_bwd": (I, [I, I, P, P, P, I, I, I, I, P]),
     "scd_version": (ctypes.c_char_p, []),

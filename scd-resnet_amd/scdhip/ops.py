@@ -612,3 +612,22 @@ def decode_topk(heat, offset, regr, K=100):
            ptr(regr.contiguous()) if regr is not None else 0, od_regr, ptr(scores), ptr(inds), ptr(ys), ptr(xs),
            ptr(off_out), ptr(regr_out), ptr(ws), stream())
     return scores, inds, ys, xs, (off_out if offset is not None else None), (regr_out if regr is not None else None)
+
+
+def render_center_targets(locs, counts, size=128, threshold=0.5):
+    """CenterNet targets on the GPU (scd_render_center_targets): locs (B,K,8) fp32 object rows, counts (B,)
+    objects per tile -> [heat (B,1,size,size) f32, mask (B,K) bool, regr (B,K,6) f32, inds (B,K) i64], the
+    dataset contract of scdx16p100.py:376-379 batched."""
+    _need_gpu(locs)
+    locs = locs.float().contiguous()
+    counts = counts.to(device=locs.device, dtype=torch.int32).contiguous()
+    B, K, _ = locs.shape
+    dev = locs.device
+    heat = torch.empty(B, 1, size, size, device=dev)
+    mask = torch.empty(B, K, dtype=torch.bool, device=dev)
+    regr = torch.empty(B, K, 6, device=dev)
+    inds = torch.empty(B, K, dtype=torch.int64, device=dev)
+    L.call("scd_render_center_targets", ptr(locs), ptr(counts), B, K, size, float(threshold), ptr(heat),
+           ptr(mask), ptr(regr), ptr(inds), stream())
+    return [heat, mask, regr, inds]
+

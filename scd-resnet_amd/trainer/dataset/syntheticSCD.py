@@ -99,6 +99,24 @@ class SCD(Dataset):
         tile, _, ys = self.item(index, self.seed)
         return {"xs": [tile], "ys": ys}
 
+    def gpu_batch(self, indices, device):
+        """A training batch with its targets rendered on the GPU (scdhip.ops.render_center_targets, one launch
+        for the whole batch) instead of per sample on the host: {"xs": [(B,1,S,S)], "ys": [heat, mask, regr,
+        inds]} on `device`, equal to stacking __getitem__(i) for i in indices (tests/test_targets_gpu.py)."""
+        from scdhip import ops
+        tiles, locs = [], np.zeros((len(indices), MAXTAGLEN, 8), dtype=np.float32)
+        counts = np.zeros(len(indices), dtype=np.int32)
+        for b, i in enumerate(indices):
+            rs = np.random.RandomState((self.seed + i) & 0x7FFFFFFF)
+            objs = sample_objects(rs, self.heat)
+            tiles.append(torch.from_numpy(rs.standard_normal((1, self.size, self.size)).astype(np.float32)))
+            n = min(len(objs), MAXTAGLEN)
+            locs[b, :n] = objs[:n]
+            counts[b] = n
+        ys = ops.render_center_targets(torch.from_numpy(locs).to(device), torch.from_numpy(counts).to(device),
+                                       self.heat, THRESHOLDIOU)
+        return {"xs": [torch.stack(tiles).to(device)], "ys": ys}
+
     def getValidationSet(self, batch=None):
         from configuration import defaultConfig
         batch = batch or min(VALID_SAMPLES, defaultConfig.validationBatchSize)
