@@ -76,6 +76,21 @@ def main():
             runs = [("fwd", lambda: ops.deconv_fwd(x, wt, Cout)),
                     ("dgrad", lambda: ops.deconv_dgrad(gy, wp, Cin)),
                     ("wgrad", lambda: ops.conv_wgrad(x, gy, k, k, s, p, dw, (Cout * k * k, k * k, 1)))]
+        if name.startswith("heads") and dt == torch.bfloat16:
+            # the fused head GEMM of the model (bias + ReLU + the three 1x1 tails in the epilogue)
+            L = ops.L
+            od = [1, 4, 2]
+            b0 = torch.randn(Cout, device=dev) * 0.1
+            w1 = [torch.randn(o, 128, device=dev) / 128 ** 0.5 for o in od]
+            b1 = [torch.randn(o, device=dev) * 0.1 for o in od]
+            outs = [torch.empty(B, o, H, W, device=dev) for o in od]
+            hid = torch.empty(B, H, W, Cout, device=dev, dtype=dt)
+            odarr, w1p, b1p = L.int_array(od), L.ptr_array([t.data_ptr() for t in w1]), \
+                L.ptr_array([t.data_ptr() for t in b1])
+            op = L.ptr_array([t.data_ptr() for t in outs])
+            runs.insert(1, ("fused", lambda: L.call(
+                "scd_conv_gemm_heads", ops.dt(x), ops.ptr(x), ops.ptr(wp), ops.ptr(hid), ops.ptr(b0), B, H, W, Cin,
+                len(od), odarr, w1p, b1p, op, ops.stream())))
         for pas, fn in runs:
             ms = timed(fn, a.reps)
             tot_ms += ms
