@@ -58,6 +58,18 @@ int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, const float*
                   int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
                   void* stream);
 
+/* scd_conv_gemm (no bias / ReLU / accumulate) whose output y is the gradient dout of a following BN+ReLU
+ * layer (pre-BN activation bn_y, same NHWC shape as y): the GEMM epilogue also accumulates that layer's
+ * backward sums -- bn_stats[rep][0][c] += sum dz, [rep][1][c] += sum dz*(bn_y-mean)*invstd with
+ * dz = y (as stored) where bn_y*relu_scale + relu_shift > 0 -- i.e. what scd_bn_bwd_reduce(y, NULL, bn_y,
+ * relu_scale, relu_shift, ...) adds, without re-reading y (ping-pong bf16 GEMM; other shapes run the GEMM and
+ * then scd_bn_bwd_reduce).  Replaces the cuDNN input-gradient + BatchNorm2d backward pair of
+ * residuals.py:298-307 / centerNetOffset.py:106-110 followed by residuals.py:306. */
+int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void* y, int N, int Hi, int Wi, int Ci, int Ho,
+                        int Wo, int Co, int in_stride, int out_stride, int wrow, int nphase,
+                        const scd_gemm_phase* phases, const void* bn_y, const float* mean, const float* invstd,
+                        const float* relu_scale, const float* relu_shift, double* bn_stats, void* stream);
+
 /* Head convolution with the CenterNet tails fused into the epilogue: hid = relu(conv3x3(x, w) + bias)
  * (N,H,W,nh*128) NHWC and, from the same tile, outs[h] (N,od[h],H,W) fp32 = w1[h] . hid_h + b1[h].
  * Replaces the three terminal Sequentials (centerNetOffset.py:106-110) in one launch; w is the

@@ -46,6 +46,15 @@ struct GemmParams {
     const float* head_w[4];
     const float* head_b[4];
     float* head_out[4];
+    // BN-backward sums in the epilogue (ping-pong kernel; scd_conv_gemm_bnbwd): the GEMM output is the gradient
+    // dout of a following BN+ReLU layer whose pre-BN activation is bny; stats accumulates sum dz and
+    // sum dz*(y-mean)*invstd with dz = dout (as stored) where y*rsc + rsh > 0
+    int bnbwd;
+    const char* bny;
+    const float* bn_mean;
+    const float* bn_invstd;
+    const float* bn_rsc;
+    const float* bn_rsh;
 };
 
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
@@ -797,12 +806,37 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
+    // BN-backward mode: output pixel of each of the lane's 8 rows (-1 past the end)
+    int pix[8];
+    if (p.bnbwd) {
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+            const int m = mt * BM + 128 * grp + a * 16 + l16;
+            const int n = m / QQ;
+            const int rem = m - n * QQ;
+            const int qh = rem / ph.Qw, qw = rem - (rem / ph.Qw) * ph.Qw;
+            pix[a] = m < M ? (n * p.Ho + p.os * qh + ph.rho_h) * p.Wo + p.os * qw + ph.rho_w : -1;
+        }
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
         float bias[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+        float bmu[4], bis[4], bsc[4], bsh[4];
+        uint2 yq[8];
+        if (p.bnbwd) {
+            const float4 f0 = *(const float4*)(p.bn_mean + col0), f1 = *(const float4*)(p.bn_invstd + col0);
+            const float4 f2 = *(const float4*)(p.bn_rsc + col0), f3 = *(const float4*)(p.bn_rsh + col0);
+            bmu[0] = f0.x; bmu[1] = f0.y; bmu[2] = f0.z; bmu[3] = f0.w;
+            bis[0] = f1.x; bis[1] = f1.y; bis[2] = f1.z; bis[3] = f1.w;
+            bsc[0] = f2.x; bsc[1] = f2.y; bsc[2] = f2.z; bsc[3] = f2.w;
+            bsh[0] = f3.x; bsh[1] = f3.y; bsh[2] = f3.z; bsh[3] = f3.w;
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+                yq[a] = pix[a] >= 0 ? *(const uint2*)(p.bny + ((long)pix[a] * p.Co + col0) * 2) : make_uint2(0, 0);
+        }
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
             const int m = mt * BM + 128 * grp + a * 16 + l16;
@@ -811,7 +845,22 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             for (int r = 0; r < 4; ++r) {
                 v[r] = acc[a][b][r] + bias[r];
                 if (p.relu) v[r] = fmaxf(v[r], 0.f);
-                if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+            }
+            if (m < M) {
+                if (p.bnbwd) {
+                    const unsigned yw[2] = {yq[a].x, yq[a].y};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float yv = __uint_as_float(r & 1 ? (yw[r >> 1] & 0xffff0000u) : (yw[r >> 1] << 16));
+                        const float d = (float)(__bf16)v[r];            // the stored gradient
+                        const float dz = yv * bsc[r] + bsh[r] > 0.f ? d : 0.f;
+                        csum[b][r] += dz;
+                        csq[b][r] += dz * (yv - bmu[r]) * bis[r];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+                }
             }
             typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
             bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
@@ -2246,7 +2295,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
                     f.rho_w == 0 && f.Qh == p.Ho && f.Qw == p.Wo && p.Hi == p.Ho && p.Wi == p.Wo && p.Wo % 16 == 0;
         for (int t = 0; halo && t < 9; ++t)
             halo = f.dh[t] >= -1 && f.dh[t] <= 1 && f.dw[t] >= -1 && f.dw[t] <= 1;
-        if (halo) {
+        if (halo && !p.bnbwd) {
             const int TW = p.Wo % 32 == 0 ? 32 : 16, TH = 256 / TW;
             const long mtiles = (long)p.N * ((p.Ho + TH - 1) / TH) * (p.Wo / TW);
             if (mtiles * (p.Co / bn) >= 256) {
@@ -2302,6 +2351,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
             SCD_RETURN_LAUNCH();
         }
     }
+    if (p.bnbwd) return SCD_ERR_ARG;      // BN-backward sums only in the ping-pong epilogue (caller falls back)
     bool ring = false;
     if (dtype == SCD_DT_BF16 && !narrow) {
         const int rm = ring_mode();
@@ -2343,6 +2393,7 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.N = N; p.Hi = Hi; p.Wi = Wi; p.Ci = Ci; p.Ho = Ho; p.Wo = Wo; p.Co = Co;
     p.is = in_stride; p.os = out_stride; p.wrow = wrow; p.relu = relu; p.accumulate = accumulate;
     p.head_on = 0;
+    p.bnbwd = 0; p.bny = nullptr; p.bn_mean = p.bn_invstd = p.bn_rsc = p.bn_rsh = nullptr;
     {
         static int dbg = -1;
         if (dbg < 0) { const char* e = getenv("SCD_GEMM_DEBUG"); dbg = e ? atoi(e) : 0; }
@@ -2358,6 +2409,28 @@ extern "C" int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, c
     GemmParams p;
     fill_params(p, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu, accumulate);
     return conv_gemm_launch(dtype, p, nphase, phases, stream);
+}
+
+extern "C" int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void* y, int N, int Hi, int Wi, int Ci,
+                                   int Ho, int Wo, int Co, int in_stride, int out_stride, int wrow, int nphase,
+                                   const scd_gemm_phase* phases, const void* bn_y, const float* mean,
+                                   const float* invstd, const float* relu_scale, const float* relu_shift,
+                                   double* bn_stats, void* stream) {
+    if (!bn_y || !mean || !invstd || !relu_scale || !relu_shift || !bn_stats || Co % 4) return SCD_ERR_ARG;
+    GemmParams p;
+    fill_params(p, x, w, y, nullptr, bn_stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, 0, 0);
+    p.bnbwd = 1;
+    p.bny = (const char*)bn_y; p.bn_mean = mean; p.bn_invstd = invstd; p.bn_rsc = relu_scale; p.bn_rsh = relu_shift;
+    if (dtype == SCD_DT_BF16) {
+        const int rc = conv_gemm_launch(dtype, p, nphase, phases, stream);
+        if (rc != SCD_ERR_ARG) return rc;
+    }
+    // shapes the ping-pong kernel does not take: plain GEMM, then the separate BN-backward reduction
+    fill_params(p, x, w, y, nullptr, nullptr, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, 0, 0);
+    const int rc = conv_gemm_launch(dtype, p, nphase, phases, stream);
+    if (rc) return rc;
+    return scd_bn_bwd_reduce(dtype, y, nullptr, bn_y, relu_scale, relu_shift, mean, invstd, Co, (long)N * Ho * Wo * Co,
+                             bn_stats, stream);
 }
 
 extern "C" int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void* hid, const float* bias, int N,

@@ -194,6 +194,8 @@ class DeconvBNFn(torch.autograd.Function):
         out = ops.bn_apply(y, st, True)
         ctx.save_for_backward(x, y, out)
         ctx.st, ctx.deconv, ctx.bn = st, deconv, bn
+        ctx.prod = ops.bn_producer(x)           # a BN+ReLU layer before this one: its sums come from our dgrad
+        ops.set_bn_producer(out, bn, st, y)
         return out
 
     @staticmethod
@@ -203,11 +205,16 @@ class DeconvBNFn(torch.autograd.Function):
         w = deconv.weight
         k = w.shape[2]
         s, p = deconv.stride[0], deconv.padding[0]
-        dy = ops.bn_backward(bn, st, _c(dout), y, relu=True)
+        dout = _c(dout)
+        dy = ops.bn_backward(bn, st, dout, y, relu=True, stats=ops.take_bn_bwd_fused(bn, dout))
         # dW_t[i][o][r][s] = sum x[i at q] * dy[o at s*q + r - p]: weight-gradient GEMM with G = x
         T = k * k
         ops.conv_wgrad(x, dy, k, k, s, p, ops.grad_of(w), (w.shape[1] * T, T, 1))
-        dx = ops.deconv_dgrad(dy, ops.pack_weight(w, x.dtype, 0), w.shape[0], k, s, p)
+        fuse = ctx.prod is not None and x.dtype == torch.bfloat16
+        dx = ops.deconv_dgrad(dy, ops.pack_weight(w, x.dtype, 0), w.shape[0], k, s, p,
+                              bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
+        if fuse:
+            ops.mark_bn_bwd_fused(ctx.prod[0], dx)
         return dx, None, None, None
 
 
@@ -269,6 +276,7 @@ class HeadsFn(torch.autograd.Function):
         ctx.save_for_backward(feat, hid)
         ctx.w0s = w0s
         ctx.heads, ctx.od, ctx.Hd = heads, od, Hd
+        ctx.prod = ops.bn_producer(feat)        # the deconv BN+ReLU: its backward sums come from our dgrad
         return tuple(outs)
 
     @staticmethod
@@ -295,7 +303,11 @@ class HeadsFn(torch.autograd.Function):
         ld = (Cin * 9, 9, 1)
         rows = [(i * Hd, (i + 1) * Hd, ops.grad_of(h[0].weight), ld) for i, h in enumerate(heads)]
         ops.conv_wgrad(dhid, feat, 3, 3, 1, 1, None, None, rows=rows)
-        dfeat = ops.conv_dgrad(dhid, ops.pack_concat(w0s, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1)
+        fuse = ctx.prod is not None and feat.dtype == torch.bfloat16
+        dfeat = ops.conv_dgrad(dhid, ops.pack_concat(w0s, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1,
+                               bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
+        if fuse:
+            ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
         return dfeat, None, None
 
 

@@ -48,6 +48,8 @@ IP = ctypes.POINTER(c_int)
 SIGNATURES = {
     "scd_conv_gemm": (I, [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P]),
     "scd_conv_gemm_heads": (I, [I, P, P, P, P, I, I, I, I, I, IP, PP, PP, PP, P]),
+    "scd_conv_gemm_bnbwd": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P, P, P, P,
+                                P, P, P]),
     "scd_conv_wgrad_workspace": (c_size_t, [I, I, I, I]),
     "scd_conv_wgrad_nsplit": (I, [I, L, I, I, I]),
     "scd_conv_wgrad_nsplit2": (I, [I, L, I, I, I, I, I]),

@@ -186,6 +186,7 @@ _ACTIVE_PLAN = None
 def pack_begin(plan):
     """Start of a model forward: repack every recorded operand (one launch) and activate the plan."""
     global _ACTIVE_PLAN
+    clear_bn_fusion()
     _ACTIVE_PLAN = None
     plan.refresh()
     _ACTIVE_PLAN = plan
@@ -287,9 +288,17 @@ def _dgrad_phases(kh, kw, stride, pad, Hc, Wc):
 
 
 def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, stats=None, relu=False,
-          accumulate=False):
+          accumulate=False, bn_bwd=None):
     N, Hi, Wi, Ci = x.shape
     arr = (L.GemmPhase * len(phases))(*phases)
+    if bn_bwd is not None:
+        # bn_bwd = (st, y_pre_bn, stats): the next BN+ReLU layer's backward sums from the GEMM epilogue
+        st, ybn, bstats = bn_bwd
+        assert bias is None and stats is None and not relu and not accumulate
+        L.call("scd_conv_gemm_bnbwd", dt(x), ptr(x), ptr(wpack), ptr(y), N, Hi, Wi, Ci, Ho, Wo, Co, in_stride,
+               out_stride, wpack.shape[1], len(phases), arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
+               ptr(st.shift), ptr(bstats), stream())
+        return y
     L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
            in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr, stream())
     return y
@@ -306,14 +315,14 @@ def conv_fwd(x, wpack, Co, kh, kw, stride, pad, bias=None, stats=None, relu=Fals
     return _gemm(x, wpack, out, Co, Ho, Wo, stride, 1, _fwd_phase(kh, kw, pad, Ho, Wo), bias, stats, relu)
 
 
-def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumulate=False, stats=None):
+def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumulate=False, stats=None, bn_bwd=None):
     """Input-gradient of Conv2d (NHWC) as a phase-decomposed gather-GEMM; wpack_t = pack_weight(w, mode=1).
-    Also ConvTranspose2d forward (with the transposed conv's geometry)."""
+    Also ConvTranspose2d forward (with the transposed conv's geometry).  bn_bwd: see _gemm."""
     N = dy.shape[0]
     if out is None:
         out = torch.empty(N, Hc, Wc, Cin, dtype=dy.dtype, device=dy.device)
     return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, _dgrad_phases(kh, kw, stride, pad, Hc, Wc),
-                 stats=stats, accumulate=accumulate)
+                 stats=stats, accumulate=accumulate, bn_bwd=bn_bwd)
 
 
 def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None):
@@ -325,14 +334,73 @@ def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None):
     return conv_dgrad(x, wpack_t, Cout, Ho, Wo, k, k, stride, pad, stats=stats)
 
 
-def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=False):
+def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=False, bn_bwd=None):
     """ConvTranspose2d input-gradient = Conv2d forward of dy; wpack = pack_weight(W_t, mode=0)."""
     N, H, W, _ = dy.shape
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     if out is None:
         out = torch.empty(N, Ho, Wo, Cin, dtype=dy.dtype, device=dy.device)
-    return _gemm(dy, wpack, out, Cin, Ho, Wo, stride, 1, _fwd_phase(k, k, pad, Ho, Wo), accumulate=accumulate)
+    return _gemm(dy, wpack, out, Cin, Ho, Wo, stride, 1, _fwd_phase(k, k, pad, Ho, Wo), accumulate=accumulate,
+                 bn_bwd=bn_bwd)
+
+
+# ------------------------------------------------------------------ BN-backward sums from the producing GEMM
+#
+# A BN+ReLU layer (DeconvBNFn) registers its output with (bn, BNState, pre-BN y); the module that consumes it
+# (HeadsFn, the next DeconvBNFn) looks it up in ITS forward, and in its backward computes the input gradient
+# with scd_conv_gemm_bnbwd, which adds that BN layer's backward sums in the GEMM epilogue into a dedicated
+# buffer ("bwdf").  The BN layer's backward then takes those sums instead of running scd_bn_bwd_reduce -- only
+# if the gradient it receives is exactly the tensor the GEMM wrote; otherwise it zeroes the buffer and reduces
+# as usual.  Keys carry data pointer, shape and version, so a stale or copied tensor never matches.
+
+_BN_PRODUCER = {}
+_BN_FUSED = {}
+
+
+class BNFusion:
+    enabled = os.environ.get("SCD_BN_FUSE", "1") != "0"
+
+
+def _tkey(t):
+    return (t.data_ptr(), tuple(t.shape), t._version)
+
+
+def set_bn_producer(out, bn, st, y):
+    # (called from autograd Function.forward, where grad mode is off: training mode is the condition)
+    if BNFusion.enabled and bn.training:
+        _BN_PRODUCER[_tkey(out)] = (bn, st, y)
+
+
+def bn_producer(t):
+    """(bn, st, y) of the BN+ReLU layer that produced t in this forward, or None."""
+    return _BN_PRODUCER.pop(_tkey(t), None)
+
+
+def fused_bn_bwd_args(prod):
+    """bn_bwd argument for a GEMM computing the gradient of prod's output (prod from bn_producer)."""
+    bn, st, y = prod
+    return (st, y, bn_stats(bn, "bwdf"))
+
+
+def mark_bn_bwd_fused(bn, grad):
+    _BN_FUSED[id(bn)] = _tkey(grad)
+
+
+def take_bn_bwd_fused(bn, dout):
+    """The epilogue-accumulated backward sums of bn if they belong to dout, else None (buffer re-zeroed)."""
+    k = _BN_FUSED.pop(id(bn), None)
+    if k is None:
+        return None
+    buf = bn_stats(bn, "bwdf")
+    if k != _tkey(dout):
+        buf.zero_()
+        return None
+    return buf
+
+
+def clear_bn_fusion():
+    _BN_PRODUCER.clear()
 
 
 # ------------------------------------------------------------------ weight gradients on a side stream
@@ -465,15 +533,17 @@ def bn_apply(y, st, relu, res=None, rst=None, out=None):
     return out
 
 
-def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False):
+def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None):
     """Training BN backward: dgamma/dbeta accumulated into bn.weight.grad / bn.bias.grad, returns dy.
     relu=True: the layer is BN+ReLU and its ReLU mask is recomputed from y (no activation read);
-    mask: the stored activation whose > 0 pattern is the ReLU mask (residual joins)."""
+    mask: the stored activation whose > 0 pattern is the ReLU mask (residual joins);
+    stats: the backward sums already accumulated by the producing GEMM (take_bn_bwd_fused)."""
     C = y.shape[-1]
-    stats = bn_stats(bn, "bwd")
     rsc, rsh = (ptr(st.scale), ptr(st.shift)) if (relu and mask is None) else (0, 0)
-    L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd), C,
-           y.numel(), ptr(stats), stream())
+    if stats is None:
+        stats = bn_stats(bn, "bwd")
+        L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd), C,
+               y.numel(), ptr(stats), stream())
     coef = bn_backward_coef(bn, st, stats, C)
     dy = torch.empty_like(y)
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),

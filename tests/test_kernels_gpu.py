@@ -333,3 +333,37 @@ def test_batched_pack_matches_single(dtype):
     ops.pack_end()
     for a, b in zip(first, again):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 128, 384, 256), (2, 40, 36, 384, 256)])
+def test_dgrad_with_bn_backward_sums(shape):
+    """scd_conv_gemm_bnbwd (input-gradient GEMM whose epilogue adds the following BN+ReLU layer's backward sums)
+    against scd_conv_gemm + scd_bn_bwd_reduce: identical gradient, sums within fp32 summation-order noise.
+    128x128 runs the fused ping-pong epilogue, 40x36 the fallback (plain GEMM + separate reduce)."""
+    from scdhip import ops
+    N, H, W, Co, Ci = shape
+    g = torch.Generator().manual_seed(41)
+    dy = (torch.randn(N, H, W, Co, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    w = (torch.randn(Co, Ci, 3, 3, generator=g) / (Ci * 9) ** 0.5).to(DEV)
+    ybn = torch.randn(N, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
+
+    class St:
+        pass
+    st = St()
+    st.mean = (torch.randn(Ci, generator=g) * 0.1).to(DEV)
+    st.invstd = (torch.rand(Ci, generator=g) + 0.5).to(DEV)
+    st.scale = (torch.rand(Ci, generator=g) + 0.5).to(DEV)
+    st.shift = (torch.randn(Ci, generator=g) * 0.2).to(DEV)
+    wt = ops.pack_weight(w, torch.bfloat16, 1)
+    s1 = torch.zeros(64 * 2 * Ci, dtype=torch.float64, device=DEV)
+    s2 = torch.zeros_like(s1)
+    dx1 = ops.conv_dgrad(dy, wt, Ci, H, W, 3, 3, 1, 1, bn_bwd=(st, ybn, s1))
+    dx2 = ops.conv_dgrad(dy, wt, Ci, H, W, 3, 3, 1, 1)
+    ops.L.call("scd_bn_bwd_reduce", ops.dt(dx2), ops.ptr(dx2), 0, ops.ptr(ybn), ops.ptr(st.scale), ops.ptr(st.shift),
+               ops.ptr(st.mean), ops.ptr(st.invstd), Ci, dx2.numel(), ops.ptr(s2), ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx2)
+    a = s1.view(64, 2, Ci).sum(0).cpu()
+    b = s2.view(64, 2, Ci).sum(0).cpu()
+    for i in range(2):
+        assert (a[i] - b[i]).abs().max().item() <= 1e-5 * b[i].abs().max().item() + 1e-9, i
