@@ -282,10 +282,11 @@ class FlatDDP(torch.nn.Module):
         self._queued = False
         if self.world == 1:
             return
-        self._launch_ready(final=True)
         if self.flat.grad.is_cuda:
+            # every gradient written on scdhip's side stream is ordered before the remaining buckets
             from . import ops
             ops.join_side_streams()
+        self._launch_ready(final=True)
         for b, w in enumerate(self._works):
             w.wait()                                # NCCL: the compute stream waits; gloo: blocks
             if not self._use_avg:
