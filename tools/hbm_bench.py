@@ -110,6 +110,18 @@ def main():
     report("stem_pool_fwd 32x256x256x64", timed(lambda: L.call(
         "scd_stem_pool_fwd", L.DT_BF16, y.data_ptr(), sc.data_ptr(), sh.data_ptr(), pooled.data_ptr(), am.data_ptr(),
         N, H, W, C, H // 2, W // 2, st()), a.reps), y.numel() * 2 + dout.numel() * 3)
+    # direct stem conv forward / weight gradient: x (32,1,512,512) fp32 -> y (32,256,256,64) bf16
+    xs = torch.randn(32, 1, 512, 512, device=dev)
+    w = torch.randn(64, 1, 7, 7, device=dev) / 7.0
+    wpk = ops.pack_weight(w, bf, 0, ldp=64)
+    st64 = torch.zeros(L.STAT_REPLICAS * 2 * 64, dtype=torch.float64, device=dev)
+    ys = ops.stem_conv_fwd(xs, wpk, stats=st64)
+    report("stem_conv_fwd 32x512x512 -> 64ch", timed(lambda: ops.stem_conv_fwd(xs, wpk, stats=st64), a.reps),
+           xs.numel() * 4 + ys.numel() * 2)
+    dw = torch.zeros_like(w)
+    report("stem_conv_wgrad (dz, y, coef)", timed(lambda: ops.stem_conv_wgrad(ys, xs, dw, ybn=ys,
+                                                                             coef=torch.ones(192, device=dev)),
+                                                  a.reps), xs.numel() * 4 + ys.numel() * 4)
     print("total us: %.1f" % sum(r[1] for r in rows))
 
 
