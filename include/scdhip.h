@@ -223,6 +223,30 @@ int scd_decode_topk(const float* heat, int N, int H, int W, int K, const float* 
                     const float* regr, int od_regr, float* scores, int64_t* inds, int64_t* ys, int64_t* xs,
                     float* off_out, float* regr_out, void* workspace, void* stream);
 
+/* ---- validation metrics (models/centerNetOffset.py:253-354, evaluations/detection.py:11-230,
+ * trainer/model/centerOffsetRes10.py:18-106) ----
+ * Decoded detections (scores/cty/ctx (N,K), offset (N,K,2), regr (N,K,4)) against ground truth (gt_regr (N,L,6);
+ * gt_loc = heat indices (N,L) int64 when loc_mode 0, or locs rows (N,L,loc_w) fp32 [x, y, ...] when loc_mode 1),
+ * H = heatmap width, thr = the score threshold of validMask (0.3).  K <= 256, L <= 64.
+ * Nine value streams, each the masked_select of the reference in (n,k,l) order:
+ *   0 IoUConfidence iou, 1 IoUConfidence score, 2 Orthogonity, 3 IoU centre/centre, 4 IoU centre/offset (iouoffsetwo),
+ *   5 IoU offset/offset, 6-8 MAE majL/minL/halo.   Masks: streams 0,1 -> mask 0; 2,6,7,8 -> mask 1; 3 -> 2; 4 -> 3;
+ *   5 -> 4.  scd_ceval_count writes counts (N,5) int32; scd_ceval_emit writes every stream at its exact offset
+ *   (streams[9] device pointers, sized by the column sums of counts). */
+int scd_ceval_count(const float* scores, const int64_t* cty, const int64_t* ctx, const float* offset, const float* regr,
+                    const float* gt_regr, const void* gt_loc, int loc_mode, int loc_w, int N, int K, int L, int H,
+                    float thr, int* counts, void* stream);
+int scd_ceval_emit(const float* scores, const int64_t* cty, const int64_t* ctx, const float* offset, const float* regr,
+                   const float* gt_regr, const void* gt_loc, int loc_mode, int loc_w, int N, int K, int L, int H,
+                   float thr, const int* counts, float* const* streams, void* stream);
+/* expression(): out[0..8] = fp64 means of the nine streams (stream 2 over its non-NaN values), out[9+t] = the
+ * reference's interpolated AP (averagePrecisionPlots + averagePrecisionAll) of stream 0 ranked by stream 1 at
+ * IoU threshold thr[t] (device array), objects = max(objnum, lens[0]).  Ranking: score descending, ties by
+ * descending pair index.  streams/lens are HOST arrays of 9 (device pointers / lengths). */
+size_t scd_ceval_summary_workspace(long n);
+int scd_ceval_summary(const float* const* streams, const long* lens, long objnum, const float* thr, int nthr,
+                      double* out, void* workspace, void* stream);
+
 /* ---- Adam (torch.optim.Adam defaults, networkFactory.py:79-82) over a flat fp32 buffer ---- */
 int scd_adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                   float eps, float bc1, float bc2, float gscale, void* stream);

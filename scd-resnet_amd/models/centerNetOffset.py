@@ -100,17 +100,56 @@ def decodeCenterNet(outputDictionary, K=100, nmsKernelSize=3, **kwargs):
 
 
 def centerNetEvaluation(xs, ys, ctScores, ctIndices, ctY, ctX, offset, regression, outputDictionary):
-    """Validation metrics hook (centerNetOffset.py:253-354).  The reference's IoU/AP/MAE
-    metrics are outside the accelerated path; this returns the decoded
-    detections' score statistics and object counts with the same dict shape."""
-    objNum = [int(m.sum().item()) for m in ys[1]]
-    valid = ctScores >= 0.3
-    return {"objs": objNum, "scores": ctScores.detach(), "valid": valid.detach()}, outputDictionary
+    """Validation metrics hook (centerNetOffset.py:253-354) on the GPU: the reference's predicted / ground-truth
+    boxes, validMask = score >= 0.3 and the IoUConfidence / Orthogonity / IoU x3 / MAE pair tests
+    (evaluations/detection.py:11-180) run as scd_ceval_count + scd_ceval_emit, one workgroup per image.  Same
+    dict as the reference, every value the reference's masked_select stream in the same (n, k, l) order.
+    ys = [heat, mask, regr (N,L,6), inds (N,L) or locs (N,L,8), ...]."""
+    objNum = [int(v) for v in ys[1].reshape(ys[1].shape[0], -1).sum(1).tolist()]
+    heat = outputDictionary.get("heatmap") if isinstance(outputDictionary, dict) else None
+    size = heat.shape[-1] if heat is not None else HEATMAPSIZE
+    s = ops.center_eval(ctScores, ctY, ctX, offset, regression, ys[2], ys[3], heatmap_size=size, threshold=0.3)
+    return {'iouscore': [s[0], s[1]],
+            'ortho': s[2],
+            'ioucenter': s[3],
+            'iouoffsetwo': s[4],
+            'iouoffset': s[5],
+            'maes': [s[6], s[7], s[8]],
+            'objs': objNum}, outputDictionary
 
 
 def expression(batches):
-    objs = sum(sum(b["objs"]) for b in batches)
-    scores = torch.cat([b["scores"].reshape(-1).float().cpu() for b in batches]) if batches else torch.zeros(1)
-    valid = torch.cat([b["valid"].reshape(-1).cpu() for b in batches]) if batches else torch.zeros(1, dtype=bool)
-    return "[objs] {}    [det>=0.3] {}    [avgS] {}".format(objs, int(valid.sum()),
-                                                             format(float(scores.mean()), '-6.4f'))
+    """trainer/model/centerOffsetRes10.py:18-106: the per-batch streams are concatenated on the device and
+    reduced by scd_ceval_summary (fp64 means, the reference's interpolated AP at 0.3/0.5/0.7/0.9; detections
+    ranked by score, ties by descending pair index).  Same output string."""
+    objNum = 0
+    cols = [[] for _ in range(9)]
+    for b in batches:
+        objNum += int(sum(b['objs']))
+        iou, score = b['iouscore']
+        aemaj, aemin, aerad = b['maes']
+        for c, v in zip(cols, (iou, score, b['ortho'], b['ioucenter'], b['iouoffsetwo'], b['iouoffset'],
+                                aemaj, aemin, aerad)):
+            c.append(v.reshape(-1))
+    if batches:
+        streams = [torch.cat(c) for c in cols]
+    else:
+        streams = [torch.zeros(0, device=torch.device("cuda", torch.cuda.current_device())) for _ in cols]
+    m, ap = ops.center_eval_summary(streams, objNum, (0.3, 0.5, 0.7, 0.9))
+    ev = {'mIoU': m[0], 'mIoUC': m[3], 'mIoUwoO': m[4], 'mIoUO': m[5], 'ap30': ap[0], 'ap50': ap[1], 'ap70': ap[2],
+          'ap90': ap[3], 'orthogonity': m[2], 'majMAE': m[6], 'minMAE': m[7], 'radMAE': m[8], 'avgScore': m[1]}
+    return ("[mIoU] {}    [mIoUC] {}    [mIoUwoO] {}    [mIoUO] {}    [AP30] {}    [AP50] {}    [AP70] {}    "
+            "[AP90] {}    [Orth] {}    [majMAE] {}    [minMAE] {}    [radMAE] {}    [avgS] {}").format(
+        format(ev['mIoU'] * 100, '-10.8f'),
+        format(ev['mIoUC'] * 100, '-10.8f'),
+        format(ev['mIoUwoO'] * 100, '-10.8f'),
+        format(ev['mIoUO'] * 100, '-10.8f'),
+        format(ev['ap30'] * 100, '-5.2f'),
+        format(ev['ap50'] * 100, '-5.2f'),
+        format(ev['ap70'] * 100, '-5.2f'),
+        format(ev['ap90'] * 100, '-5.2f'),
+        format(ev['orthogonity'], '-8.6f'),
+        format(ev['majMAE'], '-8.6f'),
+        format(ev['minMAE'], '-8.6f'),
+        format(ev['radMAE'], '-8.6f'),
+        format(ev['avgScore'], '-6.4f'))

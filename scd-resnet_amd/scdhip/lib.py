@@ -80,6 +80,10 @@ SIGNATURES = {
     "scd_scale_by_device": (I, [P, L, P, I, P, P]),
     "scd_decode_workspace": (c_size_t, [I, I]),
     "scd_decode_topk": (I, [P, I, I, I, I, P, I, P, I, P, P, P, P, P, P, P, P]),
+    "scd_ceval_count": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, P, P]),
+    "scd_ceval_emit": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, P, PP, P]),
+    "scd_ceval_summary_workspace": (c_size_t, [L]),
+    "scd_ceval_summary": (I, [PP, ctypes.POINTER(c_long), L, P, I, P, P, P]),
     "scd_adam_step": (I, [P, P, P, P, L, F, F, F, F, F, F, F, P]),
     "scd_render_center_targets": (I, [P, P, I, I, I, F, P, P, P, P, P]),
     "scd_cpool_fwd": (I, [I, I, P, P, P, I, I, I, I, P]),

@@ -4,6 +4,7 @@ Layouts: activations NHWC (channels innermost) in the compute dtype (fp32 parity
 bf16 performance mode); weights, grads, BN parameters fp32 in the reference layout.
 Every wrapper enqueues on torch's current HIP stream and never synchronises.
 """
+import ctypes
 import math
 import os
 
@@ -701,3 +702,58 @@ def render_center_targets(locs, counts, size=128, threshold=0.5):
            ptr(mask), ptr(regr), ptr(inds), stream())
     return [heat, mask, regr, inds]
 
+
+
+CEVAL_STREAMS = ("iou", "score", "ortho", "ioucenter", "iouoffsetwo", "iouoffset", "aemaj", "aemin", "aerad")
+_CEVAL_STREAM_MASK = (0, 0, 1, 2, 3, 4, 1, 1, 1)
+
+
+def center_eval(scores, cty, ctx, offset, regr, gt_regr, gt_loc, heatmap_size=128, threshold=0.3):
+    """centerNetEvaluation's pair metrics on the GPU (scd_ceval_count + scd_ceval_emit): the nine masked_select
+    streams of models/centerNetOffset.py:253-354 / evaluations/detection.py:11-180, in CEVAL_STREAMS order.
+    gt_loc: heat indices (N,L) int64 or locs rows (N,L,>=2) float [x, y, ...] (the reference's ys[3] dim test,
+    centerNetOffset.py:287-292).  One host read of the (N,5) per-image counts sizes the outputs."""
+    _need_gpu(scores, cty, ctx, offset, regr, gt_regr, gt_loc)
+    N, K = scores.shape
+    L_ = gt_regr.shape[1]
+    dev = scores.device
+    scores = scores.float().contiguous()
+    cty = cty.long().contiguous()
+    ctx = ctx.long().contiguous()
+    offset = offset.float().contiguous()
+    regr = regr.float().contiguous()
+    gt_regr = gt_regr.float().contiguous()
+    if offset.shape != (N, K, 2) or regr.shape != (N, K, 4) or gt_regr.shape != (N, L_, 6):
+        raise RuntimeError("center_eval: offset (N,K,2), regr (N,K,4), gt_regr (N,L,6) expected")
+    if gt_loc.dim() == 2:
+        loc_mode, loc_w, gt_loc = 0, 0, gt_loc.long().contiguous()
+    else:
+        loc_mode, loc_w, gt_loc = 1, gt_loc.shape[2], gt_loc.float().contiguous()
+    if gt_loc.shape[:2] != (N, L_):
+        raise RuntimeError("center_eval: ys[3] must be (N,L) or (N,L,w)")
+    counts = torch.empty(N, 5, dtype=torch.int32, device=dev)
+    args = (ptr(scores), ptr(cty), ptr(ctx), ptr(offset), ptr(regr), ptr(gt_regr), ptr(gt_loc), loc_mode, loc_w,
+            N, K, L_, int(heatmap_size), float(threshold))
+    L.call("scd_ceval_count", *args, ptr(counts), stream())
+    totals = counts.sum(0).cpu().tolist()
+    outs = [torch.empty(max(1, totals[m]), device=dev) for m in _CEVAL_STREAM_MASK]
+    L.call("scd_ceval_emit", *args, ptr(counts), L.ptr_array([o.data_ptr() for o in outs]), stream())
+    return [o[:totals[m]] for o, m in zip(outs, _CEVAL_STREAM_MASK)]
+
+
+def center_eval_summary(streams, objnum, thresholds=(0.3, 0.5, 0.7, 0.9)):
+    """expression()'s reductions (trainer/model/centerOffsetRes10.py:81-88; detection.py:183-230) on the GPU:
+    returns (means[9] in CEVAL_STREAMS order, APs[len(thresholds)]) as Python floats."""
+    _need_gpu(*streams)
+    if len(streams) != 9:
+        raise RuntimeError("center_eval_summary: nine streams expected")
+    dev = streams[0].device
+    streams = [s.float().contiguous() for s in streams]
+    lens = (ctypes.c_long * 9)(*[s.numel() for s in streams])
+    thr = torch.tensor(list(thresholds), dtype=torch.float32).to(dev)
+    out = torch.zeros(9 + len(thresholds), dtype=torch.float64, device=dev)
+    ws = torch.empty(max(8, L.lib().scd_ceval_summary_workspace(streams[0].numel())), dtype=torch.uint8, device=dev)
+    L.call("scd_ceval_summary", L.ptr_array([s.data_ptr() for s in streams]), lens, int(objnum), ptr(thr),
+           len(thresholds), ptr(out), ptr(ws), stream())
+    vals = out.cpu().tolist()
+    return vals[:9], vals[9:]

@@ -235,3 +235,33 @@ def test_f9_res50_bottleneck_step(golden):
     for k in g.files:
         if k.startswith("rs|"):
             np.testing.assert_allclose(st.B[k[3:]].numpy(), g[k], rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("case,loc_key", [("inds", "inds"), ("locs", "locs"), ("empty", "inds")])
+def test_f10_eval_metrics(golden, case, loc_key):
+    """oracle.metrics vs the reference's centerNetEvaluation + expression numbers (tests/golden/eval.npz)."""
+    from oracle import metrics as M
+    g = golden("eval")
+    c = M.eval_case(int(g[case + "_seed"]))
+    if case == "empty":
+        c["scores"] = c["scores"] * np.float32(0.25)
+    streams = M.center_eval(c["scores"], c["ctY"], c["ctX"], c["offset"], c["regr"], c["ys2"], c[loc_key])
+    for s, v in zip(M.STREAMS, streams):
+        np.testing.assert_array_equal(v, g["%s_%s" % (case, s)], err_msg=s)
+    np.testing.assert_array_equal(c["mask"].sum(1), g[case + "_objs"])
+    means, aps = M.summary(streams, int(g[case + "_objs"].sum()))
+    np.testing.assert_allclose(means, g[case + "_means"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(aps, g[case + "_aps"], rtol=0, atol=1e-12)
+
+
+def test_f10_ap_walk_small_cases():
+    """averagePrecisionAll restated: hand-checked plots (detection.py:208-230)."""
+    from oracle import metrics as M
+    assert M.ap_all([]) == 0
+    # one true positive of two objects: recall 0.5 at precision 1
+    assert M.ap_all([[0.5, 1.0]]) == 0.5
+    # FP then TP: precision 0 then 0.5 at recall 1 -> 0.5
+    assert M.ap_all([[0.0, 0.0], [1.0, 0.5]]) == 0.5
+    # TP, FP, TP over 2 objects: (0.5,1), (0.5,0.5), (1,2/3) -> 1*(2/3) record at the end, then (0.5-0.5)*... + 0.5*1
+    plots = [[0.5, 1.0], [0.5, 0.5], [1.0, 2 / 3]]
+    assert abs(M.ap_all(plots) - ((1.0 - 0.5) * (2 / 3) + 0.5 * 1.0)) < 1e-15
