@@ -177,7 +177,10 @@ def eval_case(seed, N=4, K=100, L=30, H=128, n_near=12):
             j = rs.randint(0, m)
             ctX[n, k] = np.clip(locs8[n, j, 0] + rs.randint(-1, 2), 0, H - 1)
             ctY[n, k] = np.clip(locs8[n, j, 1] + rs.randint(-1, 2), 0, H - 1)
-            regr[n, k, :2] = ys2[n, j, 2:4] * F(rs.uniform(0.7, 1.3))
+            a = rs.uniform(-0.3, 0.3)   # never exactly parallel: orthogonity at cos = 1 is a knife edge (NaN or 0)
+            ca, sa = np.cos(a), np.sin(a)
+            mx, my = float(ys2[n, j, 2]), float(ys2[n, j, 3])
+            regr[n, k, :2] = np.array([ca * mx - sa * my, sa * mx + ca * my]) * rs.uniform(0.7, 1.3)
             regr[n, k, 2] = ys2[n, j, 4] * F(rs.uniform(0.7, 1.3))
             regr[n, k, 3] = ys2[n, j, 5] + F(rs.uniform(-0.5, 0.5))
             offset[n, k] = ys2[n, j, :2] + rs.uniform(-0.5, 0.5, 2).astype(F)

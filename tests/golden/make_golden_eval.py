@@ -93,5 +93,20 @@ def main():
     np.savez_compressed(os.path.join(HERE, "eval.npz"), **out)
 
 
+def time_reference(N=32):
+    """CPU time of the reference's evaluation + expression for one N-image batch (build container)."""
+    import time
+    c = M.eval_case(99, N=N)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        ref_case(c, "inds")
+    print("reference centerNetEvaluation + expression, N=%d: %.1f ms per batch (%d threads)"
+          % (N, (time.perf_counter() - t0) / 3 * 1e3, torch.get_num_threads()))
+
+
 if __name__ == "__main__":
-    main()
+    if "--time" in sys.argv:
+        time_reference(32)
+        time_reference(256)
+    else:
+        main()

@@ -4,8 +4,8 @@ tests/golden/make_golden_eval.py from the real reference) and the CPU restatemen
 
 Tolerances.  The streams are float32 values from one rounding per op on both sides; the only op whose result
 can differ is sqrt: the device's is correctly rounded, the reference's torch CPU kernel is not always (see
-oracle/metrics.py), so values agree to a few ulp (rtol 2e-6) and an orthogonity of ~0 may be NaN on one side
-(1 - cos^2 a rounding below zero); stream lengths (the masks) are exact on these cases.  The AP walk is checked
+oracle/metrics.py), so values agree to a few ulp (rtol 2e-6); orthogonity = sqrt(1 - cos^2) is compared through its square (one ulp
+of cos near 1 moves it by up to 5e-4) and may be NaN on one side where it is ~0; stream lengths (the masks) are exact on these cases.  The AP walk is checked
 exactly (1e-12) against the oracle on the device's own streams, and against the reference's APs.  Means are
 fp64 on the device, fp32 torch.mean in the reference: rtol 1e-5."""
 import re
@@ -34,9 +34,13 @@ def _cmp_streams(got, want):
         g = g.cpu().numpy() if torch.is_tensor(g) else g
         assert g.shape == w.shape, (name, g.shape, w.shape)
         if name == "ortho":
+            # sqrt(1 - cos^2) is ill-conditioned near cos = 1 (one ulp of cos moves it by up to 5e-4): compare
+            # 1 - cos^2 = ortho^2 to a few ulp of 1; NaN (1 - cos^2 rounded below 0) only opposite ~0
             both = ~np.isnan(g) & ~np.isnan(w)
-            np.testing.assert_allclose(g[both], w[both], rtol=2e-6, atol=2e-6, err_msg=name)
-            assert np.all(np.nan_to_num(g[~both], nan=0.0) < 1e-3) and np.all(np.nan_to_num(w[~both], nan=0.0) < 1e-3)
+            np.testing.assert_allclose(g[both].astype(np.float64) ** 2, w[both].astype(np.float64) ** 2, rtol=1e-5,
+                                       atol=1e-6, err_msg=name)
+            assert np.all(np.nan_to_num(g[~both], nan=0.0) ** 2 < 1e-6)
+            assert np.all(np.nan_to_num(w[~both], nan=0.0) ** 2 < 1e-6)
         else:
             np.testing.assert_allclose(g, w, rtol=2e-6, atol=1e-6, err_msg=name)
 
@@ -52,7 +56,10 @@ def test_eval_streams_and_summary_vs_reference(golden, case, loc_key):
     _cmp_streams(s, [g["%s_%s" % (case, n)] for n in M.STREAMS])
     objnum = int(g[case + "_objs"].sum())
     means, aps = ops.center_eval_summary(s, objnum)
-    np.testing.assert_allclose(means, g[case + "_means"], rtol=1e-5, atol=1e-7)
+    gm = g[case + "_means"]
+    keep = [i for i in range(9) if i != 2]
+    np.testing.assert_allclose(np.array(means)[keep], gm[keep], rtol=1e-5, atol=1e-7)
+    assert abs(means[2] - gm[2]) < 1e-4    # orthogonity: see the module docstring
     np.testing.assert_allclose(aps, g[case + "_aps"], rtol=0, atol=1e-9)
     _, aps_o = M.summary([x.cpu().numpy() for x in s], objnum)
     np.testing.assert_allclose(aps, aps_o, rtol=0, atol=1e-12)
@@ -79,11 +86,12 @@ def test_plugin_evaluation_and_expression(golden):
     # means are compared on the doubled set, and the single-batch string is compared in full below
     for tag, a, b in zip(tags, got_v, ref_v):
         if not tag.startswith("AP"):
-            assert abs(a - b) <= 2e-6 * max(1.0, abs(b)) + 1e-6, (tag, a, b)
+            assert abs(a - b) <= 2e-6 * max(1.0, abs(b)) + 1e-6 + (1e-4 if tag == "Orth" else 0), (tag, a, b)
     expr1 = plugin.expression([ev])
     got1 = [float(v) for v in re.findall(r"\]\s+(-?[\d.]+)", expr1)]
     for tag, a, b in zip(tags, got1, ref_v):
-        assert abs(a - b) <= 2e-6 * max(1.0, abs(b)) + 1e-6 + (0.0051 if tag.startswith("AP") else 0), (tag, a, b)
+        slack = 0.0051 if tag.startswith("AP") else (1e-4 if tag == "Orth" else 0)
+        assert abs(a - b) <= 2e-6 * max(1.0, abs(b)) + 1e-6 + slack, (tag, a, b)
 
 
 @pytest.mark.parametrize("seed,K,L", [(5, 100, 30), (6, 256, 64), (7, 1, 1)])
