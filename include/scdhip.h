@@ -217,6 +217,14 @@ int scd_scale_by_device(float* g, long n, const float* factors, int idx, const f
  * (0 where the centre is outside the map). threshold = the IoU threshold of the radius rule (0.5). */
 int scd_render_center_targets(const float* locs, const int* counts, int B, int K, int H, float threshold,
                               float* heat, uint8_t* mask, float* regr, int64_t* inds, void* stream);
+/* SCD tile augmentation (datasets/scds/scdx16p100.py:416-441, datasets/argumentations.py:38-64):
+ * out[b] = (flip(in[b]) - mean) / sqrt(var) * jitter[b] + noise * noise_sv, mean/var over the flipped tile (fp64
+ * sums).  flips (B,2) u8 device [x (dim 2), y (dim 1)], nullable; jitter (B) device factors (1 + 0.05 g), nullable;
+ * noise (B,H,W) device N(0,1) draws, or NULL for the counter-based generator keyed by seed; noise_sv 0 = no noise
+ * (the validation set's normalize alone).  W % 4 == 0, in != out.  workspace: scd_augment_workspace(B) bytes. */
+size_t scd_augment_workspace(int B);
+int scd_augment_tiles(const float* in, float* out, int B, int H, int W, const uint8_t* flips, const float* jitter,
+                      const float* noise, float noise_sv, unsigned long long seed, void* workspace, void* stream);
 /* ---- decode (centerNetOffset.py:219-251, utility.py:87-118) ---- */
 size_t scd_decode_workspace(int N, int HW);
 int scd_decode_topk(const float* heat, int N, int H, int W, int K, const float* offset, int od_off,

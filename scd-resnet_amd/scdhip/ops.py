@@ -757,3 +757,25 @@ def center_eval_summary(streams, objnum, thresholds=(0.3, 0.5, 0.7, 0.9)):
            len(thresholds), ptr(out), ptr(ws), stream())
     vals = out.cpu().tolist()
     return vals[:9], vals[9:]
+
+
+def augment_tiles(tiles, flips=None, jitter=None, noise=None, noise_sv=0.0, seed=0, out=None):
+    """SCD.argumentation's sample half on the GPU (scd_augment_tiles; scdx16p100.py:416-441,
+    argumentations.py:38-64): per tile optional x / y flip, normalize, * jitter factor, + noise * noise_sv.
+    tiles (B,1,H,W) or (B,H,W) fp32; flips (B,2) bool/u8; jitter (B,) factors (1 + 0.05 g); noise (B,H,W)
+    N(0,1) draws or None (device counter-based generator keyed by `seed`).  Returns a new tensor."""
+    _need_gpu(tiles, flips, jitter, noise)
+    shape = tiles.shape
+    t = tiles.float().contiguous()
+    B, H, W = shape[0], shape[-2], shape[-1]
+    if t.numel() != B * H * W:
+        raise RuntimeError("augment_tiles: one channel per tile expected")
+    if out is None:
+        out = torch.empty_like(t)
+    f = flips.to(torch.uint8).contiguous() if flips is not None else None
+    j = jitter.float().contiguous() if jitter is not None else None
+    n = noise.float().contiguous() if noise is not None else None
+    ws = torch.empty(L.lib().scd_augment_workspace(B), dtype=torch.uint8, device=t.device)
+    L.call("scd_augment_tiles", ptr(t), ptr(out), B, H, W, ptr(f), ptr(j), ptr(n), float(noise_sv),
+           int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(ws), stream())
+    return out.view(shape)
