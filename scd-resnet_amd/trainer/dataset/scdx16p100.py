@@ -107,7 +107,7 @@ def _pack_locs(bounds_list, trunc):
     locs = np.zeros((B, MAXTAGLEN, 8), np.float32)
     counts = np.zeros(B, np.int32)
     for b, l in enumerate(bounds_list):
-        l = np.asarray(l, np.float32)[:MAXTAGLEN]
+        l = (l.numpy() if torch.is_tensor(l) else np.asarray(l)).astype(np.float32)[:MAXTAGLEN]
         locs[b, :len(l)] = l
         counts[b] = len(l)
     if trunc:
@@ -209,7 +209,7 @@ class SCD(Dataset):
     @staticmethod
     def flipLocs(locs, fx, fy):
         """scdx16p100.py:424-436: mirrored centre, offset and major-axis components."""
-        locs = np.array(locs, np.float32).reshape(-1, 8)
+        locs = (locs.numpy() if torch.is_tensor(locs) else np.asarray(locs)).astype(np.float32).reshape(-1, 8)
         if fx and len(locs):
             locs[:, 0] = HEATMAPSIZE - 1 - locs[:, 0]
             locs[:, 2] = -locs[:, 2]

@@ -36,3 +36,29 @@ e1.record(s)
 e1.synchronize()
 gpu_ms = e0.elapsed_time(e1) / 50
 print("B=%d targets: CPU per-sample renderer %.2f ms (1 thread), GPU %.4f ms" % (B, cpu_ms, gpu_ms))
+
+# tile augmentation (scd_augment_tiles): B=32 512x512 tiles already in HBM, flips + normalize + jitter + device noise
+tiles = torch.randn(B, 1, 512, 512, device="cuda") * 30 + 100
+flips = torch.randint(0, 2, (B, 2), dtype=torch.uint8, device="cuda")
+jit = 1 + 0.05 * torch.randn(B, device="cuda")
+out = torch.empty_like(tiles)
+ops.augment_tiles(tiles, flips, jit, None, 0.05, 1, out=out)
+e0.record(s)
+for k in range(50):
+    ops.augment_tiles(tiles, flips, jit, None, 0.05, k, out=out)
+e1.record(s)
+e1.synchronize()
+aug_ms = e0.elapsed_time(e1) / 50
+nbytes = B * 512 * 512 * 4 * 3   # stats read + apply read + write
+print("B=%d augment 512x512: GPU %.4f ms (%.0f GB/s over %d algorithmic bytes)" % (B, aug_ms, nbytes / aug_ms / 1e6, nbytes))
+x = tiles[0].cpu()
+t0 = time.perf_counter()
+for _ in range(20):
+    t = torch.flip(x, [2])
+    m = torch.mean(t)
+    t = (t - m) / torch.sqrt(torch.mean(torch.square(t - m)))
+    t = t * (1 + 0.05 * torch.randn(1))
+    t = t + torch.randn(1, 512, 512) * 0.05
+cpu_aug_ms = (time.perf_counter() - t0) / 20 * 1e3
+print("per-sample reference augmentation ops on the host (torch CPU, %d threads): %.2f ms per tile, %.1f ms per batch"
+      % (torch.get_num_threads(), cpu_aug_ms, cpu_aug_ms * B))
