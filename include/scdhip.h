@@ -225,6 +225,19 @@ int scd_render_center_targets(const float* locs, const int* counts, int B, int K
 size_t scd_augment_workspace(int B);
 int scd_augment_tiles(const float* in, float* out, int B, int H, int W, const uint8_t* flips, const float* jitter,
                       const float* noise, float noise_sv, unsigned long long seed, void* workspace, void* stream);
+/* ---- whole-slide tiled inference (test.py:19-135) ----
+ * scd_slide_tiles: RGB slide (H,W,C>=3) u8 on the device -> out (clipH*clipV, 1, tile, tile) fp32 clips, x-major,
+ * grey = round(0.1140 c0 + 0.5870 c1 + 0.2989 c2) (float64), torch-'reflect' padding by padLR / padTB, the
+ * reference's opencv column fix-up when fix != 0 (needs a padded width >= 3200), each clip normalised in float64.
+ * workspace: scd_slide_workspace(clipH*clipV) bytes.
+ * scd_slide_detections: decoded (10, T, K) fp32 Wrapper stack (trainer/wrappers/centerOffsetResidual.py:10-23)
+ * -> the detections with score > thr in tile-then-rank order: xy (n,2) int32 slide pixels, ratio (n) float64,
+ * *count = n (device); xy / ratio sized T*K. */
+size_t scd_slide_workspace(int ntiles);
+int scd_slide_tiles(const uint8_t* rgb, int H, int W, int C, int tile, int stride, int clipH, int clipV, int padLR,
+                    int padTB, int fix, float* out, void* workspace, void* stream);
+int scd_slide_detections(const float* decoded, int T, int K, int stride, int padLR, int padTB, int clipV, float thr,
+                         int* xy, double* ratio, int* count, void* stream);
 /* ---- decode (centerNetOffset.py:219-251, utility.py:87-118) ---- */
 size_t scd_decode_workspace(int N, int HW);
 int scd_decode_topk(const float* heat, int N, int H, int W, int K, const float* offset, int od_off,

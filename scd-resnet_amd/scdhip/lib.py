@@ -82,6 +82,9 @@ SIGNATURES = {
     "scd_decode_topk": (I, [P, I, I, I, I, P, I, P, I, P, P, P, P, P, P, P, P]),
     "scd_augment_workspace": (c_size_t, [I]),
     "scd_augment_tiles": (I, [P, P, I, I, I, P, P, P, F, ctypes.c_ulonglong, P, P]),
+    "scd_slide_workspace": (c_size_t, [I]),
+    "scd_slide_tiles": (I, [P, I, I, I, I, I, I, I, I, I, I, P, P, P]),
+    "scd_slide_detections": (I, [P, I, I, I, I, I, I, F, P, P, P, P]),
     "scd_ceval_count": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, P, P]),
     "scd_ceval_emit": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, P, PP, P]),
     "scd_ceval_summary_workspace": (c_size_t, [L]),

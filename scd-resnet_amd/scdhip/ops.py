@@ -779,3 +779,34 @@ def augment_tiles(tiles, flips=None, jitter=None, noise=None, noise_sv=0.0, seed
     L.call("scd_augment_tiles", ptr(t), ptr(out), B, H, W, ptr(f), ptr(j), ptr(n), float(noise_sv),
            int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(ws), stream())
     return out.view(shape)
+
+
+def slide_tiles(rgb, tile, stride, clip_h, clip_v, pad_lr, pad_tb, fix):
+    """test.py:19-87 on the GPU (scd_slide_tiles): RGB slide (H,W,C) uint8 -> (clip_h*clip_v, 1, tile, tile)
+    normalised float32 clips, x-major."""
+    _need_gpu(rgb)
+    rgb = rgb.contiguous()
+    if rgb.dtype != torch.uint8 or rgb.dim() != 3:
+        raise RuntimeError("slide_tiles: (H, W, C) uint8 slide expected")
+    H, W, C = rgb.shape
+    T = clip_h * clip_v
+    out = torch.empty(T, 1, tile, tile, device=rgb.device)
+    ws = torch.empty(L.lib().scd_slide_workspace(T), dtype=torch.uint8, device=rgb.device)
+    L.call("scd_slide_tiles", ptr(rgb), H, W, C, tile, stride, clip_h, clip_v, pad_lr, pad_tb, int(bool(fix)),
+           ptr(out), ptr(ws), stream())
+    return out
+
+
+def slide_detections(decoded, stride, pad_lr, pad_tb, clip_v, threshold=0.3):
+    """test.py:104-135 on the GPU (scd_slide_detections): decoded (10, T, K) Wrapper stack -> (xy (n,2) int32,
+    ratio (n,) float64) in the reference's order; one host read of the count."""
+    _need_gpu(decoded)
+    d = decoded.float().contiguous()
+    _, T, K = d.shape
+    xy = torch.empty(T * K, 2, dtype=torch.int32, device=d.device)
+    ratio = torch.empty(T * K, dtype=torch.float64, device=d.device)
+    count = torch.empty(1, dtype=torch.int32, device=d.device)
+    L.call("scd_slide_detections", ptr(d), T, K, stride, pad_lr, pad_tb, clip_v, float(threshold), ptr(xy),
+           ptr(ratio), ptr(count), stream())
+    n = int(count.item())
+    return xy[:n], ratio[:n]
