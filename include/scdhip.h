@@ -102,6 +102,12 @@ int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0,
 int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp,
                     int row_off, void* stream);
 
+/* Zero-extend the innermost dimension: dst[r][c] = c < C ? src[r][c] : 0 (r < rows, c < Cp).  Lets the gather-GEMM
+ * run layers narrower than its K-stage (the 16/32-channel `*h` / `*q` plugins, trainer/model/centerOffsetRes10q.py):
+ * the input (rows = pixels) and the packed operand (rows = output rows x taps) are padded to the next multiple
+ * of 64 (bf16) / 32 (fp32) channels.  C, Cp multiples of 8 (bf16) / 4 (fp32). */
+int scd_pad_channels(int dtype, const void* src, long rows, int C, int Cp, void* dst, void* stream);
+
 /* Batched weight packing: all operand layouts of one training step in one launch.  descs (device memory)
  * are sorted by start; descriptor d covers elements [start, start + count) of the concatenated index space:
  * mode 0: out[row_off + a][t*B + b] = w[a][b][t], count = A * ldp (k >= T*B zero-filled);

@@ -57,6 +57,7 @@ SIGNATURES = {
     "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, P]),
     "scd_pack_weight": (I, [I, P, P, I, I, I, I, I, I, P]),
     "scd_pack_weights_batched": (I, [I, P, I, L, P]),
+    "scd_pad_channels": (I, [I, P, L, I, I, P, P]),
     "scd_im2col_stem": (I, [I, P, P, I, I, I, I, I, I, I, I, I, I, P]),
     "scd_stem_conv_fwd": (I, [I, P, P, P, P, I, I, I, I, I, P]),
     "scd_stem_conv_wgrad_nsplit": (I, [L]),

@@ -288,9 +288,30 @@ def _dgrad_phases(kh, kw, stride, pad, Hc, Wc):
     return phases
 
 
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def pad_channels(t, C, Cp, rows):
+    """Zero-extend the innermost C channels of `t` (viewed as rows x C) to Cp (scd_pad_channels)."""
+    out = torch.empty(rows, Cp, dtype=t.dtype, device=t.device)
+    L.call("scd_pad_channels", dt(t), ptr(t), rows, C, Cp, ptr(out), stream())
+    return out
+
+
 def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, stats=None, relu=False,
           accumulate=False, bn_bwd=None):
     N, Hi, Wi, Ci = x.shape
+    bk = 64 if x.dtype == torch.bfloat16 else 32
+    if Ci % bk:
+        # narrow layer (16/32 channels): zero-extend the input per pixel and the operand per tap to the K-stage
+        Cp = -(-Ci // bk) * bk
+        T = wpack.shape[1] // Ci
+        if T * Ci != wpack.shape[1]:
+            raise RuntimeError("narrow-layer padding needs an unpadded [rows][taps*Ci] operand")
+        x = pad_channels(_c(x), Ci, Cp, N * Hi * Wi).view(N, Hi, Wi, Cp)
+        wpack = pad_channels(wpack, Ci, Cp, wpack.shape[0] * T).view(wpack.shape[0], T * Cp)
+        Ci = Cp
     arr = (L.GemmPhase * len(phases))(*phases)
     if bn_bwd is not None:
         # bn_bwd = (st, y_pre_bn, stats): the next BN+ReLU layer's backward sums from the GEMM epilogue

@@ -241,3 +241,65 @@ def test_bn_backward_sums_from_dgrad_epilogue_match_separate_reduce():
         a, b = grads[1][k], grads[0][k]
         err = (a - b).abs().max().item() / max(1e-12, b.abs().max().item())
         assert err < 1e-1, (k, err)
+
+
+NARROW = {"centerOffsetRes10q": [16, 16, 32, 64, 128, 64, 64, 64],
+          "centerOffsetRes10h": [32, 32, 64, 128, 256, 128, 128, 128]}
+
+
+@pytest.mark.parametrize("name", sorted(NARROW))
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_f11_narrow_plugins(name, dtype, golden):
+    """16/32-channel layers (zero-extended to the GEMM K-stage by scd_pad_channels) and 64-wide heads against the
+    reference (F11): fp32 heads 1e-3, loss 1e-4, gradient norms 1e-2; bf16 within 5e-2 of the reference's heads
+    and loss (10 layers of bf16 rounding)."""
+    import importlib
+    g = golden("narrow")
+    plugin = importlib.import_module("trainer.model." + name)
+    assert plugin.modelParams["dims"] == NARROW[name]
+    entries, topo = O.model_spec(10, NARROW[name], head_dim=64)
+    m = plugin.model(**plugin.modelParams)
+    m.load_state_dict(O.hash_weights(entries))
+    m = m.to(DEV).train().set_compute_dtype(dtype)
+    out = m(T.batch_inputs(21, 2, 256).to(DEV), decode=False)
+    for k in ("heatmap", "regr", "offset"):
+        a = out[0][k].detach().float().cpu().numpy()
+        ref = g["%s|%s" % (name, k)]
+        if dtype == torch.float32:
+            np.testing.assert_allclose(a, ref, rtol=1e-3, atol=1e-3, err_msg=k)
+        else:
+            assert np.abs(a - ref).max() / np.abs(ref).max() < 5e-2, k
+    loss, stats = plugin.loss(out, [y.to(DEV) for y in T.batch_targets(22, 2, 64)])
+    loss.mean().backward()
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        np.testing.assert_allclose(loss.item(), float(g[name + "|loss"].reshape(-1)[0]), rtol=1e-4)
+        for k, p in m.named_parameters():
+            np.testing.assert_allclose(p.grad.double().norm().item(), float(g["%s|gnorm|%s" % (name, k)]), rtol=1e-2,
+                                       atol=1e-6, err_msg=k)
+    else:
+        np.testing.assert_allclose(loss.item(), float(g[name + "|loss"].reshape(-1)[0]), rtol=5e-2)
+        for k, p in m.named_parameters():
+            assert p.grad is not None and torch.isfinite(p.grad).all(), k
+
+
+ALL_CENTER_PLUGINS = ["centerOffsetRes10", "centerOffsetRes10h", "centerOffsetRes10q", "centerOffsetRes18",
+                      "centerOffsetRes18h", "centerOffsetRes34", "centerOffsetRes34h", "centerOffsetRes50",
+                      "centerOffsetRes50h", "centerOffsetRes101h"]
+
+
+@pytest.mark.parametrize("name", ALL_CENTER_PLUGINS)
+def test_every_reference_plugin_trains_one_step(name):
+    """Every CenterNet model plugin the reference ships (trainer/model/*.py) runs a bf16 training step through
+    the HIP path: finite loss and gradients, every parameter touched."""
+    import importlib
+    plugin = importlib.import_module("trainer.model." + name)
+    torch.manual_seed(0)
+    m = plugin.model(**plugin.modelParams).to(DEV).train().set_compute_dtype(torch.bfloat16)
+    out = m(T.batch_inputs(31, 2, 128).to(DEV), decode=False)
+    loss, _ = plugin.loss(out, [y.to(DEV) for y in T.batch_targets(32, 2, 32)])
+    loss.mean().backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all()
+    for k, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), k

@@ -265,3 +265,24 @@ def test_f10_ap_walk_small_cases():
     # TP, FP, TP over 2 objects: (0.5,1), (0.5,0.5), (1,2/3) -> 1*(2/3) record at the end, then (0.5-0.5)*... + 0.5*1
     plots = [[0.5, 1.0], [0.5, 0.5], [1.0, 2 / 3]]
     assert abs(M.ap_all(plots) - ((1.0 - 0.5) * (2 / 3) + 0.5 * 1.0)) < 1e-15
+
+
+NARROW = {"centerOffsetRes10q": [16, 16, 32, 64, 128, 64, 64, 64],
+          "centerOffsetRes10h": [32, 32, 64, 128, 256, 128, 128, 128]}
+
+
+@pytest.mark.parametrize("name", sorted(NARROW))
+def test_f11_narrow_plugins(golden, name):
+    """Oracle on the 16/32-channel plugins with 64-wide heads (centerNetOffseth.py) vs the reference (F11)."""
+    g = golden("narrow")
+    entries, topo = O.model_spec(10, NARROW[name], head_dim=64)
+    st = O.TrainState(O.hash_weights(entries))
+    outs = O.forward(st.P, st.B, T.batch_inputs(21, 2, 256), topo)
+    for k in ("heatmap", "regr", "offset"):
+        np.testing.assert_allclose(outs[k].detach().numpy(), g["%s|%s" % (name, k)], rtol=1e-4, atol=1e-4, err_msg=k)
+    loss, stats = O.centernet_loss(outs, T.batch_targets(22, 2, 64))
+    loss.mean().backward()
+    np.testing.assert_allclose(loss.detach().numpy(), g[name + "|loss"], rtol=1e-4)
+    for k, v in st.P.items():
+        np.testing.assert_allclose(v.grad.double().norm().item(), g["%s|gnorm|%s" % (name, k)], rtol=2e-3, atol=1e-7,
+                                   err_msg=k)
