@@ -47,6 +47,24 @@ def _to_device(obj, device):
     return obj
 
 
+class GPUBatchLoader:
+    """Training batches from a dataset plugin's gpu_batch(indices, device) -- the batched HIP augmentation and
+    target rendering -- visiting indices exactly as DataLoader(batch_size, sampler, drop_last=True) would."""
+
+    def __init__(self, dataset, sampler, batch_size, device):
+        from torch.utils.data import BatchSampler, SequentialSampler
+        self.dataset, self.device = dataset, device
+        self.batches = BatchSampler(sampler if sampler is not None else SequentialSampler(dataset), batch_size,
+                                    drop_last=True)
+
+    def __len__(self):
+        return len(self.batches)
+
+    def __iter__(self):
+        for idx in self.batches:
+            yield self.dataset.gpu_batch(list(idx), self.device)
+
+
 class NetworkFactory(object):
     GPUCOUNT = 0
 
@@ -100,8 +118,11 @@ class NetworkFactory(object):
         self.device = torch.device("cuda", localRank)
         distributed = self._distributed()
         Logger.info(":: networkFactory.py :: Begin Training Task on Local Device {}".format(localRank))
-        if distributed:
-            sampler = utilsDataDist.DistributedSampler(self.dataset, drop_last=True, shuffle=False)
+        sampler = utilsDataDist.DistributedSampler(self.dataset, drop_last=True, shuffle=False) if distributed else None
+        if hasattr(self.dataset, "gpu_batch"):
+            # whole batches augmented / target-rendered on the GPU (one launch each) in the DataLoader's order
+            trainLoader = GPUBatchLoader(self.dataset, sampler, defaultConfig.batchSize, self.device)
+        elif distributed:
             trainLoader = DataLoader(self.dataset, batch_size=defaultConfig.batchSize, sampler=sampler,
                                      drop_last=True, shuffle=False)
         else:

@@ -238,6 +238,8 @@ class SCD(Dataset):
         reference's __getitem__ stacked over `indices` (positions in the shuffled order)."""
         from scdhip import ops
         dev = device or self.device
+        if 0 in indices:
+            shuffle(self.order)      # the reference reshuffles when index 0 is fetched (scdx16p100.py:302-305)
         ids = [self.order[i] for i in indices]
         B = len(ids)
         flips, jit, seed = self._draws(B)
@@ -251,8 +253,6 @@ class SCD(Dataset):
         return {"xs": [xs], "ys": ys}
 
     def __getitem__(self, index):
-        if index == 0:
-            shuffle(self.order)
         b = self.gpu_batch([index])
         return {"xs": [b["xs"][0][0]], "ys": [y[0] for y in b["ys"]]}
 

@@ -62,3 +62,32 @@ def test_flip_locs_rule():
     np.testing.assert_array_equal(l[0, 0], 10.5)   # stored bounds are not mutated
     locs, counts = D._pack_locs([f, np.zeros((0, 8), np.float32)], trunc=True)
     assert counts.tolist() == [1, 0] and locs[0, 0, 0] == 116 and locs[0, 0, 1] == 106
+
+
+def test_gpu_batch_loader_visits_dataloader_order():
+    """networkFactory.GPUBatchLoader asks gpu_batch for exactly the index batches DataLoader would build."""
+    import torch.utils.data.distributed as dd
+    from torch.utils.data import DataLoader
+
+    from models.networkFactory import GPUBatchLoader
+
+    class Fake:
+        def __init__(self):
+            self.seen = []
+
+        def __len__(self):
+            return 70
+
+        def __getitem__(self, i):
+            return i
+
+        def gpu_batch(self, idx, device):
+            self.seen.append(idx)
+            return idx
+
+    ds = Fake()
+    assert list(GPUBatchLoader(ds, None, 16, "cpu")) == [b.tolist() for b in DataLoader(ds, 16, drop_last=True)]
+    for rank in range(2):
+        s = dd.DistributedSampler(ds, num_replicas=2, rank=rank, drop_last=True, shuffle=False)
+        want = [b.tolist() for b in DataLoader(ds, 8, sampler=s, drop_last=True)]
+        assert list(GPUBatchLoader(ds, s, 8, "cpu")) == want

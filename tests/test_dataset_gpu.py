@@ -131,3 +131,31 @@ def test_augment_device_noise_statistics():
     assert not torch.equal(noisy, ops.augment_tiles(x, noise_sv=0.05, seed=124))
     with pytest.raises(RuntimeError):
         ops.augment_tiles(torch.zeros(1, 1, 8, 6, device=DEV))   # W % 4 != 0
+
+
+def test_train_loop_on_d_archive(tmp_path):
+    """NetworkFactory end to end on a `.d` archive: split profile from disk, batches through gpu_batch
+    (GPUBatchLoader), two bf16 steps, validation through evaluation / expression, evals file written."""
+    from configuration import defaultConfig
+    from models.networkFactory import NetworkFactory
+    names, samples, locs = scd_archive.archive_content(seed=5, count=48, size=512)
+    from trainer.dataset.scdx16p100 import writeArchive
+    path = str(tmp_path / "tiny.d")
+    writeArchive(path, names, samples, locs)
+    split = tmp_path / "tiny.split.json"
+    split.write_text(json.dumps({"validation": list(range(8))}))
+    old = dict(defaultConfig.config)
+    try:
+        defaultConfig.updateConfig({"modelName": "centerOffsetRes10", "datasetName": "tiny", "trainName": "dtest",
+                                    "iterations": 2, "validation": 2, "snapshot": 1000, "batchSize": 16,
+                                    "dirData": "trainer.dataset.scdx16p100", "dirDatafile": path,
+                                    "dirDataSplitProfile": str(split), "dirTemp": str(tmp_path / "t") + "/",
+                                    "dirResult": str(tmp_path / "r") + "/", "currentIter": 0})
+        f = NetworkFactory(True)
+        assert len(f.dataset) == 40
+        f.beginTraining(0)
+        text = open(str(tmp_path / "r" / "evals.dtest.txt")).read()
+    finally:
+        defaultConfig.config.clear()
+        defaultConfig.config.update(old)
+    assert "[mIoU]" in text and "[AP50]" in text and "[Tr]" in text
