@@ -367,3 +367,44 @@ def test_dgrad_with_bn_backward_sums(shape):
     b = s2.view(64, 2, Ci).sum(0).cpu()
     for i in range(2):
         assert (a[i] - b[i]).abs().max().item() <= 1e-5 * b[i].abs().max().item() + 1e-9, i
+
+
+# 64 -> 64 channel 3x3 stride-1 convs (layer1 shapes): the default 256x64 kernel, and with SCD_GEMM_H64=1 in the
+# environment the opt-in persistent halo kernel (widths 16..128 with 256 % W == 0, 1 to 8 tiles per workgroup;
+# (5, 64, 24, 16) has H % (256 / W) != 0 and always takes the default kernel)
+H64_CASES = [
+    (4, 64, 128, 128, 64, 3, 1, 1),
+    (8, 64, 128, 128, 64, 3, 1, 1),
+    (3, 64, 64, 64, 64, 3, 1, 1),
+    (2, 64, 32, 128, 64, 3, 1, 1),
+    (40, 64, 16, 16, 64, 3, 1, 1),
+    (5, 64, 24, 16, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", H64_CASES)
+def test_conv_h64_bf16(case):
+    test_conv_fwd_dgrad_wgrad(case, torch.bfloat16)
+
+
+def test_conv_h64_accumulate_and_bias_relu():
+    """Epilogue paths the block code uses on the halo kernel: dgrad += into an existing gradient, and a
+    forward with bias + ReLU."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(7)
+    N, C, H, W = 4, 64, 128, 128
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(C, C, 3, 3, generator=g) / 24).bfloat16().float()
+    b = torch.randn(C, generator=g)
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    y = ops.conv_fwd(nhwc(x, torch.bfloat16), ops.pack_weight(w.to(DEV), torch.bfloat16, 0), C, 3, 3, 1, 1,
+                     bias=b.to(DEV), relu=True)
+    assert rel_err(nchw(y), ref) < 3e-2
+    dy = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+    base = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+    dx = nhwc(base, torch.bfloat16)
+    ops.conv_dgrad(nhwc(dy, torch.bfloat16), ops.pack_weight(w.to(DEV), torch.bfloat16, 1), C, H, W, 3, 3, 1, 1,
+                   out=dx, accumulate=True)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, padding=1).backward(dy)
+    assert rel_err(nchw(dx), base + xr.grad) < 3e-2
