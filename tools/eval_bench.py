@@ -44,3 +44,27 @@ for N in (32, 256):
     sm_ms = (time.perf_counter() - t0) / reps * 1e3
     print("N=%d K=100 L=30: evaluation %.3f ms (incl. counts read), expression summary %.3f ms over %d pairs kept"
           % (N, ev_ms, sm_ms, s[0].numel()))
+
+# whole-slide tiling (scd_slide_tiles) for a 3092 x 2056 RGB slide (48 clips of 512^2) and detections
+sys.path.insert(0, os.path.join(REPO, "scd-resnet_amd"))
+import slide  # noqa: E402
+
+rs = np.random.RandomState(1)
+rgb = torch.from_numpy(rs.randint(0, 256, (2056, 3092, 3)).astype(np.uint8)).cuda()
+clips, g = slide.tiles(rgb)
+torch.cuda.synchronize()
+s = torch.cuda.current_stream()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(s)
+for _ in range(20):
+    ops.slide_tiles(rgb, 512, 384, g["clipH"], g["clipV"], g["padLR"], g["padTB"], True)
+e1.record(s)
+e1.synchronize()
+ms = e0.elapsed_time(e1) / 20
+print("slide tiles 3092x2056 -> %d clips: %.3f ms (%.0f GB/s of clip writes)" % (clips.shape[0], ms,
+                                                                             clips.numel() * 4 / ms / 1e6))
+dec = torch.rand(10, clips.shape[0], 100, device="cuda")
+t0 = time.perf_counter()
+for _ in range(20):
+    ops.slide_detections(dec, 384, g["padLR"], g["padTB"], g["clipV"], 0.3)
+print("slide detections (48 x 100, incl. count read): %.3f ms" % ((time.perf_counter() - t0) / 20 * 1e3))
