@@ -30,3 +30,42 @@ def decoded(T, K=100, seed=12):
     rows = [rs.uniform(0, 1, (T, K)), ys * 128 + xs, ys, xs, rs.uniform(-6, 6, (T, K)), rs.uniform(-6, 6, (T, K)),
             minl, minl + rs.uniform(0, 4, (T, K)), rs.uniform(0, 4, (T, K)), rs.uniform(0, 4, (T, K))]
     return np.stack(rows).astype(np.float32)
+
+
+def geometry(H, W, tile=512, pad=64):
+    """test.py:41-54."""
+    step = tile - 2 * pad
+    ch, cv = -(-(W - 2 * pad) // step), -(-(H - 2 * pad) // step)
+    rw, rh = step * ch + 2 * pad, step * cv + 2 * pad
+    rw += (rw - W) % 2
+    rh += (rh - H) % 2
+    return dict(clipH=ch, clipV=cv, resizeW=rw, resizeH=rh, padLR=(rw - W) // 2, padTB=(rh - H) // 2)
+
+
+def clip(img, g, i, j, tile=512, step=384):
+    """Clip (i, j) of test.py:19-87 restated in numpy float64: greyscale, reflect padding, the opencv column
+    fix-up, per-clip normalisation, float32."""
+    grey = np.round(0.1140 * img[:, :, 0] + 0.5870 * img[:, :, 1] + 0.2989 * img[:, :, 2])
+    pad = np.pad(grey, ((g["padTB"], g["padTB"]), (g["padLR"], g["padLR"])), mode="reflect")
+    for x in range(0, 64):
+        pad[:, x] = pad[:, 127 - x]
+    for x in range(3136, 3200):
+        pad[:, x] = pad[:, 6271 - x]
+    t = pad[j * step:j * step + tile, i * step:i * step + tile]
+    m = t.mean()
+    return ((t - m) / np.sqrt(((t - m) ** 2).mean())).astype(np.float32)
+
+
+def detections(dec, g, step=384, thr=0.3):
+    """test.py:104-135 restated: [x, y, ratio] for every slot with score > thr, tile-major."""
+    out = []
+    T = dec.shape[1]
+    for t in range(T):
+        i, j = t // g["clipV"], t % g["clipV"]
+        for k in range(dec.shape[2]):
+            if dec[0, t, k] > np.float32(thr):
+                minl, halo = float(dec[6, t, k]) * 4, float(dec[7, t, k]) * 4
+                out.append([int(i * step - g["padLR"] + float(dec[3, t, k]) * 4 + float(dec[8, t, k])),
+                            int(j * step - g["padTB"] + float(dec[2, t, k]) * 4 + float(dec[9, t, k])),
+                            (halo - minl) / (2 * minl)])
+    return np.array(out, np.float64).reshape(-1, 3)

@@ -91,3 +91,20 @@ def test_gpu_batch_loader_visits_dataloader_order():
         s = dd.DistributedSampler(ds, num_replicas=2, rank=rank, drop_last=True, shuffle=False)
         want = [b.tolist() for b in DataLoader(ds, 8, sampler=s, drop_last=True)]
         assert list(GPUBatchLoader(ds, s, 8, "cpu")) == want
+
+
+def test_slide_restatement_matches_reference(golden):
+    """oracle.slide_case (test.py restated) against the reference's own clips and detections (slide.npz)."""
+    from oracle import slide_case as S
+    g = golden("slide")
+    img = S.slide()
+    geo = S.geometry(*img.shape[:2])
+    assert (geo["clipH"], geo["clipV"], geo["padLR"], geo["padTB"]) == (8, 6, 54, 188)
+    c0 = S.clip(img, geo, 0, 0)
+    np.testing.assert_allclose(c0[:64, :64], g["win_first"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(c0[::8, ::8], g["clip_sub"][0], rtol=0, atol=1e-6)
+    last = S.clip(img, geo, geo["clipH"] - 1, geo["clipV"] - 1)
+    np.testing.assert_allclose(last[448:, 448:], g["win_last"], rtol=0, atol=1e-6)
+    det = S.detections(g["decoded"], geo)
+    np.testing.assert_array_equal(det[:, :2], g["detections"][:, :2])
+    np.testing.assert_allclose(det[:, 2], g["detections"][:, 2], rtol=1e-12)
