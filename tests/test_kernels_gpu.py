@@ -408,3 +408,25 @@ def test_conv_h64_accumulate_and_bias_relu():
     xr = x.clone().requires_grad_(True)
     F.conv2d(xr, w, padding=1).backward(dy)
     assert rel_err(nchw(dx), base + xr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("dtype,C,Cp", [(torch.bfloat16, 32, 64), (torch.bfloat16, 16, 64), (torch.float32, 16, 32),
+                                        (torch.bfloat16, 64, 128)])
+def test_pad_channels(dtype, C, Cp):
+    """scd_pad_channels: zero-extension of the innermost dimension (narrow-layer GEMM operands)."""
+    from scdhip import ops
+    x = torch.randn(37, 5, C, device=DEV).to(dtype)
+    y = ops.pad_channels(x, C, Cp, 37 * 5)
+    ref = F.pad(x.float(), (0, Cp - C)).reshape(-1, Cp)
+    assert torch.equal(y.float(), ref)
+
+
+@pytest.mark.parametrize("B,H,W", [(1, 1, 4), (2, 3, 12)])
+def test_augment_tiny_tiles(B, H, W):
+    from scdhip import ops
+    x = torch.randn(B, 1, H, W)
+    got = ops.augment_tiles(x.to(DEV)).cpu()
+    for b in range(B):
+        t = x[b].double()
+        ref = ((t - t.mean()) / ((t - t.mean()) ** 2).mean().sqrt()).float()
+        np.testing.assert_allclose(got[b].numpy(), ref.numpy(), rtol=0, atol=2e-5)

@@ -94,7 +94,7 @@ def test_plugin_evaluation_and_expression(golden):
         assert abs(a - b) <= 2e-6 * max(1.0, abs(b)) + 1e-6 + slack, (tag, a, b)
 
 
-@pytest.mark.parametrize("seed,K,L", [(5, 100, 30), (6, 256, 64), (7, 1, 1)])
+@pytest.mark.parametrize("seed,K,L", [(5, 100, 30), (6, 256, 64), (7, 1, 1), (8, 37, 5)])
 def test_eval_streams_vs_oracle_shapes(seed, K, L):
     c = M.eval_case(seed, N=9, K=K, L=L, n_near=min(K, 40))
     s = _gpu_streams(c, "inds")
