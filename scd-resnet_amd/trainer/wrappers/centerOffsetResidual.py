@@ -1,17 +1,23 @@
-"""Inference wrapper (trainer/wrappers/centerOffsetResidual.py:4-23 of the reference): the decoded detections
-as one (10, B, K) tensor, rows [scores, inds, ys, xs, majx, majy, minl, halo, offx, offy] (torch.stack promotes
-the integer rows to float32).  The decode itself is scd_decode_topk (models/centerNetOffset.decodeCenterNet)."""
+"""Inference wrapper (trainer/wrappers/centerOffsetResidual.py:4-23 of the reference).
+
+Output: one (10, B, K) float32 tensor, rows in the order slide.py / test.py unpack them --
+scores, inds, ys, xs, major-axis x, major-axis y, minor length, halo radius, offset x, offset y (the integer rows
+are promoted to float32, as the reference's torch.stack does).  The decode underneath is scd_decode_topk
+(models/centerNetOffset.decodeCenterNet)."""
 import torch
-import torch.nn
+
+# (position in the decode list, column of that tensor or None for a (B, K) row)
+_ROWS = ((0, None), (1, None), (2, None), (3, None), (5, 0), (5, 1), (5, 2), (5, 3), (4, 0), (4, 1))
 
 
 class Wrapper(torch.nn.Module):
+    """model(inp, decode=True) -> stacked detections; `model` is any CenterNet plugin model."""
 
     def __init__(self, model):
-        super(Wrapper, self).__init__()
+        super().__init__()
         self.model = model
 
     def forward(self, inp):
-        scores, inds, ys, xs, offset, regression, _ = self.model(inp, decode=True)
-        rows = [scores, inds, ys, xs] + [regression[:, :, i] for i in range(4)] + [offset[:, :, 0], offset[:, :, 1]]
-        return torch.stack([r.float() for r in rows])
+        dec = self.model(inp, decode=True)       # [scores, inds, ys, xs, offset, regr, outputDict]
+        picked = [dec[i] if col is None else dec[i][..., col] for i, col in _ROWS]
+        return torch.stack([t.to(torch.float32) for t in picked], 0)
