@@ -154,11 +154,26 @@ __global__ __launch_bounds__(CE_THREADS) void ceval_pairs_kernel(CEvalIn p, int*
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int k = tid; k < p.K; k += CE_THREADS) build_det(p, n, k, sd[k]);
     for (int l = tid; l < p.L; l += CE_THREADS) build_gt(p, n, l, sg[l]);
-    if (tid < CE_NMASK) {
-        int b = 0;
-        if (EMIT)
-            for (int j = 0; j < n; ++j) b += counts[j * CE_NMASK + tid];
-        base[tid] = b;
+    if (EMIT) {
+        // this image's output offsets: the earlier images' counts, summed by the whole workgroup
+        int part[CE_NMASK] = {0, 0, 0, 0, 0};
+        for (int j = tid; j < n; j += CE_THREADS)
+#pragma unroll
+            for (int m = 0; m < CE_NMASK; ++m) part[m] += counts[j * CE_NMASK + m];
+#pragma unroll
+        for (int m = 0; m < CE_NMASK; ++m) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) part[m] += __shfl_xor(part[m], o, 64);
+            if (lane == 0) wtot[wv][m] = part[m];
+        }
+        __syncthreads();
+        if (tid < CE_NMASK) {
+            int b = 0;
+            for (int w = 0; w < CE_THREADS / 64; ++w) b += wtot[w][tid];
+            base[tid] = b;
+        }
+    } else if (tid < CE_NMASK) {
+        base[tid] = 0;
     }
     __syncthreads();
     const int npairs = p.K * p.L;

@@ -4,7 +4,8 @@ tests/golden/make_golden_eval.py from the real reference) and the CPU restatemen
 
 Tolerances.  The streams are float32 values from one rounding per op on both sides; the only op whose result
 can differ is sqrt: the device's is correctly rounded, the reference's torch CPU kernel is not always (see
-oracle/metrics.py), so values agree to a few ulp (rtol 2e-6); orthogonity = sqrt(1 - cos^2) is compared through its square (one ulp
+oracle/metrics.py), so values agree to a few ulp: rtol 2e-5 (one ulp of a box coordinate near 128 px, 7.6e-6, over an
+intersection side of ~1 px); orthogonity = sqrt(1 - cos^2) is compared through its square (one ulp
 of cos near 1 moves it by up to 5e-4) and may be NaN on one side where it is ~0; stream lengths (the masks) are exact on these cases.  The AP walk is checked
 exactly (1e-12) against the oracle on the device's own streams, and against the reference's APs.  Means are
 fp64 on the device, fp32 torch.mean in the reference: rtol 1e-5."""
@@ -42,7 +43,7 @@ def _cmp_streams(got, want):
             assert np.all(np.nan_to_num(g[~both], nan=0.0) ** 2 < 1e-6)
             assert np.all(np.nan_to_num(w[~both], nan=0.0) ** 2 < 1e-6)
         else:
-            np.testing.assert_allclose(g, w, rtol=2e-6, atol=1e-6, err_msg=name)
+            np.testing.assert_allclose(g, w, rtol=2e-5, atol=2e-6, err_msg=name)
 
 
 @pytest.mark.parametrize("case,loc_key", [("inds", "inds"), ("locs", "locs"), ("empty", "inds")])
@@ -130,3 +131,10 @@ def test_eval_rejects_oversized_shapes():
         ops.center_eval(torch.zeros(1, 4), torch.zeros(1, 4, dtype=torch.long), torch.zeros(1, 4, dtype=torch.long),
                         torch.zeros(1, 4, 2), torch.zeros(1, 4, 4), torch.zeros(1, 3, 6),
                         torch.zeros(1, 3, dtype=torch.long))  # CPU tensors: no fallback
+
+
+def test_eval_streams_many_images():
+    """600 images: output offsets from the workgroup-wide sum of the earlier images' counts."""
+    c = M.eval_case(31, N=600, K=100, L=30, n_near=20)
+    s = _gpu_streams(c, "inds")
+    _cmp_streams(s, M.center_eval(c["scores"], c["ctY"], c["ctX"], c["offset"], c["regr"], c["ys2"], c["inds"]))
