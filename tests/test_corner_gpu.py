@@ -177,3 +177,22 @@ def test_decode_cornernet_three_maps():
         ref = O.decode({"heatmap": od[k].cpu(), "regr": torch.zeros(2, 4, 128, 128),
                         "offset": torch.zeros(2, 2, 128, 128)})
         np.testing.assert_allclose(dec[4 * i].cpu().numpy(), ref[0].numpy(), rtol=1e-6, atol=1e-7)
+
+
+def test_integration_md_binding_stub_runs():
+    """The ctypes stub INTEGRATION.md shows a maintainer (the reference's pybind11 TopPool replaced) runs as
+    written and matches the library's own binding."""
+    import os
+    import re
+
+    from scdhip import ops
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(repo, "INTEGRATION.md")).read()
+    code = re.search(r"```python\n(.*?)```", text, re.S).group(1)
+    code = code.replace('"scd-resnet_amd/scdhip/libscdhip.so"', repr(os.path.join(repo, "scd-resnet_amd", "scdhip",
+                                                                                  "libscdhip.so")))
+    ns = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    x = torch.randn(2, 9, 7, 16, device="cuda")
+    y = ns["TopPoolFunction"].apply(x)
+    torch.testing.assert_close(y, ops.cpool_fwd(x, 0), rtol=0, atol=0)
