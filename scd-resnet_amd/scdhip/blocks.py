@@ -39,6 +39,19 @@ def _train_bn_conv(x, conv, bn, stride, pad, training):
     return y, st
 
 
+def _dgrad_bn_relu_bwd(dy, wpack_t, C, Hc, Wc, kh, kw, stride, pad, bn, st, y):
+    """Input gradient of a conv whose input is a BN+ReLU layer's output (bn, st, pre-BN y), then that layer's
+    backward.  In bf16 the dgrad GEMM's epilogue accumulates the BN backward sums (scd_conv_gemm_bnbwd; shapes
+    outside the ping-pong kernel run GEMM + reduce inside the same entry point), so the BN backward is only the
+    finalize + apply."""
+    if dy.dtype == torch.bfloat16 and ops.BNFusion.enabled:
+        stats = ops.bn_stats(bn, "bwdf")
+        da = ops.conv_dgrad(dy, wpack_t, C, Hc, Wc, kh, kw, stride, pad, bn_bwd=(st, y, stats))
+        return ops.bn_backward(bn, st, da, y, relu=True, stats=stats)
+    da = ops.conv_dgrad(dy, wpack_t, C, Hc, Wc, kh, kw, stride, pad)
+    return ops.bn_backward(bn, st, da, y, relu=True)
+
+
 class StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, conv, bn, dtype):
@@ -118,8 +131,8 @@ class BasicBlockFn(torch.autograd.Function):
             dy2 = ops.bn_backward(blk.bn2, st2, dout, y2, mask=out, dz_out=dx)
         w2 = blk.conv2.weight
         ops.conv_wgrad(dy2, a1, 3, 3, 1, 1, ops.grad_of(w2), _conv_ld(w2))
-        da1 = ops.conv_dgrad(dy2, ops.pack_weight(w2, x.dtype, 1), C, a1.shape[1], a1.shape[2], 3, 3, 1, 1)
-        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, relu=True)
+        dy1 = _dgrad_bn_relu_bwd(dy2, ops.pack_weight(w2, x.dtype, 1), C, a1.shape[1], a1.shape[2], 3, 3, 1, 1,
+                                 blk.bn1, st1, y1)
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 3, 3, s, 1, ops.grad_of(w1), _conv_ld(w1))
         ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 3, 3, s, 1, out=dx, accumulate=True)
@@ -167,12 +180,12 @@ class BottleneckFn(torch.autograd.Function):
             dy3 = ops.bn_backward(blk.bn3, st3, dout, y3, mask=out, dz_out=dx)
         w3 = blk.conv3.weight
         ops.conv_wgrad(dy3, a2, 1, 1, 1, 0, ops.grad_of(w3), _conv_ld(w3))
-        da2 = ops.conv_dgrad(dy3, ops.pack_weight(w3, x.dtype, 1), P, a2.shape[1], a2.shape[2], 1, 1, 1, 0)
-        dy2 = ops.bn_backward(blk.bn2, st2, da2, y2, relu=True)
+        dy2 = _dgrad_bn_relu_bwd(dy3, ops.pack_weight(w3, x.dtype, 1), P, a2.shape[1], a2.shape[2], 1, 1, 1, 0,
+                                 blk.bn2, st2, y2)
         w2 = blk.conv2.weight
         ops.conv_wgrad(dy2, a1, 3, 3, s, 1, ops.grad_of(w2), _conv_ld(w2))
-        da1 = ops.conv_dgrad(dy2, ops.pack_weight(w2, x.dtype, 1), P, a1.shape[1], a1.shape[2], 3, 3, s, 1)
-        dy1 = ops.bn_backward(blk.bn1, st1, da1, y1, relu=True)
+        dy1 = _dgrad_bn_relu_bwd(dy2, ops.pack_weight(w2, x.dtype, 1), P, a1.shape[1], a1.shape[2], 3, 3, s, 1,
+                                 blk.bn1, st1, y1)
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 1, 1, 1, 0, ops.grad_of(w1), _conv_ld(w1))
         ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 1, 1, 1, 0, out=dx, accumulate=True)

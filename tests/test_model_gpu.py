@@ -303,3 +303,31 @@ def test_every_reference_plugin_trains_one_step(name):
     assert torch.isfinite(loss).all()
     for k, p in m.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
+
+
+@pytest.mark.parametrize("name", ["centerOffsetRes10", "centerOffsetRes50"])
+def test_block_bn_backward_sums_from_dgrad_match_separate_reduce(name):
+    """BasicBlock / Bottleneck BN+ReLU layers take their backward sums from the producing dgrad GEMM
+    (scd_conv_gemm_bnbwd); against the separate-reduce path (BNFusion off): same loss, gradients within the
+    kernel-level tolerance (sums from fp32 accumulators vs the stored bf16 gradient)."""
+    from scdhip import ops
+    import importlib
+    plugin = importlib.import_module("trainer.model." + name)
+    x = T.batch_inputs(41, 2, 256).to(DEV)
+    ys = [y.to(DEV) for y in T.batch_targets(42, 2, 64)]
+    grads = []
+    for fuse in (True, False):
+        torch.manual_seed(0)
+        m = plugin.model(**plugin.modelParams).to(DEV).train().set_compute_dtype(torch.bfloat16)
+        old = ops.BNFusion.enabled
+        ops.BNFusion.enabled = fuse
+        try:
+            loss, _ = plugin.loss(m(x, decode=False), ys)
+            loss.mean().backward()
+        finally:
+            ops.BNFusion.enabled = old
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters()})
+    for k in grads[0]:
+        a, b = grads[0][k], grads[1][k]
+        assert (a - b).abs().max().item() <= 2e-2 * max(1e-6, b.abs().max().item()), k
