@@ -1,6 +1,9 @@
 """bench.py -- 512x512 images/s training centerOffsetRes10 (bf16) on N MI355X, one process per GPU.
 
-python bench.py --gpus N --steps K --warmup W            (N>1: launched by torch.distributed.run)
+python bench.py --gpus N --steps K --warmup W
+
+N>1: started under torch.distributed.run (WORLD_SIZE set; it must equal N), or by itself -- without
+WORLD_SIZE the script launches N rank processes of itself (one per GPU) before touching the GPU.
 
 A step = NetworkFactory.train on one synthetic batch of 32 tiles per GPU (zero_grad, forward,
 CenterNetLoss, backward incl. the RCCL gradient all-reduce + SyncBN statistics, Adam) with the
@@ -134,11 +137,71 @@ def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2)):
             "launches_timed": n}
 
 
+def launch_ranks(n):
+    """`--gpus N` without a torch.distributed launcher: start N child processes of this script, one per
+    GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as torch.distributed.run would --
+    the reference's own launch model, README.md:91 / train.py:67-72), before this process touches the
+    GPU.  Rank 0's JSON line is passed through; a failing rank fails the run and stops the others."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print("bench: rank process %d exited with %d; stopping the others" % (p.pid, code),
+                          file=sys.stderr, flush=True)
+                    for q in procs:
+                        os.killpg(q.pid, signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit("bench: --gpus %d but WORLD_SIZE=%d (the launcher must start one rank per GPU)"
+                 % (args.gpus, world))
+    if os.environ.get("SCD_BENCH_PROBE") == "1":
+        # launcher rehearsal without a GPU (tests/test_host_cpu.py): rendezvous over gloo, report the world
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            world_seen = int(t.item())
+            dist.destroy_process_group()
+        else:
+            world_seen = 1
+        if rank == 0:
+            print(json.dumps({"metric": "probe", "n_gpus": world, "world_seen": world_seen}), flush=True)
+        return
     # rehearsal knob for a one-GPU box: SCD_BENCH_SHARE_GPU=1 puts every rank on cuda:0 over gloo (RCCL needs
     # one GPU per rank); the driver's multi-GPU runs use the default, one GPU per rank over RCCL
     share = os.environ.get("SCD_BENCH_SHARE_GPU", "0") == "1"

@@ -65,6 +65,18 @@ class GPUBatchLoader:
             yield self.dataset.gpu_batch(list(idx), self.device)
 
 
+def resumeSchedule(learningRate, decay, rates, current):
+    """Learning rate on resuming at iteration `current` (networkFactory.py:140-145 rebuilds it but keeps the
+    past milestones, so the loop's `it == learningRateDecay[0]` test never matches again and every later
+    decay is skipped; a milestone equal to `current` -- applied right after that snapshot was written -- is
+    missed too).  Here every milestone <= current is applied and popped from both lists, in place."""
+    while decay and decay[0] <= current:
+        learningRate /= rates[0]
+        decay.pop(0)
+        rates.pop(0)
+    return learningRate
+
+
 class NetworkFactory(object):
     GPUCOUNT = 0
 
@@ -137,10 +149,8 @@ class NetworkFactory(object):
             ops.set_bn_sync(dist.group.WORLD)       # SyncBatchNorm semantics (networkFactory.py:128-133)
         self.model = FlatDDP(self.model)
         if defaultConfig.currentIteration > 0:
-            for t in range(1, defaultConfig.currentIteration):
-                if t in defaultConfig.learningRateDecay:
-                    idx = defaultConfig.learningRateDecay.index(t)
-                    learningRate /= defaultConfig.learningRateDecayRate[idx]
+            learningRate = resumeSchedule(learningRate, defaultConfig.learningRateDecay,
+                                          defaultConfig.learningRateDecayRate, defaultConfig.currentIteration)
             self.loadParameters()
             self.setLearningRate(learningRate)
 

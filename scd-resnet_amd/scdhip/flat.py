@@ -150,10 +150,12 @@ class FlatDDP(torch.nn.Module):
     world (bucketed RCCL all-reduce of the flat gradient buffer, overlapped with backward).
 
     Gradient readiness: the model's blocks write parameter gradients straight into the flat buffer
-    (no AccumulateGrad hooks fire), so readiness is observed one level up -- every submodule that
-    holds parameters gets a forward pre-hook that hooks its first grad-requiring input; the gradient
-    w.r.t. a module's input is complete only after that module's backward has run, so the hook marks
-    all of the module's parameters ready.  Buckets are contiguous flat ranges of the parameters in
+    (no AccumulateGrad hooks fire), and the leaf Conv2d/BatchNorm2d modules that hold the parameters
+    never run their own forward (the block, deconv and head containers hand the weights to autograd
+    Functions), so readiness is observed at whichever module's forward does run -- every module that
+    holds parameters, directly or below it, gets a forward pre-hook that hooks its first grad-requiring
+    input; the gradient w.r.t. a module's input is complete only after that module's backward has run,
+    so the hook marks all of the module's (recursive) parameters ready.  Buckets are contiguous flat ranges of the parameters in
     reverse registration order (the order backward produces them, as torch DDP buckets them); a bucket
     whose parameters are all ready is all-reduced asynchronously (RCCL queues it behind the kernels
     already on the compute stream).  Parameters whose module input needs no gradient (the stem) are
@@ -175,11 +177,12 @@ class FlatDDP(torch.nn.Module):
         self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
         self._engine = set()                  # ids of parameters written by torch's AccumulateGrad
         self._learned = False                 # one backward seen: early launches allowed
+        self.early_launches = 0               # buckets launched from inside backward, last backward
         self._build_buckets()
         self._hooks = []
         if self.world > 1:
             for m in module.modules():
-                if any(True for _ in m.parameters(recurse=False)):
+                if any(p.requires_grad for p in m.parameters()):
                     self._hooks.append(m.register_forward_pre_hook(self._pre_hook))
             for p in self.flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._acc_hook))
@@ -213,6 +216,7 @@ class FlatDDP(torch.nn.Module):
         self._reset_step()
 
     def _reset_step(self):
+        self._early = 0
         self._ready = set()
         self._pending = [len(ms) for ms in self._bucket_params]
         self._works = [None] * len(self._buckets)
@@ -235,6 +239,8 @@ class FlatDDP(torch.nn.Module):
                 else:
                     self._works[b] = dist.all_reduce(bucket, group=self.group, async_op=True)
             self._next += 1
+            if not final:
+                self._early += 1
 
     def _mark(self, pid):
         b = self._bucket_of.get(pid)
@@ -287,6 +293,7 @@ class FlatDDP(torch.nn.Module):
             from . import ops
             ops.join_side_streams()
         self._launch_ready(final=True)
+        self.early_launches = self._early
         for b, w in enumerate(self._works):
             w.wait()                                # NCCL: the compute stream waits; gloo: blocks
             if not self._use_avg:

@@ -17,6 +17,73 @@ class Toy(torch.nn.Module):
         return {"y": self.bn(self.fc(x)), "aux": [self.fc.weight.sum()]}
 
 
+class _LinearInto(torch.autograd.Function):
+    """Like the model's block Functions: the weight gradient is written straight into weight.grad (the flat
+    buffer view) and no gradient is returned for the weight, so no AccumulateGrad hook fires."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.b = b
+        return x @ w.detach().t() + b.detach()
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        ctx.b.grad.add_(g.sum(0))
+        w.grad.add_(g.t() @ x)
+        return g @ w.detach(), None, None
+
+
+class Block(torch.nn.Module):
+    """A container whose forward runs while its leaf Linear's forward never does (the residual blocks)."""
+
+    def __init__(self, n):
+        super().__init__()
+        self.fc = torch.nn.Linear(n, n)
+
+    def forward(self, x):
+        return torch.relu(_LinearInto.apply(x, self.fc.weight, self.fc.bias))
+
+
+class Deep(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.stem = torch.nn.Linear(8, 8)
+        self.body = torch.nn.Sequential(Block(8), Block(8), Block(8))
+
+    def forward(self, x):
+        return self.body(self.stem(x))
+
+
+def check_early_buckets(rank, world):
+    """Buckets are all-reduced from inside backward once the hook kinds are learned, also when the
+    parameter-holding leaves never run forward (the hooks must sit on modules that run)."""
+    torch.manual_seed(5 + rank)
+    m = Deep()
+    ddp = FlatDDP(m, bucket_mb=1e-5)
+    ref = Deep()
+    ref.load_state_dict({k[len("module."):]: v.clone() for k, v in ddp.state_dict().items()})
+    g = torch.Generator().manual_seed(11)
+    xfull = torch.randn(8, 8, generator=g)
+    grads = []
+    for r in range(world):
+        ref.zero_grad(set_to_none=False)
+        for p in ref.parameters():
+            p.grad = torch.zeros_like(p)
+        ref(xfull[4 * r:4 * r + 4]).square().mean().backward()
+        grads.append({k: p.grad.clone() for k, p in ref.named_parameters()})
+    for it in range(3):
+        ddp.flat.grad.zero_()
+        ddp(xfull[4 * rank:4 * rank + 4]).square().mean().backward()
+        for k, p in m.named_parameters():
+            exp = sum(gr[k] for gr in grads) / world
+            assert torch.allclose(p.grad, exp, atol=1e-6), (it, k)
+        if it > 0:
+            # 6 body buckets (3 blocks x weight/bias) become ready inside backward; the stem's only at the end
+            assert ddp.early_launches >= 6, ddp.early_launches
+
+
 def check(rank, world, bucket_mb):
     torch.manual_seed(100 + rank)                      # different init per rank: the wrap must broadcast
     m = Toy()
@@ -65,6 +132,7 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     for bucket_mb in (25.0, 1e-5):                     # one bucket / one bucket per parameter
         check(rank, world, bucket_mb)
+    check_early_buckets(rank, world)
     dist.barrier()
     dist.destroy_process_group()
     print("OK rank", rank)

@@ -47,6 +47,8 @@ def main():
     torch.cuda.synchronize()
     for k, p in m.named_parameters():
         np.testing.assert_allclose(p.grad.double().norm().item(), first[k], rtol=1e-5, atol=1e-9, err_msg=k)
+    # the head/deconv bucket is all-reduced from inside the backward pass, not from the end-of-backward callback
+    assert ddp.early_launches >= 1, (ddp.early_launches, len(ddp._buckets))
     for k in g.files:
         if k.startswith("rs|"):
             np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)

@@ -179,3 +179,45 @@ def test_flat_ddp_gloo_world2():
         outs.append(out.decode())
         assert p.returncode == 0, out.decode()
     assert all("OK" in o for o in outs), outs
+
+
+def test_bench_launches_n_ranks_itself():
+    """`python bench.py --gpus 2` without a torch.distributed launcher starts 2 rank processes itself
+    (rendezvous over 127.0.0.1); rank 0's line reports n_gpus 2 and the all-reduce saw both ranks."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["SCD_BENCH_PROBE"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
+    text = out.stdout.decode()
+    assert out.returncode == 0, text
+    lines = [json.loads(ln) for ln in text.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, text
+    assert lines[0]["n_gpus"] == 2 and lines[0]["world_seen"] == 2
+
+
+def test_bench_refuses_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", SCD_BENCH_PROBE="1")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
+    assert out.returncode != 0 and b"WORLD_SIZE" in out.stdout
+
+
+def test_resume_schedule_pops_past_milestones():
+    """resuming past a milestone keeps the later decays (the reference skips them)."""
+    from models.networkFactory import resumeSchedule
+    decay, rates = [100, 200, 300], [10.0, 2.0, 5.0]
+    lr = resumeSchedule(1e-2, decay, rates, 150)
+    assert lr == 1e-3 and decay == [200, 300] and rates == [2.0, 5.0]
+    lr = resumeSchedule(1e-2, [100, 200], [10.0, 2.0], 200)      # milestone == resume point is applied
+    assert abs(lr - 5e-4) < 1e-15
+    d2, r2 = [100], [10.0]
+    assert resumeSchedule(1e-2, d2, r2, 99) == 1e-2 and d2 == [100]
+    # the loop's own rule then fires at the next milestone
+    it, lr = 150, 1e-3
+    while it < 300:
+        it += 1
+        if decay and it == decay[0]:
+            lr /= rates.pop(0)
+            decay.pop(0)
+    assert abs(lr - 1e-4) < 1e-15

@@ -335,16 +335,39 @@ def test_batched_pack_matches_single(dtype):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("shape", [(2, 128, 128, 384, 256), (2, 40, 36, 384, 256)])
-def test_dgrad_with_bn_backward_sums(shape):
+def _pp_taken(N, phases, Cout):
+    """The ping-pong (fused BN-sum epilogue) rule of conv_gemm_launch: bf16, Cout % 256 or % 192 == 0 and at
+    least 256 tiles of 256 pixels over all sub-pixel phases."""
+    bn = 256 if Cout % 256 == 0 else (192 if Cout % 192 == 0 else 0)
+    if not bn:
+        return False
+    return sum(-(-(N * ph.Qh * ph.Qw) // 256) for ph in phases) * (Cout // bn) >= 256
+
+
+# (N, Hc, Wc, Co = dy channels, Ci = input-gradient channels, k, stride, pad, fused?)
+BNBWD_CASES = [
+    (2, 128, 128, 384, 256, 3, 1, 1, True),      # heads / deconv shapes: one 3x3 phase
+    (2, 40, 36, 384, 256, 3, 1, 1, False),       # too few tiles: GEMM + separate reduce
+    (4, 128, 128, 64, 256, 1, 1, 0, True),       # Bottleneck conv1 1x1 (256 -> 64) dgrad
+    (4, 128, 128, 256, 256, 3, 2, 1, True),      # Bottleneck stride-2 3x3: 4 sub-pixel phases, out_stride 2
+    (4, 128, 128, 512, 256, 1, 2, 0, True),      # downsample 1x1 stride 2: one phase with taps, three empty
+    (3, 66, 70, 128, 192, 3, 2, 1, True),        # ragged phases (odd/even extents), 192-wide tiles
+]
+
+
+@pytest.mark.parametrize("case", BNBWD_CASES)
+def test_dgrad_with_bn_backward_sums(case):
     """scd_conv_gemm_bnbwd (input-gradient GEMM whose epilogue adds the following BN+ReLU layer's backward sums)
     against scd_conv_gemm + scd_bn_bwd_reduce: identical gradient, sums within fp32 summation-order noise.
-    128x128 runs the fused ping-pong epilogue, 40x36 the fallback (plain GEMM + separate reduce)."""
+    The multi-phase cases check the epilogue's pixel / sub-pixel (rho) mapping of the BN sums on the shapes the
+    Bottleneck blocks send through it; `fused` states which path the launch rule takes."""
     from scdhip import ops
-    N, H, W, Co, Ci = shape
+    N, H, W, Co, Ci, k, stride, pad, fused = case
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    assert _pp_taken(N, ops._dgrad_phases(k, k, stride, pad, H, W), Ci) == fused
     g = torch.Generator().manual_seed(41)
-    dy = (torch.randn(N, H, W, Co, generator=g) * 0.1).to(DEV, torch.bfloat16)
-    w = (torch.randn(Co, Ci, 3, 3, generator=g) / (Ci * 9) ** 0.5).to(DEV)
+    dy = (torch.randn(N, Ho, Wo, Co, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    w = (torch.randn(Co, Ci, k, k, generator=g) / (Ci * k * k) ** 0.5).to(DEV)
     ybn = torch.randn(N, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
 
     class St:
@@ -357,16 +380,23 @@ def test_dgrad_with_bn_backward_sums(shape):
     wt = ops.pack_weight(w, torch.bfloat16, 1)
     s1 = torch.zeros(64 * 2 * Ci, dtype=torch.float64, device=DEV)
     s2 = torch.zeros_like(s1)
-    dx1 = ops.conv_dgrad(dy, wt, Ci, H, W, 3, 3, 1, 1, bn_bwd=(st, ybn, s1))
-    dx2 = ops.conv_dgrad(dy, wt, Ci, H, W, 3, 3, 1, 1)
+    dx1 = ops.conv_dgrad(dy, wt, Ci, H, W, k, k, stride, pad, bn_bwd=(st, ybn, s1))
+    dx2 = ops.conv_dgrad(dy, wt, Ci, H, W, k, k, stride, pad)
     ops.L.call("scd_bn_bwd_reduce", ops.dt(dx2), ops.ptr(dx2), 0, ops.ptr(ybn), ops.ptr(st.scale), ops.ptr(st.shift),
                ops.ptr(st.mean), ops.ptr(st.invstd), Ci, dx2.numel(), ops.ptr(s2), ops.stream())
     torch.cuda.synchronize()
     assert torch.equal(dx1, dx2)
+    # independent fp64 check of the sums from the GEMM output (dz = relu-masked gradient, xhat from ybn)
+    yf = ybn.double()
+    xhat = (yf - st.mean.double()) * st.invstd.double()
+    act = (yf * st.scale.double() + st.shift.double()) > 0
+    dz = torch.where(act, dx2.double(), torch.zeros((), dtype=torch.float64, device=DEV))
+    ref = torch.stack([dz.sum((0, 1, 2)), (dz * xhat).sum((0, 1, 2))]).cpu()
     a = s1.view(64, 2, Ci).sum(0).cpu()
     b = s2.view(64, 2, Ci).sum(0).cpu()
     for i in range(2):
         assert (a[i] - b[i]).abs().max().item() <= 1e-5 * b[i].abs().max().item() + 1e-9, i
+        assert (a[i] - ref[i]).abs().max().item() <= 1e-4 * ref[i].abs().max().item() + 1e-9, i
 
 
 # 64 -> 64 channel 3x3 stride-1 convs (layer1 shapes): the default 256x64 kernel, and with SCD_GEMM_H64=1 in the
