@@ -16,6 +16,7 @@ for parameter inputs.  Activations between Functions are NHWC in the model's com
 import torch
 
 from . import ops
+from .flat import grads_ready
 
 
 def _c(t):
@@ -89,6 +90,7 @@ class StemFn(torch.autograd.Function):
             dy = ops.bn_backward(bn, st, dz, y)
             T = conv.weight.shape[2] * conv.weight.shape[3]
             ops.conv_wgrad(dy, cols, 1, 1, 1, 0, ops.grad_of(conv.weight), (T, 1, 0), cvalid=T)
+        grads_ready(conv, bn)
         return None, None, None, None, None
 
 
@@ -136,6 +138,7 @@ class BasicBlockFn(torch.autograd.Function):
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 3, 3, s, 1, ops.grad_of(w1), _conv_ld(w1))
         ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 3, 3, s, 1, out=dx, accumulate=True)
+        grads_ready(blk)
         return dx, None, None
 
 
@@ -189,6 +192,7 @@ class BottleneckFn(torch.autograd.Function):
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 1, 1, 1, 0, ops.grad_of(w1), _conv_ld(w1))
         ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 1, 1, 1, 0, out=dx, accumulate=True)
+        grads_ready(blk)
         return dx, None, None
 
 
@@ -228,6 +232,7 @@ class DeconvBNFn(torch.autograd.Function):
                               bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dx)
+        grads_ready(deconv, bn)
         return dx, None, None, None
 
 
@@ -253,6 +258,7 @@ class ConvBNFn(torch.autograd.Function):
         dy = ops.bn_backward(bn, st, _c(dout), y, relu=ctx.relu)
         ops.conv_wgrad(dy, x, kh, kw, s, p, ops.grad_of(w), _conv_ld(w))
         dx = ops.conv_dgrad(dy, ops.pack_weight(w, x.dtype, 1), x.shape[3], x.shape[1], x.shape[2], kh, kw, s, p)
+        grads_ready(conv, bn)
         return dx, None, None, None, None
 
 
@@ -321,6 +327,7 @@ class HeadsFn(torch.autograd.Function):
                                bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
+        grads_ready(*[m for h in heads for m in h if isinstance(m, torch.nn.Module)])
         return dfeat, None, None
 
 
@@ -375,6 +382,7 @@ class CornerPoolFn(torch.autograd.Function):
             ops.conv_wgrad(dy, x, 3, 3, 1, 1, ops.grad_of(br.conv.weight), _conv_ld(br.conv.weight))
             ops.conv_dgrad(dy, ops.pack_weight(br.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1, out=dx,
                            accumulate=True)
+        grads_ready(mod)
         return dx, None, None, None
 
 

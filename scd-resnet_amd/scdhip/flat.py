@@ -14,10 +14,21 @@
   joins every bucket; BN buffers are broadcast from rank 0 before each forward (DDP
   broadcast_buffers=True, coalesced per dtype); state_dict keys keep the ``module.`` prefix.
 """
+import weakref
+
 import torch
 import torch.distributed as dist
 
 _REGISTRY = {}      # id(param) -> FlatParams
+_LISTENERS = weakref.WeakSet()      # FlatDDP instances (world > 1) told when a Function wrote its gradients
+
+
+def grads_ready(*modules):
+    """Called by the scdhip autograd Functions (blocks.py) at the end of their backward: every parameter of
+    `modules` has its gradient written (or its weight-gradient GEMM queued on the side stream), so a FlatDDP
+    bucket holding them may be all-reduced now."""
+    for d in list(_LISTENERS):
+        d._written(modules)
 
 
 class FlatParams:
@@ -150,7 +161,9 @@ class FlatDDP(torch.nn.Module):
     world (bucketed RCCL all-reduce of the flat gradient buffer, overlapped with backward).
 
     Gradient readiness: the model's blocks write parameter gradients straight into the flat buffer
-    (no AccumulateGrad hooks fire), and the leaf Conv2d/BatchNorm2d modules that hold the parameters
+    (no AccumulateGrad hooks fire) and say so at the end of their backward (``grads_ready``, which marks
+    the parameters of the modules they name -- blocks, deconv+BN, heads, stem).  For other modules the
+    leaf Conv2d/BatchNorm2d modules that hold the parameters
     never run their own forward (the block, deconv and head containers hand the weights to autograd
     Functions), so readiness is observed at whichever module's forward does run -- every module that
     holds parameters, directly or below it, gets a forward pre-hook that hooks its first grad-requiring
@@ -186,6 +199,7 @@ class FlatDDP(torch.nn.Module):
                     self._hooks.append(m.register_forward_pre_hook(self._pre_hook))
             for p in self.flat.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._acc_hook))
+            _LISTENERS.add(self)
             # identical initial replicas (DDP broadcasts parameters from rank 0 at wrap time)
             dist.broadcast(self.flat.data, 0, group=process_group)
             self._sync_buffers()
@@ -255,6 +269,13 @@ class FlatDDP(torch.nn.Module):
         for p in module.parameters():
             if id(p) not in self._engine:
                 self._mark(id(p))
+        self._launch_ready()
+
+    def _written(self, modules):
+        for m in modules:
+            for p in m.parameters():
+                if id(p) not in self._engine:
+                    self._mark(id(p))
         self._launch_ready()
 
     def _acc_hook(self, p):

@@ -346,12 +346,12 @@ def _pp_taken(N, phases, Cout):
 
 # (N, Hc, Wc, Co = dy channels, Ci = input-gradient channels, k, stride, pad, fused?)
 BNBWD_CASES = [
-    (2, 128, 128, 384, 256, 3, 1, 1, True),      # heads / deconv shapes: one 3x3 phase
+    (4, 128, 128, 384, 256, 3, 1, 1, True),      # heads / deconv shapes: one 3x3 phase
     (2, 40, 36, 384, 256, 3, 1, 1, False),       # too few tiles: GEMM + separate reduce
     (4, 128, 128, 64, 256, 1, 1, 0, True),       # Bottleneck conv1 1x1 (256 -> 64) dgrad
     (4, 128, 128, 256, 256, 3, 2, 1, True),      # Bottleneck stride-2 3x3: 4 sub-pixel phases, out_stride 2
     (4, 128, 128, 512, 256, 1, 2, 0, True),      # downsample 1x1 stride 2: one phase with taps, three empty
-    (3, 66, 70, 128, 192, 3, 2, 1, True),        # ragged phases (odd/even extents), 192-wide tiles
+    (16, 66, 70, 128, 192, 3, 2, 1, True),       # ragged phases (odd/even extents), 192-wide tiles
 ]
 
 
@@ -382,8 +382,10 @@ def test_dgrad_with_bn_backward_sums(case):
     s2 = torch.zeros_like(s1)
     dx1 = ops.conv_dgrad(dy, wt, Ci, H, W, k, k, stride, pad, bn_bwd=(st, ybn, s1))
     dx2 = ops.conv_dgrad(dy, wt, Ci, H, W, k, k, stride, pad)
-    ops.L.call("scd_bn_bwd_reduce", ops.dt(dx2), ops.ptr(dx2), 0, ops.ptr(ybn), ops.ptr(st.scale), ops.ptr(st.shift),
-               ops.ptr(st.mean), ops.ptr(st.invstd), Ci, dx2.numel(), ops.ptr(s2), ops.stream())
+    separate = 256 % (Ci // 8) == 0           # scd_bn_bwd_reduce takes channel counts whose 16-B chunks divide 256
+    if separate:
+        ops.L.call("scd_bn_bwd_reduce", ops.dt(dx2), ops.ptr(dx2), 0, ops.ptr(ybn), ops.ptr(st.scale),
+                   ops.ptr(st.shift), ops.ptr(st.mean), ops.ptr(st.invstd), Ci, dx2.numel(), ops.ptr(s2), ops.stream())
     torch.cuda.synchronize()
     assert torch.equal(dx1, dx2)
     # independent fp64 check of the sums from the GEMM output (dz = relu-masked gradient, xhat from ybn)
@@ -395,7 +397,8 @@ def test_dgrad_with_bn_backward_sums(case):
     a = s1.view(64, 2, Ci).sum(0).cpu()
     b = s2.view(64, 2, Ci).sum(0).cpu()
     for i in range(2):
-        assert (a[i] - b[i]).abs().max().item() <= 1e-5 * b[i].abs().max().item() + 1e-9, i
+        if separate:
+            assert (a[i] - b[i]).abs().max().item() <= 1e-5 * b[i].abs().max().item() + 1e-9, i
         assert (a[i] - ref[i]).abs().max().item() <= 1e-4 * ref[i].abs().max().item() + 1e-9, i
 
 
