@@ -26,6 +26,7 @@ import torch.distributed as dist  # noqa: E402
 TRAIN_GFLOP_PER_IMG = 147.476      # SURVEY §6 / BASELINE.md: conv+deconv fwd+dgrad+wgrad per 512^2 Res10 image
 PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -179,6 +180,39 @@ def launch_ranks(n):
     return rc
 
 
+def cornernet_rooflines(B, dtype_name, S=512, C=256, Cp=128):
+    """cornerNetCPool (BASELINE configs[3]).  Dominant kernel class: the CornerPool lastConv 3x3 C->C GEMM at the
+    heads' resolution (conv_gemm_pp_kernel<bf16,256,256>: M = B*(S/4)^2, N = C, K = 9*C), timed live on its
+    launch stream; secondary HBM roofline: the corner pool with the addend (cpool_fwd_kernel: reads the branch
+    activation and the first pool's output, writes their sum; 3 x B*(S/4)^2*Cp elements)."""
+    from scdhip import ops
+    H = S // 4
+    M = B * H * H
+    esz = 2 if dtype_name == "bf16" else 4
+    out = {}
+    r = ops.LaunchTimer.mean_ms("cpool_lastconv")
+    if r is not None:
+        ms, n = r
+        flops = 2.0 * M * C * 9 * C
+        peak = PEAK_BF16_TFLOPS if dtype_name == "bf16" else PEAK_F32_TFLOPS
+        achieved = flops / (ms * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": "conv_gemm_pp_kernel<bf16,256,256> (CornerPool lastConv)"
+                           if dtype_name == "bf16" else "conv_gemm_kernel<f32,128,128>", "achieved": round(achieved, 1),
+                           "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                           "algorithmic_bytes": 2 * M * C * esz + 9 * C * C * esz, "flop_per_launch": flops,
+                           "avg_launch_ms": round(ms, 4), "launches_timed": n}
+    r = ops.LaunchTimer.mean_ms("cpool_fwd_add")
+    if r is not None:
+        ms, n = r
+        nbytes = 3 * M * Cp * esz
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out["pool_roofline"] = {"bound": "hbm", "kernel": "cpool_fwd_kernel (with addend)", "achieved": round(gbs, 1),
+                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+                                "traffic": None, "algorithmic_bytes": nbytes, "avg_launch_ms": round(ms, 4),
+                                "launches_timed": n}
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -268,6 +302,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ops.LaunchTimer.arm("heads_gemm")
+    if args.model.startswith("cornerNet"):
+        ops.LaunchTimer.arm("cpool_lastconv")
+        ops.LaunchTimer.arm("cpool_fwd_add")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -285,7 +322,14 @@ def main():
         imgs = B * world * args.steps
         value = imgs / elapsed
         # the fused CenterNet head GEMM (HeadsFn) is the dominant kernel of the centerOffset* plugins only
-        roof = heads_gemm_roofline(B, args.dtype, S) if args.model.startswith("centerOffset") else None
+        extra = {}
+        if args.model.startswith("centerOffset"):
+            roof = heads_gemm_roofline(B, args.dtype, S)
+        elif args.model.startswith("cornerNet"):
+            extra = cornernet_rooflines(B, args.dtype, S)
+            roof = extra.pop("roofline", None)
+        else:
+            roof = None
         core = model.module if hasattr(model, "module") else model
         gflop = TRAIN_GFLOP_PER_IMG if (args.model == "centerOffsetRes10" and S == 512) else \
             train_gflop_per_img(core, S)
@@ -303,6 +347,7 @@ def main():
                        "per_gpu_batch": B, "seq_len": None, "parallelism": "dp%d" % world,
                        "image_size": S, "train_gflop_per_img": round(gflop, 3)},
             "roofline": roof,
+            **extra,
             "step_mfma_frac": round(step_frac, 4),
             "final_loss": round(final_loss, 5),
         }

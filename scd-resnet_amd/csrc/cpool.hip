@@ -1,129 +1,256 @@
 // Directional corner pooling (models/backbones/cornerPooling/source/{top,bottom,left,right}Pool.cpp)
 // on NHWC activations.  The reference issues ~H sequential ATen launches forward and ~5H
 // backward per pool; here one launch per direction: each thread owns a (n, line, channel-chunk)
-// and scans the line in registers (coalesced across channels).  Backward routes each dy to the
-// running argmax of the same scan; ties keep the first-scanned position (strict '>' update,
-// topPool.cpp:61-65), every position is written exactly once (no memset, deterministic).
-#include <algorithm>
-
+// and scans the line in registers (coalesced across channels, 8 positions of loads in flight).
+// Backward routes each dy to the running argmax of the same scan; ties keep the first-scanned
+// position (strict '>' update, topPool.cpp:61-65); every position is written exactly once, as a
+// 16-byte vector (no memset, deterministic).  HBM-bound: fwd reads x (+ the addend) and writes y,
+// bwd reads x and dy and writes dx.
 #include "scd_common.h"
 
 namespace {
 
-// dir: 0 top (scan h descending), 1 bottom (h ascending), 2 left (w descending), 3 right (w ascending)
-template <typename T>
-__global__ void cpool_fwd_kernel(int dir, const T* x, const T* addend, T* y, int N, int H, int W, int C) {
-    constexpr int E = Vec16<T>::N;
-    const int cpp = C / E;
-    const bool vert = dir < 2;
-    const int L = vert ? H : W;                // scan length
-    const int O = vert ? W : H;                // other spatial dim
-    const long lines = (long)N * O * cpp;
-    const long step = vert ? (long)W * C : (long)C;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < lines; i += (long)gridDim.x * blockDim.x) {
-        const int ch = (int)(i % cpp);
-        const long r = i / cpp;
-        const int o = (int)(r % O);
-        const int n = (int)(r / O);
-        const long base = vert ? (((long)n * H) * W + o) * C + ch * E : (((long)n * H + o) * W) * C + ch * E;
-        const bool desc = (dir == 0 || dir == 2);
-        float m[E];
-        for (int k = 0; k < L; ++k) {
-            const int pos = desc ? (L - 1 - k) : k;
-            float v[E];
-            Vec16<T>::load(x + base + pos * step, v);
-#pragma unroll
-            for (int e = 0; e < E; ++e) m[e] = (k == 0) ? v[e] : fmaxf(m[e], v[e]);
-            if (addend) {
-                float a[E], o[E];
-                Vec16<T>::load(addend + base + pos * step, a);
-#pragma unroll
-                for (int e = 0; e < E; ++e) o[e] = m[e] + a[e];
-                Vec16<T>::store(y + base + pos * step, o);
-            } else {
-                Vec16<T>::store(y + base + pos * step, m);
-            }
-        }
+// One thread owns a (n, line, 16-B channel chunk) and scans the line in registers.  Loads of the next
+// U positions are issued before the current U are used (software pipeline; clamped indices, so no
+// branch surrounds a load and the waitcnt pass keeps them in flight).  dir: 0 top (scan h descending),
+// 1 bottom (h ascending), 2 left (w descending), 3 right (w ascending).
+// VB-byte vector of T <-> floats (VB = 16: one dwordx4 per lane; 8: dwordx2, twice the lines in flight)
+template <typename T, int VB> struct Vec;
+template <typename T> struct Vec<T, 16> {
+    typedef uint4 raw;
+    static constexpr int N = Vec16<T>::N;
+    __device__ static void load(const raw* p, float* f) { Vec16<T>::load(p, f); }
+    __device__ static void store(void* p, const float* f) { Vec16<T>::store(p, f); }
+};
+template <> struct Vec<__bf16, 8> {
+    typedef uint2 raw;
+    static constexpr int N = 4;
+    __device__ static void load(const raw* p, float* f) {
+        const uint2 v = *p;
+        f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+        f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
     }
-}
+    __device__ static void store(void* p, const float* f) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        *(bf16x4*)p = (bf16x4){(__bf16)f[0], (__bf16)f[1], (__bf16)f[2], (__bf16)f[3]};
+    }
+};
+template <> struct Vec<float, 8> {
+    typedef uint2 raw;
+    static constexpr int N = 2;
+    __device__ static void load(const raw* p, float* f) { f[0] = __uint_as_float(p->x); f[1] = __uint_as_float(p->y); }
+    __device__ static void store(void* p, const float* f) { *(float2*)p = make_float2(f[0], f[1]); }
+};
 
-template <typename T>
-__global__ void cpool_bwd_kernel(int dir, const T* x, const T* dy, T* dx, int N, int H, int W, int C) {
-    constexpr int E = Vec16<T>::N;
+struct Line {
+    long start;     // element offset of the first scanned position
+    long sstep;     // signed element step between scanned positions
+    int L;          // scan length
+};
+__device__ __forceinline__ Line line_of(int dir, long i, int N, int H, int W, int C, int E) {
     const int cpp = C / E;
     const bool vert = dir < 2;
     const int L = vert ? H : W;
     const int O = vert ? W : H;
-    const long lines = (long)N * O * cpp;
+    const int ch = (int)(i % cpp);
+    const long r = i / cpp;
+    const int o = (int)(r % O);
+    const int n = (int)(r / O);
+    const long base = vert ? (((long)n * H) * W + o) * C + ch * E : (((long)n * H + o) * W) * C + ch * E;
     const long step = vert ? (long)W * C : (long)C;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < lines; i += (long)gridDim.x * blockDim.x) {
-        const int ch = (int)(i % cpp);
-        const long r = i / cpp;
-        const int o = (int)(r % O);
-        const int n = (int)(r / O);
-        const long base = vert ? (((long)n * H) * W + o) * C + ch * E : (((long)n * H + o) * W) * C + ch * E;
-        const bool desc = (dir == 0 || dir == 2);
-        float mv[E], acc[E];
-        int mi[E];
-        for (int k = 0; k < L; ++k) {
-            const int pos = desc ? (L - 1 - k) : k;
-            float v[E], g[E];
-            Vec16<T>::load(x + base + pos * step, v);
-            Vec16<T>::load(dy + base + pos * step, g);
+    const bool desc = (dir == 0 || dir == 2);
+    Line ln;
+    ln.L = L;
+    ln.start = desc ? base + (long)(L - 1) * step : base;
+    ln.sstep = desc ? -step : step;
+    return ln;
+}
+
+template <typename T, int U, bool ADD, int VB>
+__global__ __launch_bounds__(256) void cpool_fwd_kernel(int dir, const T* __restrict__ x, const T* __restrict__ addend,
+                                                        T* __restrict__ y, int N, int H, int W, int C, long lines) {
+    typedef Vec<T, VB> V;
+    typedef typename V::raw R;
+    constexpr int E = V::N;
+    const long i = blockIdx.x * 256L + threadIdx.x;
+    if (i >= lines) return;
+    const Line ln = line_of(dir, i, N, H, W, C, E);
+    const int L = ln.L;
+    R cx[U], ca[U];
 #pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const bool upd = (k == 0) || (v[e] > mv[e]);
-                // a replaced argmax is final: flush its accumulated gradient
-                if (upd && k > 0) dx[base + mi[e] * step + e] = from_f<T>(acc[e]);
-                if (upd) { mv[e] = v[e]; mi[e] = pos; acc[e] = 0.f; }
-                acc[e] += g[e];
-                // a position that is not the running argmax now can never become one later
-                if (!upd) dx[base + pos * step + e] = from_f<T>(0.f);
+    for (int u = 0; u < U; ++u) {
+        const long off = ln.start + (long)min(u, L - 1) * ln.sstep;
+        cx[u] = *(const R*)(x + off);
+        if constexpr (ADD) ca[u] = *(const R*)(addend + off);
+    }
+    float m[E];
+    for (int k0 = 0; k0 < L; k0 += U) {
+        R nx[U], na[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {          // prefetch the next U positions (clamped: always a valid address)
+            const long off = ln.start + (long)min(k0 + U + u, L - 1) * ln.sstep;
+            nx[u] = *(const R*)(x + off);
+            if constexpr (ADD) na[u] = *(const R*)(addend + off);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = k0 + u;
+            if (k >= L) break;
+            float v[E];
+            V::load(&cx[u], v);
+#pragma unroll
+            for (int e = 0; e < E; ++e) m[e] = (k == 0) ? v[e] : fmaxf(m[e], v[e]);
+            T* dst = y + ln.start + (long)k * ln.sstep;
+            if constexpr (ADD) {
+                float a[E], o[E];
+                V::load(&ca[u], a);
+#pragma unroll
+                for (int e = 0; e < E; ++e) o[e] = m[e] + a[e];
+                V::store(dst, o);
+            } else {
+                V::store(dst, m);
             }
         }
 #pragma unroll
-        for (int e = 0; e < E; ++e) dx[base + mi[e] * step + e] = from_f<T>(acc[e]);
+        for (int u = 0; u < U; ++u) { cx[u] = nx[u]; if constexpr (ADD) ca[u] = na[u]; }
     }
 }
 
-inline int ew_blocks(long n) { return (int)std::min<long>(4096, std::max<long>(1, (n + 255) / 256)); }
+// Backward in two register scans per line, every dx position written once as a 16-B vector:
+//  1. forward over x: position k is a record of element e iff k == 0 or x[k][e] > the running max (strict:
+//     ties keep the first-scanned position, topPool.cpp:61-65); one byte of record bits per position goes to
+//     this thread's column of an LDS table [L/8][256 threads] of 8-byte words;
+//  2. reverse over dy: acc += dy[k]; a record takes dx[k] = acc and restarts acc, any other position gets 0.
+//     A record's dx is then the sum of dy over its run up to the next record -- the positions whose running
+//     argmax it is (the reference's scatter_add, summed in the reverse order).
+template <typename T, int U>
+__global__ __launch_bounds__(256) void cpool_bwd_kernel(int dir, const T* __restrict__ x, const T* __restrict__ dy,
+                                                        T* __restrict__ dx, int N, int H, int W, int C, long lines) {
+    static_assert(U == 8, "one 8-byte flag word per 8 positions");
+    constexpr int E = Vec16<T>::N;
+    extern __shared__ uint2 flags[];
+    const long i = blockIdx.x * 256L + threadIdx.x;
+    if (i >= lines) return;
+    const Line ln = line_of(dir, i, N, H, W, C, E);
+    const int L = ln.L;
+    uint4 cx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cx[u] = *(const uint4*)(x + ln.start + (long)min(u, L - 1) * ln.sstep);
+    float mv[E];
+    for (int k0 = 0; k0 < L; k0 += U) {
+        uint4 nx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) nx[u] = *(const uint4*)(x + ln.start + (long)min(k0 + U + u, L - 1) * ln.sstep);
+        unsigned fb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = k0 + u;
+            float v[E];
+            Vec16<T>::load(&cx[u], v);
+            unsigned b = 0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const bool rec = (k == 0) || (v[e] > mv[e]);
+                if (rec) mv[e] = v[e];
+                b |= (rec ? 1u : 0u) << e;
+            }
+            fb[u] = k < L ? b : 0u;
+        }
+        flags[(k0 / U) * 256 + threadIdx.x] =
+            make_uint2(fb[0] | fb[1] << 8 | fb[2] << 16 | fb[3] << 24, fb[4] | fb[5] << 8 | fb[6] << 16 | fb[7] << 24);
+#pragma unroll
+        for (int u = 0; u < U; ++u) cx[u] = nx[u];
+    }
+    // pass 2: chunks in reverse scan order, positions inside a chunk from the last down
+    const int nch = (L + U - 1) / U;
+    uint4 cg[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cg[u] = *(const uint4*)(dy + ln.start + (long)min((nch - 1) * U + u, L - 1) * ln.sstep);
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+    for (int c = nch - 1; c >= 0; --c) {
+        uint4 ng[U];
+        const int cn = c > 0 ? c - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) ng[u] = *(const uint4*)(dy + ln.start + (long)min(cn * U + u, L - 1) * ln.sstep);
+        const uint2 fw = flags[c * 256 + threadIdx.x];
+#pragma unroll
+        for (int u = U - 1; u >= 0; --u) {
+            const int k = c * U + u;
+            if (k >= L) continue;
+            const unsigned b = ((u < 4 ? fw.x : fw.y) >> (8 * (u & 3))) & 0xffu;
+            float g[E], o[E];
+            Vec16<T>::load(&cg[u], g);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                acc[e] += g[e];
+                const bool rec = (b >> e) & 1u;
+                o[e] = rec ? acc[e] : 0.f;
+                if (rec) acc[e] = 0.f;
+            }
+            Vec16<T>::store(dx + ln.start + (long)k * ln.sstep, o);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) cg[u] = ng[u];
+    }
+}
+
+#ifndef CPOOL_FWD_VB
+#define CPOOL_FWD_VB 16
+#endif
+constexpr int CPOOL_MAX_L = 640;      // LDS record table: L/8 words of 8 B per thread, 256 threads (<= 160 KiB)
+
+template <typename T>
+int launch_fwd(int dir, const void* x, const void* addend, void* y, int N, int H, int W, int C, hipStream_t st) {
+    constexpr int VB = CPOOL_FWD_VB;
+    const long lines = (long)N * (dir < 2 ? W : H) * (C / Vec<T, VB>::N);
+    if (lines == 0) return 0;
+    const int grid = (int)((lines + 255) / 256);
+    if (addend)
+        hipLaunchKernelGGL((cpool_fwd_kernel<T, 8, true, VB>), dim3(grid), dim3(256), 0, st, dir, (const T*)x,
+                           (const T*)addend, (T*)y, N, H, W, C, lines);
+    else
+        hipLaunchKernelGGL((cpool_fwd_kernel<T, 8, false, VB>), dim3(grid), dim3(256), 0, st, dir, (const T*)x,
+                           (const T*)nullptr, (T*)y, N, H, W, C, lines);
+    SCD_RETURN_LAUNCH();
+}
+
+template <typename T>
+int launch_bwd(int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C, hipStream_t st) {
+    const long lines = (long)N * (dir < 2 ? W : H) * (C / Vec16<T>::N);
+    if (lines == 0) return 0;
+    const int L = dir < 2 ? H : W;
+    if (L > CPOOL_MAX_L) return SCD_ERR_ARG;
+    const int grid = (int)((lines + 255) / 256);
+    const size_t lds = (size_t)((L + 7) / 8) * 256 * 8;
+    hipLaunchKernelGGL((cpool_bwd_kernel<T, 8>), dim3(grid), dim3(256), lds, st, dir, (const T*)x, (const T*)dy,
+                       (T*)dx, N, H, W, C, lines);
+    SCD_RETURN_LAUNCH();
+}
 
 }  // namespace
 
 extern "C" int scd_cpool_fwd(int dtype, int dir, const void* x, const void* addend, void* y, int N, int H, int W, int C,
                              void* stream) {
-    if (dir < 0 || dir > 3) return SCD_ERR_ARG;
+    if (dir < 0 || dir > 3 || N < 0 || H < 1 || W < 1) return SCD_ERR_ARG;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
-    const long lines = (long)N * (dir < 2 ? W : H) * (C / E);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((cpool_fwd_kernel<__bf16>), dim3(ew_blocks(lines)), dim3(256), 0, st, dir, (const __bf16*)x,
-                           (const __bf16*)addend, (__bf16*)y, N, H, W, C);
-    else if (dtype == SCD_DT_F32)
-        hipLaunchKernelGGL((cpool_fwd_kernel<float>), dim3(ew_blocks(lines)), dim3(256), 0, st, dir, (const float*)x,
-                           (const float*)addend, (float*)y, N, H, W, C);
-    else
-        return SCD_ERR_ARG;
-    SCD_RETURN_LAUNCH();
+    if (dtype == SCD_DT_BF16) return launch_fwd<__bf16>(dir, x, addend, y, N, H, W, C, st);
+    if (dtype == SCD_DT_F32) return launch_fwd<float>(dir, x, addend, y, N, H, W, C, st);
+    return SCD_ERR_ARG;
 }
 
 extern "C" int scd_cpool_bwd(int dtype, int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C,
                              void* stream) {
-    if (dir < 0 || dir > 3) return SCD_ERR_ARG;
+    if (dir < 0 || dir > 3 || N < 0 || H < 1 || W < 1) return SCD_ERR_ARG;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
-    const long lines = (long)N * (dir < 2 ? W : H) * (C / E);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((cpool_bwd_kernel<__bf16>), dim3(ew_blocks(lines)), dim3(256), 0, st, dir, (const __bf16*)x,
-                           (const __bf16*)dy, (__bf16*)dx, N, H, W, C);
-    else if (dtype == SCD_DT_F32)
-        hipLaunchKernelGGL((cpool_bwd_kernel<float>), dim3(ew_blocks(lines)), dim3(256), 0, st, dir, (const float*)x,
-                           (const float*)dy, (float*)dx, N, H, W, C);
-    else
-        return SCD_ERR_ARG;
-    SCD_RETURN_LAUNCH();
+    if (dtype == SCD_DT_BF16) return launch_bwd<__bf16>(dir, x, dy, dx, N, H, W, C, st);
+    if (dtype == SCD_DT_F32) return launch_bwd<float>(dir, x, dy, dx, N, H, W, C, st);
+    return SCD_ERR_ARG;
 }
 
 extern "C" const char* scd_version(void) { return "libscdhip 0.1 gfx950"; }

@@ -29,13 +29,16 @@ def _conv_ld(w):
     return (w.shape[1] * T, T, 1)
 
 
-def _train_bn_conv(x, conv, bn, stride, pad, training):
-    """conv (no bias) -> raw y + BN statistics -> BNState."""
+def _train_bn_conv(x, conv, bn, stride, pad, training, timer=None):
+    """conv (no bias) -> raw y + BN statistics -> BNState.  timer: LaunchTimer name for the GEMM (bench.py)."""
     C = conv.weight.shape[0]
     kh, kw = conv.weight.shape[2], conv.weight.shape[3]
     wp = ops.pack_weight(conv.weight, x.dtype, 0)
     stats = ops.bn_stats(bn, "fwd") if training else None
+    t0 = ops.LaunchTimer.record(timer) if timer else None
     y = ops.conv_fwd(x, wp, C, kh, kw, stride, pad, stats=stats)
+    if timer:
+        ops.LaunchTimer.close(timer, t0)
     st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
     return y, st
 
@@ -345,12 +348,14 @@ class CornerPoolFn(torch.autograd.Function):
         y2, st2 = _train_bn_conv(x, b2.conv, b2.bn, 1, 1, tr)
         a2 = ops.bn_apply(y2, st2, True)
         p1 = ops.cpool_fwd(a1, dirs[0])
+        t0 = ops.LaunchTimer.record("cpool_fwd_add")
         s = ops.cpool_fwd(a2, dirs[1], addend=p1)
+        ops.LaunchTimer.close("cpool_fwd_add", t0)
         del p1
         ym, stm = _train_bn_conv(s, mod.branchMerge, mod.branchMergeBn, 1, 1, tr)
         ysc, sts = _train_bn_conv(x, mod.shortcutConv, mod.shortcutBn, 1, 0, tr)
         r = ops.bn_apply(ym, stm, True, res=ysc, rst=sts)
-        yl, stl = _train_bn_conv(r, lc.conv, lc.bn, 1, 1, tr)
+        yl, stl = _train_bn_conv(r, lc.conv, lc.bn, 1, 1, tr, timer="cpool_lastconv")
         out = ops.bn_apply(yl, stl, True)
         ctx.save_for_backward(x, y1, a1, y2, a2, s, ym, ysc, r, yl, out)
         ctx.sts = (st1, st2, stm, sts, stl)

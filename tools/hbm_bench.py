@@ -31,7 +31,9 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="bn,heads,stem,cpool", help="comma list of groups")
     a = ap.parse_args()
+    groups = set(a.only.split(","))
     dev = "cuda"
     bf = torch.bfloat16
     st = ops.stream
@@ -41,7 +43,18 @@ def main():
         rows.append((name, us, nbytes))
         print("%-34s %9.1f us %9.1f MB %8.0f GB/s" % (name, us, nbytes / 1e6, nbytes / us / 1e3), flush=True)
 
-    for (N, H, W, C) in [(32, 128, 128, 256), (32, 128, 128, 64), (32, 64, 64, 128)]:
+    if "cpool" in groups:
+        # corner pools at the cornerNetCPool B=32 shape (32,128,128,128) bf16: fwd x(+addend) -> y, bwd x, dy -> dx
+        x = torch.randn(32, 128, 128, 128, device=dev).to(bf)
+        ad = torch.randn_like(x)
+        g = torch.randn_like(x)
+        B = x.numel() * 2
+        for d in range(4):
+            report("cpool_fwd+add dir%d 32x128x128x128" % d, timed(lambda: ops.cpool_fwd(x, d, addend=ad), a.reps),
+                   3 * B)
+            report("cpool_bwd dir%d 32x128x128x128" % d, timed(lambda: ops.cpool_bwd(x, g, d), a.reps), 3 * B)
+        del x, ad, g
+    for (N, H, W, C) in ([(32, 128, 128, 256), (32, 128, 128, 64), (32, 64, 64, 128)] if "bn" in groups else []):
         y = torch.randn(N, H, W, C, device=dev).to(bf)
         r = torch.randn(N, H, W, C, device=dev).to(bf)
         d = torch.randn(N, H, W, C, device=dev).to(bf)
@@ -75,6 +88,14 @@ def main():
             coef.data_ptr(), C, n, out.data_ptr(), r.data_ptr(), st()), a.reps), 5 * B)
         del y, r, d, out
 
+    if "heads" in groups:
+        heads_rows(a, report, dev, bf, st)
+    if "stem" in groups:
+        stem_rows(a, report, dev, bf, st)
+    print("total us: %.1f" % sum(r[1] for r in rows))
+
+
+def heads_rows(a, report, dev, bf, st):
     # heads tail backward: hid (32,128,128,384) bf16, douts NCHW fp32 (1,4,2 channels)
     N, HW, nh, Hd = 32, 128 * 128, 3, 128
     od = [1, 4, 2]
@@ -91,6 +112,8 @@ def main():
         st()), a.reps), hid.numel() * 4 + N * HW * 7 * 4)
     del hid, dhid
 
+
+def stem_rows(a, report, dev, bf, st):
     # stem pool backward + BN reduce: y (32,256,256,64), dout (32,128,128,64), argmax u8
     N, H, W, C = 32, 256, 256, 64
     y = torch.randn(N, H, W, C, device=dev).to(bf)
@@ -122,7 +145,6 @@ def main():
     report("stem_conv_wgrad (dz, y, coef)", timed(lambda: ops.stem_conv_wgrad(ys, xs, dw, ybn=ys,
                                                                              coef=torch.ones(192, device=dev)),
                                                   a.reps), xs.numel() * 4 + ys.numel() * 4)
-    print("total us: %.1f" % sum(r[1] for r in rows))
 
 
 if __name__ == "__main__":
