@@ -1,0 +1,301 @@
+"""bf16 performance-mode parity, layer by layer, and the BASELINE configs that train in bf16 at full size.
+
+Whole-network bf16-vs-fp32 comparisons of a deep hash-initialised net are chaotic (a 2^-9 relative
+perturbation of the Res50 weights alone moves its heads by ~25%, tools/diag_chaos.py), so they bound
+nothing.  Instead every module group of the HIP bf16 forward is checked against a plain PyTorch fp32
+recomputation of the SAME group (F.conv2d / F.batch_norm(training=True) / F.max_pool2d /
+F.conv_transpose2d, residuals.py:84-165, 209-216, 286-310; centerNetOffset.py:106-110) from the SAME bf16
+input the HIP group received, at the benchmark shapes.
+
+Bound (in units of the reference's rms): the HIP group rounds its weights to bf16 (relative 2^-9 each) and its
+stored intermediates (pre-BN y, the post-BN/ReLU activations) and its output to bf16 (2^-9 each); a conv over K
+products with independently rounded weights moves its output by ~2^-9 of its rms, BN normalises to unit scale,
+so a group of c such roundings in series has an rms error of ~sqrt(c)..c x 2^-9 (c <= 6 for a Bottleneck:
+3 weights, 2 intermediates, the output): TOL_MEAN = 2^-6 = 8 x 2^-9.  Rounding errors are relative, so the
+largest errors sit on the largest values and the maximum over 10^6 (Res50 128^2) to 10^8 (Res50 1024^2 B=16)
+elements reaches ~11x the rms error: TOL_RMS = 2^-3.  Measured on MI355X (gpurun_out/tests_bf16.log, r2):
+rms error 0.0006-0.0072 x rms, max 0.002-0.080 x rms.  A wrong tap, channel or BN term gives O(1).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import centernet as O
+from oracle import targets as T
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL_RMS = 2.0 ** -3          # max |err| / rms(ref), see the module docstring
+TOL_MEAN = 2.0 ** -6         # rms(err) / rms(ref)
+
+
+def _model(name, dtype):
+    import importlib
+    plugin = importlib.import_module("trainer.model." + name)
+    entries, topo = O.model_spec(plugin.modelParams["numLayers"], plugin.modelParams["dims"])
+    m = plugin.model(**plugin.modelParams)
+    m.load_state_dict(O.hash_weights(entries))
+    return m.to(DEV).train().set_compute_dtype(dtype), plugin
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2).float()
+
+
+def _bn(h, m):
+    return F.batch_norm(h, m.running_mean.clone(), m.running_var.clone(), m.weight, m.bias, True, 0.1, m.eps)
+
+
+def ref_block(blk, x):
+    """BasicBlock.forward (residuals.py:99-120) / Bottleneck.forward (:145-165) in fp32."""
+    s = blk.stride
+    if hasattr(blk, "conv3"):
+        o = F.relu(_bn(F.conv2d(x, blk.conv1.weight), blk.bn1))
+        o = F.relu(_bn(F.conv2d(o, blk.conv2.weight, stride=s, padding=1), blk.bn2))
+        o = _bn(F.conv2d(o, blk.conv3.weight), blk.bn3)
+    else:
+        o = F.relu(_bn(F.conv2d(x, blk.conv1.weight, stride=s, padding=1), blk.bn1))
+        o = _bn(F.conv2d(o, blk.conv2.weight, padding=1), blk.bn2)
+    idn = x
+    if blk.downsample is not None:
+        idn = _bn(F.conv2d(x, blk.downsample[0].weight, stride=s), blk.downsample[1])
+    return F.relu(o + idn)
+
+
+def ref_stem(pre, x):
+    """preprocess: Conv7x7 s2 p3 + BN + ReLU + MaxPool 3/2/1 (residuals.py:209-216) in fp32."""
+    h = F.relu(_bn(F.conv2d(x, pre[0].weight, stride=2, padding=3), pre[1]))
+    return F.max_pool2d(h, 3, stride=2, padding=1)
+
+
+def ref_deconv(dc, bn, x):
+    """ConvTranspose2d(k4, s2, p1) + BN + ReLU (residuals.py:286-310) in fp32."""
+    return F.relu(_bn(F.conv_transpose2d(x, dc.weight, stride=2, padding=1), bn))
+
+
+def ref_heads(heads, feat):
+    """conv3x3 + bias -> ReLU -> conv1x1 + bias (centerNetOffset.py:106-110) in fp32."""
+    return [F.conv2d(F.relu(F.conv2d(feat, h[0].weight, h[0].bias, padding=1)), h[2].weight, h[2].bias)
+            for h in heads]
+
+
+def check(name, got, ref, report):
+    got, ref = got.float(), ref.float()
+    assert got.shape == ref.shape, (name, got.shape, ref.shape)
+    assert torch.isfinite(got).all(), name
+    rms = ref.square().mean().sqrt().item()
+    err = (got - ref).abs()
+    mx = err.max().item() / rms
+    me = err.square().mean().sqrt().item() / rms
+    report.append((name, mx, me))
+    assert mx <= TOL_RMS and me <= TOL_MEAN, (name, mx, me)
+
+
+def capture_forward(m, x, monkeypatch):
+    """Run the HIP forward once, recording every module group's input and output."""
+    from scdhip import blocks
+    rec = []
+    hooks = []
+    for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
+        for i, blk in enumerate(layer):
+            hooks.append(blk.register_forward_hook(
+                lambda mod, inp, out: rec.append(("block", mod, inp[0].detach().clone(), out.detach().clone()))))
+    stem_apply, dec_apply, heads_apply = blocks.StemFn.apply, blocks.DeconvBNFn.apply, blocks.HeadsFn.apply
+
+    def stem(x, w, conv, bn, dtype):
+        out = stem_apply(x, w, conv, bn, dtype)
+        rec.append(("stem", None, x.detach().clone(), out.detach().clone()))
+        return out
+
+    def dec(h, w, dc, bn):
+        out = dec_apply(h, w, dc, bn)
+        rec.append(("deconv", (dc, bn), h.detach().clone(), out.detach().clone()))
+        return out
+
+    def heads(feat, w, hm):
+        outs = heads_apply(feat, w, hm)
+        rec.append(("heads", hm, feat.detach().clone(), [o.detach().clone() for o in outs]))
+        return outs
+
+    monkeypatch.setattr(blocks.StemFn, "apply", stem)
+    monkeypatch.setattr(blocks.DeconvBNFn, "apply", dec)
+    monkeypatch.setattr(blocks.HeadsFn, "apply", heads)
+    try:
+        with torch.no_grad():
+            m(x, decode=False)
+        torch.cuda.synchronize()
+    finally:
+        for h in hooks:
+            h.remove()
+    return rec
+
+
+def check_groups(m, rec, report):
+    kinds = [r[0] for r in rec]
+    assert kinds[0] == "stem" and kinds[-1] == "heads" and "deconv" in kinds and "block" in kinds, kinds
+    with torch.no_grad():
+        for kind, mod, inp, out in rec:
+            if kind == "stem":
+                check("stem", _nchw(out), ref_stem(m.preprocess, inp.float()), report)
+            elif kind == "block":
+                check("block %s" % mod.conv1.weight.shape[0], _nchw(out), ref_block(mod, _nchw(inp)), report)
+            elif kind == "deconv":
+                check("deconv %d" % mod[0].weight.shape[1], _nchw(out), ref_deconv(mod[0], mod[1], _nchw(inp)), report)
+            else:
+                for i, (o, r) in enumerate(zip(out, ref_heads(mod, _nchw(inp)))):
+                    check("head %d" % i, o, r, report)
+
+
+def _print(report):
+    for name, mx, me in report:
+        print("%-14s max|err|/rms %.5f  rms(err)/rms %.6f" % (name, mx, me))
+
+
+@pytest.mark.parametrize("case", [("centerOffsetRes10", 32, 512), ("centerOffsetRes50", 2, 128),
+                                  ("centerOffsetRes50", 16, 1024)])
+def test_bf16_groups_match_fp32(case, monkeypatch):
+    """Every module group of the bf16 forward vs PyTorch fp32 from the same bf16 input: Res10 at the benchmark
+    configuration (BASELINE configs[1], B=32 512^2), Res50 at F9's size and at BASELINE configs[4] (1024^2, 16
+    images per GPU)."""
+    name, B, S = case
+    m, _ = _model(name, torch.bfloat16)
+    x = T.batch_inputs(31, B, S).to(DEV) if S == 512 else torch.randn(B, 1, S, S, device=DEV,
+                                                                       generator=torch.Generator(DEV).manual_seed(3))
+    rec = capture_forward(m, x, monkeypatch)
+    report = []
+    try:
+        check_groups(m, rec, report)
+    finally:
+        _print(report)
+    nblk = sum(len(layer) for layer in (m.layer1, m.layer2, m.layer3, m.layer4))
+    assert len([r for r in report if r[0].startswith("block")]) == nblk
+
+
+def test_f1_decode_indices_on_hip_heatmap():
+    """Decode parity on the HIP path's own F1 heatmap (fp32 parity mode, B=2 512^2): the oracle's decode
+    (centerNetOffset.py:219-251; sigmoid, 3x3 NMS, top-K, gathers) fed the same heads gives bit-identical
+    indices / ys / xs / gathered offsets and sizes wherever its top-K ordering is strict."""
+    from models.centerNetOffset import decodeCenterNet
+    m, _ = _model("centerOffsetRes10", torch.float32)
+    with torch.no_grad():
+        out = m(T.batch_inputs(1, 2, 512).to(DEV), decode=False)[0]
+    cpu = {k: v.detach().cpu().clone() for k, v in out.items()}
+    dec = decodeCenterNet({k: v.clone() for k, v in out.items()})
+    ref = O.decode({k: v.clone() for k, v in cpu.items()})
+    rs, ri, ry, rx = [r.numpy() for r in ref[:4]]
+    np.testing.assert_allclose(dec[0].cpu().numpy(), rs, rtol=1e-6, atol=1e-7)
+    nstrict = 0
+    for b in range(rs.shape[0]):
+        s = rs[b]
+        strict = np.ones_like(s, dtype=bool)
+        gap = np.abs(np.diff(s)) > 1e-6 * np.abs(s[1:])
+        strict[1:] &= gap
+        strict[:-1] &= gap
+        nstrict += int(strict.sum())
+        np.testing.assert_array_equal(dec[1].cpu().numpy()[b][strict], ri[b][strict])
+        np.testing.assert_array_equal(dec[2].cpu().numpy()[b][strict], ry[b][strict])
+        np.testing.assert_array_equal(dec[3].cpu().numpy()[b][strict], rx[b][strict])
+        np.testing.assert_array_equal(dec[4].cpu().numpy()[b][strict], ref[4].numpy()[b][strict])
+        np.testing.assert_array_equal(dec[5].cpu().numpy()[b][strict], ref[5].numpy()[b][strict])
+    assert nstrict >= 100, nstrict          # most of the 2 x 100 slots are strictly ordered
+
+
+def _train_steps(m, plugin, x, ys, n):
+    from scdhip.flat import FlatAdam
+    opt = FlatAdam(filter(lambda p: p.requires_grad, m.parameters()))
+    losses = []
+    for _ in range(n):
+        opt.zero_grad()
+        loss, _ = plugin.loss(m(x, decode=False), ys)
+        loss.mean().backward()
+        opt.step()
+        losses.append(loss.item())
+    for p in m.parameters():
+        assert torch.isfinite(p).all()
+    return losses
+
+
+def test_cornernet_b32_bf16_config3(monkeypatch):
+    """BASELINE configs[3]: cornerNetCPool, 512^2, B=32, bf16.  Trains (finite, decreasing loss over 4 Adam
+    steps); its forward heads match the same network in fp32 parity mode within 5e-2 of their max (Res10 depth:
+    not chaotic), and the CornerPool groups (conv+BN+ReLU branches, corner pools, merge, shortcut, lastConv;
+    cornerNetCPool.py:83-122) match PyTorch fp32 from the same bf16 input at the per-group bound."""
+    from scdhip import blocks
+    from trainer.dataset.syntheticCorner import CornerSCD
+    import trainer.model.cornerNetCPool as plugin
+    from oracle import cornernet as OC
+    from oracle import cpool as CP
+    ds = CornerSCD(None, True, seed=77)
+    items = [ds[i] for i in range(32)]
+    x = torch.stack([it["xs"][0] for it in items]).to(DEV)
+    ys = [torch.stack([it["ys"][k] for it in items]).to(DEV) for k in range(len(items[0]["ys"]))]
+    entries, _ = OC.model_spec(10)
+    state = OC.hash_weights(entries)
+
+    def build(dtype):
+        mm = plugin.model(**plugin.modelParams)
+        mm.load_state_dict(state)
+        return mm.to(DEV).train().set_compute_dtype(dtype)
+
+    rec = []
+    cp_apply = blocks.CornerPoolFn.apply
+
+    def cp(xx, w, mod, dirs):
+        out = cp_apply(xx, w, mod, dirs)
+        rec.append((mod, dirs, xx.detach().clone(), out.detach().clone()))
+        return out
+
+    m16 = build(torch.bfloat16)
+    monkeypatch.setattr(blocks.CornerPoolFn, "apply", cp)
+    with torch.no_grad():
+        o16 = m16(x, decode=False)[0]
+    monkeypatch.setattr(blocks.CornerPoolFn, "apply", cp_apply)
+    m32 = build(torch.float32)
+    with torch.no_grad():
+        o32 = m32(x, decode=False)[0]
+    for k in o32:
+        a, b = o16[k].float(), o32[k].float()
+        assert torch.isfinite(a).all(), k
+        err = (a - b).abs().max().item() / b.abs().max().item()
+        assert err < 5e-2, (k, err)
+    del m32, o32
+    assert len(rec) == 2
+    report = []
+    with torch.no_grad():
+        for mod, dirs, inp, out in rec:
+            xi = _nchw(inp)
+            a1 = F.relu(_bn(F.conv2d(xi, mod.branch1.conv.weight, padding=1), mod.branch1.bn))
+            a2 = F.relu(_bn(F.conv2d(xi, mod.branch2.conv.weight, padding=1), mod.branch2.bn))
+            s = CP.forward(a1, dirs[0]) + CP.forward(a2, dirs[1])
+            mg = _bn(F.conv2d(s, mod.branchMerge.weight, padding=1), mod.branchMergeBn)
+            sc = _bn(F.conv2d(xi, mod.shortcutConv.weight), mod.shortcutBn)
+            r = F.relu(mg + sc)
+            ref = F.relu(_bn(F.conv2d(r, mod.lastConv.conv.weight, padding=1), mod.lastConv.bn))
+            check("cornerpool %d%d" % dirs, _nchw(out), ref, report)
+    _print(report)
+    losses = _train_steps(m16, plugin, x, ys, 4)
+    assert all(math.isfinite(v) for v in losses) and losses[-1] < losses[0], losses
+
+
+def test_res50_1024_b16_bf16_config4_trains():
+    """BASELINE configs[4] per GPU: centerOffsetRes50 at 1024^2, 16 images, bf16, the reference's own initialisation
+    (seed 42, residuals.py:336-353) -- finite, decreasing loss over 6 Adam steps (per-group numerics:
+    test_bf16_groups_match_fp32)."""
+    import trainer.model.centerOffsetRes50 as plugin
+    torch.random.manual_seed(42)
+    m = plugin.model(**plugin.modelParams).to(DEV).train().set_compute_dtype(torch.bfloat16)
+    g = torch.Generator().manual_seed(1000)
+    B, S = 16, 1024
+    H = S // 4
+    x = torch.randn(B, 1, S, S, generator=g).to(DEV)
+    heat = (torch.rand(B, 1, H, H, generator=g) > 0.999).float()
+    mask = torch.arange(30)[None, :] < torch.randint(5, 21, (B, 1), generator=g)
+    regr = torch.rand(B, 30, 6, generator=g) * 4
+    inds = torch.randint(0, H * H, (B, 30), generator=g) * mask
+    ys = [heat.to(DEV), mask.to(DEV), regr.to(DEV), inds.to(DEV)]
+    losses = _train_steps(m, plugin, x, ys, 6)
+    print("res50 1024^2 B=16 bf16 losses", losses)
+    assert all(math.isfinite(v) for v in losses) and max(losses[-2:]) < losses[0], losses
