@@ -66,7 +66,7 @@ def cpu_baseline(steps):
                       "after 1 warm-up (%.1f s)" % (steps, dt)}
 
 
-HEADS_KERNEL = "conv_gemm_pp_kernel<bf16,256,192,heads>"
+HEADS_KERNEL = "conv_gemm_heads384_kernel"
 
 
 def train_gflop_per_img(model, S):

@@ -1097,6 +1097,246 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
 }
 
 // -------------------------------------------------------------------------------------
+// CenterNet head convolution (centerNetOffset.py:106-110) for the three 128-wide heads: ONE 192 x 384 tile
+// covers every hidden channel of 192 pixels, so the input (A) panel is read once (the 256 x 192 ping-pong
+// tiles above read it twice, through L2) and each head's 1x1 tail sees its whole hidden vector in the same
+// workgroup (no partial sums, no atomics, no memset).  8 waves in two staggered groups of 4 (ping-pong, as
+// conv_gemm_pp_kernel): group g owns pixel rows 96g..96g+95, wave wc of a group owns channels 96wc..96wc+95
+// (6 x 6 blocks of 16 x 16, 144 accumulator registers), BK = 64, two LDS stage buffers filled by LDS-DMA.
+// A K-stage runs as 3 phases (one 32-pixel third of the group's rows each), each an L part (fragment reads
+// + DMA issues for the next stage) and a C part (24 MFMAs: twice the MFMAs per DMA instruction and per
+// barrier of the 256 x 192 tile).  DMA per wave and stage: P1 A third 0 + B rows 0..23 of the wave (4
+// instructions), P2 B rows 24..47 (3), P3 A thirds 1, 2 (2).  Waits: end of L3 vmcnt(2) (A third 0 and all
+// of B for the next stage: B is read by both groups, so every wave's B DMAs land before the barrier that
+// opens the other group's next L1), end of C1 vmcnt(5) (A third 1 of this stage), end of C2 vmcnt(7)
+// (A third 2).  Every region is rewritten >= 3 segments after its last fragment read.
+// Epilogue: bias + ReLU, the 192 x 384 hidden tile staged in LDS (rows of 784 B), coalesced 16-B NHWC
+// stores of the hidden activation, then the 1x1 tails: one thread per (pixel, head) with the head
+// wave-uniform, so its 1x1 weights come through the scalar cache; outputs NCHW fp32.
+__global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p) {
+    typedef __bf16 T;
+    constexpr int BM = 192, BN = 384, BK = 64, EPC = 8;
+    constexpr int NA = 6, NB = 6;                     // 16-row / 16-column blocks per wave
+    constexpr int STAGE = (BM + BN) * 128;
+    constexpr int EROW = BN * 2 + 16;
+    constexpr int EPI = BM * EROW;
+    constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    int bid;
+    {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+    }
+    const scd_gemm_phase& ph = p.ph[0];
+    const int mt = bid;
+    const int QQ = ph.Qh * ph.Qw;
+    const int M = p.N * QQ;
+
+    const int lrow = lane >> 3;
+    const int cch = (lane & 7) ^ lrow;
+    // A: this lane's DMA rows 96*grp + 32*j + 8*wc + lrow (j = third), byte offset at tap (0,0) + in-image tap mask
+    int a_base[3];
+    unsigned a_mask[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int m = mt * BM + 96 * grp + 32 * j + 8 * wc + lrow;
+        const bool ok = m < M;
+        const int mm = ok ? m : 0;
+        const int n = mm / QQ;
+        const int rem = mm - n * QQ;
+        const int qh = rem / ph.Qw;
+        const int qw = rem - qh * ph.Qw;
+        a_base[j] = ((n * p.Hi + qh) * p.Wi + qw) * p.Ci * 2 + cch * EPC * 2;
+        unsigned msk = 0;
+        for (int t = 0; t < ph.ntaps; ++t) {
+            const int ih = qh + ph.dh[t], iw = qw + ph.dw[t];
+            if (ok && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) msk |= 1u << t;
+        }
+        a_mask[j] = msk;
+    }
+    // B: rows 192*grp + 48*wc + 8*o + lrow, o = 0..5 (part 1: o < 3, part 2: o >= 3)
+    int b_base[6];
+#pragma unroll
+    for (int o = 0; o < 6; ++o) b_base[o] = ((192 * grp + 48 * wc + 8 * o + lrow) * p.wrow + cch * EPC) * 2;
+    const int cpt = p.Ci / BK;
+    const int KT = ph.ntaps * cpt;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+
+    struct StageArgs { int live, tap, adelta, bdelta; };
+    auto stage_args = [&](int kt_req) {
+        StageArgs a;
+        a.live = kt_req < KT;
+        const int kt = min(kt_req, KT - 1);
+        const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
+        a.tap = tap;
+        a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * BK) * 2;
+        a.bdelta = (ph.wt[tap] * p.Ci + chunk * BK) * 2;
+        return a;
+    };
+    auto issue_a = [&](const StageArgs& g, char* buf, int j) {
+        const bool ok = g.live && ((a_mask[j] >> g.tap) & 1u);
+        dma16(xrs, buf + (96 * grp + 32 * j + 8 * wc) * 128, sel_off(ok, a_base[j] + g.adelta));
+    };
+    auto issue_b = [&](const StageArgs& g, char* buf, int part) {
+        char* Bs = buf + BM * 128;
+#pragma unroll
+        for (int o = 3 * part; o < 3 * part + 3; ++o)
+            dma16(wrs, Bs + (192 * grp + 48 * wc + 8 * o) * 128, sel_off(g.live, b_base[o] + g.bdelta));
+    };
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int l7 = l16 & 7;
+    const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
+    f32x4 acc[NA][NB];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 bfr[NB][2], af[2][2];
+
+    auto read_b = [&](const char* buf) {
+        const char* Bs = buf + BM * 128;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const char* row = Bs + (96 * wc + 16 * b + l16) * 128;
+            bfr[b][0] = *(const bf16x8*)(row + co0);
+            bfr[b][1] = *(const bf16x8*)(row + co1);
+        }
+    };
+    auto read_a = [&](const char* buf, int q) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const char* row = buf + (96 * grp + 32 * q + 16 * a + l16) * 128;
+            af[a][0] = *(const bf16x8*)(row + co0);
+            af[a][1] = *(const bf16x8*)(row + co1);
+        }
+    };
+    auto mfma_q = [&](int q) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b][s], af[a][s], acc[2 * q + a][b], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    if (KT > 0) {
+        {
+            const StageArgs g0 = stage_args(0);
+            issue_a(g0, smem, 0);
+            issue_b(g0, smem, 0);
+            issue_b(g0, smem, 1);
+            issue_a(g0, smem, 1);
+            issue_a(g0, smem, 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
+        for (int t = 0; t < KT; ++t) {
+            char* cur = smem + (t & 1) * STAGE;
+            char* nxt = smem + ((t & 1) ^ 1) * STAGE;
+            const StageArgs g = stage_args(t + 1);
+            // P1
+            read_b(cur);
+            read_a(cur, 0);
+            issue_a(g, nxt, 0);
+            issue_b(g, nxt, 0);
+            bar();
+            mfma_q(0);
+            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");     // A third 1 of this stage (issued in P3 of t-1)
+            bar();
+            // P2
+            read_a(cur, 1);
+            issue_b(g, nxt, 1);
+            bar();
+            mfma_q(1);
+            asm volatile("s_waitcnt vmcnt(7)" ::: "memory");     // A third 2 of this stage
+            bar();
+            // P3
+            read_a(cur, 2);
+            issue_a(g, nxt, 1);
+            issue_a(g, nxt, 2);
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");     // next stage: A third 0 and every B row
+            bar();
+            mfma_q(2);
+            bar();
+        }
+        if (grp == 0) bar();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- epilogue: bias + ReLU, the hidden tile staged in LDS
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int col0 = 96 * wc + 16 * b + 4 * lg;
+        const float4 bb = *(const float4*)(p.bias + col0);
+        const float bias[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[a][b][r] + bias[r], 0.f);
+            *(bf16x4*)(smem + (96 * grp + 16 * a + l16) * EROW + col0 * 2) = o;
+        }
+    }
+    __syncthreads();
+    // hidden activation (NHWC, 384 channels): 48 16-B chunks per pixel row
+    for (int idx = tid; idx < BM * 48; idx += 512) {
+        const int row = idx / 48, ch = idx - (idx / 48) * 48;
+        const int m = mt * BM + row;
+        if (m < M) *(uint4*)(p.y + ((long)m * BN + ch * EPC) * 2) = *(const uint4*)(smem + row * EROW + ch * 16);
+    }
+    // 1x1 tails: (pixel, head) = (i % 192, i / 192), the head wave-uniform
+    for (int i = tid; i < BM * 3; i += 512) {
+        const int h = __builtin_amdgcn_readfirstlane(i / BM);
+        const int r = i - h * BM;
+        const int m = mt * BM + r;
+        const int od = p.head_od[h];
+        const float* w = p.head_w[h];
+        float o4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int c = 0; c < 128; c += EPC) {
+            float v[EPC];
+            Vec16<T>::load(smem + r * EROW + (128 * h + c) * 2, v);
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (o < od) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) a += v[e] * w[o * 128 + c + e];
+                    o4[o] += a;
+                }
+            }
+        }
+        if (m < M) {
+            const int n = m / QQ, pix = m - (m / QQ) * QQ;
+#pragma unroll
+            for (int o = 0; o < 4; ++o)
+                if (o < od) p.head_out[h][((long)n * od + o) * QQ + pix] = o4[o] + p.head_b[h][o];
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------
 // Halo variant of the ping-pong kernel for 3x3 stride-1 convolutions (Conv2d fwd and its dgrad, the
 // head convolution): the 256-pixel tile is a TH x TW block of one image (TW = 32 or 16, TH = 256/TW), the
 // K loop runs channel chunks of 64 (outer) x 9 taps (inner), and each chunk's (TH+2) x (TW+2) input halo is
@@ -2377,6 +2617,15 @@ static int h64_mode() {
     return mode;
 }
 
+static int heads384_mode() {
+    static int mode = -2;
+    if (mode == -2) {
+        const char* e = getenv("SCD_GEMM_HEADS384");
+        mode = e ? atoi(e) : 1;
+    }
+    return mode;
+}
+
 static int num_cus() {
     static int n = 0;
     if (n == 0) {
@@ -2424,6 +2673,21 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         for (int t = 0; t < phases[i].ntaps; ++t)
             if (phases[i].wt[t] < 0 || (long)(phases[i].wt[t] + 1) * p.Ci > p.wrow) return SCD_ERR_ARG;
         Mtot += (long)p.N * phases[i].Qh * phases[i].Qw;
+    }
+    if (p.head_on && dtype == SCD_DT_BF16 && heads384_mode() && nphase == 1 && p.Co == 384 && p.head_out[0] &&
+        p.head_out[1] && p.head_out[2] && !p.head_out[3] && p.is == 1 && p.os == 1 && p.Ho == phases[0].Qh &&
+        p.Wo == phases[0].Qw && p.bias && p.relu && !p.accumulate && !p.stats) {
+        // the three 128-wide CenterNet heads: one 192 x 384 tile per 192 pixels, tails fused
+        const long wb = (long)p.Co * p.wrow * esz;
+        if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
+        p.xbytes = (int)xb;
+        p.wbytes = (int)wb;
+        p.ntn = 1;
+        p.ph[0] = phases[0];
+        for (int i = 0; i <= SCD_MAX_PHASES; ++i) p.tile_start[i] = 0;
+        const int tiles = cdiv(Mtot, 192);
+        hipLaunchKernelGGL(conv_gemm_heads384_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, p);
+        SCD_RETURN_LAUNCH();
     }
     {
         // ping-pong 256 x BN kernel when the grid fills the chip (fused head tails are run as a separate pass)

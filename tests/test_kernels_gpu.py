@@ -122,15 +122,15 @@ def test_deconv_fwd_dgrad_wgrad(case, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("N", [1, 2])
-def test_heads_fused_gemm(N, dtype):
+@pytest.mark.parametrize("N,H,W", [(1, 128, 128), (2, 128, 128), (3, 37, 45)])
+def test_heads_fused_gemm(N, H, W, dtype):
     """scd_conv_gemm_heads (3x3 conv + bias + ReLU with the three 1x1 tails in the epilogue) against
-    torch fp32; N=2 runs the bf16 ping-pong kernel, whose 192-wide column tiles split head 1 (two partial
-    sums added onto its zeroed output)."""
+    torch fp32, hidden activation and head outputs; bf16 runs conv_gemm_heads384_kernel (one 192 x 384 tile
+    per 192 pixels; 3x37x45 ends in a ragged tile and has image borders inside tiles)."""
     from scdhip import ops
     L = ops.L
     g = torch.Generator().manual_seed(31 + N)
-    Cin, H, W, od = 256, 128, 128, [1, 4, 2]
+    Cin, od = 256, [1, 4, 2]
     x = torch.randn(N, Cin, H, W, generator=g)
     w0 = [torch.randn(128, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5 for _ in od]
     b0 = [0.1 * torch.randn(128, generator=g) for _ in od]
@@ -155,6 +155,8 @@ def test_heads_fused_gemm(N, dtype):
     for o, r in zip(outs, refs):
         assert torch.isfinite(o).all()
         assert rel_err(o, r) < TOL[dtype] * (3 if dtype == torch.bfloat16 else 10)
+    hid_ref = torch.cat([F.relu(F.conv2d(x, a, b, padding=1)) for a, b in zip(w0, b0)], 1)
+    assert rel_err(nchw(hid), hid_ref) < TOL[dtype] * 2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
