@@ -22,6 +22,19 @@
 #ifndef SCD_ABLATE
 #define SCD_ABLATE 0
 #endif
+#ifndef H384_PRIO
+#define H384_PRIO 0   // heads384 kernel MFMA priority: 0 = s_setprio 1 around each C part, 1 = group 1 static, 2 = none
+#endif
+#ifndef H384_PERSIST
+#define H384_PERSIST 0  // heads384 kernel persistent over tiles (SCD_GEMM_HEADS384_GRID workgroups per CU)
+#endif
+#ifndef H384_ABL
+#define H384_ABL 0    // heads384 timing ablations (wrong results): 1 no MFMA, 2 loop DMAs read nothing, 4 no loop
+                      // fragment reads, 8 no hidden store / tails, 16 no loop barriers, 32 no tails, 64 no hidden store
+#endif
+#ifndef H384_SCHED
+#define H384_SCHED 0  // heads384 DMA order: 0 = P1 {A0, B part 1}, 1 = P1 {B part 1}, P2 {A0, B part 2}
+#endif
 #ifndef SCD_ABM
 #define SCD_ABM 0     // halo kernel ablation bitmask: 1 no MFMA, 2 no loop DMA, 4 no loop fragment reads, 8 no loop barriers
 #endif
@@ -1133,206 +1146,256 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
     }
     const scd_gemm_phase& ph = p.ph[0];
-    const int mt = bid;
     const int QQ = ph.Qh * ph.Qw;
     const int M = p.N * QQ;
 
+    const int ntiles = (M + BM - 1) / BM;
     const int lrow = lane >> 3;
     const int cch = (lane & 7) ^ lrow;
-    // A: this lane's DMA rows 96*grp + 32*j + 8*wc + lrow (j = third), byte offset at tap (0,0) + in-image tap mask
-    int a_base[3];
-    unsigned a_mask[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int m = mt * BM + 96 * grp + 32 * j + 8 * wc + lrow;
-        const bool ok = m < M;
-        const int mm = ok ? m : 0;
-        const int n = mm / QQ;
-        const int rem = mm - n * QQ;
-        const int qh = rem / ph.Qw;
-        const int qw = rem - qh * ph.Qw;
-        a_base[j] = ((n * p.Hi + qh) * p.Wi + qw) * p.Ci * 2 + cch * EPC * 2;
-        unsigned msk = 0;
-        for (int t = 0; t < ph.ntaps; ++t) {
-            const int ih = qh + ph.dh[t], iw = qw + ph.dw[t];
-            if (ok && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) msk |= 1u << t;
+#if H384_PERSIST
+    // persistent over tiles (measured no faster than one workgroup per tile; SCD_GEMM_HEADS384_GRID)
+    for (int mt = bid; mt < ntiles; mt += gridDim.x) {
+#else
+    {
+        const int mt = bid;
+        (void)ntiles;
+#endif
+        // A: this lane's DMA rows 96*grp + 32*j + 8*wc + lrow (j = third), byte offset at tap (0,0) + in-image tap mask
+        int a_base[3];
+        unsigned a_mask[3];
+    #pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int m = mt * BM + 96 * grp + 32 * j + 8 * wc + lrow;
+            const bool ok = m < M;
+            const int mm = ok ? m : 0;
+            const int n = mm / QQ;
+            const int rem = mm - n * QQ;
+            const int qh = rem / ph.Qw;
+            const int qw = rem - qh * ph.Qw;
+            a_base[j] = ((n * p.Hi + qh) * p.Wi + qw) * p.Ci * 2 + cch * EPC * 2;
+            unsigned msk = 0;
+            for (int t = 0; t < ph.ntaps; ++t) {
+                const int ih = qh + ph.dh[t], iw = qw + ph.dw[t];
+                if (ok && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) msk |= 1u << t;
+            }
+            a_mask[j] = msk;
         }
-        a_mask[j] = msk;
-    }
-    // B: rows 192*grp + 48*wc + 8*o + lrow, o = 0..5 (part 1: o < 3, part 2: o >= 3)
-    int b_base[6];
-#pragma unroll
-    for (int o = 0; o < 6; ++o) b_base[o] = ((192 * grp + 48 * wc + 8 * o + lrow) * p.wrow + cch * EPC) * 2;
-    const int cpt = p.Ci / BK;
-    const int KT = ph.ntaps * cpt;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+        // B: rows 192*grp + 48*wc + 8*o + lrow, o = 0..5 (part 1: o < 3, part 2: o >= 3)
+        int b_base[6];
+    #pragma unroll
+        for (int o = 0; o < 6; ++o) b_base[o] = ((192 * grp + 48 * wc + 8 * o + lrow) * p.wrow + cch * EPC) * 2;
+        const int cpt = p.Ci / BK;
+        const int KT = ph.ntaps * cpt;
+        const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
 
-    struct StageArgs { int live, tap, adelta, bdelta; };
-    auto stage_args = [&](int kt_req) {
-        StageArgs a;
-        a.live = kt_req < KT;
-        const int kt = min(kt_req, KT - 1);
-        const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
-        a.tap = tap;
-        a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * BK) * 2;
-        a.bdelta = (ph.wt[tap] * p.Ci + chunk * BK) * 2;
-        return a;
-    };
-    auto issue_a = [&](const StageArgs& g, char* buf, int j) {
-        const bool ok = g.live && ((a_mask[j] >> g.tap) & 1u);
-        dma16(xrs, buf + (96 * grp + 32 * j + 8 * wc) * 128, sel_off(ok, a_base[j] + g.adelta));
-    };
-    auto issue_b = [&](const StageArgs& g, char* buf, int part) {
-        char* Bs = buf + BM * 128;
-#pragma unroll
-        for (int o = 3 * part; o < 3 * part + 3; ++o)
-            dma16(wrs, Bs + (192 * grp + 48 * wc + 8 * o) * 128, sel_off(g.live, b_base[o] + g.bdelta));
-    };
+        struct StageArgs { int live, tap, adelta, bdelta; };
+        auto stage_args = [&](int kt_req) {
+            StageArgs a;
+            a.live = kt_req < KT;
+            const int kt = min(kt_req, KT - 1);
+            const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
+            a.tap = tap;
+            a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * BK) * 2;
+            a.bdelta = (ph.wt[tap] * p.Ci + chunk * BK) * 2;
+            return a;
+        };
+        auto issue_a = [&](const StageArgs& g, char* buf, int j) {
+            const bool ok = g.live && ((a_mask[j] >> g.tap) & 1u);
+            dma16(xrs, buf + (96 * grp + 32 * j + 8 * wc) * 128, sel_off(ok, a_base[j] + g.adelta));
+        };
+        auto issue_b = [&](const StageArgs& g, char* buf, int part) {
+            char* Bs = buf + BM * 128;
+    #pragma unroll
+            for (int o = 3 * part; o < 3 * part + 3; ++o)
+                dma16(wrs, Bs + (192 * grp + 48 * wc + 8 * o) * 128, sel_off(g.live, b_base[o] + g.bdelta));
+        };
 
-    const int l16 = lane & 15, lg = lane >> 4;
-    const int l7 = l16 & 7;
-    const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
-    f32x4 acc[NA][NB];
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 bfr[NB][2], af[2][2];
+        const int l16 = lane & 15, lg = lane >> 4;
+        const int l7 = l16 & 7;
+        const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
+        f32x4 acc[NA][NB];
+    #pragma unroll
+        for (int a = 0; a < NA; ++a)
+    #pragma unroll
+            for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        bf16x8 bfr[NB][2], af[2][2];
 
-    auto read_b = [&](const char* buf) {
-        const char* Bs = buf + BM * 128;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const char* row = Bs + (96 * wc + 16 * b + l16) * 128;
-            bfr[b][0] = *(const bf16x8*)(row + co0);
-            bfr[b][1] = *(const bf16x8*)(row + co1);
-        }
-    };
-    auto read_a = [&](const char* buf, int q) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            const char* row = buf + (96 * grp + 32 * q + 16 * a + l16) * 128;
-            af[a][0] = *(const bf16x8*)(row + co0);
-            af[a][1] = *(const bf16x8*)(row + co1);
-        }
-    };
-    auto mfma_q = [&](int q) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int b = 0; b < NB; ++b)
-                    acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b][s], af[a][s], acc[2 * q + a][b], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto bar = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
+        auto read_b = [&](const char* buf) {
+            const char* Bs = buf + BM * 128;
+    #pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const char* row = Bs + (96 * wc + 16 * b + l16) * 128;
+                bfr[b][0] = *(const bf16x8*)(row + co0);
+                bfr[b][1] = *(const bf16x8*)(row + co1);
+            }
+        };
+        auto read_a = [&](const char* buf, int q) {
+    #pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const char* row = buf + (96 * grp + 32 * q + 16 * a + l16) * 128;
+                af[a][0] = *(const bf16x8*)(row + co0);
+                af[a][1] = *(const bf16x8*)(row + co1);
+            }
+        };
+        auto mfma_q = [&](int q) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (H384_PRIO == 0) __builtin_amdgcn_s_setprio(1);
+            if constexpr (H384_ABL & 1) {
+    #pragma unroll
+                for (int s = 0; s < 2; ++s) {
+    #pragma unroll
+                    for (int a = 0; a < 2; ++a) asm volatile("" ::"v"(af[a][s]));
+    #pragma unroll
+                    for (int b = 0; b < NB; ++b) asm volatile("" ::"v"(bfr[b][s]));
+                }
+            } else {
+    #pragma unroll
+            for (int s = 0; s < 2; ++s)
+    #pragma unroll
+                for (int a = 0; a < 2; ++a)
+    #pragma unroll
+                    for (int b = 0; b < NB; ++b)
+                        acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b][s], af[a][s], acc[2 * q + a][b], 0, 0, 0);
+            }
+            if constexpr (H384_PRIO == 0) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto bar = [&]() {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(H384_ABL & 16)) __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
 
-    if (KT > 0) {
-        {
-            const StageArgs g0 = stage_args(0);
-            issue_a(g0, smem, 0);
-            issue_b(g0, smem, 0);
-            issue_b(g0, smem, 1);
-            issue_a(g0, smem, 1);
-            issue_a(g0, smem, 2);
+        if (KT > 0) {
+            {
+                const StageArgs g0 = stage_args(0);
+                issue_a(g0, smem, 0);
+                issue_b(g0, smem, 0);
+                issue_b(g0, smem, 1);
+                issue_a(g0, smem, 1);
+                issue_a(g0, smem, 2);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();
+            if constexpr (H384_ABL & 4) { read_b(smem); read_a(smem, 0); }
+            if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
+            if constexpr (H384_PRIO == 1) { if (grp == 1) __builtin_amdgcn_s_setprio(1); }
+            for (int t = 0; t < KT; ++t) {
+                char* cur = smem + (t & 1) * STAGE;
+                char* nxt = smem + ((t & 1) ^ 1) * STAGE;
+                StageArgs g = stage_args(t + 1);
+                if constexpr (H384_ABL & 2) g.live = 0;
+                // P1
+                if constexpr (!(H384_ABL & 4)) { read_b(cur); read_a(cur, 0); }
+                if constexpr (H384_SCHED == 0) issue_a(g, nxt, 0);
+                issue_b(g, nxt, 0);
+                bar();
+                mfma_q(0);
+                if constexpr (H384_SCHED == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // A third 1 (P3 of t-1)
+                else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                bar();
+                // P2
+                if constexpr (!(H384_ABL & 4)) read_a(cur, 1);
+                if constexpr (H384_SCHED == 1) issue_a(g, nxt, 0);
+                issue_b(g, nxt, 1);
+                bar();
+                mfma_q(1);
+                asm volatile("s_waitcnt vmcnt(7)" ::: "memory");     // A third 2 of this stage
+                bar();
+                // P3
+                if constexpr (!(H384_ABL & 4)) read_a(cur, 2);
+                issue_a(g, nxt, 1);
+                issue_a(g, nxt, 2);
+                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");     // next stage: A third 0 and every B row
+                bar();
+                mfma_q(2);
+                bar();
+            }
+            if (grp == 0) bar();
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();
-        if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
-        for (int t = 0; t < KT; ++t) {
-            char* cur = smem + (t & 1) * STAGE;
-            char* nxt = smem + ((t & 1) ^ 1) * STAGE;
-            const StageArgs g = stage_args(t + 1);
-            // P1
-            read_b(cur);
-            read_a(cur, 0);
-            issue_a(g, nxt, 0);
-            issue_b(g, nxt, 0);
-            bar();
-            mfma_q(0);
-            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");     // A third 1 of this stage (issued in P3 of t-1)
-            bar();
-            // P2
-            read_a(cur, 1);
-            issue_b(g, nxt, 1);
-            bar();
-            mfma_q(1);
-            asm volatile("s_waitcnt vmcnt(7)" ::: "memory");     // A third 2 of this stage
-            bar();
-            // P3
-            read_a(cur, 2);
-            issue_a(g, nxt, 1);
-            issue_a(g, nxt, 2);
-            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");     // next stage: A third 0 and every B row
-            bar();
-            mfma_q(2);
-            bar();
-        }
-        if (grp == 0) bar();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+        __syncthreads();
 
-    // ---- epilogue: bias + ReLU, the hidden tile staged in LDS
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int col0 = 96 * wc + 16 * b + 4 * lg;
-        const float4 bb = *(const float4*)(p.bias + col0);
-        const float bias[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[a][b][r] + bias[r], 0.f);
-            *(bf16x4*)(smem + (96 * grp + 16 * a + l16) * EROW + col0 * 2) = o;
+        // ---- epilogue: bias + ReLU, the hidden tile staged in LDS
+    #pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int col0 = 96 * wc + 16 * b + 4 * lg;
+            const float4 bb = *(const float4*)(p.bias + col0);
+            const float bias[4] = {bb.x, bb.y, bb.z, bb.w};
+    #pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                bf16x4 o;
+    #pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[a][b][r] + bias[r], 0.f);
+                *(bf16x4*)(smem + (96 * grp + 16 * a + l16) * EROW + col0 * 2) = o;
+            }
         }
-    }
-    __syncthreads();
-    // hidden activation (NHWC, 384 channels): 48 16-B chunks per pixel row
-    for (int idx = tid; idx < BM * 48; idx += 512) {
-        const int row = idx / 48, ch = idx - (idx / 48) * 48;
-        const int m = mt * BM + row;
-        if (m < M) *(uint4*)(p.y + ((long)m * BN + ch * EPC) * 2) = *(const uint4*)(smem + row * EROW + ch * 16);
-    }
-    // 1x1 tails: (pixel, head) = (i % 192, i / 192), the head wave-uniform
-    for (int i = tid; i < BM * 3; i += 512) {
-        const int h = __builtin_amdgcn_readfirstlane(i / BM);
-        const int r = i - h * BM;
-        const int m = mt * BM + r;
-        const int od = p.head_od[h];
-        const float* w = p.head_w[h];
-        float o4[4] = {0.f, 0.f, 0.f, 0.f};
+        __syncthreads();
+        if constexpr (H384_ABL & 8) { __syncthreads(); return; }
+        // 1x1 tails as a small MFMA GEMM on the staged hidden tile: out[px][o] = sum_c hid[px][c] * W1[c][o] with the
+        // three heads' 1x1 weights block-diagonal in W1 (o < sum od <= 16 columns, K = 384): 12 k-steps per
+        // 16-pixel block, fp32 weights split into bf16 hi + lo parts (two MFMAs per k-step, ~2^-17 relative weight
+        // error); wave w takes the pixel blocks w and w + 8
+        if constexpr (!(H384_ABL & 32)) {
+            int o = lane & 15;
+            asm volatile("" : "+v"(o));          // tile-invariant setup stays here (not hoisted across the K loop)
+            const int od0 = p.head_od[0], od1 = p.head_od[1], od2 = p.head_od[2];
+            const int hh = o < od0 ? 0 : o < od0 + od1 ? 1 : o < od0 + od1 + od2 ? 2 : -1;
+            const int oo = hh == 0 ? o : hh == 1 ? o - od0 : o - od0 - od1;
+            const int odh = hh == 0 ? od0 : hh == 1 ? od1 : od2;
+            const float* wsel = hh == 0 ? p.head_w[0] : hh == 1 ? p.head_w[1] : p.head_w[2];
+            const float bsel = hh < 0 ? 0.f : (hh == 0 ? p.head_b[0] : hh == 1 ? p.head_b[1] : p.head_b[2])[oo];
+            float* osel = hh == 0 ? p.head_out[0] : hh == 1 ? p.head_out[1] : p.head_out[2];
+            for (int rb = wave; rb < BM / 16; rb += 8) {
+                f32x4 c = (f32x4){0.f, 0.f, 0.f, 0.f};
+                const char* arow = smem + (16 * rb + l16) * EROW + 16 * lg;
 #pragma unroll 4
-        for (int c = 0; c < 128; c += EPC) {
-            float v[EPC];
-            Vec16<T>::load(smem + r * EROW + (128 * h + c) * 2, v);
+                for (int ks = 0; ks < 12; ++ks) {
+                    const int c0 = 32 * ks + 8 * lg;
+                    float w8[8];
+                    if (hh == (c0 >> 7)) {
+                        const float4 u = *(const float4*)(wsel + oo * 128 + (c0 & 127));
+                        const float4 v = *(const float4*)(wsel + oo * 128 + (c0 & 127) + 4);
+                        w8[0] = u.x; w8[1] = u.y; w8[2] = u.z; w8[3] = u.w;
+                        w8[4] = v.x; w8[5] = v.y; w8[6] = v.z; w8[7] = v.w;
+                    } else {
 #pragma unroll
-            for (int o = 0; o < 4; ++o) {
-                if (o < od) {
-                    float a = 0.f;
+                        for (int e = 0; e < 8; ++e) w8[e] = 0.f;
+                    }
+                    bf16x8 whi, wlo;
 #pragma unroll
-                    for (int e = 0; e < EPC; ++e) a += v[e] * w[o * 128 + c + e];
-                    o4[o] += a;
+                    for (int e = 0; e < 8; ++e) {
+                        whi[e] = (__bf16)w8[e];
+                        wlo[e] = (__bf16)(w8[e] - (float)whi[e]);
+                    }
+                    const bf16x8 av = *(const bf16x8*)(arow + 64 * ks);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, whi, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wlo, c, 0, 0, 0);
+                }
+                if (hh >= 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int m = mt * BM + 16 * rb + 4 * lg + r;
+                        if (m < M) {
+                            const int n = m / QQ, pix = m - (m / QQ) * QQ;
+                            osel[((long)n * odh + oo) * QQ + pix] = c[r] + bsel;
+                        }
+                    }
                 }
             }
         }
-        if (m < M) {
-            const int n = m / QQ, pix = m - (m / QQ) * QQ;
-#pragma unroll
-            for (int o = 0; o < 4; ++o)
-                if (o < od) p.head_out[h][((long)n * od + o) * QQ + pix] = o4[o] + p.head_b[h][o];
+        // hidden activation (NHWC, 384 channels): 48 16-B chunks per pixel row, stored last so that no later load
+        // of the tile (the tails' weights) waits behind these stores in vmcnt order
+        if constexpr (!(H384_ABL & 64))
+        for (int idx = tid; idx < BM * 48; idx += 512) {
+            const int row = idx / 48, ch = idx - (idx / 48) * 48;
+            const int m = mt * BM + row;
+            if (m < M) *(uint4*)(p.y + ((long)m * BN + ch * EPC) * 2) = *(const uint4*)(smem + row * EROW + ch * 16);
         }
+        __syncthreads();                 // staging consumed before the next tile's prologue DMA
     }
 }
 
@@ -2626,6 +2689,15 @@ static int heads384_mode() {
     return mode;
 }
 
+static int heads384_grid() {
+    static int mode = -2;
+    if (mode == -2) {
+        const char* e = getenv("SCD_GEMM_HEADS384_GRID");
+        mode = e ? atoi(e) : 1;
+    }
+    return mode;
+}
+
 static int num_cus() {
     static int n = 0;
     if (n == 0) {
@@ -2686,7 +2758,9 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         p.ph[0] = phases[0];
         for (int i = 0; i <= SCD_MAX_PHASES; ++i) p.tile_start[i] = 0;
         const int tiles = cdiv(Mtot, 192);
-        hipLaunchKernelGGL(conv_gemm_heads384_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, p);
+        const int per = H384_PERSIST ? heads384_grid() : 0;   // 0: one workgroup per tile; k: k per CU, persistent
+        const int grid = per > 0 ? std::min(tiles, per * num_cus()) : tiles;
+        hipLaunchKernelGGL(conv_gemm_heads384_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p);
         SCD_RETURN_LAUNCH();
     }
     {

@@ -31,6 +31,9 @@ def short(name):
     m = re.search(r"conv_gemm_ring_kernel(ILb([01])E|<(true|false)>)", n)
     if m:
         return "conv_gemm_ring_kernel<bf16,256,128%s>" % (",heads" if m.group(2) == "1" or m.group(3) == "true" else "")
+    m = re.match(r"(\w+?)ENS_\d+\w*Params", n)         # mangled, non-template kernels of the anonymous namespace
+    if m:
+        return m.group(1)
     return n.split("(")[0][:80]
 
 
