@@ -277,6 +277,11 @@ int scd_ceval_summary(const float* const* streams, const long* lens, long objnum
 /* ---- Adam (torch.optim.Adam defaults, networkFactory.py:79-82) over a flat fp32 buffer ---- */
 int scd_adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                   float eps, float bc1, float bc2, float gscale, void* stream);
+/* Same update with the step state in device memory: hyper = {lr, step} (fp64, step advanced by 1 on the stream
+ * before the update), so a captured training-step graph (scdhip/graph.py) replays with the live learning rate and
+ * bias corrections (networkFactory.py:228-234, :273-276). */
+int scd_adam_step_dev(float* p, const float* g, float* m, float* v, long n, double* hyper, float beta1, float beta2,
+                      float eps, float gscale, void* stream);
 
 /* ---- corner pooling (cornerPooling/source/{top,bottom,left,right}Pool.cpp) ----
  * dir: 0 top (max over k>=h), 1 bottom (k<=h), 2 left (k>=w), 3 right (k<=w); NHWC dtype.
@@ -288,6 +293,14 @@ int scd_cpool_bwd(int dtype, int dir, const void* x, const void* dy, void* dx, i
                   void* stream);
 
 /* library self-description (for the loader / tests) */
+/* ---- HIP events for live kernel timing (bench.py roofline; scdhip.ops.LaunchTimer) ----
+ * scd_event_record stamps the event on `stream`; while the stream is being captured into a graph the record is an
+ * external event node (hipEventRecordExternal), re-stamped by every replay.  scd_event_elapsed_ms waits for `end`. */
+int scd_event_create(void** ev);
+int scd_event_destroy(void* ev);
+int scd_event_record(void* ev, void* stream);
+int scd_event_elapsed_ms(void* start, void* end, float* ms);
+
 const char* scd_version(void);
 
 #ifdef __cplusplus

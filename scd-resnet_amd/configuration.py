@@ -2,8 +2,10 @@
 
 Same default keys and the same overlay rule: a JSON config replaces only keys that already
 exist (configuration.py:150-153); string values may reference other keys as `{key}` format
-fields.  One key is added: ``computeDtype`` ("bf16" | "fp32"), the MFMA precision of the
-HIP path (the reference trains in fp32 without AMP).
+fields.  Two keys are added: ``computeDtype`` ("bf16" | "fp32"), the MFMA precision of the
+HIP path (the reference trains in fp32 without AMP), and ``stepGraph`` (true | false, default false):
+replay the training step as a captured HIP graph after two eager steps (single-process runs;
+scdhip/graph.py -- measured slower than eager issue on ROCm 7).
 """
 import os
 
@@ -40,6 +42,7 @@ class Configuration:
         c["dirDataSplitProfile"] = "{dirDataset}{datasetName}.split.json"
         c["useGPU"] = False
         c["computeDtype"] = "bf16"
+        c["stepGraph"] = False
         self.config = c
 
     # -- formatted / plain accessors (configuration.py:46-146)
@@ -77,6 +80,7 @@ class Configuration:
     dirDatafile = property(lambda s: s._fmt("dirDatafile"))
     dirDataSplitProfile = property(lambda s: s._fmt("dirDataSplitProfile"))
     computeDtype = property(lambda s: s.config["computeDtype"])
+    stepGraph = property(lambda s: bool(s.config["stepGraph"]))
 
     def useGPU(self):
         # a bound method, hence always truthy when tested without a call (reference quirk)

@@ -611,6 +611,33 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n
     }
 }
 
+// Device-resident step state (hyper = {lr, step}, fp64) so a captured step graph replays with the current learning
+// rate and bias corrections: the tick advances the step, the update kernel derives the corrections exactly as
+// the host path does (fp64 powers rounded to fp32, torch/optim/adam.py _single_tensor_adam).
+__global__ void adam_tick_kernel(double* hyper) {
+    if (threadIdx.x == 0) hyper[1] = hyper[1] + 1.0;
+}
+
+__global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, long n, const double* hyper, float b1,
+                                float b2, float eps, float gscale) {
+    const double s = hyper[1];
+    const float lr = (float)hyper[0];
+    const float bc1 = (float)(1.0 - pow((double)b1, s));
+    const float bc2 = (float)(1.0 - pow((double)b2, s));
+    const float step = lr / bc1;
+    const float bc2_sqrt = sqrtf(bc2);
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float gi = g[i] * gscale;
+        float mi = m[i];
+        mi = mi + (1.f - b1) * (gi - mi);
+        float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = p[i] - step * (mi / denom);
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
 inline int ew_blocks(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + 255) / 256)); }
 
 }  // namespace
@@ -799,5 +826,14 @@ extern "C" int scd_adam_step(float* p, const float* g, float* m, float* v, long 
                              float eps, float bc1, float bc2, float gscale, void* stream) {
     hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
                        beta2, eps, bc1, sqrtf(bc2), gscale);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_adam_step_dev(float* p, const float* g, float* m, float* v, long n, double* hyper, float beta1,
+                                 float beta2, float eps, float gscale, void* stream) {
+    if (!hyper) return SCD_ERR_ARG;
+    hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                       (const double*)hyper, beta1, beta2, eps, gscale);
     SCD_RETURN_LAUNCH();
 }

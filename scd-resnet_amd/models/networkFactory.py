@@ -11,6 +11,8 @@ execution side:
     (enabled by the reference rule: more than one GPU on the machine, networkFactory.py:128);
   * torch.optim.Adam -> scdhip.flat.FlatAdam (same defaults: lr 1e-3 until the first decay);
   * batches are moved to this rank's device (the reference datasets pin cuda:0);
+  * with ``stepGraph`` (opt-in) a single-process run replays the step as a captured HIP graph after two
+    eager steps (scdhip.graph.StepGraph: same kernels, one hipGraphLaunch per step);
   * resume loads after the wrap and uses learningRateDecayRate[index] (fixes the reference's
     `module.` prefix mismatch and [t] index, networkFactory.py:116-124).
 The CPU path (no -gpu) is not part of this framework: the CPU restatement is oracle/.
@@ -31,6 +33,7 @@ from configuration import defaultConfig
 from logger import Logger, monitorStdOutStream
 from scdhip import ops
 from scdhip.flat import FlatAdam, FlatDDP
+from scdhip.graph import StepGraph
 
 torch.random.manual_seed(42)
 
@@ -117,6 +120,7 @@ class NetworkFactory(object):
                 defaultConfig.optimizer))
             sys.exit()
         self.device = None
+        self.stepGraph = None
 
     @property
     def isGPU(self):
@@ -148,6 +152,8 @@ class NetworkFactory(object):
         if distributed and self.GPUCOUNT > 1 and dist.get_world_size() > 1:
             ops.set_bn_sync(dist.group.WORLD)       # SyncBatchNorm semantics (networkFactory.py:128-133)
         self.model = FlatDDP(self.model)
+        if defaultConfig.stepGraph and not (distributed and dist.get_world_size() > 1):
+            self.stepGraph = StepGraph(self._trainStep, optimizer=self.optimizer, warmup=2)
         if defaultConfig.currentIteration > 0:
             learningRate = resumeSchedule(learningRate, defaultConfig.learningRateDecay,
                                           defaultConfig.learningRateDecayRate, defaultConfig.currentIteration)
@@ -233,8 +239,13 @@ class NetworkFactory(object):
         return self.loss(preds, ys)
 
     def train(self, xs, ys, **kwargs):
-        """networkFactory.py:257-263"""
+        """networkFactory.py:257-263 (replayed as a HIP graph when stepGraph is on)"""
         xs, ys = _to_device(xs, self.device), _to_device(ys, self.device)
+        if self.stepGraph is not None and not kwargs:
+            return self.stepGraph(xs, ys)
+        return self._trainStep(xs, ys, **kwargs)
+
+    def _trainStep(self, xs, ys, **kwargs):
         self.optimizer.zero_grad()
         loss, lossStats = self._passParams(xs, ys, decode=False)
         loss = loss.mean()

@@ -91,7 +91,9 @@ class FlatAdam(torch.optim.Optimizer):
         super(FlatAdam, self).__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._flat = None
         self._m = self._v = None
-        self._step = 0
+        self._step = 0          # host mirror of the device step counter (state_dict)
+        self._hyper = None      # device {lr, step} fp64, read by scd_adam_step_dev
+        self._dev_lr = None     # the lr last written to _hyper
 
     def _all_params(self):
         return [p for g in self.param_groups for p in g["params"]]
@@ -101,7 +103,18 @@ class FlatAdam(torch.optim.Optimizer):
             self._flat = ensure_flat(self._all_params())
             self._m = torch.zeros_like(self._flat.data)
             self._v = torch.zeros_like(self._flat.data)
+            self._hyper = torch.tensor([self.param_groups[0]["lr"], float(self._step)], dtype=torch.float64,
+                                       device=self._flat.data.device)
+            self._dev_lr = self.param_groups[0]["lr"]
         return self._flat
+
+    def sync_lr(self):
+        """Write the param group's lr to the device state if setLearningRate changed it (a captured step graph
+        calls this before each replay; the eager step does it itself)."""
+        lr = self.param_groups[0]["lr"]
+        if self._hyper is not None and lr != self._dev_lr:
+            self._hyper[0].fill_(lr)
+            self._dev_lr = lr
 
     def zero_grad(self, set_to_none=False):
         fp = self.flat() if self._all_params()[0].is_cuda else None
@@ -117,9 +130,10 @@ class FlatAdam(torch.optim.Optimizer):
         fp = self.flat()
         fp.rebind_grads()
         g = self.param_groups[0]
+        self.sync_lr()
         self._step += 1
-        ops.adam_step(fp.data, fp.grad, self._m, self._v, g["lr"], g["betas"][0], g["betas"][1], g["eps"],
-                      self._step, gscale=fp.grad_scale)
+        ops.adam_step_dev(fp.data, fp.grad, self._m, self._v, self._hyper, g["betas"][0], g["betas"][1], g["eps"],
+                          gscale=fp.grad_scale)
         return None
 
     def state_dict(self):
@@ -132,6 +146,9 @@ class FlatAdam(torch.optim.Optimizer):
         self._step = sd["step"]
         for g, s in zip(self.param_groups, sd["param_groups"]):
             g.update(s)
+        if self._hyper is not None:
+            self._hyper.copy_(torch.tensor([self.param_groups[0]["lr"], float(self._step)], dtype=torch.float64))
+            self._dev_lr = self.param_groups[0]["lr"]
         if sd.get("exp_avg") is not None:
             self.flat()
             self._m.copy_(sd["exp_avg"])

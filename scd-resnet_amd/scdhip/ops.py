@@ -31,6 +31,11 @@ def ptr(t):
     return 0 if t is None else t.data_ptr()
 
 
+def capturing():
+    """True while torch's current stream is being captured into a HIP graph (scdhip.graph)."""
+    return torch.cuda.is_initialized() and torch.cuda.is_current_stream_capturing()
+
+
 def _need_gpu(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -40,38 +45,94 @@ def _need_gpu(*ts):
 
 # ------------------------------------------------------------------ live kernel timing
 
+class _Event:
+    """A HIP event of libscdhip (scd_event_*): torch's ROCm build refuses external event records, which a graph
+    capture needs, so the timing events come from the library."""
+    __slots__ = ("h",)
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        L.call("scd_event_create", ctypes.byref(h))
+        self.h = h.value
+
+    def record(self):
+        L.call("scd_event_record", self.h, stream())
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        L.call("scd_event_elapsed_ms", self.h, end.h, ctypes.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        try:
+            L.lib().scd_event_destroy(self.h)
+        except Exception:
+            pass
+
+
 class LaunchTimer:
     """HIP-event pairs recorded around selected launches on the stream they are issued on
     (bench.py's roofline: the dominant kernel timed inside the timed steps).  Disabled unless
-    a name is armed, so the product path records nothing."""
+    a name is armed, so the product path records nothing.
+
+    Inside a step-graph capture (scdhip.graph) the pair is recorded as external event nodes of the graph
+    (hipEventRecordWithFlags(..., hipEventRecordExternal)): every replay re-stamps the same two events, so the
+    graph owner harvests them (``harvest``) after that replay has finished and before the graph is replayed
+    again."""
     armed = set()
-    events = {}
+    events = {}           # name -> [(start, end)] eager pairs, not yet read
+    times = {}            # name -> [ms] read pairs
+    captured = []         # (name, start, end) recorded during the current graph capture
 
     @classmethod
     def arm(cls, name):
         cls.armed.add(name)
         cls.events[name] = []
+        cls.times[name] = []
+
+    @classmethod
+    def reset(cls):
+        """Drop what was timed so far (the armed names stay armed)."""
+        for name in cls.armed:
+            cls.events[name] = []
+            cls.times[name] = []
 
     @classmethod
     def record(cls, name):
         if name not in cls.armed:
             return None
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(torch.cuda.current_stream())
+        e = _Event()
+        e.record()
         return e
 
     @classmethod
     def close(cls, name, start):
-        if start is not None:
-            cls.events[name].append((start, cls.record(name)))
+        if start is None:
+            return
+        end = cls.record(name)
+        if capturing():
+            cls.captured.append((name, start, end))
+        else:
+            cls.events[name].append((start, end))
+
+    @classmethod
+    def take_captured(cls):
+        out, cls.captured = cls.captured, []
+        return out
+
+    @classmethod
+    def harvest(cls, pairs):
+        """Read the graph-recorded pairs of a finished replay into the armed names' times."""
+        for name, a, b in pairs:
+            if name in cls.armed:
+                cls.times[name].append(a.elapsed_ms(b))
 
     @classmethod
     def mean_ms(cls, name):
-        ev = cls.events.get(name, [])
-        if not ev:
+        ts = cls.times.get(name, []) + [a.elapsed_ms(b) for a, b in cls.events.get(name, [])]
+        if not ts:
             return None
-        ev[-1][1].synchronize()
-        return sum(a.elapsed_time(b) for a, b in ev) / len(ev), len(ev)
+        return sum(ts) / len(ts), len(ts)
 
 
 # ------------------------------------------------------------------ SyncBN / process group
@@ -136,6 +197,8 @@ class PackPlan:
         self.entries = {}           # key -> [out tensor, parts, dtype, used]
         self._sig = None
         self._dev = {}              # dtype -> (device descriptor tensor, n, total)
+        self.frozen = False         # a captured step graph uses the operands / descriptors: never free them
+        self._retired = []
 
     def lookup(self, key):
         e = self.entries.get(key)
@@ -148,13 +211,22 @@ class PackPlan:
         self.entries[key] = [out, parts, dtype, True]
 
     def refresh(self):
-        # drop entries the previous step did not use, then repack the rest (one launch per dtype)
-        self.entries = {k: e for k, e in self.entries.items() if e[3]}
+        # drop entries the previous step did not use, then repack the rest (one launch per dtype); a plan that a
+        # captured step graph refers to keeps every operand and descriptor table it ever built alive
+        if capturing():
+            self.frozen = True
+        if not self.frozen:
+            self.entries = {k: e for k, e in self.entries.items() if e[3]}
         if not self.entries:
             return
         sig = tuple((k, e[0].data_ptr(), tuple(p[0].data_ptr() for p in e[1])) for k, e in self.entries.items())
         if sig != self._sig:
+            if capturing():
+                raise RuntimeError("PackPlan: the operand set changed inside a step-graph capture (run an eager "
+                                   "step first)")
             self._sig = sig
+            if self.frozen:
+                self._retired.append(self._dev)
             self._dev = {}
             per = {}
             for e in self.entries.values():
@@ -682,6 +754,12 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, gscale=1.0):
     bc2 = 1 - beta2 ** step
     L.call("scd_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(beta1), float(beta2),
            float(eps), float(bc1), float(bc2), float(gscale), stream())
+
+
+def adam_step_dev(p, g, m, v, hyper, beta1, beta2, eps, gscale=1.0):
+    """Adam with the step state on the device (hyper = {lr, step} fp64, step advanced on the stream)."""
+    L.call("scd_adam_step_dev", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(hyper), float(beta1), float(beta2),
+           float(eps), float(gscale), stream())
 
 
 def decode_topk(heat, offset, regr, K=100):

@@ -133,9 +133,12 @@ def test_augment_device_noise_statistics():
         ops.augment_tiles(torch.zeros(1, 1, 8, 6, device=DEV))   # W % 4 != 0
 
 
-def test_train_loop_on_d_archive(tmp_path):
+@pytest.mark.parametrize("graph", [False, True])
+def test_train_loop_on_d_archive(tmp_path, graph):
     """NetworkFactory end to end on a `.d` archive: split profile from disk, batches through gpu_batch
-    (GPUBatchLoader), two bf16 steps, validation through evaluation / expression, evals file written."""
+    (GPUBatchLoader), bf16 steps, validation through evaluation / expression, evals file written.  graph: the
+    stepGraph mode -- two eager steps, capture on the third, replays after; validation (eager forwards of the same
+    model) runs between replays."""
     from configuration import defaultConfig
     from models.networkFactory import NetworkFactory
     names, samples, locs = scd_archive.archive_content(seed=5, count=48, size=512)
@@ -147,7 +150,8 @@ def test_train_loop_on_d_archive(tmp_path):
     old = dict(defaultConfig.config)
     try:
         defaultConfig.updateConfig({"modelName": "centerOffsetRes10", "datasetName": "tiny", "trainName": "dtest",
-                                    "iterations": 2, "validation": 2, "snapshot": 1000, "batchSize": 16,
+                                    "iterations": 5 if graph else 2, "validation": 2, "snapshot": 1000,
+                                    "batchSize": 16, "stepGraph": graph,
                                     "dirData": "trainer.dataset.scdx16p100", "dirDatafile": path,
                                     "dirDataSplitProfile": str(split), "dirTemp": str(tmp_path / "t") + "/",
                                     "dirResult": str(tmp_path / "r") + "/", "currentIter": 0})
@@ -155,6 +159,9 @@ def test_train_loop_on_d_archive(tmp_path):
         assert len(f.dataset) == 40
         f.beginTraining(0)
         text = open(str(tmp_path / "r" / "evals.dtest.txt")).read()
+        if graph:
+            assert f.stepGraph is not None and len(f.stepGraph.graphs) == 1 and f.stepGraph.calls == 5
+            assert f.optimizer.state_dict()["step"] == 5
     finally:
         defaultConfig.config.clear()
         defaultConfig.config.update(old)

@@ -309,6 +309,30 @@ def test_adam_matches_torch():
     np.testing.assert_allclose(p.cpu().numpy(), pt.detach().numpy(), rtol=1e-6, atol=1e-7)
 
 
+def test_adam_device_state_matches_torch():
+    """scd_adam_step_dev: {lr, step} in device memory (the step-graph form), step advanced on the stream; an lr
+    change between steps is picked up."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(10)
+    p0 = torch.randn(10007, generator=g)
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=1e-3)
+    p = p0.clone().to(DEV)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    hyper = torch.tensor([1e-3, 0.0], dtype=torch.float64, device=DEV)
+    for step in range(1, 7):
+        if step == 4:
+            opt.param_groups[0]["lr"] = 2.5e-4
+            hyper[0].fill_(2.5e-4)
+        gr = torch.randn(10007, generator=g)
+        pt.grad = gr.clone()
+        opt.step()
+        ops.adam_step_dev(p, gr.to(DEV), m, v, hyper, 0.9, 0.999, 1e-8)
+    assert hyper[1].item() == 6.0
+    np.testing.assert_allclose(p.cpu().numpy(), pt.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_batched_pack_matches_single(dtype):
     """PackPlan's one-launch batched packing (mode 0 rows, mode 1 LDS-tiled transposes, concatenated head

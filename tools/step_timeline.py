@@ -11,7 +11,7 @@ with open(sys.argv[1]) as f:
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                      int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)))
 rows.sort()
-idx = [i for i, r in enumerate(rows) if r[2].startswith("adam")]
+idx = [i for i, r in enumerate(rows) if r[2].startswith("adam") and "tick" not in r[2]]
 s, e = idx[-2] + 1, idx[-1] + 1
 tot = 0
 for st, en, name, g in rows[s:e]:
