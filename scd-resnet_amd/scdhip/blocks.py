@@ -62,8 +62,21 @@ class StemFn(torch.autograd.Function):
         training = bn.training
         C = conv.weight.shape[0]
         stats = ops.bn_stats(bn, "fwd") if training else None
-        direct = (ops.stem_direct_ok(x, dtype) and tuple(conv.weight.shape) == (64, 1, 7, 7)
-                  and conv.stride[0] == 2 and conv.padding[0] == 3)
+        ref_geom = tuple(conv.weight.shape) == (64, 1, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3
+        ctx.fused = ref_geom and ops.stem_fused_ok(x, dtype)
+        ctx.st, ctx.conv, ctx.bn = None, conv, bn
+        if ctx.fused:
+            # no full-resolution activation: BN statistics from the im2col Gram matrix, conv+BN+ReLU+pool in one pass
+            x = _c(x)
+            wpk = ops.pack_weight(conv.weight, dtype, 0, ldp=64)
+            G = ops.stem_gram(x, wpk, stats) if training else None
+            st = ops.bn_finalize(bn, stats, C, x.shape[0] * ((x.shape[2] - 1) // 2 + 1) * ((x.shape[3] - 1) // 2 + 1),
+                                 training)
+            out, am, yam = ops.stem_fused_fwd(x, wpk, st)
+            ctx.save_for_backward(x, am, yam, G, wpk)
+            ctx.st = st
+            return out
+        direct = ops.stem_direct_ok(x, dtype) and ref_geom
         if direct:
             # direct 7x7/s2 conv: the tap tile is built in LDS from the input patch (no column tensor)
             x = _c(x)
@@ -82,8 +95,13 @@ class StemFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        cols, y, am = ctx.saved_tensors
         conv, bn, st = ctx.conv, ctx.bn, ctx.st
+        if ctx.fused:
+            x, am, yam, G, wpk = ctx.saved_tensors
+            ops.stem_fused_bwd(bn, st, _c(dout), am, yam, x, G, wpk, ops.grad_of(conv.weight))
+            grads_ready(conv, bn)
+            return None, None, None, None, None
+        cols, y, am = ctx.saved_tensors
         if ctx.direct:
             # pool/ReLU backward + BN reduction in one pass; the BN apply runs inside the weight gradient
             dz, coef = ops.stem_pool_bwd_bn(bn, _c(dout), am, y, st)

@@ -63,6 +63,11 @@ SIGNATURES = {
     "scd_stem_conv_wgrad_nsplit": (I, [L]),
     "scd_stem_conv_wgrad": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_pool_bwd_bn": (I, [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),
+    "scd_stem_gram": (I, [P, P, I, I, I, I, I, I, P]),
+    "scd_stem_gram_stats": (I, [P, P, P, P]),
+    "scd_stem_fused_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, P]),
+    "scd_stem_wgrad_pooled": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
+    "scd_stem_wgrad_combine": (I, [P, I, P, P, P, P, I, P]),
     "scd_stats_collapse": (I, [P, I, I, P]),
     "scd_bn_finalize": (I, [P, I, I, D, P, P, P, P, P, F, F, P, P, P, P, P]),
     "scd_bn_apply": (I, [I, P, P, I, L, P, P, P, P, P, I, P]),

@@ -705,6 +705,64 @@ def stem_conv_wgrad(dy, x, dst, accumulate=True, ybn=None, coef=None):
     L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 49, 49, 1, 0, ptr(dst), int(accumulate), stream())
 
 
+class StemFused:
+    """Stem without the full-resolution activation (stem.hip: Gram statistics, fused conv+BN+ReLU+pool forward,
+    weight gradient from the pooled side).  Opt-in (SCD_STEM_FUSED=1) until it beats the conv / pool kernel pair:
+    first version measured 0.91 ms per B=32 step against 0.67 ms (profiles)."""
+    enabled = os.environ.get("SCD_STEM_FUSED", "0") == "1"
+
+
+def stem_fused_ok(x, dtype):
+    N, _, H, W = x.shape
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+    return StemFused.enabled and dtype == torch.bfloat16 and Wo % 64 == 0 and Hp % 2 == 0 and Wp % 32 == 0
+
+
+def _stem_geom(x):
+    N, _, H, W = x.shape
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    return N, H, W, Ho, Wo, (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+
+
+def stem_gram(x, wpk, stats):
+    """G = sum over the stem's im2col rows of col col^T (fp32 [64][64], ones column at tap 49) and, into `stats`
+    (fp64 BN buffer, replica 0), the batch sums of y and y^2 it implies for the packed bf16 weight wpk."""
+    N, H, W, Ho, Wo, _, _ = _stem_geom(x)
+    ns = L.lib().scd_stem_conv_wgrad_nsplit(N * Ho * Wo)
+    ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=x.device)
+    L.call("scd_stem_gram", ptr(x), ptr(ws), ns, N, H, W, Ho, Wo, stream())
+    G = torch.empty(64 * 64, dtype=torch.float32, device=x.device)
+    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(G), 0, stream())
+    if stats is not None:
+        L.call("scd_stem_gram_stats", ptr(G), ptr(wpk), ptr(stats), stream())
+    return G
+
+
+def stem_fused_fwd(x, wpk, st):
+    """conv7x7/s2 + BN(st) + ReLU + MaxPool(3,2,1) -> (out (N,Hp,Wp,64) bf16, argmax u8, y at argmax bf16)."""
+    N, H, W, Ho, Wo, Hp, Wp = _stem_geom(x)
+    out = torch.empty(N, Hp, Wp, 64, dtype=torch.bfloat16, device=x.device)
+    am = torch.empty(N, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
+    yam = torch.empty_like(out)
+    L.call("scd_stem_fused_fwd", ptr(x), ptr(wpk), ptr(st.scale), ptr(st.shift), ptr(out), ptr(am), ptr(yam), N, H,
+           W, Ho, Wo, Hp, Wp, stream())
+    return out, am, yam
+
+
+def stem_fused_bwd(bn, st, dout, am, yam, x, G, wpk, dst):
+    """Stem backward from the pooled side: BN backward sums + the dz (x) col GEMM in one pass, SyncBN / finalize,
+    then dst (+)= a * (dz col) + b * W G + c * s."""
+    N, H, W, Ho, Wo, Hp, Wp = _stem_geom(x)
+    ns = L.lib().scd_stem_conv_wgrad_nsplit(N * Ho * Wo)
+    ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=x.device)
+    stats = bn_stats(bn, "bwd")
+    L.call("scd_stem_wgrad_pooled", ptr(dout), ptr(am), ptr(yam), ptr(st.scale), ptr(st.shift), ptr(st.mean),
+           ptr(st.invstd), ptr(x), ptr(ws), ptr(stats), ns, N, H, W, Ho, Wo, Hp, Wp, stream())
+    coef = bn_backward_coef(bn, st, stats, 64)
+    L.call("scd_stem_wgrad_combine", ptr(ws), ns, ptr(coef), ptr(G), ptr(wpk), ptr(dst), 1, stream())
+
+
 def stem_pool_fwd(y, st):
     N, H, W, C = y.shape
     Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
