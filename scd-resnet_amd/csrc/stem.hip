@@ -293,36 +293,59 @@ __global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __re
 //     dW = a * sum dz col^T + b * W G + c * s^T  (stem_wgrad_combine_kernel).
 constexpr int GONE = KK;                               // tap index of the ones column
 
-__device__ __forceinline__ void stage_patch(float* patch, const float* xn, int H, int W, int ih0, int iw0, int rows,
-                                            int cols, int tid) {
-    for (int i = tid; i < rows * cols; i += 256) {
-        const int r = i / cols, c = i - (i / cols) * cols;
+// The tap operand of a 64-pixel stage (conv row oh, pixels ow0 .. ow0+63) without an im2col tile: 8 copies of the
+// stage's 7 input rows in bf16, copy (par, u) holding x[row][2 (j + u) + par] at j = 0..63 (tile-relative input
+// columns), so the 8 pixels px0 .. px0+7 of tap (kh, kw) -- input columns 2 px + kw -- are copy (kw & 1, kw >> 1),
+// row kh, j = px0 .. px0+7: one aligned 16-B LDS read per MFMA fragment.
+constexpr int TCOPY = 128;                             // bytes per copy row (64 bf16)
+constexpr int TSZ = 8 * KS * TCOPY;                    // 7168 B per stage buffer
+constexpr int TPL = (KS * WPCOLS + 255) / 256;         // patch elements per thread (4)
+
+__device__ __forceinline__ void tap_load(float (&pv)[TPL], const float* __restrict__ x, int H, int W, int Ho, int Wo,
+                                         long ps, int tid) {
+    const int n = (int)(ps / ((long)Ho * Wo));
+    const int rem = (int)(ps - (long)n * Ho * Wo);
+    const int oh = rem / Wo, ow0 = rem - (rem / Wo) * Wo;
+    const int ih0 = oh * SP - PD, iw0 = ow0 * SP - PD;
+    const float* xn = x + (size_t)n * H * W;
+#pragma unroll
+    for (int q = 0; q < TPL; ++q) {
+        const int i = tid + 256 * q;
+        const int r = i / WPCOLS, c = i - (i / WPCOLS) * WPCOLS;
         const int ih = ih0 + r, iw = iw0 + c;
-        patch[i] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? xn[(size_t)ih * W + iw] : 0.f;
+        pv[q] = (i < KS * WPCOLS && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? xn[(size_t)ih * W + iw] : 0.f;
     }
 }
 
-// [64 taps][64 px] bf16 tile of one 64-pixel stage (pixels along one conv row), tap 49 = 1 when `ones`
-__device__ __forceinline__ void build_tap_tile(char* Cs, const float* patch, int tid, bool ones) {
-    const int k = tid >> 2, pq = tid & 3;
-    const int kh = k / KS, kw = k - (k / KS) * KS;
+__device__ __forceinline__ void tap_store(char* Ts, const float (&pv)[TPL], int tid) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        bf16x8 v;
+    for (int q = 0; q < TPL; ++q) {
+        const int i = tid + 256 * q;
+        if (i >= KS * WPCOLS) break;
+        const int r = i / WPCOLS, c = i - (i / WPCOLS) * WPCOLS;
+        const __bf16 v = (__bf16)pv[q];
+        const int par = c & 1, j = c >> 1;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int px = pq * 16 + h * 8 + e;
-            v[e] = (__bf16)(k < KK ? patch[kh * WPCOLS + SP * px + kw] : (ones && k == GONE ? 1.f : 0.f));
+        for (int u = 0; u < 4; ++u) {
+            const int jj = j - u;
+            if (jj >= 0 && jj < WPX) *(__bf16*)(Ts + ((par * 4 + u) * KS + r) * TCOPY + jj * 2) = v;
         }
-        *(bf16x8*)(Cs + swz128(k, pq * 2 + h)) = v;
     }
+}
+
+// fragment of tap k (MFMA row), pixels 8*chunk .. +7; tap 49 = ones when `ones`, taps > 49 zero
+__device__ __forceinline__ bf16x8 tap_frag(const char* Ts, int k, int chunk, bool ones) {
+    if (k < KK) {
+        const int kh = k / KS, kw = k - (k / KS) * KS;
+        return *(const bf16x8*)(Ts + (((kw & 1) * 4 + (kw >> 1)) * KS + kh) * TCOPY + chunk * 16);
+    }
+    const __bf16 v = (__bf16)((ones && k == GONE) ? 1.f : 0.f);
+    return (bf16x8){v, v, v, v, v, v, v, v};
 }
 
 __global__ __launch_bounds__(256) void stem_gram_kernel(const float* __restrict__ x, float* __restrict__ ws, int H,
                                                         int W, int Ho, int Wo, long M, int chunk) {
-    __shared__ __attribute__((aligned(16))) char smem[64 * 128 + KS * WPCOLS * 4];
-    char* Cs = smem;
-    float* patch = (float*)(smem + 64 * 128);
+    __shared__ __attribute__((aligned(16))) char smem[2 * TSZ];
     const int tid = threadIdx.x;
     const int z = blockIdx.x;
     const long p0 = (long)z * chunk;
@@ -335,22 +358,21 @@ __global__ __launch_bounds__(256) void stem_gram_kernel(const float* __restrict_
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (long ps = p0; ps < p1; ps += WPX) {
-        const int n = (int)(ps / ((long)Ho * Wo));
-        const int rem = (int)(ps - (long)n * Ho * Wo);
-        const int oh = rem / Wo, ow0 = rem - (rem / Wo) * Wo;
-        __syncthreads();
-        stage_patch(patch, x + (size_t)n * H * W, H, W, oh * SP - PD, ow0 * SP - PD, KS, WPCOLS, tid);
-        __syncthreads();
-        build_tap_tile(Cs, patch, tid, true);
+    float pv[TPL];
+    if (p0 < p1) tap_load(pv, x, H, W, Ho, Wo, p0, tid);
+    int buf = 0;
+    for (long ps = p0; ps < p1; ps += WPX, buf ^= 1) {
+        char* Ts = smem + buf * TSZ;
+        tap_store(Ts, pv, tid);                       // (double buffer: the last readers of Ts passed the previous barrier)
+        if (ps + WPX < p1) tap_load(pv, x, H, W, Ho, Wo, ps + WPX, tid);
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             bf16x8 ta[2], tb[2];
 #pragma unroll
-            for (int a = 0; a < 2; ++a) ta[a] = *(const bf16x8*)(Cs + swz128(wm * 32 + a * 16 + l16, s * 4 + lg));
+            for (int a = 0; a < 2; ++a) ta[a] = tap_frag(Ts, wm * 32 + a * 16 + l16, s * 4 + lg, true);
 #pragma unroll
-            for (int b = 0; b < 2; ++b) tb[b] = *(const bf16x8*)(Cs + swz128(wn * 32 + b * 16 + l16, s * 4 + lg));
+            for (int b = 0; b < 2; ++b) tb[b] = tap_frag(Ts, wn * 32 + b * 16 + l16, s * 4 + lg, true);
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -367,27 +389,24 @@ __global__ __launch_bounds__(256) void stem_gram_kernel(const float* __restrict_
             *(f32x4*)(wz + (wm * 32 + a * 16 + l16) * 64 + wn * 32 + b * 16 + lg * 4) = acc[a][b];
 }
 
-// stats[0][0][co] += sum_p y = W[co] . s,  stats[0][1][co] += sum_p y^2 = W[co] G W[co]^T (fp64)
-__global__ __launch_bounds__(256) void stem_gram_stats_kernel(const float* __restrict__ G, const __bf16* __restrict__ wpk,
-                                                              double* __restrict__ stats) {
-    __shared__ float Gs[KK][KK + 1];
-    __shared__ float Ws[CO][KK + 1];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < KK * KK; i += 256) Gs[i / KK][i % KK] = G[(i / KK) * 64 + i % KK];
-    for (int i = tid; i < CO * KK; i += 256) Ws[i / KK][i % KK] = (float)wpk[(i / KK) * 64 + i % KK];
+// stats[0][0][co] += sum_p y = W[co] . s,  stats[0][1][co] += sum_p y^2 = W[co] G W[co]^T (fp64); one workgroup
+// (one wave) per channel, lane k < 49 forms (G W[co]^T)[k]
+__global__ __launch_bounds__(64) void stem_gram_stats_kernel(const float* __restrict__ G, const __bf16* __restrict__ wpk,
+                                                             double* __restrict__ stats) {
+    __shared__ double Ws[KK];
+    const int co = blockIdx.x, k = threadIdx.x;
+    if (k < KK) Ws[k] = (double)(float)wpk[co * 64 + k];
     __syncthreads();
-    // 4 threads per channel: thread q of channel co sums rows k = q, q+4, ...
-    const int co = tid >> 2, q = tid & 3;
     double s1 = 0.0, s2 = 0.0;
-    for (int k = q; k < KK; k += 4) {
+    if (k < KK) {
         double t = 0.0;
-        for (int l = 0; l < KK; ++l) t += (double)Ws[co][l] * (double)Gs[k][l];
-        s2 += (double)Ws[co][k] * t;
-        s1 += (double)Ws[co][k] * (double)G[k * 64 + GONE];
+        for (int l = 0; l < KK; ++l) t += Ws[l] * (double)G[k * 64 + l];
+        s2 = Ws[k] * t;
+        s1 = Ws[k] * (double)G[k * 64 + GONE];
     }
-    s1 += __shfl_xor(s1, 1, 64); s1 += __shfl_xor(s1, 2, 64);
-    s2 += __shfl_xor(s2, 1, 64); s2 += __shfl_xor(s2, 2, 64);
-    if (q == 0) {
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    if (k == 0) {
         stats[co] += s1;
         stats[CO + co] += s2;
     }
@@ -408,14 +427,17 @@ __global__ __launch_bounds__(256) void stem_fused_fwd_kernel(const float* __rest
                                                              const float* __restrict__ shift, __bf16* __restrict__ out,
                                                              uint8_t* __restrict__ argmax, __bf16* __restrict__ yam,
                                                              int H, int W, int Ho, int Wo, int Hp, int Wp) {
-    constexpr int AT = FNB * 16 * 128;                  // 43008 B im2col tile
-    constexpr int YT = FNP * FYROW;                     // 46800 B staged y (aliases the A tile)
-    constexpr int U = AT > YT ? AT : YT;
-    __shared__ __attribute__((aligned(16))) char smem[U + CO * 128 + FIR * FIC * 4];
-    char* As = smem;
+    // No im2col tile: with K ordered (kh, kw) and kw padded to 8, the A fragment of pixel (r, c) for K chunk kh is
+    // the 8 consecutive bf16 patch[2r + kh][2c .. 2c + 7] (the 8th meets a zero weight).  The patch is kept as 4
+    // copies shifted by 0/2/4/6 elements, so every fragment is one aligned 16-B LDS read.
+    constexpr int PROW = FIC * 2;                       // 272 B per bf16 patch row
+    constexpr int PT = 4 * FIR * PROW;                  // 16320 B
+    constexpr int YT = FNP * FYROW;                     // 46800 B staged y (aliases patch + weights after the MFMAs)
+    constexpr int U = YT > PT + CO * 128 ? YT : PT + CO * 128;
+    __shared__ __attribute__((aligned(16))) char smem[U];
+    char* Ps = smem;
+    char* Bs = smem + PT;
     char* Ys = smem;
-    char* Bs = smem + U;
-    float* patch = (float*)(smem + U + CO * 128);
 
     const int tid = threadIdx.x;
     const int tiles_w = Wp / FPC, tiles_h = Hp / FPR;
@@ -426,24 +448,21 @@ __global__ __launch_bounds__(256) void stem_fused_fwd_kernel(const float* __rest
     const int cr0 = 2 * pi0 - 1, cc0 = 2 * pj0 - 1;     // conv region origin (may be -1)
     const int ih0 = cr0 * SP - PD, iw0 = cc0 * SP - PD;
 
-    for (int i = tid; i < CO * 8; i += 256) {
-        const int r = i >> 3, c = i & 7;
-        *(uint4*)(Bs + swz128(r, c)) = *(const uint4*)(wpk + r * 64 + c * 8);
+    // weights re-laid [co][kh*8 + kw] (kw = 7 and kh = 7 zero), 128-B swizzled rows
+    for (int i = tid; i < CO * 64; i += 256) {
+        const int co = i >> 6, kk = i & 63, kh = kk >> 3, kw = kk & 7;
+        const __bf16 v = (kh < KS && kw < KS) ? wpk[co * 64 + kh * KS + kw] : (__bf16)0.f;
+        *(__bf16*)(Bs + swz128(co, kk >> 3) + (kk & 7) * 2) = v;
     }
-    stage_patch(patch, x + (size_t)n * H * W, H, W, ih0, iw0, FIR, FIC, tid);
-    __syncthreads();
-    for (int p = tid; p < FNB * 16; p += 256) {
-        const int r = p / FCC, c = p - (p / FCC) * FCC;
-        const float* pp = patch + (SP * r) * FIC + SP * c;
+    {
+        const float* xn = x + (size_t)n * H * W;
+        for (int i = tid; i < FIR * FIC; i += 256) {
+            const int r = i / FIC, c = i - (i / FIC) * FIC;
+            const int ih = ih0 + r, iw = iw0 + c;
+            const __bf16 v = (__bf16)(((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? xn[(size_t)ih * W + iw] : 0.f);
 #pragma unroll
-        for (int ch = 0; ch < 8; ++ch) {
-            bf16x8 v;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int k = ch * 8 + e;
-                v[e] = (__bf16)((k < KK && p < FNP) ? pp[(k / KS) * FIC + (k % KS)] : 0.f);
-            }
-            *(bf16x8*)(As + swz128(p, ch)) = v;
+            for (int t = 0; t < 4; ++t)
+                if (c - 2 * t >= 0) *(__bf16*)(Ps + (t * FIR + r) * PROW + (c - 2 * t) * 2) = v;
         }
     }
     __syncthreads();
@@ -464,16 +483,20 @@ __global__ __launch_bounds__(256) void stem_fused_fwd_kernel(const float* __rest
         for (int b = 0; b < 4; ++b) acc[i][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
         if (blk < FNB) {
             nblk = i + 1;
+            const int p = min(blk * 16 + l16, FNP - 1);
+            const int r = p / FCC, c = p - (p / FCC) * FCC;
+            const char* pb = Ps + ((c & 3) * FIR + 2 * r) * PROW + (c >> 2) * 16;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const bf16x8 af = *(const bf16x8*)(As + (blk * 16 + l16) * 128 + (((s * 4 + lg) ^ l7) << 4));
+                const int kh = s * 4 + lg;
+                const bf16x8 af = kh < KS ? *(const bf16x8*)(pb + kh * PROW) : (bf16x8){};
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
                     acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][b], af, acc[i][b], 0, 0, 0);
             }
         }
     }
-    __syncthreads();                                    // A tile dead: stage y (bf16, as the unfused kernel stores it)
+    __syncthreads();                                    // patch dead: stage y (bf16, as the unfused kernel stores it)
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         if (i >= nblk) break;
@@ -532,19 +555,90 @@ __global__ __launch_bounds__(256) void stem_fused_fwd_kernel(const float* __rest
 }
 
 // ---- backward weight gradient from the pooled side: stage = 64 conv pixels of one row; dz (pool + ReLU gradient)
-// built from the pooled gradient / argmax / y-at-argmax, BN backward sums accumulated (stats, fp64 replicas)
+// built from the pooled gradient / argmax / y-at-argmax, BN backward sums accumulated (stats, fp64 replicas).
+// The stage's pooled neighbourhood (1 or 2 pooled rows x 33 columns: gradient, y-at-argmax, argmax) is read with
+// coalesced 16-B loads into LDS (prefetched into registers one stage ahead, like the input patch), then every
+// conv pixel gathers its <= 4 window candidates from LDS.
+constexpr int PNC = WPX / 2 + 1;                       // 33 pooled columns
+constexpr int PNCH = PNC * 20;                         // 16-B chunks per pooled row: 8 gradient + 8 y + 4 argmax per px
+constexpr int PNL = (2 * PNCH + 255) / 256;            // chunks per thread (6)
+constexpr int PN_D = 0, PN_Y = 2 * PNC * 128, PN_A = 4 * PNC * 128, PNSZ = PN_A + 2 * PNC * 64;   // 21120 B
+
+struct PooledStage {
+    int n, oh, ow0, nrows, ja0;
+};
+
+__device__ __forceinline__ PooledStage pooled_stage(long ps, int Ho, int Wo, int Hp) {
+    PooledStage st;
+    st.n = (int)(ps / ((long)Ho * Wo));
+    const int rem = (int)(ps - (long)st.n * Ho * Wo);
+    st.oh = rem / Wo;
+    st.ow0 = rem - (rem / Wo) * Wo;
+    st.nrows = ((st.oh & 1) && (st.oh >> 1) + 1 < Hp) ? 2 : 1;
+    st.ja0 = st.ow0 >> 1;
+    return st;
+}
+
+__device__ __forceinline__ void pooled_load(uint4 (&pr)[PNL], const __bf16* __restrict__ dout,
+                                            const __bf16* __restrict__ yam, const uint8_t* __restrict__ argmax,
+                                            const PooledStage& st, int Hp, int Wp, int tid) {
+#pragma unroll
+    for (int q = 0; q < PNL; ++q) {
+        const int i = tid + 256 * q;
+        const int ri = i / PNCH, k = i - (i / PNCH) * PNCH;
+        int jl, off;
+        const char* base;
+        if (k < 2 * PNC * 8) {                         // gradient / y chunks: [kind][jl][8]
+            const int kind = k / (PNC * 8), kk = k - kind * PNC * 8;
+            jl = kk >> 3;
+            off = (kk & 7) * 16;
+            base = kind ? (const char*)yam : (const char*)dout;
+            off += jl * 128;
+            const long row = ((long)st.n * Hp + (st.oh >> 1) + ri) * Wp + st.ja0;
+            base += row * 128;
+        } else {                                       // argmax chunks: [jl][4]
+            const int kk = k - 2 * PNC * 8;
+            jl = kk >> 2;
+            off = jl * 64 + (kk & 3) * 16;
+            const long row = ((long)st.n * Hp + (st.oh >> 1) + ri) * Wp + st.ja0;
+            base = (const char*)argmax + row * 64;
+        }
+        const bool ok = ri < st.nrows && st.ja0 + jl < Wp;
+        pr[q] = ok ? *(const uint4*)(base + off) : make_uint4(0, 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void pooled_store(char* Pn, const uint4 (&pr)[PNL], int tid) {
+#pragma unroll
+    for (int q = 0; q < PNL; ++q) {
+        const int i = tid + 256 * q;
+        if (i >= 2 * PNCH) break;
+        const int ri = i / PNCH, k = i - (i / PNCH) * PNCH;
+        int dst;
+        if (k < 2 * PNC * 8) {
+            const int kind = k / (PNC * 8), kk = k - kind * PNC * 8;
+            dst = (kind ? PN_Y : PN_D) + (ri * PNC + (kk >> 3)) * 128 + (kk & 7) * 16;
+        } else {
+            const int kk = k - 2 * PNC * 8;
+            dst = PN_A + (ri * PNC + (kk >> 2)) * 64 + (kk & 3) * 16;
+        }
+        *(uint4*)(Pn + dst) = pr[q];
+    }
+}
+
 __global__ __launch_bounds__(256) void stem_wgrad_pooled_kernel(const __bf16* __restrict__ dout, const uint8_t* __restrict__ argmax,
                                                                 const __bf16* __restrict__ yam, const float* __restrict__ scale,
                                                                 const float* __restrict__ shift, const float* __restrict__ mean,
                                                                 const float* __restrict__ invstd, const float* __restrict__ x,
                                                                 float* __restrict__ ws, double* __restrict__ stats, int H,
                                                                 int W, int Ho, int Wo, int Hp, int Wp, long M, int chunk) {
-    constexpr int DT = WPX * DROW;
-    __shared__ __attribute__((aligned(16))) char smem[DT + 64 * 128 + KS * WPCOLS * 4];
+    constexpr int DT = WPX * DROW;                     // 18432 B dz stage
+    __shared__ __attribute__((aligned(16))) char smem[DT + 2 * TSZ + PNSZ];
     char* Ds = smem;
-    char* Cs = smem + DT;
-    float* patch = (float*)(smem + DT + 64 * 128);
+    char* Tb = smem + DT;
+    char* Pn = smem + DT + 2 * TSZ;
     __shared__ float red[2][4][CO];
+    __shared__ float bnp[4][CO];                        // scale, shift, mean, invstd (kept out of registers)
 
     const int tid = threadIdx.x;
     const int z = blockIdx.x;
@@ -555,12 +649,12 @@ __global__ __launch_bounds__(256) void stem_wgrad_pooled_kernel(const __bf16* __
     const int q4 = l16 >> 2, qq = l16 & 3;
     const int wm = wave >> 1, wn = wave & 1;
     const int cch = tid & 7;                            // this thread's channel chunk in every stage
-    float sc[8], sh[8], mu[8], is[8], s1[8], s2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        sc[e] = scale[cch * 8 + e]; sh[e] = shift[cch * 8 + e]; mu[e] = mean[cch * 8 + e]; is[e] = invstd[cch * 8 + e];
-        s1[e] = 0.f; s2[e] = 0.f;
+    if (tid < CO) {
+        bnp[0][tid] = scale[tid]; bnp[1][tid] = shift[tid]; bnp[2][tid] = mean[tid]; bnp[3][tid] = invstd[tid];
     }
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
     f32x4 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -568,65 +662,72 @@ __global__ __launch_bounds__(256) void stem_wgrad_pooled_kernel(const __bf16* __
         for (int b = 0; b < 2; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
     typedef __attribute__((ext_vector_type(8))) short s16x8;
 
-    for (long ps = p0; ps < p1; ps += WPX) {
-        const int n = (int)(ps / ((long)Ho * Wo));
-        const int rem = (int)(ps - (long)n * Ho * Wo);
-        const int oh = rem / Wo, ow0 = rem - (rem / Wo) * Wo;
+    float pv[TPL];
+    uint4 pr[PNL];
+    PooledStage st = pooled_stage(p0, Ho, Wo, Hp);
+    if (p0 < p1) {
+        tap_load(pv, x, H, W, Ho, Wo, p0, tid);
+        pooled_load(pr, dout, yam, argmax, st, Hp, Wp, tid);
+    }
+    int buf = 0;
+    for (long ps = p0; ps < p1; ps += WPX, buf ^= 1) {
+        char* Ts = Tb + buf * TSZ;
+        tap_store(Ts, pv, tid);
+        pooled_store(Pn, pr, tid);
+        const PooledStage cur = st;
+        if (ps + WPX < p1) {
+            st = pooled_stage(ps + WPX, Ho, Wo, Hp);
+            tap_load(pv, x, H, W, Ho, Wo, ps + WPX, tid);
+            pooled_load(pr, dout, yam, argmax, st, Hp, Wp, tid);
+        }
         __syncthreads();
-        // pooled rows covering conv row oh: even -> oh/2 (di 1); odd -> (oh-1)/2 (di 2), (oh+1)/2 (di 0)
-        const int ia = (oh - 1) >> 1 < 0 ? 0 : (oh & 1 ? (oh - 1) >> 1 : oh >> 1);
-        const int dia = oh & 1 ? 2 : 1;
-        const bool hasb = (oh & 1) && (oh + 1) / 2 < Hp;
-#pragma unroll
+        // dz for (pixel r, chunk cch): window candidates (row slot, column) in (row, col) order; an even conv row /
+        // column has one pooled row / column (window position 1), an odd one two (positions 2 then 0)
+        const int dia = cur.oh & 1 ? 2 : 1;
+#pragma unroll 1
         for (int j = 0; j < 2; ++j) {
-            const int idx = tid + 256 * j;
-            const int r = idx >> 3;                       // pixel in the stage; channel chunk = cch
-            const int ow = ow0 + r;
-            const int ja = ow & 1 ? (ow - 1) >> 1 : ow >> 1;
+            const int r = (tid + 256 * j) >> 3;
+            const int ow = cur.ow0 + r;
             const int dja = ow & 1 ? 2 : 1;
-            const bool hasbj = (ow & 1) && (ow + 1) / 2 < Wp;
+            const bool hasb = cur.nrows == 2;
+            const bool hasbj = (ow & 1) && (ow >> 1) + 1 < Wp;
             float accv[8], yv[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) { accv[e] = 0.f; yv[e] = 0.f; }
-            // candidates in (row, col) order: (ia,ja) (ia,jb) (ib,ja) (ib,jb); missing ones read (ia,ja), never match
 #pragma unroll
             for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
                 for (int cj = 0; cj < 2; ++cj) {
                     const bool ok = (ci == 0 || hasb) && (cj == 0 || hasbj);
-                    const int pi = ia + (ok ? ci : 0), pj = ja + (ok ? cj : 0);
+                    const int slot = ok ? ci * PNC + (r >> 1) + cj : (r >> 1);
                     const int sel = ok ? (ci ? 0 : dia) * 3 + (cj ? 0 : dja) : 255;
-                    const size_t o = (((size_t)n * Hp + pi) * Wp + pj) * CO + cch * 8;
-                    const bf16x8 d8 = *(const bf16x8*)(dout + o);
-                    const bf16x8 y8 = *(const bf16x8*)(yam + o);
+                    const bf16x8 d8 = *(const bf16x8*)(Pn + PN_D + slot * 128 + cch * 16);
+                    const bf16x8 y8 = *(const bf16x8*)(Pn + PN_Y + slot * 128 + cch * 16);
                     uint8_t a8[8];
-                    *(uint2*)a8 = *(const uint2*)(argmax + o);
+                    *(uint2*)a8 = *(const uint2*)(Pn + PN_A + slot * 64 + cch * 8);
 #pragma unroll
                     for (int e = 0; e < 8; ++e)
                         if (a8[e] == sel) { accv[e] += (float)d8[e]; yv[e] = (float)y8[e]; }
                 }
-            bf16x8 st;
+            bf16x8 stv;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const float dz = (yv[e] * sc[e] + sh[e] > 0.f) ? accv[e] : 0.f;
-                st[e] = (__bf16)dz;
-                const float rr = (float)st[e];
+                const int c = cch * 8 + e;
+                const float dz = (yv[e] * bnp[0][c] + bnp[1][c] > 0.f) ? accv[e] : 0.f;
+                stv[e] = (__bf16)dz;
+                const float rr = (float)stv[e];
                 s1[e] += rr;
-                s2[e] += rr * (yv[e] - mu[e]) * is[e];
+                s2[e] += rr * (yv[e] - bnp[2][c]) * bnp[3][c];
             }
-            *(bf16x8*)(Ds + dswz(r, cch * 16)) = st;
+            *(bf16x8*)(Ds + dswz(r, cch * 16)) = stv;
         }
-        stage_patch(patch, x + (size_t)n * H * W, H, W, oh * SP - PD, ow0 * SP - PD, KS, WPCOLS, tid);
-        __syncthreads();
-        build_tap_tile(Cs, patch, tid, false);
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int r0 = 32 * s + 8 * lg + q4;
             bf16x8 tf[2], df[2];
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
-                tf[b] = *(const bf16x8*)(Cs + swz128(wn * 32 + b * 16 + l16, s * 4 + lg));
+            for (int b = 0; b < 2; ++b) tf[b] = tap_frag(Ts, wn * 32 + b * 16 + l16, s * 4 + lg, false);
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
                 const int cb = (wm * 32 + a * 16 + 4 * qq) * 2;
@@ -660,11 +761,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_pooled_kernel(const __bf16* __
     }
     __syncthreads();
     if (tid < 2 * CO) {
-        const int st = tid / CO, c = tid - (tid / CO) * CO;
+        const int sti = tid / CO, c = tid - (tid / CO) * CO;
         double a = 0.0;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) a += red[st][w][c];
-        atomic_add_f64(stats + ((long)(z % SCD_STAT_REPLICAS) * 2 + st) * CO + c, a);
+        for (int w = 0; w < 4; ++w) a += red[sti][w][c];
+        atomic_add_f64(stats + ((long)(z % SCD_STAT_REPLICAS) * 2 + sti) * CO + c, a);
     }
 }
 
@@ -738,7 +839,7 @@ extern "C" int scd_stem_gram(const float* x, float* ws, int nsplit, int N, int H
 }
 
 extern "C" int scd_stem_gram_stats(const float* G, const void* wpk, double* stats, void* stream) {
-    hipLaunchKernelGGL(stem_gram_stats_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, G, (const __bf16*)wpk, stats);
+    hipLaunchKernelGGL(stem_gram_stats_kernel, dim3(CO), dim3(64), 0, (hipStream_t)stream, G, (const __bf16*)wpk, stats);
     SCD_RETURN_LAUNCH();
 }
 

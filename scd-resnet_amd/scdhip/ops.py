@@ -707,8 +707,9 @@ def stem_conv_wgrad(dy, x, dst, accumulate=True, ybn=None, coef=None):
 
 class StemFused:
     """Stem without the full-resolution activation (stem.hip: Gram statistics, fused conv+BN+ReLU+pool forward,
-    weight gradient from the pooled side).  Opt-in (SCD_STEM_FUSED=1) until it beats the conv / pool kernel pair:
-    first version measured 0.91 ms per B=32 step against 0.67 ms (profiles)."""
+    weight gradient from the pooled side).  Opt-in (SCD_STEM_FUSED=1): the kernels are VALU-bound (pool window
+    selects, dz gathers) and measured 0.75 ms against 0.60 ms for the chain that keeps the activation at B=32
+    (profiles/r2_stem_bench.txt)."""
     enabled = os.environ.get("SCD_STEM_FUSED", "0") == "1"
 
 
@@ -759,8 +760,10 @@ def stem_fused_bwd(bn, st, dout, am, yam, x, G, wpk, dst):
     stats = bn_stats(bn, "bwd")
     L.call("scd_stem_wgrad_pooled", ptr(dout), ptr(am), ptr(yam), ptr(st.scale), ptr(st.shift), ptr(st.mean),
            ptr(st.invstd), ptr(x), ptr(ws), ptr(stats), ns, N, H, W, Ho, Wo, Hp, Wp, stream())
+    T1 = torch.empty(64 * 64, dtype=torch.float32, device=x.device)
+    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(T1), 0, stream())
     coef = bn_backward_coef(bn, st, stats, 64)
-    L.call("scd_stem_wgrad_combine", ptr(ws), ns, ptr(coef), ptr(G), ptr(wpk), ptr(dst), 1, stream())
+    L.call("scd_stem_wgrad_combine", ptr(T1), 1, ptr(coef), ptr(G), ptr(wpk), ptr(dst), 1, stream())
 
 
 def stem_pool_fwd(y, st):

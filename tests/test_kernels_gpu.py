@@ -336,7 +336,8 @@ def test_stem_without_full_res_activation(shape):
     jj = torch.arange(Wp, device=DEV).view(1, 1, Wp, 1) * 2 - 1 + am2.long() % 3
     nn = torch.arange(N, device=DEV).view(N, 1, 1, 1)
     cc = torch.arange(64, device=DEV).view(1, 1, 1, 64)
-    assert torch.equal(y[nn, ii.clamp(0), jj.clamp(0), cc], yam2)
+    yg = y[nn, ii.clamp(0), jj.clamp(0), cc].float()
+    assert ((yam2.float() - yg).abs() <= 2 ** -7 * yg.abs() + 1e-6).all()    # 1 bf16 ulp (conv sum order)
     for a, b in ((bns[0].weight.grad, bns[1].weight.grad), (bns[0].bias.grad, bns[1].bias.grad)):
         assert rel_err(b, a) < 1e-3
     assert rel_err(dwb, dwa) < 1e-2
