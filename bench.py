@@ -24,7 +24,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 TRAIN_GFLOP_PER_IMG = 147.476      # SURVEY §6 / BASELINE.md: conv+deconv fwd+dgrad+wgrad per 512^2 Res10 image
-PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 (= dense fp16) MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -35,7 +35,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="compute dtype (BASELINE configs[4] names fp16: Res50 1024^2)")
     ap.add_argument("--model", default="centerOffsetRes10")
     ap.add_argument("--image-size", type=int, default=512,
                     help="tile size; 512 uses the synthetic SCD dataset plugin, other sizes N(0,1) tiles with "
@@ -128,11 +129,11 @@ def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2)):
     M = B * (S // 4) ** 2
     ct = hd * len(ods)
     flops = 2.0 * M * (ct * 9 * cin + hd * sum(ods))
-    esz = 2 if dtype_name == "bf16" else 4
+    esz = 4 if dtype_name == "fp32" else 2
     algo_bytes = M * cin * esz + M * ct * esz + M * sum(ods) * 4 + ct * 9 * cin * esz
     achieved = flops / (ms * 1e-3) / 1e12
-    peak = PEAK_BF16_TFLOPS if dtype_name == "bf16" else PEAK_F32_TFLOPS
-    kernel = HEADS_KERNEL if dtype_name == "bf16" else "conv_gemm_kernel<f32,128,128,heads>"
+    peak = PEAK_F32_TFLOPS if dtype_name == "fp32" else PEAK_BF16_TFLOPS      # dense fp16 = dense bf16 MFMA rate
+    kernel = "conv_gemm_kernel<f32,128,128,heads>" if dtype_name == "fp32" else HEADS_KERNEL
     traffic, src = pmc_traffic(kernel, B, dtype_name) if S == 512 else (None, None)
     return {"bound": "mfma", "kernel": kernel, "achieved": round(achieved, 1), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
@@ -258,7 +259,7 @@ def main():
     from scdhip.flat import FlatAdam, FlatDDP
     from trainer.dataset.syntheticSCD import SCD
     plugin = importlib.import_module("trainer.model." + args.model)
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
 
     model = plugin.model(**plugin.modelParams).to(dev).set_compute_dtype(dtype).train()
     opt = FlatAdam(filter(lambda p: p.requires_grad, model.parameters()))
@@ -355,15 +356,15 @@ def main():
         core = model.module if hasattr(model, "module") else model
         gflop = TRAIN_GFLOP_PER_IMG if (args.model == "centerOffsetRes10" and S == 512) else \
             train_gflop_per_img(core, S)
-        step_frac = value * gflop / 1e3 / (world * (PEAK_BF16_TFLOPS if dtype == torch.bfloat16
-                                                    else PEAK_F32_TFLOPS))
+        step_frac = value * gflop / 1e3 / (world * (PEAK_F32_TFLOPS if dtype == torch.float32
+                                                    else PEAK_BF16_TFLOPS))
         line = {
             "metric": "512x512 images/sec training, centerOffsetRes10, at 1/2/4/8 MI355X" if (
                 args.model == "centerOffsetRes10" and S == 512) else "%dx%d images/sec training, %s" % (S, S, args.model),
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": nwarm, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32", "data": "synthetic",
+            "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": "%s train step (fwd+focal/L1 loss+bwd+Adam, DDP over RCCL), %dx%d synthetic "
                                    "SCD tiles" % (args.model, S, S), "model": args.model, "global_batch": B * world,
                        "step_issue": "hip graph replay" if graph is not None else "eager launches",

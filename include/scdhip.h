@@ -28,6 +28,7 @@ extern "C" {
 
 #define SCD_DT_F32 0
 #define SCD_DT_BF16 1
+#define SCD_DT_F16 2           /* fp16 operands / activations (v_mfma_f32_16x16x32_f16), fp32 accumulation */
 
 #define SCD_ERR_ARG 9001       /* invalid argument / unsupported shape */
 
@@ -92,9 +93,10 @@ int scd_conv_wgrad_nsplit2(int dtype, long M, int Ho, int Wo, int Cg, int T, int
 int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws, int nsplit,
                    int N, int Ho, int Wo, int Cg, int Hi, int Wi, int Ci, int in_stride,
                    int T, const int* dh, const int* dw, void* stream);
-/* dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= sum_z ws[z, r, t*Ci+ci]   for r in [r0,r1), ci < cvalid */
+/* dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= alpha * sum_z ws[z, r, t*Ci+ci]   for r in [r0,r1), ci < cvalid
+ * (alpha = 1 / the fp16 loss scale, else 1) */
 int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
-                     long ld_n, long ld_c, long ld_t, float* dst, int accumulate, void* stream);
+                     long ld_n, long ld_c, long ld_t, float* dst, int accumulate, float alpha, void* stream);
 
 /* Pack an fp32 (A, B, T) weight (OIHW / IOHW flattening) into the GEMM operand layout:
  * mode 0: out[row_off + a][t*B + b] = w[a][b][t]; mode 1: out[row_off + b][t*A + a] = w[a][b][t];
@@ -221,7 +223,7 @@ int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, con
                   const float* const* w1, const float* const* douts, void* dhid, double* acc, void* stream);
 /* collapse (and re-zero) acc; (+)= into dw1[h] (od[h],Hd), db1[h] (od[h]), db0[h] (Hd: 3x3 conv bias) */
 int scd_heads_bwd_weight_finalize(double* acc, int nh, int Hd, const int* od, float* const* dw1,
-                                  float* const* db1, float* const* db0, int accumulate, void* stream);
+                                  float* const* db1, float* const* db0, int accumulate, float alpha, void* stream);
 
 /* ---- losses (focal.py:25-53, regression.py:37-44, centerNetOffset.py:182-217) ---- */
 /* per element: g = d/dlogit [pos: log(p)(1-p)^2 | neg: log(1-p) p^2 (1-gt)^4] with

@@ -2,7 +2,7 @@
 
 Same default keys and the same overlay rule: a JSON config replaces only keys that already
 exist (configuration.py:150-153); string values may reference other keys as `{key}` format
-fields.  Two keys are added: ``computeDtype`` ("bf16" | "fp32"), the MFMA precision of the
+fields.  Two keys are added: ``computeDtype`` ("bf16" | "fp16" | "fp32"), the MFMA precision of the
 HIP path (the reference trains in fp32 without AMP), and ``stepGraph`` (true | false, default false):
 replay the training step as a captured HIP graph after two eager steps (single-process runs;
 scdhip/graph.py -- measured slower than eager issue on ROCm 7).

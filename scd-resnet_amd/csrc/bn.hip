@@ -320,6 +320,7 @@ extern "C" int scd_bn_finalize(double* stats, int nrep, int C, double count, con
 extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const float* scale,
                             const float* shift, const void* res, const float* rscale, const float* rshift, int relu,
                             void* stream) {
+    SCD_F16_FWD(scd_bn_apply, y, out, C, total, scale, shift, res, rscale, rshift, relu, stream);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16) {
         if (C % 8 || !ew_rows_ok(C / 8)) return SCD_ERR_ARG;
@@ -342,6 +343,7 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
 extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
                                  const float* relu_shift, const float* mean,
                                  const float* invstd, int C, long total, double* stats, void* stream) {
+    SCD_F16_FWD(scd_bn_bwd_reduce, dout, mask, y, relu_scale, relu_shift, mean, invstd, C, total, stats, stream);
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
@@ -391,6 +393,7 @@ extern "C" int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count,
 extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
                                 const float* relu_shift, const float* coef, int C, long total, void* dy, void* dz,
                                 void* stream) {
+    SCD_F16_FWD(scd_bn_bwd_apply, dout, mask, y, relu_scale, relu_shift, coef, C, total, dy, dz, stream);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16) {
         if (C % 8 || !ew_rows_ok(C / 8)) return SCD_ERR_ARG;

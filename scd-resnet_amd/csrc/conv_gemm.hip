@@ -971,7 +971,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                     const unsigned yw[2] = {yq[a].x, yq[a].y};
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float yv = __uint_as_float(r & 1 ? (yw[r >> 1] & 0xffff0000u) : (yw[r >> 1] << 16));
+                        const float yv = h16_word_half(yw[r >> 1], r & 1);
                         const float d = (float)(__bf16)v[r];            // the stored gradient
                         const float dz = yv * bsc[r] + bsh[r] > 0.f ? d : 0.f;
                         csum[b][r] += dz;
@@ -2603,7 +2603,7 @@ __global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs, long 
 }
 
 __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
-                                    long ld_n, long ld_c, long ld_t, float* dst, int accumulate) {
+                                    long ld_n, long ld_c, long ld_t, float* dst, int accumulate, float alpha) {
     const unsigned KK = (unsigned)(T * Ci);
     const unsigned total = (unsigned)(r1 - r0) * KK;
     const size_t zs = (size_t)Cg * KK;
@@ -2623,7 +2623,7 @@ __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cg, int T, 
             s3 += src[(size_t)(z + 3) * zs];
         }
         for (; z < nsplit; ++z) s0 += src[(size_t)z * zs];
-        const float s = (s0 + s1) + (s2 + s3);
+        const float s = ((s0 + s1) + (s2 + s3)) * alpha;
         float* d = dst + r * ld_n + c * ld_c + t * ld_t;
         *d = accumulate ? (*d + s) : s;
     }
@@ -2898,6 +2898,7 @@ extern "C" int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, c
                              int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride,
                              int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
                              void* stream) {
+    SCD_F16_FWD(scd_conv_gemm, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu, accumulate, nphase, phases, stream);
     GemmParams p;
     fill_params(p, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu, accumulate);
     return conv_gemm_launch(dtype, p, nphase, phases, stream);
@@ -2908,6 +2909,7 @@ extern "C" int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void
                                    const scd_gemm_phase* phases, const void* bn_y, const float* mean,
                                    const float* invstd, const float* relu_scale, const float* relu_shift,
                                    double* bn_stats, void* stream) {
+    SCD_F16_FWD(scd_conv_gemm_bnbwd, x, w, y, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, nphase, phases, bn_y, mean, invstd, relu_scale, relu_shift, bn_stats, stream);
     if (!bn_y || !mean || !invstd || !relu_scale || !relu_shift || !bn_stats || Co % 4) return SCD_ERR_ARG;
     GemmParams p;
     fill_params(p, x, w, y, nullptr, bn_stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, 0, 0);
@@ -2928,6 +2930,7 @@ extern "C" int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void
 extern "C" int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void* hid, const float* bias, int N,
                                    int H, int W, int Ci, int nh, const int* od, const float* const* w1,
                                    const float* const* b1, float* const* outs, void* stream) {
+    SCD_F16_FWD(scd_conv_gemm_heads, x, w, hid, bias, N, H, W, Ci, nh, od, w1, b1, outs, stream);
     if (nh < 1 || nh > 4) return SCD_ERR_ARG;
     GemmParams p;
     fill_params(p, x, w, hid, bias, nullptr, N, H, W, Ci, H, W, nh * 128, 1, 1, 9 * Ci, 1, 0);
@@ -3031,11 +3034,13 @@ static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
 }
 
 extern "C" int scd_conv_wgrad_nsplit2(int dtype, long M, int Ho, int Wo, int Cg, int T, int Ci) {
+    SCD_F16_FWD(scd_conv_wgrad_nsplit2, M, Ho, Wo, Cg, T, Ci);
     if (wgrad_use_pp2(dtype, M, Ho, Wo, Cg)) return wgrad_pp2_nsplit(M, Cg, T * Ci);
     return scd_conv_wgrad_nsplit(dtype, M, Cg, T, Ci);
 }
 
 extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
+    SCD_F16_FWD(scd_conv_wgrad_nsplit, M, Cg, T, Ci);
     if (wgrad_use_pp(dtype, M, Cg, T * Ci)) {
         // about three rounds of one-per-CU workgroups, whole XCD groups of splits, >= 1024 pixels per split,
         // fp32 slabs capped at 192 MB
@@ -3071,6 +3076,7 @@ extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
 extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws, int nsplit, int N, int Ho, int Wo,
                               int Cg, int Hi, int Wi, int Ci, int in_stride, int T, const int* dh, const int* dw,
                               void* stream) {
+    SCD_F16_FWD(scd_conv_wgrad, g, x, ws, nsplit, N, Ho, Wo, Cg, Hi, Wi, Ci, in_stride, T, dh, dw, stream);
     const int EPC = dtype == SCD_DT_BF16 ? 8 : 4;
     if (T < 1 || T > SCD_MAX_TAPS || Ci % EPC != 0 || Cg % EPC != 0 || nsplit < 1) return SCD_ERR_ARG;
     WgradParams p;
@@ -3180,7 +3186,8 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
 }
 
 extern "C" int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
-                                long ld_n, long ld_c, long ld_t, float* dst, int accumulate, void* stream) {
+                                long ld_n, long ld_c, long ld_t, float* dst, int accumulate, float alpha,
+                                void* stream) {
     if (r0 < 0 || r1 > Cg || r0 >= r1) return SCD_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     const long zs = (long)Cg * T * Ci;
@@ -3201,6 +3208,6 @@ extern "C" int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int 
     const long total = (long)(r1 - r0) * T * Ci;
     const int blocks = (int)std::min<long>(4096, (total + 255) / 256);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, ns, (int)(Cg * zstride_mult), T, Ci,
-                       r0, r1, cvalid, ld_n, ld_c, ld_t, dst, accumulate);
+                       r0, r1, cvalid, ld_n, ld_c, ld_t, dst, accumulate, alpha);
     SCD_RETURN_LAUNCH();
 }

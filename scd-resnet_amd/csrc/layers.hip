@@ -96,6 +96,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
 }
 
 extern "C" int scd_pack_weights_batched(int dtype, const scd_pack_desc* descs, int n, long total, void* stream) {
+    SCD_F16_FWD(scd_pack_weights_batched, descs, n, total, stream);
     if (n < 1 || total < 1 || total >= (1L << 31) || total % PACK_UNIT || (dtype != SCD_DT_BF16 && dtype != SCD_DT_F32)) return SCD_ERR_ARG;
     hipLaunchKernelGGL(pack_weights_batched_kernel, dim3((unsigned)(total / PACK_UNIT)), dim3(256), 0, (hipStream_t)stream,
                        descs, n, dtype == SCD_DT_BF16 ? 1 : 0);
@@ -555,7 +556,8 @@ struct HeadsGrad {
     float* db0[4];
 };
 
-__global__ void heads_bwd_weight_finalize_kernel(double* acc, int accsz, HeadsDesc d, HeadsGrad g, int accumulate) {
+__global__ void heads_bwd_weight_finalize_kernel(double* acc, int accsz, HeadsDesc d, HeadsGrad g, int accumulate,
+                                                 double alpha) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < accsz; i += gridDim.x * blockDim.x) {
         double s = 0.0;
         for (int r = 0; r < SCD_STAT_REPLICAS; ++r) {
@@ -578,6 +580,7 @@ __global__ void heads_bwd_weight_finalize_kernel(double* acc, int accsz, HeadsDe
             const int h = c / d.Hd;
             dst = g.db0[h] + (c - h * d.Hd);
         }
+        s *= alpha;
         *dst = accumulate ? (*dst + (float)s) : (float)s;
     }
 }
@@ -644,6 +647,7 @@ inline int ew_blocks(long n) { return (int)std::min<long>(8192, std::max<long>(1
 
 extern "C" int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp, int row_off,
                                void* stream) {
+    SCD_F16_FWD(scd_pack_weight, w, out, A, B, T, mode, ldp, row_off, stream);
     const long total = (long)(mode == 0 ? A : B) * ldp;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
@@ -659,6 +663,7 @@ extern "C" int scd_pack_weight(int dtype, const float* w, void* out, int A, int 
 
 extern "C" int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int H, int W, int Ho, int Wo, int kh,
                                int kw, int stride, int pad, int Kpad, void* stream) {
+    SCD_F16_FWD(scd_im2col_stem, x, cols, N, H, W, Ho, Wo, kh, kw, stride, pad, Kpad, stream);
     hipStream_t st = (hipStream_t)stream;
     if (Kpad % 8 || Kpad < kh * kw) return SCD_ERR_ARG;
     const long total = (long)N * Ho * Wo * (Kpad / (dtype == SCD_DT_BF16 ? 8 : 4));
@@ -675,6 +680,7 @@ extern "C" int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int
 
 extern "C" int scd_stem_pool_fwd(int dtype, const void* y, const float* scale, const float* shift, void* out,
                                  uint8_t* argmax, int N, int H, int W, int C, int Ho, int Wo, void* stream) {
+    SCD_F16_FWD(scd_stem_pool_fwd, y, scale, shift, out, argmax, N, H, W, C, Ho, Wo, stream);
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
@@ -692,6 +698,7 @@ extern "C" int scd_stem_pool_fwd(int dtype, const void* y, const float* scale, c
 
 extern "C" int scd_stem_pool_bwd(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
                                  const float* shift, void* dz, int N, int H, int W, int C, int Ho, int Wo, void* stream) {
+    SCD_F16_FWD(scd_stem_pool_bwd, dout, argmax, y, scale, shift, dz, N, H, W, C, Ho, Wo, stream);
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
@@ -710,6 +717,7 @@ extern "C" int scd_stem_pool_bwd(int dtype, const void* dout, const uint8_t* arg
 extern "C" int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
                                     const float* shift, const float* mean, const float* invstd, void* dz, double* stats,
                                     int N, int H, int W, int C, int Ho, int Wo, void* stream) {
+    SCD_F16_FWD(scd_stem_pool_bwd_bn, dout, argmax, y, scale, shift, mean, invstd, dz, stats, N, H, W, C, Ho, Wo, stream);
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E || 256 % (C / E)) return SCD_ERR_ARG;
@@ -747,6 +755,7 @@ extern "C" int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* 
 
 extern "C" int scd_heads_fwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
                              const float* const* w1, const float* const* b1, float* const* outs, void* stream) {
+    SCD_F16_FWD(scd_heads_fwd, hid, N, HW, nh, Hd, od, w1, b1, outs, stream);
     HeadsDesc d;
     if (!make_desc(d, nh, Hd, od)) return SCD_ERR_ARG;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
@@ -774,6 +783,7 @@ extern "C" size_t scd_heads_bwd_accsize(int nh, int Hd, const int* od) {
 extern "C" int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
                              const float* const* w1, const float* const* douts, void* dhid, double* acc,
                              void* stream) {
+    SCD_F16_FWD(scd_heads_bwd, hid, N, HW, nh, Hd, od, w1, douts, dhid, acc, stream);
     HeadsDesc d;
     if (!make_desc(d, nh, Hd, od)) return SCD_ERR_ARG;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
@@ -807,7 +817,7 @@ extern "C" int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, 
 }
 
 extern "C" int scd_heads_bwd_weight_finalize(double* acc, int nh, int Hd, const int* od, float* const* dw1,
-                                             float* const* db1, float* const* db0, int accumulate, void* stream) {
+                                             float* const* db1, float* const* db0, int accumulate, float alpha, void* stream) {
     HeadsDesc d;
     if (!make_desc(d, nh, Hd, od)) return SCD_ERR_ARG;
     HeadsGrad g;
@@ -818,7 +828,7 @@ extern "C" int scd_heads_bwd_weight_finalize(double* acc, int nh, int Hd, const 
     }
     const int accsz = d.nout * Hd + d.nout + nh * Hd;
     hipLaunchKernelGGL(heads_bwd_weight_finalize_kernel, dim3(cdiv(accsz, 256)), dim3(256), 0, (hipStream_t)stream, acc,
-                       accsz, d, g, accumulate);
+                       accsz, d, g, accumulate, (double)alpha);
     SCD_RETURN_LAUNCH();
 }
 

@@ -20,6 +20,7 @@ __global__ __launch_bounds__(256) void pad_channels_kernel(const uint4* __restri
 }  // namespace
 
 extern "C" int scd_pad_channels(int dtype, const void* src, long rows, int C, int Cp, void* dst, void* stream) {
+    SCD_F16_FWD(scd_pad_channels, src, rows, C, Cp, dst, stream);
     const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
     const int vec = 16 / esz;
     if (rows < 1 || C < 1 || Cp < C || C % vec || Cp % vec || src == dst) return SCD_ERR_ARG;

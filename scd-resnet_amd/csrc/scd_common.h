@@ -3,7 +3,89 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// fp16 compute mode (SCD_DT_F16).  The type-generic sources (conv_gemm, bn, layers, stem, pad) are compiled twice:
+// once as written (16-bit type __bf16, v_mfma_f32_16x16x32_bf16) and once with SCD_F16_BUILD, where the 16-bit type
+// is _Float16, the MFMA is v_mfma_f32_16x16x32_f16 and every entry point gets the suffix __f16.  A call with
+// dtype SCD_DT_F16 is forwarded by the first build to the second with dtype SCD_DT_BF16 ("the 16-bit type"), so
+// every kernel, tile shape and dispatch rule is shared and the C-ABI takes SCD_DT_F16 like any other dtype.
+#ifdef SCD_F16_BUILD
+#define scd_conv_gemm scd_conv_gemm__f16
+#define scd_conv_gemm_bnbwd scd_conv_gemm_bnbwd__f16
+#define scd_conv_gemm_heads scd_conv_gemm_heads__f16
+#define scd_conv_wgrad_workspace scd_conv_wgrad_workspace__f16
+#define scd_conv_wgrad_nsplit2 scd_conv_wgrad_nsplit2__f16
+#define scd_conv_wgrad_nsplit scd_conv_wgrad_nsplit__f16
+#define scd_conv_wgrad scd_conv_wgrad__f16
+#define scd_wgrad_reduce scd_wgrad_reduce__f16
+#define scd_stats_collapse scd_stats_collapse__f16
+#define scd_bn_finalize scd_bn_finalize__f16
+#define scd_bn_apply scd_bn_apply__f16
+#define scd_bn_bwd_reduce scd_bn_bwd_reduce__f16
+#define scd_bn_bwd_finalize scd_bn_bwd_finalize__f16
+#define scd_bn_bwd_apply scd_bn_bwd_apply__f16
+#define scd_pack_weights_batched scd_pack_weights_batched__f16
+#define scd_pack_weight scd_pack_weight__f16
+#define scd_im2col_stem scd_im2col_stem__f16
+#define scd_stem_pool_fwd scd_stem_pool_fwd__f16
+#define scd_stem_pool_bwd scd_stem_pool_bwd__f16
+#define scd_stem_pool_bwd_bn scd_stem_pool_bwd_bn__f16
+#define scd_heads_fwd scd_heads_fwd__f16
+#define scd_heads_bwd_accsize scd_heads_bwd_accsize__f16
+#define scd_heads_bwd scd_heads_bwd__f16
+#define scd_heads_bwd_weight_finalize scd_heads_bwd_weight_finalize__f16
+#define scd_adam_step scd_adam_step__f16
+#define scd_adam_step_dev scd_adam_step_dev__f16
+#define scd_stem_conv_fwd scd_stem_conv_fwd__f16
+#define scd_stem_conv_wgrad_nsplit scd_stem_conv_wgrad_nsplit__f16
+#define scd_stem_conv_wgrad scd_stem_conv_wgrad__f16
+#define scd_stem_gram scd_stem_gram__f16
+#define scd_stem_gram_stats scd_stem_gram_stats__f16
+#define scd_stem_fused_fwd scd_stem_fused_fwd__f16
+#define scd_stem_wgrad_pooled scd_stem_wgrad_pooled__f16
+#define scd_stem_wgrad_combine scd_stem_wgrad_combine__f16
+#define scd_pad_channels scd_pad_channels__f16
+#define __bf16 _Float16
+#define __builtin_amdgcn_mfma_f32_16x16x32_bf16 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#endif
+
 #include "../../include/scdhip.h"
+
+#ifdef SCD_F16_BUILD
+#define SCD_F16_FWD(fn, ...) ((void)0)
+#else
+#define SCD_F16_DECL(fn) extern "C" decltype(fn) fn##__f16;
+SCD_F16_DECL(scd_conv_gemm)
+SCD_F16_DECL(scd_conv_gemm_bnbwd)
+SCD_F16_DECL(scd_conv_gemm_heads)
+SCD_F16_DECL(scd_conv_wgrad_nsplit2)
+SCD_F16_DECL(scd_conv_wgrad_nsplit)
+SCD_F16_DECL(scd_conv_wgrad)
+SCD_F16_DECL(scd_bn_apply)
+SCD_F16_DECL(scd_bn_bwd_reduce)
+SCD_F16_DECL(scd_bn_bwd_apply)
+SCD_F16_DECL(scd_pack_weights_batched)
+SCD_F16_DECL(scd_pack_weight)
+SCD_F16_DECL(scd_im2col_stem)
+SCD_F16_DECL(scd_stem_pool_fwd)
+SCD_F16_DECL(scd_stem_pool_bwd)
+SCD_F16_DECL(scd_stem_pool_bwd_bn)
+SCD_F16_DECL(scd_heads_fwd)
+SCD_F16_DECL(scd_heads_bwd)
+SCD_F16_DECL(scd_stem_conv_fwd)
+SCD_F16_DECL(scd_stem_conv_wgrad)
+SCD_F16_DECL(scd_pad_channels)
+#define SCD_F16_FWD(fn, ...) \
+    do { if (dtype == SCD_DT_F16) return fn##__f16(SCD_DT_BF16, __VA_ARGS__); } while (0)
+#endif
+
+// half `hi` of a 32-bit word holding two 16-bit values, as float
+__device__ __forceinline__ float h16_word_half(unsigned w, int hi) {
+#ifdef SCD_F16_BUILD
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(hi ? w >> 16 : w & 0xffffu));
+#else
+    return __uint_as_float(hi ? (w & 0xffff0000u) : (w << 16));
+#endif
+}
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

@@ -796,6 +796,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_combine_kernel(const float* __
 
 extern "C" int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H,
                                  int W, int Ho, int Wo, void* stream) {
+    SCD_F16_FWD(scd_stem_conv_fwd, x, wpk, y, stats, N, H, W, Ho, Wo, stream);
     if (dtype != SCD_DT_BF16 || N <= 0 || Ho != (H + 2 * PD - KS) / SP + 1 || Wo != (W + 2 * PD - KS) / SP + 1 ||
         Wo % FTW || Ho % FTH)
         return SCD_ERR_ARG;
@@ -813,6 +814,7 @@ extern "C" int scd_stem_conv_wgrad_nsplit(long M) {
 
 extern "C" int scd_stem_conv_wgrad(int dtype, const void* dy, const void* ybn, const float* coef, const float* x,
                                    float* ws, int nsplit, int N, int H, int W, int Ho, int Wo, void* stream) {
+    SCD_F16_FWD(scd_stem_conv_wgrad, dy, ybn, coef, x, ws, nsplit, N, H, W, Ho, Wo, stream);
     if (dtype != SCD_DT_BF16 || nsplit < 1 || Wo % WPX || Ho != (H + 2 * PD - KS) / SP + 1 ||
         Wo != (W + 2 * PD - KS) / SP + 1)
         return SCD_ERR_ARG;

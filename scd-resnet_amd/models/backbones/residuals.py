@@ -83,7 +83,8 @@ def _is_corner_head(m):
 class ResNet(torch.nn.Module):
     """ResNet(inputDimension, block, layers, preprocess, terminals, decoder, dimensions) -- residuals.py:184-353.
 
-    ``compute_dtype`` (torch.bfloat16 default, torch.float32 for parity) selects the MFMA
+    ``compute_dtype`` (torch.bfloat16 default, torch.float16 with a static loss scale, torch.float32 for parity)
+    selects the MFMA
     path: bf16 v_mfma_f32_16x16x32_bf16 or exact-f32 v_mfma_f32_16x16x4_f32.
     """
 
@@ -242,8 +243,8 @@ class ResNet(torch.nn.Module):
                                 self.terminals[head].initializer(mm)
 
     def set_compute_dtype(self, dtype):
-        if dtype not in (torch.float32, torch.bfloat16):
-            raise ValueError("compute dtype must be torch.float32 or torch.bfloat16")
+        if dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            raise ValueError("compute dtype must be torch.float32, torch.bfloat16 or torch.float16")
         self.compute_dtype = dtype
         return self
 

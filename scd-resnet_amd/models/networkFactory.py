@@ -37,7 +37,8 @@ from scdhip.graph import StepGraph
 
 torch.random.manual_seed(42)
 
-_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32}
+_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16, "float16": torch.float16,
+           "fp32": torch.float32, "float32": torch.float32}
 
 
 def _to_device(obj, device):

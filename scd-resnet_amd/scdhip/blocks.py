@@ -48,7 +48,7 @@ def _dgrad_bn_relu_bwd(dy, wpack_t, C, Hc, Wc, kh, kw, stride, pad, bn, st, y):
     backward.  In bf16 the dgrad GEMM's epilogue accumulates the BN backward sums (scd_conv_gemm_bnbwd; shapes
     outside the ping-pong kernel run GEMM + reduce inside the same entry point), so the BN backward is only the
     finalize + apply."""
-    if dy.dtype == torch.bfloat16 and ops.BNFusion.enabled:
+    if dy.dtype in ops.HALF and ops.BNFusion.enabled:
         stats = ops.bn_stats(bn, "bwdf")
         da = ops.conv_dgrad(dy, wpack_t, C, Hc, Wc, kh, kw, stride, pad, bn_bwd=(st, y, stats))
         return ops.bn_backward(bn, st, da, y, relu=True, stats=stats)
@@ -248,7 +248,7 @@ class DeconvBNFn(torch.autograd.Function):
         # dW_t[i][o][r][s] = sum x[i at q] * dy[o at s*q + r - p]: weight-gradient GEMM with G = x
         T = k * k
         ops.conv_wgrad(x, dy, k, k, s, p, ops.grad_of(w), (w.shape[1] * T, T, 1))
-        fuse = ctx.prod is not None and x.dtype == torch.bfloat16
+        fuse = ctx.prod is not None and x.dtype in ops.HALF
         dx = ops.deconv_dgrad(dy, ops.pack_weight(w, x.dtype, 0), w.shape[0], k, s, p,
                               bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
         if fuse:
@@ -328,6 +328,10 @@ class HeadsFn(torch.autograd.Function):
         nh = len(heads)
         douts = [(_c(d) if d is not None else torch.zeros(N, o, H, W, device=feat.device))
                  for d, o in zip(douts, od)]
+        S = ops.begin_loss_scale(feat.dtype)
+        if S != 1.0:
+            # fp16: the backward below runs on loss-scaled gradients (ops.LossScale), unscaled into every .grad
+            douts = [d * S for d in douts]
         dptrs = ops.L.ptr_array([d.data_ptr() for d in douts])
         odarr = ops.L.int_array(od)
         dhid = torch.empty_like(hid)
@@ -339,11 +343,11 @@ class HeadsFn(torch.autograd.Function):
         ops.L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), nh, Hd, odarr,
                    ops.L.ptr_array([ops.grad_of(h[2].weight).data_ptr() for h in heads]),
                    ops.L.ptr_array([ops.grad_of(h[2].bias).data_ptr() for h in heads]),
-                   ops.L.ptr_array([ops.grad_of(h[0].bias).data_ptr() for h in heads]), 1, ops.stream())
+                   ops.L.ptr_array([ops.grad_of(h[0].bias).data_ptr() for h in heads]), 1, 1.0 / S, ops.stream())
         ld = (Cin * 9, 9, 1)
         rows = [(i * Hd, (i + 1) * Hd, ops.grad_of(h[0].weight), ld) for i, h in enumerate(heads)]
         ops.conv_wgrad(dhid, feat, 3, 3, 1, 1, None, None, rows=rows)
-        fuse = ctx.prod is not None and feat.dtype == torch.bfloat16
+        fuse = ctx.prod is not None and feat.dtype in ops.HALF
         dfeat = ops.conv_dgrad(dhid, ops.pack_concat(w0s, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1,
                                bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
         if fuse:

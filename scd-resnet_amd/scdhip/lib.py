@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("SCDHIP_LIB", os.path.join(HERE, "libscdhip.so"))
 
 DT_F32 = 0
 DT_BF16 = 1
+DT_F16 = 2
 MAX_TAPS = 16
 MAX_PHASES = 4
 STAT_REPLICAS = 64
@@ -54,7 +55,7 @@ SIGNATURES = {
     "scd_conv_wgrad_nsplit": (I, [I, L, I, I, I]),
     "scd_conv_wgrad_nsplit2": (I, [I, L, I, I, I, I, I]),
     "scd_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, IP, IP, P]),
-    "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, P]),
+    "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, F, P]),
     "scd_pack_weight": (I, [I, P, P, I, I, I, I, I, I, P]),
     "scd_pack_weights_batched": (I, [I, P, I, L, P]),
     "scd_pad_channels": (I, [I, P, L, I, I, P, P]),
@@ -79,7 +80,7 @@ SIGNATURES = {
     "scd_heads_fwd": (I, [I, P, I, I, I, I, IP, PP, PP, PP, P]),
     "scd_heads_bwd_accsize": (c_size_t, [I, I, IP]),
     "scd_heads_bwd": (I, [I, P, I, I, I, I, IP, PP, PP, P, P, P]),
-    "scd_heads_bwd_weight_finalize": (I, [P, I, I, IP, PP, PP, PP, I, P]),
+    "scd_heads_bwd_weight_finalize": (I, [P, I, I, IP, PP, PP, PP, I, F, P]),
     "scd_focal_fwd": (I, [P, P, L, P, P, P]),
     "scd_l1_gather_fwd": (I, [P, I, I, I, P, P, P, I, I, I, P, P, P]),
     "scd_centernet_loss_finalize": (I, [P, I, P, I, P, P, P, P]),

@@ -13,7 +13,40 @@ import torch.distributed as dist
 
 from . import lib as L
 
-_DT = {torch.float32: L.DT_F32, torch.bfloat16: L.DT_BF16}
+_DT = {torch.float32: L.DT_F32, torch.bfloat16: L.DT_BF16, torch.float16: L.DT_F16}
+HALF = (torch.bfloat16, torch.float16)      # 16-bit compute dtypes (same kernels, tiles and dispatch rules)
+
+
+class LossScale:
+    """Static loss scale of the fp16 compute mode: fp16 has 5 exponent bits, so the backward runs on gradients
+    multiplied by `f16` (HeadsFn.backward scales the head-output gradients) and every parameter-gradient
+    reduction multiplies by 1/scale on its way into .grad (scd_wgrad_reduce / scd_heads_bwd_weight_finalize alpha,
+    scd_bn_bwd_finalize gscale): parameters see the unscaled gradient, bit-exact power-of-two unscaling.
+    bf16 / fp32 run unscaled.  SCD_F16_LOSS_SCALE overrides the default 1024.  The unscaling applies inside the
+    backward pass (autograd graph task) whose head gradients were scaled (``scaled_task``), so direct kernel calls
+    and other models see unscaled gradients."""
+    f16 = float(os.environ.get("SCD_F16_LOSS_SCALE", "1024"))
+    scaled_task = None
+
+
+def loss_scale(dtype):
+    return LossScale.f16 if dtype == torch.float16 else 1.0
+
+
+def begin_loss_scale(dtype):
+    """Called where a backward pass enters the fp16 path (HeadsFn.backward): returns the factor to multiply the
+    incoming gradients by and marks the running backward pass as scaled."""
+    S = loss_scale(dtype)
+    if S != 1.0:
+        LossScale.scaled_task = _graph_task()
+    return S
+
+
+def grad_alpha(t):
+    """1 / loss scale for a parameter gradient computed from activations / gradients like t in the running backward."""
+    if t.dtype == torch.float16 and LossScale.scaled_task is not None and _graph_task() == LossScale.scaled_task:
+        return 1.0 / LossScale.f16
+    return 1.0
 
 
 def dt(t):
@@ -374,7 +407,7 @@ def pad_channels(t, C, Cp, rows):
 def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, stats=None, relu=False,
           accumulate=False, bn_bwd=None):
     N, Hi, Wi, Ci = x.shape
-    bk = 64 if x.dtype == torch.bfloat16 else 32
+    bk = 64 if x.dtype in HALF else 32
     if Ci % bk:
         # narrow layer (16/32 channels): zero-extend the input per pixel and the operand per tap to the K-stage
         Cp = -(-Ci // bk) * bk
@@ -586,7 +619,7 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
     cv = Ci if cvalid is None else cvalid
     for r0, r1, d, (ldn, ldc, ldt) in rows:
         L.call("scd_wgrad_reduce", ptr(ws), ns, Cg, T, Ci, r0, r1, cv, ldn, ldc, ldt, ptr(d), int(accumulate),
-               stream())
+               grad_alpha(g), stream())
 
 
 # ------------------------------------------------------------------ BatchNorm (training)
@@ -638,19 +671,20 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None)
         stats = bn_stats(bn, "bwd")
         L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd), C,
                y.numel(), ptr(stats), stream())
-    coef = bn_backward_coef(bn, st, stats, C)
+    coef = bn_backward_coef(bn, st, stats, C, grad_alpha(y))
     dy = torch.empty_like(y)
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),
            ptr(dz_out), stream())
     return dy
 
 
-def bn_backward_coef(bn, st, stats, C):
-    """SyncBN all-reduce of the backward sums, dgamma/dbeta accumulation and the apply coefficients."""
+def bn_backward_coef(bn, st, stats, C, alpha=1.0):
+    """SyncBN all-reduce of the backward sums, dgamma/dbeta accumulation (times alpha: 1 / the fp16 loss scale)
+    and the apply coefficients."""
     nrep = _allreduce_stats(stats, C)
     coef = torch.empty(3 * C, device=stats.device)
     L.call("scd_bn_bwd_finalize", ptr(stats), nrep, C, float(st.count), ptr(bn.weight), ptr(st.mean),
-           ptr(st.invstd), ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), 1.0 / bn_sync_world(), ptr(coef),
+           ptr(st.invstd), ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), alpha / bn_sync_world(), ptr(coef),
            stream())
     return coef
 
@@ -679,7 +713,7 @@ def stem_direct_ok(x, dtype):
     """The direct stem kernels (bf16; Conv2d(1,64,7,s2,p3) with an output width that is a multiple of 128)."""
     N, _, H, W = x.shape
     Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    return dtype == torch.bfloat16 and Wo % 128 == 0 and Ho % 2 == 0
+    return dtype in HALF and Wo % 128 == 0 and Ho % 2 == 0
 
 
 def stem_conv_fwd(x, wpk, stats=None):
@@ -687,8 +721,8 @@ def stem_conv_fwd(x, wpk, stats=None):
     _need_gpu(x)
     N, _, H, W = x.shape
     Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    y = torch.empty(N, Ho, Wo, 64, dtype=torch.bfloat16, device=x.device)
-    L.call("scd_stem_conv_fwd", L.DT_BF16, ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo, stream())
+    y = torch.empty(N, Ho, Wo, 64, dtype=wpk.dtype, device=x.device)
+    L.call("scd_stem_conv_fwd", dt(wpk), ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo, stream())
     return y
 
 
@@ -700,9 +734,10 @@ def stem_conv_wgrad(dy, x, dst, accumulate=True, ybn=None, coef=None):
     M = N * Ho * Wo
     ns = L.lib().scd_stem_conv_wgrad_nsplit(M)
     ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=dy.device)
-    L.call("scd_stem_conv_wgrad", L.DT_BF16, ptr(dy), ptr(ybn), ptr(coef), ptr(x), ptr(ws), ns, N, H, W, Ho, Wo,
+    L.call("scd_stem_conv_wgrad", dt(dy), ptr(dy), ptr(ybn), ptr(coef), ptr(x), ptr(ws), ns, N, H, W, Ho, Wo,
            stream())
-    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 49, 49, 1, 0, ptr(dst), int(accumulate), stream())
+    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 49, 49, 1, 0, ptr(dst), int(accumulate), grad_alpha(dy),
+           stream())
 
 
 class StemFused:
@@ -734,7 +769,7 @@ def stem_gram(x, wpk, stats):
     ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=x.device)
     L.call("scd_stem_gram", ptr(x), ptr(ws), ns, N, H, W, Ho, Wo, stream())
     G = torch.empty(64 * 64, dtype=torch.float32, device=x.device)
-    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(G), 0, stream())
+    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(G), 0, 1.0, stream())
     if stats is not None:
         L.call("scd_stem_gram_stats", ptr(G), ptr(wpk), ptr(stats), stream())
     return G
@@ -761,7 +796,7 @@ def stem_fused_bwd(bn, st, dout, am, yam, x, G, wpk, dst):
     L.call("scd_stem_wgrad_pooled", ptr(dout), ptr(am), ptr(yam), ptr(st.scale), ptr(st.shift), ptr(st.mean),
            ptr(st.invstd), ptr(x), ptr(ws), ptr(stats), ns, N, H, W, Ho, Wo, Hp, Wp, stream())
     T1 = torch.empty(64 * 64, dtype=torch.float32, device=x.device)
-    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(T1), 0, stream())
+    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(T1), 0, 1.0, stream())
     coef = bn_backward_coef(bn, st, stats, 64)
     L.call("scd_stem_wgrad_combine", ptr(T1), 1, ptr(coef), ptr(G), ptr(wpk), ptr(dst), 1, stream())
 
@@ -784,7 +819,7 @@ def stem_pool_bwd_bn(bn, dout, am, y, st):
     stats = bn_stats(bn, "bwd")
     L.call("scd_stem_pool_bwd_bn", dt(y), ptr(dout), ptr(am), ptr(y), ptr(st.scale), ptr(st.shift), ptr(st.mean),
            ptr(st.invstd), ptr(dz), ptr(stats), N, H, W, C, dout.shape[1], dout.shape[2], stream())
-    return dz, bn_backward_coef(bn, st, stats, C)
+    return dz, bn_backward_coef(bn, st, stats, C, grad_alpha(y))
 
 
 def stem_pool_bwd(dout, am, y, st):

@@ -82,7 +82,8 @@ def ref_heads(heads, feat):
             for h in heads]
 
 
-def check(name, got, ref, report):
+def check(name, got, ref, report, scale=1.0):
+    """scale: the 16-bit type's rounding relative to bf16's (fp16: 2^-11 / 2^-9 = 1/4)."""
     got, ref = got.float(), ref.float()
     assert got.shape == ref.shape, (name, got.shape, ref.shape)
     assert torch.isfinite(got).all(), name
@@ -91,7 +92,7 @@ def check(name, got, ref, report):
     mx = err.max().item() / rms
     me = err.square().mean().sqrt().item() / rms
     report.append((name, mx, me))
-    assert mx <= TOL_RMS and me <= TOL_MEAN, (name, mx, me)
+    assert mx <= TOL_RMS * scale and me <= TOL_MEAN * scale, (name, mx, me)
 
 
 def capture_forward(m, x, monkeypatch):
@@ -133,20 +134,20 @@ def capture_forward(m, x, monkeypatch):
     return rec
 
 
-def check_groups(m, rec, report):
+def check_groups(m, rec, report, scale=1.0):
     kinds = [r[0] for r in rec]
     assert kinds[0] == "stem" and kinds[-1] == "heads" and "deconv" in kinds and "block" in kinds, kinds
     with torch.no_grad():
         for kind, mod, inp, out in rec:
             if kind == "stem":
-                check("stem", _nchw(out), ref_stem(m.preprocess, inp.float()), report)
+                check("stem", _nchw(out), ref_stem(m.preprocess, inp.float()), report, scale)
             elif kind == "block":
-                check("block %s" % mod.conv1.weight.shape[0], _nchw(out), ref_block(mod, _nchw(inp)), report)
+                check("block %s" % mod.conv1.weight.shape[0], _nchw(out), ref_block(mod, _nchw(inp)), report, scale)
             elif kind == "deconv":
-                check("deconv %d" % mod[0].weight.shape[1], _nchw(out), ref_deconv(mod[0], mod[1], _nchw(inp)), report)
+                check("deconv %d" % mod[0].weight.shape[1], _nchw(out), ref_deconv(mod[0], mod[1], _nchw(inp)), report, scale)
             else:
                 for i, (o, r) in enumerate(zip(out, ref_heads(mod, _nchw(inp)))):
-                    check("head %d" % i, o, r, report)
+                    check("head %d" % i, o, r, report, scale)
 
 
 def _print(report):
@@ -154,20 +155,21 @@ def _print(report):
         print("%-14s max|err|/rms %.5f  rms(err)/rms %.6f" % (name, mx, me))
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", [("centerOffsetRes10", 32, 512), ("centerOffsetRes50", 2, 128),
                                   ("centerOffsetRes50", 16, 1024)])
-def test_bf16_groups_match_fp32(case, monkeypatch):
-    """Every module group of the bf16 forward vs PyTorch fp32 from the same bf16 input: Res10 at the benchmark
+def test_bf16_groups_match_fp32(case, dtype, monkeypatch):
+    """Every module group of the 16-bit forward vs PyTorch fp32 from the same 16-bit input: Res10 at the benchmark
     configuration (BASELINE configs[1], B=32 512^2), Res50 at F9's size and at BASELINE configs[4] (1024^2, 16
-    images per GPU)."""
+    images per GPU).  fp16 (the dtype BASELINE configs[4] names) rounds at 2^-11: a quarter of the bf16 bound."""
     name, B, S = case
-    m, _ = _model(name, torch.bfloat16)
+    m, _ = _model(name, dtype)
     x = T.batch_inputs(31, B, S).to(DEV) if S == 512 else torch.randn(B, 1, S, S, device=DEV,
                                                                        generator=torch.Generator(DEV).manual_seed(3))
     rec = capture_forward(m, x, monkeypatch)
     report = []
     try:
-        check_groups(m, rec, report)
+        check_groups(m, rec, report, 0.25 if dtype == torch.float16 else 1.0)
     finally:
         _print(report)
     nblk = sum(len(layer) for layer in (m.layer1, m.layer2, m.layer3, m.layer4))
@@ -280,13 +282,14 @@ def test_cornernet_b32_bf16_config3(monkeypatch):
     assert all(math.isfinite(v) for v in losses) and losses[-1] < losses[0], losses
 
 
-def test_res50_1024_b16_bf16_config4_trains():
-    """BASELINE configs[4] per GPU: centerOffsetRes50 at 1024^2, 16 images, bf16, the reference's own initialisation
-    (seed 42, residuals.py:336-353) -- finite, decreasing loss over 6 Adam steps (per-group numerics:
-    test_bf16_groups_match_fp32)."""
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_res50_1024_b16_bf16_config4_trains(dtype):
+    """BASELINE configs[4] per GPU: centerOffsetRes50 at 1024^2, 16 images, fp16 (as named) and bf16, the
+    reference's own initialisation (seed 42, residuals.py:336-353) -- finite, decreasing loss over 6 Adam steps
+    (per-group numerics: test_bf16_groups_match_fp32)."""
     import trainer.model.centerOffsetRes50 as plugin
     torch.random.manual_seed(42)
-    m = plugin.model(**plugin.modelParams).to(DEV).train().set_compute_dtype(torch.bfloat16)
+    m = plugin.model(**plugin.modelParams).to(DEV).train().set_compute_dtype(dtype)
     g = torch.Generator().manual_seed(1000)
     B, S = 16, 1024
     H = S // 4
@@ -297,5 +300,36 @@ def test_res50_1024_b16_bf16_config4_trains():
     inds = torch.randint(0, H * H, (B, 30), generator=g) * mask
     ys = [heat.to(DEV), mask.to(DEV), regr.to(DEV), inds.to(DEV)]
     losses = _train_steps(m, plugin, x, ys, 6)
-    print("res50 1024^2 B=16 bf16 losses", losses)
+    print("res50 1024^2 B=16 %s losses" % dtype, losses)
     assert all(math.isfinite(v) for v in losses) and max(losses[-2:]) < losses[0], losses
+
+
+def test_f16_loss_scaled_gradients_match_fp32():
+    """fp16 mode trains on loss-scaled gradients (ops.LossScale: head-output gradients x 1024, every parameter
+    gradient reduction x 1/1024): one Res10 step at B=4 512^2 -- every parameter gradient of the fp16 path against
+    the fp32 parity path, normwise, compared with the same for bf16 (fp16 must be at least 2x closer), and no
+    gradient is inf / nan."""
+    from scdhip import ops
+    assert ops.loss_scale(torch.float16) > 1.0
+    x = T.batch_inputs(41, 4, 512).to(DEV)
+    ys = [y.to(DEV) for y in T.batch_targets(42, 4, 128)]
+    grads = {}
+    for dtype in (torch.float32, torch.float16, torch.bfloat16):
+        m, plugin = _model("centerOffsetRes10", dtype)
+        loss, _ = plugin.loss(m(x, decode=False), ys)
+        loss.mean().backward()
+        grads[dtype] = {k: p.grad.detach().double().clone() for k, p in m.named_parameters()}
+    worst = {torch.float16: 0.0, torch.bfloat16: 0.0}
+    for k, g32 in grads[torch.float32].items():
+        n = g32.norm().item()
+        for dt in worst:
+            g = grads[dt][k]
+            assert torch.isfinite(g).all(), (dt, k)
+            if n > 0:
+                worst[dt] = max(worst[dt], (g - g32).norm().item() / n)
+    print("worst normwise gradient error vs fp32: fp16 %.4f bf16 %.4f" % (worst[torch.float16], worst[torch.bfloat16]))
+    # measured (MI355X): fp16 0.157, bf16 0.418 -- the BN backward's cancellation amplifies 16-bit rounding in the
+    # small-norm gradients; with 3 fewer mantissa bits lost, fp16 must sit well below bf16 (an underflowing, unscaled
+    # fp16 backward would not)
+    assert worst[torch.float16] < 0.25
+    assert worst[torch.float16] < 0.5 * worst[torch.bfloat16]

@@ -26,7 +26,7 @@ def nchw(t):
     return t.float().permute(0, 3, 1, 2).cpu()
 
 
-TOL = {torch.float32: 1e-4, torch.bfloat16: 3e-2}
+TOL = {torch.float32: 1e-4, torch.bfloat16: 3e-2, torch.float16: 1e-2}
 CONV_CASES = [  # N, Cin, H, W, Cout, k, stride, pad
     (2, 64, 16, 16, 64, 3, 1, 1),
     (2, 64, 16, 16, 128, 3, 2, 1),
@@ -39,7 +39,7 @@ CONV_CASES = [  # N, Cin, H, W, Cout, k, stride, pad
 ]
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd_dgrad_wgrad(case, dtype):
     from scdhip import ops
@@ -47,14 +47,14 @@ def test_conv_fwd_dgrad_wgrad(case, dtype):
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
     x = torch.randn(N, Cin, H, W, generator=g)
     w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
-    if dtype == torch.bfloat16:       # compare on bf16-representable operands
-        x, w = x.bfloat16().float(), w.bfloat16().float()
+    if dtype != torch.float32:        # compare on operands representable in the 16-bit type
+        x, w = x.to(dtype).float(), w.to(dtype).float()
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     yr = F.conv2d(xr, wr, stride=s, padding=p)
     dy = torch.randn(yr.shape, generator=g)
-    if dtype == torch.bfloat16:
-        dy = dy.bfloat16().float()
+    if dtype != torch.float32:
+        dy = dy.to(dtype).float()
     yr.backward(dy)
     wd = w.to(DEV)
     xg = nhwc(x, dtype)
@@ -85,12 +85,13 @@ LARGE_CONV_CASES = [
 ]
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", LARGE_CONV_CASES)
-def test_conv_large_bf16(case):
-    test_conv_fwd_dgrad_wgrad(case, torch.bfloat16)
+def test_conv_large_bf16(case, dtype):
+    test_conv_fwd_dgrad_wgrad(case, dtype)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", [(2, 128, 5, 7, 64), (1, 256, 8, 8, 256), (2, 64, 16, 16, 128),
                                   (8, 256, 64, 64, 256)])
 def test_deconv_fwd_dgrad_wgrad(case, dtype):
@@ -99,14 +100,14 @@ def test_deconv_fwd_dgrad_wgrad(case, dtype):
     g = torch.Generator().manual_seed(7)
     x = torch.randn(N, Cin, H, W, generator=g)
     w = torch.randn(Cin, Cout, 4, 4, generator=g) / (Cin * 4) ** 0.5
-    if dtype == torch.bfloat16:
-        x, w = x.bfloat16().float(), w.bfloat16().float()
+    if dtype != torch.float32:
+        x, w = x.to(dtype).float(), w.to(dtype).float()
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     yr = F.conv_transpose2d(xr, wr, stride=2, padding=1)
     dy = torch.randn(yr.shape, generator=g)
-    if dtype == torch.bfloat16:
-        dy = dy.bfloat16().float()
+    if dtype != torch.float32:
+        dy = dy.to(dtype).float()
     yr.backward(dy)
     wd = w.to(DEV)
     xg = nhwc(x, dtype)
@@ -121,7 +122,7 @@ def test_deconv_fwd_dgrad_wgrad(case, dtype):
     assert rel_err(dw, wr.grad) < TOL[dtype] * 3
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,H,W", [(1, 128, 128), (2, 128, 128), (3, 37, 45)])
 def test_heads_fused_gemm(N, H, W, dtype):
     """scd_conv_gemm_heads (3x3 conv + bias + ReLU with the three 1x1 tails in the epilogue) against
@@ -136,9 +137,9 @@ def test_heads_fused_gemm(N, H, W, dtype):
     b0 = [0.1 * torch.randn(128, generator=g) for _ in od]
     w1 = [torch.randn(o, 128, 1, 1, generator=g) / 128 ** 0.5 for o in od]
     b1 = [0.1 * torch.randn(o, generator=g) for o in od]
-    if dtype == torch.bfloat16:
-        x = x.bfloat16().float()
-        w0 = [w.bfloat16().float() for w in w0]
+    if dtype != torch.float32:
+        x = x.to(dtype).float()
+        w0 = [w.to(dtype).float() for w in w0]
     refs = [F.conv2d(F.relu(F.conv2d(x, a, b, padding=1)), c, d) for a, b, c, d in zip(w0, b0, w1, b1)]
     xg = nhwc(x, dtype)
     w0c = torch.cat(w0, 0).to(DEV)
@@ -154,12 +155,12 @@ def test_heads_fused_gemm(N, H, W, dtype):
     torch.cuda.synchronize()
     for o, r in zip(outs, refs):
         assert torch.isfinite(o).all()
-        assert rel_err(o, r) < TOL[dtype] * (3 if dtype == torch.bfloat16 else 10)
+        assert rel_err(o, r) < TOL[dtype] * (10 if dtype == torch.float32 else 3)
     hid_ref = torch.cat([F.relu(F.conv2d(x, a, b, padding=1)) for a, b in zip(w0, b0)], 1)
     assert rel_err(nchw(hid), hid_ref) < TOL[dtype] * 2
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("HW", [(128, 128), (9, 11)])
 def test_heads_tail_backward(HW, dtype):
     """scd_heads_bwd + finalize (CenterNet tails, centerNetOffset.py:108-110): dhid = relu'(hid) * W1^T dout,
@@ -171,8 +172,8 @@ def test_heads_tail_backward(HW, dtype):
     N, (H, W), Hd, od = 2, HW, 128, [1, 4, 2]
     P = N * H * W
     hid = F.relu(torch.randn(N, H, W, Hd * 3, generator=g))
-    if dtype == torch.bfloat16:
-        hid = hid.bfloat16().float()
+    if dtype != torch.float32:
+        hid = hid.to(dtype).float()
     w1 = [torch.randn(o, Hd, generator=g) / Hd ** 0.5 for o in od]
     douts = [torch.randn(N, o, H, W, generator=g) for o in od]
     hd = hid.to(DEV, dtype).contiguous()
@@ -188,10 +189,10 @@ def test_heads_tail_backward(HW, dtype):
            L.ptr_array([w.data_ptr() for w in w1d]), L.ptr_array([d.data_ptr() for d in dd]), ops.ptr(dhid),
            ops.ptr(acc), ops.stream())
     L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), 3, Hd, odarr, L.ptr_array([t.data_ptr() for t in dw1]),
-           L.ptr_array([t.data_ptr() for t in db1]), L.ptr_array([t.data_ptr() for t in db0]), 0, ops.stream())
+           L.ptr_array([t.data_ptr() for t in db1]), L.ptr_array([t.data_ptr() for t in db0]), 0, 1.0, ops.stream())
     torch.cuda.synchronize()
     hp = hid.reshape(P, 3 * Hd)
-    tol = TOL[dtype] if dtype == torch.bfloat16 else 1e-5
+    tol = TOL[dtype] if dtype != torch.float32 else 1e-5
     for h, o in enumerate(od):
         hh = hp[:, h * Hd:(h + 1) * Hd]
         dh = douts[h].permute(0, 2, 3, 1).reshape(P, o)
@@ -218,30 +219,31 @@ def test_stem_im2col_gemm_pool(dtype):
     assert rel_err(nchw(y), yr) < TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(2, 512, 512), (1, 260, 256)])
-def test_stem_direct_bf16(shape):
+def test_stem_direct_bf16(shape, dtype):
     """Direct stem conv (tap tile built in LDS) forward + BN sums and its weight gradient vs torch fp32."""
     from scdhip import ops
     N, H, W = shape
     g = torch.Generator().manual_seed(5)
-    x = torch.randn(N, 1, H, W, generator=g).bfloat16().float()
-    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).bfloat16().float()
+    x = torch.randn(N, 1, H, W, generator=g).to(dtype).float()
+    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).to(dtype).float()
     xr = x.clone()
     wr = w.clone().requires_grad_(True)
     yr = F.conv2d(xr, wr, stride=2, padding=3)
-    dy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    dy = torch.randn(yr.shape, generator=g).to(dtype).float()
     yr.backward(dy)
     xd = x.to(DEV)
-    assert ops.stem_direct_ok(xd, torch.bfloat16)
+    assert ops.stem_direct_ok(xd, dtype)
     stats = ops.new_stats(64, DEV)
-    y = ops.stem_conv_fwd(xd, ops.pack_weight(w.to(DEV), torch.bfloat16, 0, ldp=64), stats=stats)
-    assert rel_err(nchw(y), yr) < TOL[torch.bfloat16]
+    y = ops.stem_conv_fwd(xd, ops.pack_weight(w.to(DEV), dtype, 0, ldp=64), stats=stats)
+    assert rel_err(nchw(y), yr) < TOL[dtype]
     st = stats.view(-1, 2, 64).sum(0).cpu()
     yd = yr.detach().double()
     np.testing.assert_allclose(st[0].numpy(), yd.sum((0, 2, 3)).numpy(), rtol=1e-3, atol=1e-2 * yd.numel() ** 0.5)
     dw = torch.full((64, 1, 7, 7), 0.25, device=DEV)
-    ops.stem_conv_wgrad(nhwc(dy, torch.bfloat16), xd, dw, accumulate=True)
-    assert rel_err(dw - 0.25, wr.grad) < TOL[torch.bfloat16] * 3
+    ops.stem_conv_wgrad(nhwc(dy, dtype), xd, dw, accumulate=True)
+    assert rel_err(dw - 0.25, wr.grad) < TOL[dtype] * 3
 
 
 def test_stem_fused_backward_matches_unfused():
