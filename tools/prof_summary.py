@@ -10,17 +10,20 @@ import sys
 from collections import defaultdict
 
 
+_TY = {"DF16b": "bf16", "DF16_": "f16", "f": "f32"}
+
+
 def short(name):
     n = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", name)
-    m = re.match(r"(\w+?)I(DF16b|f)Li(\d+)ELi(\d+)E(Lb([01])E)?", n)
+    m = re.match(r"(\w+?)I(DF16b|DF16_|f)Li(\d+)ELi(\d+)E(Lb([01])E)?", n)
     if m:
         tail = ""
         if m.group(6) == "1":
             tail = ",fastx" if m.group(1).startswith("conv_wgrad") else ",heads"
-        return "%s<%s,%s,%s%s>" % (m.group(1), "bf16" if m.group(2) == "DF16b" else "f32", m.group(3), m.group(4), tail)
-    m = re.match(r"(\w+?)I(DF16b|f)E", n)
+        return "%s<%s,%s,%s%s>" % (m.group(1), _TY[m.group(2)], m.group(3), m.group(4), tail)
+    m = re.match(r"(\w+?)I(DF16b|DF16_|f)E", n)
     if m:
-        return "%s<%s>" % (m.group(1), "bf16" if m.group(2) == "DF16b" else "f32")
+        return "%s<%s>" % (m.group(1), _TY[m.group(2)])
     n = n.replace("(anonymous namespace)::", "")
     m = re.search(r"conv_gemm_pp_kernel<(\d+)(, (true|false))?>", n)
     if m:
