@@ -89,7 +89,7 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
 // Shared GEMM epilogue (NT = 2*BM threads, waves of 64x64 outputs, WN waves along N): bias / ReLU in
 // registers, the wave's tile staged in LDS, coalesced 16-B NHWC stores (+= when accumulating), BN
 // channel sums into fp64 replicas, and optionally the fused 1x1 head tails (n-tile t == head t).
-template <typename T, int BM, int BN, int WN, bool HEADS>
+template <typename T, int BM, int BN, int WN, bool HEADS, bool BNB = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[4][4], char* smem, int tid, int bid,
                                               int mt, int nt, int M, int QQ, const scd_gemm_phase& ph) {
     constexpr int ESZ = sizeof(T);
@@ -107,21 +107,65 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
+    // BN-backward mode (BNB: 16-bit types, scd_conv_gemm_bnbwd): output pixel of each of the lane's 4 rows
+    // (-1 past the end); a separate instantiation, so the other kernels keep their register allocation
+    int pix[4];
+    if constexpr (BNB) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const int m = mt * BM + wm * 64 + a * 16 + l16;
+            const int n = m / QQ;
+            const int rem = m - n * QQ;
+            const int qh = rem / ph.Qw, qw = rem - (rem / ph.Qw) * ph.Qw;
+            pix[a] = m < M ? (n * p.Ho + p.os * qh + ph.rho_h) * p.Wo + p.os * qw + ph.rho_w : -1;
+        }
+    }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         const int col0 = nt * BN + wn * 64 + b * 16 + lg * 4;
         float bias[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+        float bmu[4], bis[4], bsc[4], bsh[4];
+        uint2 yq[4];
+        if constexpr (BNB) {
+            const bool okc = col0 < p.Co;
+            const float4 f0 = okc ? *(const float4*)(p.bn_mean + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 f1 = okc ? *(const float4*)(p.bn_invstd + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 f2 = okc ? *(const float4*)(p.bn_rsc + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 f3 = okc ? *(const float4*)(p.bn_rsh + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            bmu[0] = f0.x; bmu[1] = f0.y; bmu[2] = f0.z; bmu[3] = f0.w;
+            bis[0] = f1.x; bis[1] = f1.y; bis[2] = f1.z; bis[3] = f1.w;
+            bsc[0] = f2.x; bsc[1] = f2.y; bsc[2] = f2.z; bsc[3] = f2.w;
+            bsh[0] = f3.x; bsh[1] = f3.y; bsh[2] = f3.z; bsh[3] = f3.w;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                yq[a] = (pix[a] >= 0 && okc) ? *(const uint2*)(p.bny + ((long)pix[a] * p.Co + col0) * 2)
+                                             : make_uint2(0, 0);
+        }
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
             const int m = mt * BM + wm * 64 + a * 16 + l16;
             float v[4];
+            if constexpr (!BNB) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = acc[a][b][r] + bias[r];
-                if (p.relu) v[r] = fmaxf(v[r], 0.f);
-                if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[a][b][r] + bias[r];
+                    if (p.relu) v[r] = fmaxf(v[r], 0.f);
+                    if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+                }
+            } else {
+                // the following BN+ReLU layer's backward sums over the gradient as stored (16-bit)
+                const unsigned yw[2] = {yq[a].x, yq[a].y};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[a][b][r];
+                    const float yv = h16_word_half(yw[r >> 1], r & 1);
+                    const float d = (float)(T)v[r];
+                    const float dz = yv * bsc[r] + bsh[r] > 0.f ? d : 0.f;
+                    csum[b][r] += dz;
+                    csq[b][r] += dz * (yv - bmu[r]) * bis[r];
+                }
             }
             char* dst = ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * ESZ;
             if constexpr (ESZ == 2) {
@@ -232,7 +276,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     }
 }
 
-template <typename T, int BM, int BN, bool HEADS>
+template <typename T, int BM, int BN, bool HEADS, bool BNB = false>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;       // elements per 16-B chunk
@@ -410,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
         }
     }
 
-    gemm_epilogue<T, BM, BN, WN, HEADS>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
+    gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
 }
 
 // -------------------------------------------------------------------------------------
@@ -547,7 +591,7 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, const char* 
                  : "memory");
 }
 
-template <bool HEADS>
+template <bool HEADS, bool BNB = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
     typedef __bf16 T;
     constexpr int BM = 256, BN = 128, WN = 2, BK = 64, EPC = 8;
@@ -686,7 +730,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    gemm_epilogue<T, BM, BN, WN, HEADS>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
+    gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
 }
 
 // -------------------------------------------------------------------------------------
@@ -2634,6 +2678,9 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st) {
     if (p.head_on) {
         if constexpr (BN == 128) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, true>), dim3(Mtot_tiles), dim3(256), 0, st, p);
         else return SCD_ERR_ARG;
+    } else if (p.bnbwd) {
+        if constexpr (sizeof(T) == 2) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false, true>), dim3(Mtot_tiles), dim3(256), 0, st, p);
+        else return SCD_ERR_ARG;
     } else {
         hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false>), dim3(Mtot_tiles), dim3(256), 0, st, p);
     }
@@ -2828,7 +2875,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
             SCD_RETURN_LAUNCH();
         }
     }
-    if (p.bnbwd) return SCD_ERR_ARG;      // BN-backward sums only in the ping-pong epilogue (caller falls back)
+    if (p.bnbwd && dtype != SCD_DT_BF16) return SCD_ERR_ARG;   // BN-backward sums: 16-bit epilogues (caller falls back)
     if (dtype == SCD_DT_BF16 && h64_mode() && h64_ok(p, nphase, phases)) {
         p.ntn = 1;
         p.ph[0] = phases[0];
@@ -2868,6 +2915,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     hipStream_t st = (hipStream_t)stream;
     if (ring) {
         if (p.head_on) hipLaunchKernelGGL((conv_gemm_ring_kernel<true>), dim3(tiles), dim3(512), 0, st, p);
+        else if (p.bnbwd) hipLaunchKernelGGL((conv_gemm_ring_kernel<false, true>), dim3(tiles), dim3(512), 0, st, p);
         else hipLaunchKernelGGL((conv_gemm_ring_kernel<false>), dim3(tiles), dim3(512), 0, st, p);
         SCD_RETURN_LAUNCH();
     }

@@ -463,6 +463,12 @@ BNBWD_CASES = [
     (4, 128, 128, 256, 256, 3, 2, 1, True),      # Bottleneck stride-2 3x3: 4 sub-pixel phases, out_stride 2
     (4, 128, 128, 512, 256, 1, 2, 0, True),      # downsample 1x1 stride 2: one phase with taps, three empty
     (16, 66, 70, 128, 192, 3, 2, 1, True),       # ragged phases (odd/even extents), 192-wide tiles
+    # the shared epilogue of the ring / register-staged kernels (BasicBlock layer1/layer2 bn1 shapes)
+    (4, 128, 128, 64, 64, 3, 1, 1, False),       # 64 channels: 256 x 64 register-staged kernel
+    (16, 64, 64, 128, 128, 3, 1, 1, False),      # 128 channels, >= 256 tiles: LDS-DMA ring kernel
+    (4, 64, 64, 128, 128, 3, 1, 1, False),       # 128 channels, few tiles: 128 x 128 register-staged kernel
+    (8, 64, 64, 128, 64, 3, 2, 1, False),        # stride-2 3x3 into 64 channels: 4 phases, narrow kernel
+    (3, 33, 35, 64, 128, 3, 2, 1, False),        # ragged odd extents, 128 x 128 kernel
 ]
 
 

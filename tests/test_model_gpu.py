@@ -315,6 +315,12 @@ def test_block_bn_backward_sums_from_dgrad_match_separate_reduce(name):
             ops.BNFusion.enabled = old
         torch.cuda.synchronize()
         grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters()})
+    # (the sums differ from the separate reduce's by fp32 summation order only -- the kernel tests check them
+    # exactly; the BN backward's cancellation amplifies that noise layer by layer down to the stem BN: measured
+    # 2.7% (Res10) / 6.9% (Res50, chaotic in bf16) on its bias gradient; the layers above the
+    # backbone see almost none of it; a wrong pixel / channel gives O(1))
+    deep = 5e-2 if name.endswith("Res10") else 0.15
     for k in grads[0]:
         a, b = grads[0][k], grads[1][k]
-        assert (a - b).abs().max().item() <= 2e-2 * max(1e-6, b.abs().max().item()), k
+        tol = 1e-2 if k.startswith(("heatmap", "offset", "regr", "deconvolutionLayers")) else deep
+        assert (a - b).abs().max().item() <= tol * max(1e-6, b.abs().max().item()), k
