@@ -317,6 +317,21 @@ int scd_cpool_bwd(int dtype, int dir, const void* x, const void* dy, void* dx, i
                   void* stream);
 
 /* library self-description (for the loader / tests) */
+/* ---- the reference's functional helpers, for user code that calls them directly (fp32, device pointers) ----
+ * scd_nms: out = x * (x == max over its k x k window, -inf padded), k odd -- utility.py:87-92 nonMaximumSuppression.
+ * scd_topk: per row of B x n scores, the K (<= 1024) largest (ties by ascending index) with the reference's split of
+ * the flat index into category = i / HW, index = i % HW, y = index / W, x = index % W -- utility.py:106-118.
+ * scd_focal_prob_fwd: focal.py:25-53 on probabilities: g = d(posL + negL)/dp per element, acc[rep][4] += {posL, negL,
+ * #pos}; scd_centernet_loss_finalize(acc, 1, NULL, 0, ...) forms the loss and the normaliser factor.
+ * scd_masked_l1_fwd: regression.py:28-44 on (rows, C) gathered values: acc[0..1] += {sum of |d| (smooth: smooth-L1,
+ * beta 1) over masked rows, #masked rows}, g = d/d(r) of that sum (0 on unmasked rows). */
+int scd_nms(const float* x, long planes, int H, int W, int k, float* out, void* stream);
+int scd_topk(const float* scores, int B, long n, int K, int HW, int W, float* out_scores, int64_t* inds, int* cats,
+             float* ys, float* xs, void* stream);
+int scd_focal_prob_fwd(const float* p, const float* gt, long n, float* g, double* acc, void* stream);
+int scd_masked_l1_fwd(const float* r, const float* t, const uint8_t* mask, long rows, int C, int smooth, float* g,
+                      double* acc, void* stream);
+
 /* ---- HIP events for live kernel timing (bench.py roofline; scdhip.ops.LaunchTimer) ----
  * scd_event_record stamps the event on `stream`; while the stream is being captured into a graph the record is an
  * external event node (hipEventRecordExternal), re-stamped by every replay.  scd_event_elapsed_ms waits for `end`. */

@@ -1,14 +1,13 @@
 """Backbone utilities (models/backbones/utility.py of the reference).
 
 ``convolution3x3`` builds the module used by BasicBlock.  The functional helpers keep the
-reference API for user code and evaluation; on the training/decode path they are replaced
-by fused kernels: gather + clampSigmoid inside scdhip.loss.CenterNetLossFn, NMS + top-K +
-gather inside scdhip.ops.decode_topk.
+reference API for user code and evaluation and run on libscdhip (scdhip.api: scd_nms, scd_topk);
+on the training/decode path the fused kernels take their place: gather + clampSigmoid inside
+scdhip.loss.CenterNetLossFn, NMS + top-K + gather inside scdhip.ops.decode_topk.
 """
 import torch
-import torch.nn.functional as F
 
-from scdhip import ops
+from scdhip import api, ops
 
 
 def convolution3x3(inputDimension, outputDimension, stride=1):
@@ -35,18 +34,13 @@ def reshapeGatherFeatures(feat, ind):
 
 
 def nonMaximumSuppression(heat, kernelSize=3):
-    """utility.py:87-92"""
-    hmax = F.max_pool2d(heat, (kernelSize, kernelSize), stride=1, padding=(kernelSize - 1) // 2)
-    return heat * (hmax == heat).float()
+    """utility.py:87-92: heat * (maxpool_kxk(heat) == heat) (scd_nms)."""
+    return api.nms(heat, kernelSize)
 
 
 def extractTopK(scores, K=20):
-    """utility.py:106-118 (returns scores, inds, categories, ys, xs)."""
-    batch, category, height, width = scores.size()
-    topKScores, topKIndices = torch.topk(scores.view(batch, -1), K)
-    topKCategories = (topKIndices // (height * width)).int()
-    topKIndices = topKIndices % (height * width)
-    return topKScores, topKIndices, topKCategories, (topKIndices // width).float(), (topKIndices % width).float()
+    """utility.py:106-118 (returns scores, inds, categories, ys, xs; scd_topk, ties by ascending index)."""
+    return api.topk(scores, K)
 
 
 def clampSigmoid(x):

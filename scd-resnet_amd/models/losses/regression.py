@@ -1,19 +1,15 @@
 """Masked regression losses (models/losses/regression.py:28-44 of the reference).
 
-``L1LossMask`` keeps the reference signature; CenterNetLoss recognises it and runs the
-fused gather + L1 kernel (scd_l1_gather_fwd) instead.  ``smoothL1LossMask`` is API-only
-(unused by the benchmarked plugins).
+``L1LossMask`` / ``smoothL1LossMask`` keep the reference signatures and run on libscdhip (scdhip.api.masked_l1:
+scd_masked_l1_fwd, normaliser #mask + 1e-4 kept on the device).  CenterNetLoss recognises L1LossMask and runs the
+fused gather + L1 kernel (scd_l1_gather_fwd) instead.
 """
-import torch.nn.functional as F
+from scdhip import api
 
 
 def smoothL1LossMask(regression, groundTruth, mask):
-    num = mask.float().sum()
-    m = mask.bool().unsqueeze(2).expand_as(groundTruth)
-    return F.smooth_l1_loss(regression[m], groundTruth[m], reduction="sum") / (num + 1e-4)
+    return api.masked_l1(regression, groundTruth, mask, smooth=True)
 
 
 def L1LossMask(regression, groundTruth, mask):
-    num = mask.float().sum()
-    m = mask.bool().unsqueeze(2).expand_as(groundTruth)
-    return F.l1_loss(regression[m], groundTruth[m], reduction="sum") / (num + 1e-4)
+    return api.masked_l1(regression, groundTruth, mask, smooth=False)

@@ -101,6 +101,10 @@ SIGNATURES = {
     "scd_render_center_targets": (I, [P, P, I, I, I, F, P, P, P, P, P]),
     "scd_cpool_fwd": (I, [I, I, P, P, P, I, I, I, I, P]),
     "scd_cpool_bwd": (I, [I, I, P, P, P, I, I, I, I, P]),
+    "scd_nms": (I, [P, L, I, I, I, P, P]),
+    "scd_topk": (I, [P, I, L, I, I, I, P, P, P, P, P, P]),
+    "scd_focal_prob_fwd": (I, [P, P, L, P, P, P]),
+    "scd_masked_l1_fwd": (I, [P, P, P, L, I, I, P, P, P]),
     "scd_event_create": (I, [PP]),
     "scd_event_destroy": (I, [P]),
     "scd_event_record": (I, [P, P]),
