@@ -8,7 +8,7 @@ slide resized to whole strides by torch-'reflect' padding plus its opencv column
 Clip extraction + greyscale + normalisation run as scd_slide_tiles (nothing padded is materialised), the score
 threshold and the projection back to slide pixels as scd_slide_detections; the slide goes to the device once.
 
-CLI:  python slide.py <architecture> <state_dict.pt> <image> [<image> ...]   (-eval: BN in eval mode)
+CLI:  python slide.py <architecture> <state_dict.pt | traced.pt> <image> [<image> ...]   (-eval: BN in eval mode)
 """
 import sys
 from math import ceil
@@ -79,12 +79,19 @@ def main(argv):
         print(__doc__)
         return 2
     arch, ckpt, images = argv[0], argv[1], argv[2:]
-    plugin = importlib.import_module("trainer.model." + arch)
-    model = plugin.model(**plugin.modelParams)
-    model.load_state_dict(torch.load(ckpt, map_location="cpu", weights_only=True))
-    model = model.cuda()
-    model.train(not evalMode)
-    wrapper = importlib.import_module("trainer.wrappers.centerOffsetResidual").Wrapper(model)
+    import zipfile
+    if zipfile.is_zipfile(ckpt) and any(n.endswith("constants.pkl") for n in zipfile.ZipFile(ckpt).namelist()):
+        # a TorchScript archive (test.py:145 loads the trace.py output): ours replays scd::centernet_decode, a
+        # reference trace has its weights moved into the plugin model (scdhip/export.py)
+        from scdhip import export
+        wrapper = export.load(ckpt, arch=arch, mode="eval" if evalMode else "train")
+    else:
+        plugin = importlib.import_module("trainer.model." + arch)
+        model = plugin.model(**plugin.modelParams)
+        model.load_state_dict(torch.load(ckpt, map_location="cpu", weights_only=True))
+        model = model.cuda()
+        model.train(not evalMode)
+        wrapper = importlib.import_module("trainer.wrappers.centerOffsetResidual").Wrapper(model)
     for img in images:
         for d in analyseImages(wrapper, img):
             print("%s\t%d\t%d\t%.6f" % (img, d[0], d[1], d[2]))
