@@ -332,6 +332,23 @@ int scd_focal_prob_fwd(const float* p, const float* gt, long n, float* g, double
 int scd_masked_l1_fwd(const float* r, const float* t, const uint8_t* mask, long rows, int C, int smooth, float* g,
                       double* acc, void* stream);
 
+/* ---- SyncBN over peer memory (networkFactory.py:128-133: SyncBatchNorm on multi-GPU runs) ----
+ * A one-shot all-reduce of <= cap doubles for R <= 8 ranks without a collective library: every rank allocates a
+ * fine-grained mailbox (scd_peer_alloc, scd_peer_mailbox_bytes(R, cap) bytes, zeroed), exports it
+ * (scd_peer_ipc_handle: 64 bytes) and maps the others' (scd_peer_ipc_open); scd_peer_allreduce_f64 then writes
+ * `data` into every mailbox, flags it with `epoch` (1, 2, 3, ... one per call, the same on every rank), waits for
+ * all flags and leaves the rank-ordered sum in `data` (identical bits on every rank).  boxes[r] = rank r's mailbox
+ * as mapped in this process.  *err is set (and data left unreduced) if a peer's flag is missing after ~0.5 s.
+ * The allocation entry points are the only ones in this library that allocate. */
+size_t scd_peer_mailbox_bytes(int R, int cap);
+int scd_peer_alloc(size_t bytes, void** ptr);
+int scd_peer_free(void* ptr);
+int scd_peer_ipc_handle(void* ptr, void* handle64);
+int scd_peer_ipc_open(const void* handle64, void** ptr);
+int scd_peer_ipc_close(void* ptr);
+int scd_peer_allreduce_f64(double* data, int n, int rank, int R, void* const* boxes, int cap, unsigned long long epoch,
+                           int* err, void* stream);
+
 /* ---- HIP events for live kernel timing (bench.py roofline; scdhip.ops.LaunchTimer) ----
  * scd_event_record stamps the event on `stream`; while the stream is being captured into a graph the record is an
  * external event node (hipEventRecordExternal), re-stamped by every replay.  scd_event_elapsed_ms waits for `end`. */

@@ -1,0 +1,107 @@
+// One-shot all-reduce of small fp64 vectors over peer memory (SyncBN statistics; networkFactory.py:128-133 turns
+// SyncBatchNorm on for multi-GPU runs).  Each BN layer reduces 2C doubles (<= 4096) twice per step; through RCCL
+// that is a library call per layer on the critical path.  Here every rank owns a fine-grained "mailbox" that the
+// others map through hipIpc handles (xGMI on MI355X): one kernel writes the rank's vector into its slot of every
+// mailbox, raises its flag (the call's epoch) in each, waits for all flags in its own mailbox and sums the slots in
+// rank order -- the same bits on every rank.  Slots alternate by epoch parity, so a fast rank's next call never
+// overwrites a slot a slow rank is still summing (a rank can only be one call ahead: it waits for everyone's flag).
+// The wait gives up after ~0.5 s and reports it (*err), so a missing peer cannot hang the GPU.
+// Mailbox layout: [2 parities][R slots][cap doubles] then [R] 64-bit flags.
+#include <string.h>
+
+#include "scd_common.h"
+
+namespace {
+
+constexpr int PEER_MAX = 8;
+
+struct Boxes {
+    double* box[PEER_MAX];
+};
+
+__device__ __forceinline__ unsigned long long* flags_of(double* box, int R, int cap) {
+    return (unsigned long long*)(box + (size_t)2 * R * cap);
+}
+
+__global__ __launch_bounds__(256) void peer_allreduce_kernel(double* data, int n, int rank, int R, Boxes b, int cap,
+                                                             unsigned long long epoch, int* err) {
+    const int tid = threadIdx.x;
+    const int par = (int)(epoch & 1ull);
+    // 1. this rank's vector into slot `rank` of every mailbox (remote stores over xGMI for the peers)
+    for (int p = 0; p < R; ++p) {
+        double* dst = b.box[p] + ((size_t)par * R + rank) * cap;
+        for (int i = tid; i < n; i += blockDim.x) dst[i] = data[i];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < R)
+        __hip_atomic_store(flags_of(b.box[tid], R, cap) + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // 2. every rank's flag for this epoch in our own mailbox
+    __shared__ int timed_out;
+    if (tid == 0) timed_out = 0;
+    __syncthreads();
+    if (tid < R) {
+        unsigned long long* f = flags_of(b.box[rank], R, cap) + tid;
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+            if (wall_clock64() - t0 > 50000000ull) {             // ~0.5 s at the 100 MHz constant clock
+                timed_out = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    if (timed_out) {
+        if (tid == 0) *err = 1;
+        return;
+    }
+    __threadfence_system();
+    // 3. the sum in rank order (identical on every rank)
+    const double* mine = b.box[rank] + (size_t)par * R * cap;
+    for (int i = tid; i < n; i += blockDim.x) {
+        double s = 0.0;
+        for (int r = 0; r < R; ++r) s += mine[(size_t)r * cap + i];
+        data[i] = s;
+    }
+}
+
+}  // namespace
+
+extern "C" size_t scd_peer_mailbox_bytes(int R, int cap) {
+    return (size_t)2 * R * cap * sizeof(double) + (size_t)R * sizeof(unsigned long long);
+}
+
+extern "C" int scd_peer_alloc(size_t bytes, void** ptr) {
+    if (!ptr || bytes == 0) return SCD_ERR_ARG;
+    hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) return (int)e;
+    return (int)hipMemset(*ptr, 0, bytes);
+}
+
+extern "C" int scd_peer_free(void* ptr) { return ptr ? (int)hipFree(ptr) : 0; }
+
+extern "C" int scd_peer_ipc_handle(void* ptr, void* handle64) {
+    if (!ptr || !handle64) return SCD_ERR_ARG;
+    return (int)hipIpcGetMemHandle((hipIpcMemHandle_t*)handle64, ptr);
+}
+
+extern "C" int scd_peer_ipc_open(const void* handle64, void** ptr) {
+    if (!ptr || !handle64) return SCD_ERR_ARG;
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle64, sizeof(h));
+    return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+extern "C" int scd_peer_ipc_close(void* ptr) { return ptr ? (int)hipIpcCloseMemHandle(ptr) : 0; }
+
+extern "C" int scd_peer_allreduce_f64(double* data, int n, int rank, int R, void* const* boxes, int cap,
+                                      unsigned long long epoch, int* err, void* stream) {
+    if (!data || !boxes || !err || R < 1 || R > PEER_MAX || rank < 0 || rank >= R || n < 0 || n > cap || epoch == 0)
+        return SCD_ERR_ARG;
+    Boxes b;
+    for (int i = 0; i < PEER_MAX; ++i) b.box[i] = i < R ? (double*)boxes[i] : nullptr;
+    hipLaunchKernelGGL(peer_allreduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, data, n, rank, R, b, cap,
+                       epoch, err);
+    SCD_RETURN_LAUNCH();
+}

@@ -105,6 +105,13 @@ SIGNATURES = {
     "scd_topk": (I, [P, I, L, I, I, I, P, P, P, P, P, P]),
     "scd_focal_prob_fwd": (I, [P, P, L, P, P, P]),
     "scd_masked_l1_fwd": (I, [P, P, P, L, I, I, P, P, P]),
+    "scd_peer_mailbox_bytes": (c_size_t, [I, I]),
+    "scd_peer_alloc": (I, [c_size_t, PP]),
+    "scd_peer_free": (I, [P]),
+    "scd_peer_ipc_handle": (I, [P, P]),
+    "scd_peer_ipc_open": (I, [P, PP]),
+    "scd_peer_ipc_close": (I, [P]),
+    "scd_peer_allreduce_f64": (I, [P, I, I, I, PP, I, ctypes.c_ulonglong, P, P]),
     "scd_event_create": (I, [PP]),
     "scd_event_destroy": (I, [P]),
     "scd_event_record": (I, [P, P]),

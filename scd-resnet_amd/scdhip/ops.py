@@ -173,12 +173,26 @@ class LaunchTimer:
 class _BNSync:
     group = None          # torch.distributed group for SyncBatchNorm semantics (None = local BN)
     world = 1
+    peer = None           # scdhip.peer.PeerAllReduce when the peer-memory path is on
 
 
-def set_bn_sync(group):
-    """Enable global-batch BN statistics (SyncBatchNorm, networkFactory.py:128-133)."""
+def set_bn_sync(group, peer=None):
+    """Enable global-batch BN statistics (SyncBatchNorm, networkFactory.py:128-133).  peer=True (or
+    SCD_SYNCBN_PEER=1) all-reduces them over peer memory (scdhip/peer.py) instead of through torch.distributed."""
+    if _BNSync.peer is not None:
+        _BNSync.peer.close()
+        _BNSync.peer = None
     _BNSync.group = group
     _BNSync.world = dist.get_world_size(group) if group is not None else 1
+    if peer is None:
+        peer = os.environ.get("SCD_SYNCBN_PEER", "0") == "1"
+    if group is not None and peer and _BNSync.world > 1:
+        from .peer import PeerAllReduce
+        _BNSync.peer = PeerAllReduce(group)
+
+
+def bn_sync_peer():
+    return _BNSync.peer
 
 
 def bn_sync_world():
@@ -190,7 +204,10 @@ def _allreduce_stats(stats, C):
     if _BNSync.group is None:
         return L.STAT_REPLICAS
     L.call("scd_stats_collapse", ptr(stats), L.STAT_REPLICAS, C, stream())
-    dist.all_reduce(stats[:2 * C], group=_BNSync.group)
+    if _BNSync.peer is not None:
+        _BNSync.peer.all_reduce(stats[:2 * C])
+    else:
+        dist.all_reduce(stats[:2 * C], group=_BNSync.group)
     return 1
 
 

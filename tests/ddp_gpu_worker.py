@@ -26,7 +26,27 @@ def main():
     m = plugin.model(**plugin.modelParams)
     m.load_state_dict(O.hash_weights(entries))
     m = m.cuda().train().set_compute_dtype(torch.float32)
-    ops.set_bn_sync(dist.group.WORLD)
+    ops.set_bn_sync(dist.group.WORLD)          # SCD_SYNCBN_PEER=1: statistics over peer memory (scdhip/peer.py)
+    peer = ops.bn_sync_peer()
+    assert (peer is not None) == (os.environ.get("SCD_SYNCBN_PEER") == "1")
+    if peer is not None:
+        # the primitive first (fails fast if the peers cannot see each other): rank-ordered sums, identical bits
+        # on both ranks, and its latency
+        v = torch.arange(4096, dtype=torch.float64, device="cuda") * (rank + 1) + 0.1
+        peer.all_reduce(v)
+        want = torch.arange(4096, dtype=torch.float64, device="cuda") * 3 + 0.2
+        assert torch.allclose(v, want, rtol=0, atol=1e-9)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        small = torch.ones(1024, dtype=torch.float64, device="cuda")
+        e0.record()
+        for _ in range(200):
+            peer.all_reduce(small)
+        e1.record()
+        e1.synchronize()
+        peer.check()
+        assert small[0].item() == 2.0 ** 200
+        print("peer all-reduce of 1024 doubles, 2 ranks on one GPU: %.1f us per call" % (e0.elapsed_time(e1) * 5.0))
     ddp = FlatDDP(m)
     x = T.batch_inputs(8, 4, 128)[2 * rank:2 * rank + 2].cuda()
     ys = [y[2 * rank:2 * rank + 2].cuda() for y in T.batch_targets(9, 4, 32)]
@@ -52,6 +72,8 @@ def main():
     for k in g.files:
         if k.startswith("rs|"):
             np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    if peer is not None:
+        peer.check()
     dist.barrier()
     dist.destroy_process_group()
     print("OK rank", rank)
