@@ -222,6 +222,12 @@ size_t scd_heads_bwd_accsize(int nh, int Hd, const int* od);
 int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
                   const float* const* w1, const float* const* douts, void* dhid, double* acc, void* stream);
 /* collapse (and re-zero) acc; (+)= into dw1[h] (od[h],Hd), db1[h] (od[h]), db0[h] (Hd: 3x3 conv bias) */
+/* scd_heads_bwd with the head-output gradients first repacked pixel-major into `packed` ([N*HW][nh][4] fp32,
+ * caller-allocated, zero padded) and multiplied by dscale (the fp16 loss scale, else 1): one 16-B gradient read per
+ * pixel and head instead of od scalar reads. */
+int scd_heads_bwd_packed(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
+                         const float* const* w1, const float* const* douts, float dscale, float* packed, void* dhid,
+                         double* acc, void* stream);
 int scd_heads_bwd_weight_finalize(double* acc, int nh, int Hd, const int* od, float* const* dw1,
                                   float* const* db1, float* const* db0, int accumulate, float alpha, void* stream);
 

@@ -400,7 +400,23 @@ struct HeadsDesc {
     const float* b1[4];
     const float* dout[4];
     float* out[4];
+    const float* pk;        // packed head-output gradients [pixel][nh][4] (scd_heads_bwd_packed), or null
 };
+
+// the head-output gradients (NCHW fp32, od[h] channels each) repacked pixel-major, 4 floats per head (zero padded)
+// and multiplied by `scale` (the fp16 loss scale): the tail backward then reads one 16-B vector per pixel and head
+__global__ void heads_pack_kernel(int N, int HW, HeadsDesc d, float scale, float* pk) {
+    const long P = (long)N * HW;
+    for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < P; px += (long)gridDim.x * blockDim.x) {
+        const long n = px / HW, q = px - n * HW;
+        for (int h = 0; h < d.nh; ++h) {
+            float v[4];
+#pragma unroll
+            for (int o = 0; o < 4; ++o) v[o] = o < d.od[h] ? d.dout[h][(n * d.od[h] + o) * HW + q] * scale : 0.f;
+            *(float4*)(pk + (px * d.nh + h) * 4) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
 
 // thread = (pixel, 16-B channel chunk): coalesced hidden reads; per-head partial dot products
 // reduced over the head's Hd/E chunk-lanes with xor-shuffles (aligned groups: Hd/E | 64).
@@ -449,7 +465,7 @@ __global__ void heads_fwd_kernel(const T* hid, int N, int HW, HeadsDesc d) {
 // Block = PXB pixels, blockDim = G pixel-lanes x cpp chunk-lanes; each thread streams its chunk over
 // every G-th pixel, 4 pixels per step with all loads issued before use; block partials are folded in
 // LDS by all threads and added to fp64 replicas (SCD_STAT_REPLICAS).
-template <typename T, int U>
+template <typename T, int U, bool PK = false>
 __global__ __launch_bounds__(512) void heads_bwd_kernel(const T* hid, int N, int HW, HeadsDesc d, T* dhid,
                                                         double* acc, int accsz, int PXB) {
     constexpr int E = Vec16<T>::N;
@@ -492,10 +508,15 @@ __global__ __launch_bounds__(512) void heads_bwd_kernel(const T* hid, int N, int
         Vec16<T>::store(dhid + px * Ctot + ct, r);
     };
     auto load_gd = [&](unsigned px, float* gd) {
-        const unsigned n = px / (unsigned)HW;
-        const unsigned q = px - n * HW;
+        if constexpr (PK) {
+            const float4 v = *(const float4*)(d.pk + ((size_t)px * d.nh + h) * 4);
+            gd[0] = v.x; gd[1] = v.y; gd[2] = v.z; gd[3] = v.w;
+        } else {
+            const unsigned n = px / (unsigned)HW;
+            const unsigned q = px - n * HW;
 #pragma unroll
-        for (int o = 0; o < 4; ++o) gd[o] = o < od ? dout[(n * od + o) * (unsigned)HW + q] : 0.f;
+            for (int o = 0; o < 4; ++o) gd[o] = o < od ? dout[(n * od + o) * (unsigned)HW + q] : 0.f;
+        }
     };
     if (g < G) {
         unsigned px = p0 + g;
@@ -594,6 +615,7 @@ bool make_desc(HeadsDesc& d, int nh, int Hd, const int* od) {
         d.orow[h] = d.nout;
         d.nout += d.od[h];
         d.w1[h] = nullptr; d.b1[h] = nullptr; d.dout[h] = nullptr; d.out[h] = nullptr;
+        d.pk = nullptr;
     }
     return d.nout * Hd <= 8 * 512;
 }
@@ -845,5 +867,40 @@ extern "C" int scd_adam_step_dev(float* p, const float* g, float* m, float* v, l
     hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
     hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                        (const double*)hyper, beta1, beta2, eps, gscale);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_heads_bwd_packed(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
+                                    const float* const* w1, const float* const* douts, float dscale, float* packed,
+                                    void* dhid, double* acc, void* stream) {
+    SCD_F16_FWD(scd_heads_bwd_packed, hid, N, HW, nh, Hd, od, w1, douts, dscale, packed, dhid, acc, stream);
+    HeadsDesc d;
+    if (!make_desc(d, nh, Hd, od) || !packed) return SCD_ERR_ARG;
+    const int E = dtype == SCD_DT_BF16 ? 8 : 4;
+    const int cpp = nh * Hd / E;
+    if (cpp > 256 || (Hd % E)) return SCD_ERR_ARG;
+    for (int h = 0; h < nh; ++h) { d.w1[h] = w1[h]; d.dout[h] = douts[h]; }
+    const int accsz = d.nout * Hd + d.nout + nh * Hd;
+    const long P = (long)N * HW;
+    if (P * nh * Hd >= (1L << 31)) return SCD_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(heads_pack_kernel, dim3(ew_blocks(P)), dim3(256), 0, st, N, HW, d, dscale, packed);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    d.pk = packed;
+    const int G = 512 / cpp;
+    const int threads = G * cpp;
+    static int pxb_env = -1;
+    if (pxb_env < 0) { const char* ev = getenv("SCD_HEADS_PXB"); pxb_env = ev ? atoi(ev) : 0; }
+    const int PXB = pxb_env > 0 ? pxb_env : 2048;
+    const int blocks = cdiv(P, PXB);
+    if (dtype == SCD_DT_BF16)
+        hipLaunchKernelGGL((heads_bwd_kernel<__bf16, 8, true>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid,
+                           N, HW, d, (__bf16*)dhid, acc, accsz, PXB);
+    else if (dtype == SCD_DT_F32)
+        hipLaunchKernelGGL((heads_bwd_kernel<float, 4, true>), dim3(blocks), dim3(threads), 0, st, (const float*)hid,
+                           N, HW, d, (float*)dhid, acc, accsz, PXB);
+    else
+        return SCD_ERR_ARG;
     SCD_RETURN_LAUNCH();
 }

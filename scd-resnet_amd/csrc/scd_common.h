@@ -32,6 +32,7 @@
 #define scd_heads_fwd scd_heads_fwd__f16
 #define scd_heads_bwd_accsize scd_heads_bwd_accsize__f16
 #define scd_heads_bwd scd_heads_bwd__f16
+#define scd_heads_bwd_packed scd_heads_bwd_packed__f16
 #define scd_heads_bwd_weight_finalize scd_heads_bwd_weight_finalize__f16
 #define scd_adam_step scd_adam_step__f16
 #define scd_adam_step_dev scd_adam_step_dev__f16
@@ -71,6 +72,7 @@ SCD_F16_DECL(scd_stem_pool_bwd)
 SCD_F16_DECL(scd_stem_pool_bwd_bn)
 SCD_F16_DECL(scd_heads_fwd)
 SCD_F16_DECL(scd_heads_bwd)
+SCD_F16_DECL(scd_heads_bwd_packed)
 SCD_F16_DECL(scd_stem_conv_fwd)
 SCD_F16_DECL(scd_stem_conv_wgrad)
 SCD_F16_DECL(scd_pad_channels)

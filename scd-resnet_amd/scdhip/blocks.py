@@ -328,18 +328,18 @@ class HeadsFn(torch.autograd.Function):
         nh = len(heads)
         douts = [(_c(d) if d is not None else torch.zeros(N, o, H, W, device=feat.device))
                  for d, o in zip(douts, od)]
+        # fp16: the backward below runs on loss-scaled gradients (ops.LossScale: the repack multiplies the head
+        # gradients by S), unscaled into every .grad
         S = ops.begin_loss_scale(feat.dtype)
-        if S != 1.0:
-            # fp16: the backward below runs on loss-scaled gradients (ops.LossScale), unscaled into every .grad
-            douts = [d * S for d in douts]
         dptrs = ops.L.ptr_array([d.data_ptr() for d in douts])
         odarr = ops.L.int_array(od)
         dhid = torch.empty_like(hid)
         acc = ops.persistent_zeros(heads[0][2].weight, "_scd_heads_acc",
                                    ops.L.lib().scd_heads_bwd_accsize(nh, Hd, odarr) // 8, torch.float64)
-        ops.L.call("scd_heads_bwd", ops.dt(hid), ops.ptr(hid), N, H * W, nh, Hd, odarr,
-                   ops.L.ptr_array([h[2].weight.data_ptr() for h in heads]), dptrs, ops.ptr(dhid), ops.ptr(acc),
-                   ops.stream())
+        packed = torch.empty(N * H * W * nh * 4, device=feat.device)
+        ops.L.call("scd_heads_bwd_packed", ops.dt(hid), ops.ptr(hid), N, H * W, nh, Hd, odarr,
+                   ops.L.ptr_array([h[2].weight.data_ptr() for h in heads]), dptrs, float(S), ops.ptr(packed),
+                   ops.ptr(dhid), ops.ptr(acc), ops.stream())
         ops.L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), nh, Hd, odarr,
                    ops.L.ptr_array([ops.grad_of(h[2].weight).data_ptr() for h in heads]),
                    ops.L.ptr_array([ops.grad_of(h[2].bias).data_ptr() for h in heads]),

@@ -80,6 +80,7 @@ SIGNATURES = {
     "scd_heads_fwd": (I, [I, P, I, I, I, I, IP, PP, PP, PP, P]),
     "scd_heads_bwd_accsize": (c_size_t, [I, I, IP]),
     "scd_heads_bwd": (I, [I, P, I, I, I, I, IP, PP, PP, P, P, P]),
+    "scd_heads_bwd_packed": (I, [I, P, I, I, I, I, IP, PP, PP, F, P, P, P, P]),
     "scd_heads_bwd_weight_finalize": (I, [P, I, I, IP, PP, PP, PP, I, F, P]),
     "scd_focal_fwd": (I, [P, P, L, P, P, P]),
     "scd_l1_gather_fwd": (I, [P, I, I, I, P, P, P, I, I, I, P, P, P]),

@@ -160,9 +160,10 @@ def test_heads_fused_gemm(N, H, W, dtype):
     assert rel_err(nchw(hid), hid_ref) < TOL[dtype] * 2
 
 
+@pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("HW", [(128, 128), (9, 11)])
-def test_heads_tail_backward(HW, dtype):
+def test_heads_tail_backward(HW, dtype, packed):
     """scd_heads_bwd + finalize (CenterNet tails, centerNetOffset.py:108-110): dhid = relu'(hid) * W1^T dout,
     dW1 = sum dout x hid, db1 = sum dout, db0 = sum dhid against torch fp32 on the same hidden tensor
     (128x128: whole 4-pixel unrolled steps; 9x11: ragged tail)."""
@@ -185,11 +186,19 @@ def test_heads_tail_backward(HW, dtype):
     dw1 = [torch.zeros(o, Hd, device=DEV) for o in od]
     db1 = [torch.zeros(o, device=DEV) for o in od]
     db0 = [torch.zeros(Hd, device=DEV) for o in od]
-    L.call("scd_heads_bwd", ops.dt(hd), ops.ptr(hd), N, H * W, 3, Hd, odarr,
-           L.ptr_array([w.data_ptr() for w in w1d]), L.ptr_array([d.data_ptr() for d in dd]), ops.ptr(dhid),
-           ops.ptr(acc), ops.stream())
+    if packed:        # gradients repacked pixel-major (x 0.5, undone below: the dscale path of the fp16 loss scale)
+        pk = torch.empty(P * 3 * 4, device=DEV)
+        L.call("scd_heads_bwd_packed", ops.dt(hd), ops.ptr(hd), N, H * W, 3, Hd, odarr,
+               L.ptr_array([w.data_ptr() for w in w1d]), L.ptr_array([d.data_ptr() for d in dd]), 0.5, ops.ptr(pk),
+               ops.ptr(dhid), ops.ptr(acc), ops.stream())
+        dhid.mul_(2)
+    else:
+        L.call("scd_heads_bwd", ops.dt(hd), ops.ptr(hd), N, H * W, 3, Hd, odarr,
+               L.ptr_array([w.data_ptr() for w in w1d]), L.ptr_array([d.data_ptr() for d in dd]), ops.ptr(dhid),
+               ops.ptr(acc), ops.stream())
     L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), 3, Hd, odarr, L.ptr_array([t.data_ptr() for t in dw1]),
-           L.ptr_array([t.data_ptr() for t in db1]), L.ptr_array([t.data_ptr() for t in db0]), 0, 1.0, ops.stream())
+           L.ptr_array([t.data_ptr() for t in db1]), L.ptr_array([t.data_ptr() for t in db0]), 0,
+           2.0 if packed else 1.0, ops.stream())
     torch.cuda.synchronize()
     hp = hid.reshape(P, 3 * Hd)
     tol = TOL[dtype] if dtype != torch.float32 else 1e-5
