@@ -318,6 +318,12 @@ def main():
 
     # with the graph: 2 eager steps, the capture step and the first replay of the second copy are warm-up
     nwarm = max(args.warmup, 4) if graph is not None else args.warmup
+    # the step runs on a high-priority stream (SCD_STEP_PRIORITY=0: the default stream): the weight-gradient side
+    # stream has the lowest priority, so the critical chain's small kernels are dispatched ahead of its GEMM tiles
+    prio = os.environ.get("SCD_STEP_PRIORITY", "1") != "0"
+    step_stream = torch.cuda.Stream(device=dev, priority=-10) if prio else torch.cuda.current_stream(dev)
+    step_stream.wait_stream(torch.cuda.current_stream(dev))
+    torch.cuda.set_stream(step_stream)
     for _ in range(nwarm):
         step()
     if world > 1:

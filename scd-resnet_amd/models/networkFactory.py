@@ -149,6 +149,9 @@ class NetworkFactory(object):
         Logger.info("Loaded with Training Samples: {}".format(len(self.dataset)))
 
         learningRate = defaultConfig.learningRate
+        # the step runs on a high-priority stream: scdhip's weight-gradient side stream has the lowest priority, so
+        # the input-gradient chain's small kernels are dispatched first when both have work (bench.py: +1.3%)
+        torch.cuda.set_stream(torch.cuda.Stream(device=self.device, priority=-10))
         self.cuda()
         if distributed and self.GPUCOUNT > 1 and dist.get_world_size() > 1:
             ops.set_bn_sync(dist.group.WORLD)       # SyncBatchNorm semantics (networkFactory.py:128-133)

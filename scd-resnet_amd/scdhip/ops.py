@@ -559,6 +559,7 @@ def clear_bn_fusion():
 
 class _Side:
     enabled = os.environ.get("SCD_WGRAD_STREAM", "1") != "0"
+    priority = 10         # mapped to the lowest valid stream priority
     streams = {}          # device index -> side stream
     joined_task = {}      # device index -> graph task whose end-of-backward join is queued
 
@@ -578,7 +579,10 @@ def side_stream(dev):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _Side.streams.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        # the lowest priority the device offers: when both queues have work ready, the CP dispatches the critical
+        # input-gradient chain's workgroups first (a training step run on a high-priority stream benefits; on the
+        # default stream both are equal)
+        s = torch.cuda.Stream(device=idx, priority=_Side.priority)
         _Side.streams[idx] = s
     s.wait_stream(torch.cuda.current_stream(idx))
     if _Side.joined_task.get(idx) != task:
