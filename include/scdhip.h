@@ -97,6 +97,12 @@ int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws, int nspli
  * (alpha = 1 / the fp16 loss scale, else 1) */
 int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
                      long ld_n, long ld_c, long ld_t, float* dst, int accumulate, float alpha, void* stream);
+/* The same over 1..4 row slices [r0[s], r1[s]) with their own destinations and strides, in one launch (the three
+ * CenterNet heads' 3x3 weights, centerNetOffset.py:106-110, from one fused weight-gradient workspace).  Requires
+ * Ci % 4 == 0.  The summation order over the splits is fixed (independent of the launch geometry). */
+int scd_wgrad_reduce_rows(const float* ws, int nsplit, int Cg, int T, int Ci, int nslices, const int* r0,
+                          const int* r1, const long* ld_n, const long* ld_c, const long* ld_t, float* const* dst,
+                          int cvalid, int accumulate, float alpha, void* stream);
 
 /* Pack an fp32 (A, B, T) weight (OIHW / IOHW flattening) into the GEMM operand layout:
  * mode 0: out[row_off + a][t*B + b] = w[a][b][t]; mode 1: out[row_off + b][t*A + a] = w[a][b][t];
@@ -354,6 +360,12 @@ int scd_peer_ipc_open(const void* handle64, void** ptr);
 int scd_peer_ipc_close(void* ptr);
 int scd_peer_allreduce_f64(double* data, int n, int rank, int R, void* const* boxes, int cap, unsigned long long epoch,
                            int* err, void* stream);
+
+/* A HIP stream restricted to `keep` of every `of` compute units (hipExtStreamCreateWithCUMask, the mask spread
+ * evenly over the XCDs); used for the weight-gradient side stream when SCD_SIDE_CUS is set.  No reference
+ * counterpart (the reference runs one default stream, networkFactory.py:257-263). */
+int scd_stream_create_cumask(int keep, int of, void** stream);
+int scd_stream_destroy(void* stream);
 
 /* ---- HIP events for live kernel timing (bench.py roofline; scdhip.ops.LaunchTimer) ----
  * scd_event_record stamps the event on `stream`; while the stream is being captured into a graph the record is an

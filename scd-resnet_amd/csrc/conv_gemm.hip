@@ -2631,45 +2631,70 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     }
 }
 
-// sums groups of G consecutive split slabs into the group's first slab (first pass of a wide reduce)
-// (elements [e0, e0 + n) of each slab only: the rows one reduce call consumes)
-__global__ void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs, long e0, long n) {
+// Split reduction of the weight-gradient slabs (HBM-bound: nsplit slab reads of 4 B per weight).  Every
+// thread owns 4 consecutive fp32 columns of one slab row and keeps 8 independent 16-B slab loads in flight;
+// the summation order is fixed (accumulator j takes slabs j, j+8, ..., then a fixed pairwise tree), so the
+// result does not depend on the launch geometry.
+__device__ __forceinline__ f32x4 wred_sum(const float* src, int n, long zs) {
+    f32x4 a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= n; z += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *(const f32x4*)(src + (long)(z + j) * zs);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+        if (z + j < n) a[j] += *(const f32x4*)(src + (long)(z + j) * zs);
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// first pass of a wide reduce: groups of G consecutive slabs summed into the group's first slab, over the
+// 4-column units [e0/4, e0/4 + n4) of each slab (the rows the reduce consumes)
+__global__ __launch_bounds__(256) void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs, long e0, long n4) {
     const long ngroups = (nsplit + G - 1) / G;
-    const long total = ngroups * n;
+    const long total = ngroups * n4;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const long g = i / n, e = i - g * n;
-        float* base = ws + g * G * zs + e0 + e;
-        float s = 0.f;
-        const int n = (int)min((long)G, nsplit - g * G);
-        for (int k = 0; k < n; ++k) s += base[(long)k * zs];
-        base[0] = s;
+        const long g = i / n4, e = i - g * n4;
+        float* base = ws + g * G * zs + e0 + 4 * e;
+        const f32x4 s = wred_sum(base, (int)min((long)G, nsplit - g * G), zs);
+        *(f32x4*)base = s;
     }
 }
 
-__global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
-                                    long ld_n, long ld_c, long ld_t, float* dst, int accumulate, float alpha) {
-    const unsigned KK = (unsigned)(T * Ci);
-    const unsigned total = (unsigned)(r1 - r0) * KK;
-    const size_t zs = (size_t)Cg * KK;
-    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const unsigned r = i / KK;
-        const unsigned k = i - r * KK;
-        const unsigned t = k / (unsigned)Ci;
-        const unsigned c = k - t * (unsigned)Ci;
-        if ((int)c >= cvalid) continue;
-        const float* src = ws + (size_t)(r0 + r) * KK + k;
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        int z = 0;
-        for (; z + 4 <= nsplit; z += 4) {
-            s0 += src[(size_t)z * zs];
-            s1 += src[(size_t)(z + 1) * zs];
-            s2 += src[(size_t)(z + 2) * zs];
-            s3 += src[(size_t)(z + 3) * zs];
+// row slices of one reduce launch (the three heads of a fused head weight gradient go to three parameters)
+struct WredSlices {
+    int n;
+    int r0[4], r1[4];
+    long ldn[4], ldc[4], ldt[4];
+    float* dst[4];
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int nsplit, long zs, int T, int Ci,
+                                                           int cvalid, WredSlices sl, long total4, int accumulate,
+                                                           float alpha) {
+    const int KK = T * Ci;
+    const int KK4 = KK >> 2;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+        long e = i;
+        int s = 0;
+        while (s < sl.n - 1 && e >= (long)(sl.r1[s] - sl.r0[s]) * KK4) { e -= (long)(sl.r1[s] - sl.r0[s]) * KK4; ++s; }
+        const int r = (int)(e / KK4);
+        const int k = (int)(e - (long)r * KK4) * 4;
+        const f32x4 v = wred_sum(ws + (long)(sl.r0[s] + r) * KK + k, nsplit, zs) * alpha;
+        float* drow = sl.dst[s] + r * sl.ldn[s];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // Ci % 4 == 0: the 4 columns share one tap
+            const int t = (k + j) / Ci, c = k + j - t * Ci;
+            if (c >= cvalid) continue;
+            float* d = drow + c * sl.ldc[s] + t * sl.ldt[s];
+            *d = accumulate ? (*d + v[j]) : v[j];
         }
-        for (; z < nsplit; ++z) s0 += src[(size_t)z * zs];
-        const float s = ((s0 + s1) + (s2 + s3)) * alpha;
-        float* d = dst + r * ld_n + c * ld_c + t * ld_t;
-        *d = accumulate ? (*d + s) : s;
     }
 }
 
@@ -3233,29 +3258,53 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
-                                long ld_n, long ld_c, long ld_t, float* dst, int accumulate, float alpha,
-                                void* stream) {
-    if (r0 < 0 || r1 > Cg || r0 >= r1) return SCD_ERR_ARG;
+extern "C" int scd_wgrad_reduce_rows(const float* ws, int nsplit, int Cg, int T, int Ci, int nslices, const int* r0,
+                                     const int* r1, const long* ld_n, const long* ld_c, const long* ld_t,
+                                     float* const* dst, int cvalid, int accumulate, float alpha, void* stream) {
+    if (nslices < 1 || nslices > 4 || nsplit < 1 || Ci % 4 != 0) return SCD_ERR_ARG;
+    WredSlices sl;
+    sl.n = nslices;
+    int rmin = Cg, rmax = 0;
+    long rows = 0;
+    for (int s = 0; s < nslices; ++s) {
+        if (r0[s] < 0 || r1[s] > Cg || r0[s] >= r1[s] || dst[s] == nullptr) return SCD_ERR_ARG;
+        sl.r0[s] = r0[s]; sl.r1[s] = r1[s];
+        sl.ldn[s] = ld_n[s]; sl.ldc[s] = ld_c[s]; sl.ldt[s] = ld_t[s];
+        sl.dst[s] = dst[s];
+        rmin = std::min(rmin, r0[s]);
+        rmax = std::max(rmax, r1[s]);
+        rows += r1[s] - r0[s];
+    }
     hipStream_t st = (hipStream_t)stream;
-    const long zs = (long)Cg * T * Ci;
+    const long KK = (long)T * Ci;
+    const long zs = (long)Cg * KK;
+    const long total4 = rows * KK / 4;
     int ns = nsplit;
-    long zstride_mult = 1;
-    if (nsplit > 32) {
-        // two-pass: groups of 16 slabs summed in place (parallel over groups), then the group heads
-        const int G = 16;
-        const long e0 = (long)r0 * T * Ci, n = (long)(r1 - r0) * T * Ci;
-        const long total = (long)((nsplit + G - 1) / G) * n;
-        hipLaunchKernelGGL(wgrad_presum_kernel, dim3((int)std::min<long>(8192, (total + 255) / 256)), dim3(256), 0, st,
-                           (float*)ws, nsplit, G, zs, e0, n);
+    long zsr = zs;
+    // one pass keeps >= 8 loads in flight per thread; too few threads for the HBM (small weights, many
+    // splits): first sum groups of G slabs in place, parallel over the groups, over the rows [rmin, rmax)
+    const long want = 128L * 1024;
+    if (nsplit > 16 && total4 < want) {
+        const long ngroups = std::min<long>(cdiv(want, total4), nsplit / 8);
+        const int G = (int)cdiv((long)nsplit, ngroups);
+        const long n4 = (long)(rmax - rmin) * KK / 4;
+        const long tot = (long)((nsplit + G - 1) / G) * n4;
+        hipLaunchKernelGGL(wgrad_presum_kernel, dim3((int)std::min<long>(16384, (tot + 255) / 256)), dim3(256), 0, st,
+                           (float*)ws, nsplit, G, zs, (long)rmin * KK, n4);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
         ns = (nsplit + G - 1) / G;
-        zstride_mult = G;
+        zsr = zs * G;
     }
-    const long total = (long)(r1 - r0) * T * Ci;
-    const int blocks = (int)std::min<long>(4096, (total + 255) / 256);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, ns, (int)(Cg * zstride_mult), T, Ci,
-                       r0, r1, cvalid, ld_n, ld_c, ld_t, dst, accumulate, alpha);
+    const int blocks = (int)std::min<long>(16384, (total4 + 255) / 256);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, ns, zsr, T, Ci, cvalid, sl, total4,
+                       accumulate, alpha);
     SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_wgrad_reduce(const float* ws, int nsplit, int Cg, int T, int Ci, int r0, int r1, int cvalid,
+                                long ld_n, long ld_c, long ld_t, float* dst, int accumulate, float alpha,
+                                void* stream) {
+    return scd_wgrad_reduce_rows(ws, nsplit, Cg, T, Ci, 1, &r0, &r1, &ld_n, &ld_c, &ld_t, &dst, cvalid, accumulate,
+                                 alpha, stream);
 }

@@ -17,6 +17,7 @@
 #define scd_conv_wgrad_nsplit scd_conv_wgrad_nsplit__f16
 #define scd_conv_wgrad scd_conv_wgrad__f16
 #define scd_wgrad_reduce scd_wgrad_reduce__f16
+#define scd_wgrad_reduce_rows scd_wgrad_reduce_rows__f16
 #define scd_stats_collapse scd_stats_collapse__f16
 #define scd_bn_finalize scd_bn_finalize__f16
 #define scd_bn_apply scd_bn_apply__f16

@@ -44,6 +44,7 @@ F = c_float
 D = c_double
 PP = ctypes.POINTER(c_void_p)
 IP = ctypes.POINTER(c_int)
+LP = ctypes.POINTER(c_long)
 
 # name -> (restype, argtypes); mirrors include/scdhip.h one to one
 SIGNATURES = {
@@ -56,6 +57,7 @@ SIGNATURES = {
     "scd_conv_wgrad_nsplit2": (I, [I, L, I, I, I, I, I]),
     "scd_conv_wgrad": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, IP, IP, P]),
     "scd_wgrad_reduce": (I, [P, I, I, I, I, I, I, I, L, L, L, P, I, F, P]),
+    "scd_wgrad_reduce_rows": (I, [P, I, I, I, I, I, IP, IP, LP, LP, LP, PP, I, I, F, P]),
     "scd_pack_weight": (I, [I, P, P, I, I, I, I, I, I, P]),
     "scd_pack_weights_batched": (I, [I, P, I, L, P]),
     "scd_pad_channels": (I, [I, P, L, I, I, P, P]),
@@ -113,6 +115,8 @@ SIGNATURES = {
     "scd_peer_ipc_open": (I, [P, PP]),
     "scd_peer_ipc_close": (I, [P]),
     "scd_peer_allreduce_f64": (I, [P, I, I, I, PP, I, ctypes.c_ulonglong, P, P]),
+    "scd_stream_create_cumask": (I, [I, I, PP]),
+    "scd_stream_destroy": (I, [P]),
     "scd_event_create": (I, [PP]),
     "scd_event_destroy": (I, [P]),
     "scd_event_record": (I, [P, P]),
@@ -164,6 +168,13 @@ def ptr_array(ptrs):
 
 def int_array(vals):
     arr = (c_int * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
+    return arr
+
+
+def long_array(vals):
+    arr = (c_long * max(1, len(vals)))()
     for i, v in enumerate(vals):
         arr[i] = int(v)
     return arr

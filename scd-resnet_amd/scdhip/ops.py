@@ -582,13 +582,27 @@ def side_stream(dev):
         # the lowest priority the device offers: when both queues have work ready, the CP dispatches the critical
         # input-gradient chain's workgroups first (a training step run on a high-priority stream benefits; on the
         # default stream both are equal)
-        s = torch.cuda.Stream(device=idx, priority=_Side.priority)
+        s = _new_side_stream(idx)
         _Side.streams[idx] = s
     s.wait_stream(torch.cuda.current_stream(idx))
     if _Side.joined_task.get(idx) != task:
         _Side.joined_task[idx] = task
         torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
     return s
+
+
+def _new_side_stream(idx):
+    """SCD_SIDE_CUS="keep/of" (e.g. "3/4"): the side stream may use only that share of the compute units
+    (scd_stream_create_cumask), so that its one-workgroup-per-CU weight-gradient GEMMs cannot hold every CU
+    while the input-gradient chain's HBM-bound BN kernels wait for a slot."""
+    spec = os.environ.get("SCD_SIDE_CUS", "")
+    if not spec:
+        return torch.cuda.Stream(device=idx, priority=_Side.priority)
+    keep, of = (int(v) for v in spec.split("/"))
+    with torch.cuda.device(idx):
+        h = ctypes.c_void_p()
+        L.call("scd_stream_create_cumask", keep, of, ctypes.byref(h))
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
 
 
 def join_side_streams():
@@ -638,9 +652,12 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
     if rows is None:
         rows = [(0, Cg, dst, ld)]
     cv = Ci if cvalid is None else cvalid
-    for r0, r1, d, (ldn, ldc, ldt) in rows:
-        L.call("scd_wgrad_reduce", ptr(ws), ns, Cg, T, Ci, r0, r1, cv, ldn, ldc, ldt, ptr(d), int(accumulate),
-               grad_alpha(g), stream())
+    for i in range(0, len(rows), 4):      # up to four row slices per reduce launch
+        part = rows[i:i + 4]
+        L.call("scd_wgrad_reduce_rows", ptr(ws), ns, Cg, T, Ci, len(part), L.int_array([r[0] for r in part]),
+               L.int_array([r[1] for r in part]), L.long_array([r[3][0] for r in part]),
+               L.long_array([r[3][1] for r in part]), L.long_array([r[3][2] for r in part]),
+               L.ptr_array([ptr(r[2]) for r in part]), cv, int(accumulate), grad_alpha(g), stream())
 
 
 # ------------------------------------------------------------------ BatchNorm (training)

@@ -589,3 +589,36 @@ def test_augment_tiny_tiles(B, H, W):
         t = x[b].double()
         ref = ((t - t.mean()) / ((t - t.mean()) ** 2).mean().sqrt()).float()
         np.testing.assert_allclose(got[b].numpy(), ref.numpy(), rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("ns,Cg,T,Ci", [(1, 64, 9, 64), (7, 64, 9, 64), (17, 64, 1, 64), (56, 384, 9, 256),
+                                        (200, 128, 9, 128), (64, 8, 3, 4)])
+def test_wgrad_reduce_rows(ns, Cg, T, Ci):
+    """scd_wgrad_reduce_rows (split-slab sum into 1..4 OIHW row slices, with and without the in-place group
+    pre-pass) against a float64 sum of the same slabs: fp32 accumulation of ns terms, 1e-5 relative."""
+    from scdhip import lib as L
+    from scdhip.ops import ptr, stream
+    g = torch.Generator().manual_seed(ns * 1000 + Cg)
+    ws = torch.randn(ns, Cg, T * Ci, generator=g)
+    ref = ws.double().sum(0)                      # (Cg, T*Ci), column = t*Ci + ci
+    wsd = ws.to(DEV)
+    cuts = sorted({0, Cg // 3 // 4 * 4, Cg // 2, Cg})
+    slices = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    cvalid = Ci - 1 if Ci > 4 else Ci
+    alpha = 0.5
+    dst = [torch.randn(b - a, Ci, T, generator=g).to(DEV) for a, b in slices]   # OIHW-flattened rows
+    before = [d.clone() for d in dst]
+    for accumulate in (1, 0):
+        d_in = [d.clone() for d in before]
+        wsd = ws.to(DEV)                          # the group pre-pass sums in place
+        L.call("scd_wgrad_reduce_rows", ptr(wsd), ns, Cg, T, Ci, len(slices),
+               L.int_array([a for a, _ in slices]), L.int_array([b for _, b in slices]),
+               L.long_array([Ci * T] * len(slices)), L.long_array([T] * len(slices)), L.long_array([1] * len(slices)),
+               L.ptr_array([ptr(d) for d in d_in]), cvalid, accumulate, alpha, stream())
+        torch.cuda.synchronize()
+        for (a, b), d, d0 in zip(slices, d_in, before):
+            exp = ref[a:b].view(b - a, T, Ci).permute(0, 2, 1) * alpha      # (rows, Ci, T)
+            want = d0.cpu().double().clone()
+            want[:, :cvalid] = exp[:, :cvalid] + (want[:, :cvalid] if accumulate else 0)
+            err = (d.cpu().double() - want).abs().max().item() / max(1e-6, want.abs().max().item())
+            assert err < 1e-5, (a, b, accumulate, err)
