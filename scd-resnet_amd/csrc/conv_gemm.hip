@@ -35,6 +35,10 @@
 #ifndef H384_SCHED
 #define H384_SCHED 0  // heads384 DMA order: 0 = P1 {A0, B part 1}, 1 = P1 {B part 1}, P2 {A0, B part 2}
 #endif
+#ifndef H384_EPI
+#define H384_EPI 1    // heads384 epilogue: 0 = hidden tile staged in LDS (16-B stores, tails from the staged rows),
+                      // 1 = from the accumulators (8-B stores, tails as 16x16x16 MFMAs on the same registers)
+#endif
 #ifndef SCD_ABM
 #define SCD_ABM 0     // halo kernel ablation bitmask: 1 no MFMA, 2 no loop DMA, 4 no loop fragment reads, 8 no loop barriers
 #endif
@@ -73,6 +77,16 @@ struct GemmParams {
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
 // chunk c ^ (r & 7).  ds_read_b128 fragment reads (16 consecutive rows, one chunk) and the
 // ds_write_b128 staging stores (8 chunks of one row) are then bank-conflict free.
+// 16x16x16 MFMA on 4-element 16-bit vectors (the 16-bit type is __bf16, or _Float16 in the SCD_F16_BUILD pass)
+typedef __attribute__((ext_vector_type(4))) __bf16 hx4;
+__device__ __forceinline__ f32x4 mfma_16x16x16(hx4 a, hx4 b, f32x4 c) {
+#ifdef SCD_F16_BUILD
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+#else
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c, 0, 0, 0);
+#endif
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
 // Buffer-load offset or an out-of-range one (the load then returns zeros).  The offset is made
@@ -1177,7 +1191,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     constexpr int STAGE = (BM + BN) * 128;
     constexpr int EROW = BN * 2 + 16;
     constexpr int EPI = BM * EROW;
-    constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+    constexpr int SMEM = (H384_EPI == 1 || 2 * STAGE > EPI) ? 2 * STAGE : EPI;
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
     const int tid = threadIdx.x;
@@ -1361,7 +1375,101 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-
+#if H384_EPI == 1
+        // ---- epilogue from the accumulators.  Lane (l16, lg) of block (a, b) holds hidden channels
+        // 96wc + 16b + 4lg .. +3 of pixel 96grp + 16a + l16: after bias + ReLU those 4 bf16 are (1) an 8-B piece of
+        // the pixel's NHWC row, stored at once, and (2) exactly the B operand of a 16x16x16 MFMA (B[k = 4lg + j][n =
+        // l16]), so the 1x1 tails out[o][px] = sum_c W1[o][c] hid[c][px] run on the same registers: A = the
+        // block-diagonal W1 slice of the wave's 16 channels (A[m = l16][k = 4lg + j], fp32 weights as bf16 hi + lo,
+        // ~2^-17), 12 MFMAs per 16-pixel block.  The four channel waves of a group meet in LDS (48 KiB of fp32
+        // partials), then one pass adds them, the bias, and writes the NCHW fp32 outputs.
+        {
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            const int od0 = p.head_od[0], od1 = p.head_od[1], od2 = p.head_od[2];
+            const int odsum = od0 + od1 + od2;
+            const int o = l16;                                       // tail output row of this lane's W1 fragment
+            const int hh = o < od0 ? 0 : o < od0 + od1 ? 1 : o < odsum ? 2 : -1;
+            const int oo = hh == 0 ? o : hh == 1 ? o - od0 : o - od0 - od1;
+            const float* wsel = hh == 0 ? p.head_w[0] : hh == 1 ? p.head_w[1] : p.head_w[2];
+            f32x4 tl[NA];
+    #pragma unroll
+            for (int a = 0; a < NA; ++a) tl[a] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            // blocks in pairs (b, b+1): after the tails, v_permlane16_swap trades the odd rows' block-b halves for
+            // the even rows' block-(b+1) halves, so every lane holds 8 consecutive channels (16-B stores: even rows
+            // channels 16b + 4lg .., odd rows 16(b+1) + 4(lg-1) ..; 64 contiguous bytes per pixel and instruction)
+    #pragma unroll
+            for (int b = 0; b < NB; b += 2) {
+                hx4 whi[2], wlo[2];
+                float bias[2][4];
+    #pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int col0 = 96 * wc + 16 * (b + e) + 4 * lg;
+                    const float4 bb = *(const float4*)(p.bias + col0);
+                    bias[e][0] = bb.x; bias[e][1] = bb.y; bias[e][2] = bb.z; bias[e][3] = bb.w;
+                    // W1[o][col0 .. col0 + 3] when those channels belong to output o's head, else 0
+                    float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (hh >= 0 && (col0 >> 7) == hh) wv = *(const float4*)(wsel + oo * 128 + (col0 & 127));
+                    const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        whi[e][j] = (__bf16)w4[j];
+                        wlo[e][j] = (__bf16)(w4[j] - (float)whi[e][j]);
+                    }
+                }
+                const int colst = 96 * wc + 16 * b + ((lg & 1) ? 16 + 4 * (lg - 1) : 4 * lg);
+    #pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    hx4 hv[2];
+    #pragma unroll
+                    for (int e = 0; e < 2; ++e)
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r) hv[e][r] = (__bf16)fmaxf(acc[a][b + e][r] + bias[e][r], 0.f);
+                    if constexpr (!(H384_ABL & 32)) {
+    #pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            tl[a] = mfma_16x16x16(whi[e], hv[e], tl[a]);
+                            tl[a] = mfma_16x16x16(wlo[e], hv[e], tl[a]);
+                        }
+                    }
+                    typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+                    const u32x2 x = __builtin_bit_cast(u32x2, hv[0]), y = __builtin_bit_cast(u32x2, hv[1]);
+                    uint4 st;
+                    {
+                        const auto s0 = __builtin_amdgcn_permlane16_swap(x[0], y[0], false, false);
+                        const auto s1 = __builtin_amdgcn_permlane16_swap(x[1], y[1], false, false);
+                        st.x = s0[0]; st.y = s1[0]; st.z = s0[1]; st.w = s1[1];
+                    }
+                    const int m = mt * BM + 96 * grp + 16 * a + l16;
+                    if constexpr (!(H384_ABL & 64))
+                        if (m < M) *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
+                }
+            }
+            if constexpr (!(H384_ABL & 32)) {
+                // partials [wc][o][pixel of tile]: D[o = 4lg + r][px = l16] of block a
+                float* part = (float*)smem;
+    #pragma unroll
+                for (int a = 0; a < NA; ++a)
+    #pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        part[(wc * 16 + 4 * lg + r) * BM + 96 * grp + 16 * a + l16] = tl[a][r];
+                __syncthreads();
+                for (int idx = tid; idx < odsum * BM; idx += 512) {
+                    const int oi = idx / BM, r = idx - oi * BM;
+                    const int m = mt * BM + r;
+                    if (m >= M) continue;
+                    const float v = (part[(0 * 16 + oi) * BM + r] + part[(1 * 16 + oi) * BM + r]) +
+                                    (part[(2 * 16 + oi) * BM + r] + part[(3 * 16 + oi) * BM + r]);
+                    const int h = oi < od0 ? 0 : oi < od0 + od1 ? 1 : 2;
+                    const int ob = oi - (h == 0 ? 0 : h == 1 ? od0 : od0 + od1);
+                    const int odh = h == 0 ? od0 : h == 1 ? od1 : od2;
+                    float* out = h == 0 ? p.head_out[0] : h == 1 ? p.head_out[1] : p.head_out[2];
+                    const float bo = (h == 0 ? p.head_b[0] : h == 1 ? p.head_b[1] : p.head_b[2])[ob];
+                    const int n = m / QQ, pix = m - (m / QQ) * QQ;
+                    out[((long)n * odh + ob) * QQ + pix] = v + bo;
+                }
+            }
+        }
+#else
         // ---- epilogue: bias + ReLU, the hidden tile staged in LDS
     #pragma unroll
         for (int b = 0; b < NB; ++b) {
@@ -1439,6 +1547,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
             const int m = mt * BM + row;
             if (m < M) *(uint4*)(p.y + ((long)m * BN + ch * EPC) * 2) = *(const uint4*)(smem + row * EROW + ch * 16);
         }
+#endif
         __syncthreads();                 // staging consumed before the next tile's prologue DMA
     }
 }

@@ -8,5 +8,5 @@ SRC=conv_gemm.hip
 if [[ "$1" == SRC=* ]]; then SRC=${1#SRC=}; shift; fi
 mkdir -p build/var_$NAME
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics -Wno-unused-function -I. "$@" -c $SRC -o build/var_$NAME/conv_gemm.o
-OBJS=$(ls build/*.o | grep -v conv_gemm.o)
+OBJS="$(ls build/*.o | grep -v conv_gemm.o) $(ls build/f16/*.o)"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build/var_$NAME/conv_gemm.o $OBJS -o ../scdhip/libscdhip_$NAME.so
