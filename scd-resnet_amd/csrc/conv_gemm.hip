@@ -26,7 +26,8 @@
 #define H384_PRIO 0   // heads384 kernel MFMA priority: 0 = s_setprio 1 around each C part, 1 = group 1 static, 2 = none
 #endif
 #ifndef H384_PERSIST
-#define H384_PERSIST 0  // heads384 kernel persistent over tiles (SCD_GEMM_HEADS384_GRID workgroups per CU)
+#define H384_PERSIST 0  // heads384 kernel persistent over tiles, next tile's first stage prefetched under the epilogue
+                        // (SCD_GEMM_HEADS384_GRID workgroups per CU; measured 0.826 vs 0.80 ms one-workgroup-per-tile)
 #endif
 #ifndef H384_ABL
 #define H384_ABL 0    // heads384 timing ablations (wrong results): 1 no MFMA, 2 loop DMAs read nothing, 4 no loop
@@ -1210,17 +1211,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     const int ntiles = (M + BM - 1) / BM;
     const int lrow = lane >> 3;
     const int cch = (lane & 7) ^ lrow;
-#if H384_PERSIST
-    // persistent over tiles (measured no faster than one workgroup per tile; SCD_GEMM_HEADS384_GRID)
-    for (int mt = bid; mt < ntiles; mt += gridDim.x) {
-#else
-    {
-        const int mt = bid;
-        (void)ntiles;
-#endif
-        // A: this lane's DMA rows 96*grp + 32*j + 8*wc + lrow (j = third), byte offset at tap (0,0) + in-image tap mask
-        int a_base[3];
-        unsigned a_mask[3];
+    static_assert(!(H384_PERSIST && H384_EPI == 0), "the persistent heads384 kernel needs the register epilogue");
+    // A: this lane's DMA rows 96*grp + 32*j + 8*wc + lrow (j = third), byte offset at tap (0,0) + in-image tap mask
+    int a_base[3];
+    unsigned a_mask[3];
+    auto tile_setup = [&](int mt) {
     #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const int m = mt * BM + 96 * grp + 32 * j + 8 * wc + lrow;
@@ -1238,37 +1233,59 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
             }
             a_mask[j] = msk;
         }
-        // B: rows 192*grp + 48*wc + 8*o + lrow, o = 0..5 (part 1: o < 3, part 2: o >= 3)
-        int b_base[6];
+    };
+    // B: rows 192*grp + 48*wc + 8*o + lrow, o = 0..5 (part 1: o < 3, part 2: o >= 3)
+    int b_base[6];
     #pragma unroll
-        for (int o = 0; o < 6; ++o) b_base[o] = ((192 * grp + 48 * wc + 8 * o + lrow) * p.wrow + cch * EPC) * 2;
-        const int cpt = p.Ci / BK;
-        const int KT = ph.ntaps * cpt;
-        const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
-        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+    for (int o = 0; o < 6; ++o) b_base[o] = ((192 * grp + 48 * wc + 8 * o + lrow) * p.wrow + cch * EPC) * 2;
+    const int cpt = p.Ci / BK;
+    const int KT = ph.ntaps * cpt;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
 
-        struct StageArgs { int live, tap, adelta, bdelta; };
-        auto stage_args = [&](int kt_req) {
-            StageArgs a;
-            a.live = kt_req < KT;
-            const int kt = min(kt_req, KT - 1);
-            const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
-            a.tap = tap;
-            a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * BK) * 2;
-            a.bdelta = (ph.wt[tap] * p.Ci + chunk * BK) * 2;
-            return a;
-        };
-        auto issue_a = [&](const StageArgs& g, char* buf, int j) {
-            const bool ok = g.live && ((a_mask[j] >> g.tap) & 1u);
-            dma16(xrs, buf + (96 * grp + 32 * j + 8 * wc) * 128, sel_off(ok, a_base[j] + g.adelta));
-        };
-        auto issue_b = [&](const StageArgs& g, char* buf, int part) {
-            char* Bs = buf + BM * 128;
+    struct StageArgs { int live, tap, adelta, bdelta; };
+    auto stage_args = [&](int kt_req) {
+        StageArgs a;
+        a.live = kt_req < KT;
+        const int kt = min(kt_req, KT - 1);
+        const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
+        a.tap = tap;
+        a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * BK) * 2;
+        a.bdelta = (ph.wt[tap] * p.Ci + chunk * BK) * 2;
+        return a;
+    };
+    auto issue_a = [&](const StageArgs& g, char* buf, int j) {
+        const bool ok = g.live && ((a_mask[j] >> g.tap) & 1u);
+        dma16(xrs, buf + (96 * grp + 32 * j + 8 * wc) * 128, sel_off(ok, a_base[j] + g.adelta));
+    };
+    auto issue_b = [&](const StageArgs& g, char* buf, int part) {
+        char* Bs = buf + BM * 128;
     #pragma unroll
-            for (int o = 3 * part; o < 3 * part + 3; ++o)
-                dma16(wrs, Bs + (192 * grp + 48 * wc + 8 * o) * 128, sel_off(g.live, b_base[o] + g.bdelta));
-        };
-
+        for (int o = 3 * part; o < 3 * part + 3; ++o)
+            dma16(wrs, Bs + (192 * grp + 48 * wc + 8 * o) * 128, sel_off(g.live, b_base[o] + g.bdelta));
+    };
+    // the first K-stage of a tile into stage buffer 0
+    auto issue_stage0 = [&]() {
+        const StageArgs g0 = stage_args(0);
+        issue_a(g0, smem, 0);
+        issue_b(g0, smem, 0);
+        issue_b(g0, smem, 1);
+        issue_a(g0, smem, 1);
+        issue_a(g0, smem, 2);
+    };
+#if H384_PERSIST
+    // persistent over tiles (SCD_GEMM_HEADS384_GRID workgroups per CU): the next tile's first K-stage is issued
+    // right after this tile's hidden stores, so its DMA latency hides under the tails' LDS exchange and the
+    // output pass (their partials then live in stage buffer 1)
+    if (bid < ntiles && KT > 0) { tile_setup(bid); issue_stage0(); }
+    for (int mt = bid; mt < ntiles; mt += gridDim.x) {
+#else
+    {
+        const int mt = bid;
+        (void)ntiles;
+        tile_setup(mt);
+        if (KT > 0) issue_stage0();
+#endif
         const int l16 = lane & 15, lg = lane >> 4;
         const int l7 = l16 & 7;
         const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
@@ -1327,14 +1344,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         };
 
         if (KT > 0) {
-            {
-                const StageArgs g0 = stage_args(0);
-                issue_a(g0, smem, 0);
-                issue_b(g0, smem, 0);
-                issue_b(g0, smem, 1);
-                issue_a(g0, smem, 1);
-                issue_a(g0, smem, 2);
-            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
             if constexpr (H384_ABL & 4) { read_b(smem); read_a(smem, 0); }
@@ -1444,9 +1453,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                         if (m < M) *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
                 }
             }
+#if H384_PERSIST
+            if (mt + (int)gridDim.x < ntiles) { tile_setup(mt + gridDim.x); issue_stage0(); }
+#endif
             if constexpr (!(H384_ABL & 32)) {
                 // partials [wc][o][pixel of tile]: D[o = 4lg + r][px = l16] of block a
-                float* part = (float*)smem;
+                float* part = (float*)(smem + (H384_PERSIST ? STAGE : 0));
     #pragma unroll
                 for (int a = 0; a < NA; ++a)
     #pragma unroll
