@@ -236,6 +236,29 @@ int scd_heads_bwd_packed(int dtype, const void* hid, int N, int HW, int nh, int 
                          double* acc, void* stream);
 int scd_heads_bwd_weight_finalize(double* acc, int nh, int Hd, const int* od, float* const* dw1,
                                   float* const* db1, float* const* db0, int accumulate, float alpha, void* stream);
+/* The same tail backward over the dense heads [0, nd) only: dhid has row stride nd*Hd (hid keeps nh*Hd), packed
+ * is [pixel][nd][4].  scd_heads_bwd_packed == scd_heads_bwd_packed_split with nd = nh. */
+int scd_heads_bwd_packed_split(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od, int nd,
+                               const float* const* w1, const float* const* douts, float dscale, float* packed,
+                               void* dhid, double* acc, void* stream);
+/* Heads [nd, nh) whose output gradients vanish outside the pixels inds[b][k] (b < N, k < K; HW-local indices): the
+ * regression / offset terminals under L1LossMask(gather(out, inds), ..., mask) (centerNetOffset.py:199-214,
+ * regression.py:37-44; utility.py:76-85 gather).  Slot s = b*K + k; the first slot naming a pixel is active.
+ * scd_heads_sparse_bwd: dhid_s[s][(nh-nd)*Hd] = relu'(hid) * W1^T g (zero rows for inactive slots),
+ * xcol[s][Cin*9] = the slot pixel's 3x3 patch of feat (ci-major, tap-minor: an OIHW weight-gradient row), the
+ * heads' dW1/db1/db0 into acc (scd_heads_bwd_weight_finalize), slotmap[pixel] = s, ownermap[q] = min(s*9 + t)
+ * over the (slot, tap) pairs reaching q.  scd_heads_sparse_fixup: dx[q] += sum over taps t of
+ * cols[slot(q - d_t)][ci*9 + t] (cols = dhid_s x W0^T, the 3x3 conv's transposed weight as a [Cin*9][Cs] GEMM
+ * operand) at every reached q, with the following BN+ReLU layer's backward sums corrected when bn_y != NULL
+ * (scd_conv_gemm_bnbwd's definition); both maps are restored (slotmap = -1, ownermap = INT_MAX: persistent
+ * int32[N*H*W] buffers initialised once).  (nh-nd)*Hd <= 256, Cin <= 256. */
+int scd_heads_sparse_bwd(int dtype, const void* hid, const void* feat, int N, int H, int W, int Cin, int nh, int Hd,
+                         const int* od, int nd, const float* const* w1, const float* const* douts, float dscale,
+                         const long* inds, int K, void* dhid_s, void* xcol, double* acc, int* slotmap, int* ownermap,
+                         void* stream);
+int scd_heads_sparse_fixup(int dtype, void* dx, const void* cols, int N, int H, int W, int Cin, const long* inds, int K,
+                           int* slotmap, int* ownermap, const void* bn_y, const float* mean, const float* invstd,
+                           const float* relu_scale, const float* relu_shift, double* bn_stats, void* stream);
 
 /* ---- losses (focal.py:25-53, regression.py:37-44, centerNetOffset.py:182-217) ---- */
 /* per element: g = d/dlogit [pos: log(p)(1-p)^2 | neg: log(1-p) p^2 (1-gt)^4] with

@@ -396,6 +396,8 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_bn_2x2_kernel(const T* dout
 // ---------------------------------------------------------------- CenterNet head tails
 struct HeadsDesc {
     int nh, Hd, od[4], orow[4], nout;
+    int nd;                 // the tail backward covers heads [0, nd) (the rest: scd_heads_sparse_bwd)
+    int hstride, dstride;   // row strides (elements) of the hidden activation and of the written dhid
     const float* w1[4];
     const float* b1[4];
     const float* dout[4];
@@ -409,11 +411,11 @@ __global__ void heads_pack_kernel(int N, int HW, HeadsDesc d, float scale, float
     const long P = (long)N * HW;
     for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < P; px += (long)gridDim.x * blockDim.x) {
         const long n = px / HW, q = px - n * HW;
-        for (int h = 0; h < d.nh; ++h) {
+        for (int h = 0; h < d.nd; ++h) {
             float v[4];
 #pragma unroll
             for (int o = 0; o < 4; ++o) v[o] = o < d.od[h] ? d.dout[h][(n * d.od[h] + o) * HW + q] * scale : 0.f;
-            *(float4*)(pk + (px * d.nh + h) * 4) = make_float4(v[0], v[1], v[2], v[3]);
+            *(float4*)(pk + (px * d.nd + h) * 4) = make_float4(v[0], v[1], v[2], v[3]);
         }
     }
 }
@@ -471,7 +473,7 @@ __global__ __launch_bounds__(512) void heads_bwd_kernel(const T* hid, int N, int
     constexpr int E = Vec16<T>::N;
     constexpr int NA = 4 * E + E + 4;               // dW1 partials, db0 partials, db1 partials
     const int cph = d.Hd / E;
-    const int cpp = d.nh * cph;
+    const int cpp = d.nd * cph;
     const int G = blockDim.x / cpp;
     const int tid = threadIdx.x;
     const int c = tid % cpp;
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(512) void heads_bwd_kernel(const T* hid, int N, int
     const unsigned P = (unsigned)N * HW;
     const unsigned p0 = blockIdx.x * (unsigned)PXB;
     const unsigned p1 = min(P, p0 + PXB);
-    const unsigned Ctot = d.nh * d.Hd;
+    const unsigned Ctot = d.hstride, Dtot = d.dstride;
     auto body = [&](unsigned px, const float* gd, float* v) {
         float r[E];
 #pragma unroll
@@ -505,11 +507,11 @@ __global__ __launch_bounds__(512) void heads_bwd_kernel(const T* hid, int N, int
         }
 #pragma unroll
         for (int o = 0; o < 4; ++o) a[5 * E + o] += gd[o];
-        Vec16<T>::store(dhid + px * Ctot + ct, r);
+        Vec16<T>::store(dhid + px * Dtot + ct, r);
     };
     auto load_gd = [&](unsigned px, float* gd) {
         if constexpr (PK) {
-            const float4 v = *(const float4*)(d.pk + ((size_t)px * d.nh + h) * 4);
+            const float4 v = *(const float4*)(d.pk + ((size_t)px * d.nd + h) * 4);
             gd[0] = v.x; gd[1] = v.y; gd[2] = v.z; gd[3] = v.w;
         } else {
             const unsigned n = px / (unsigned)HW;
@@ -609,6 +611,7 @@ __global__ void heads_bwd_weight_finalize_kernel(double* acc, int accsz, HeadsDe
 bool make_desc(HeadsDesc& d, int nh, int Hd, const int* od) {
     if (nh < 1 || nh > 4 || Hd % 8 != 0) return false;
     d.nh = nh; d.Hd = Hd; d.nout = 0;
+    d.nd = nh; d.hstride = d.dstride = nh * Hd;
     for (int h = 0; h < 4; ++h) {
         d.od[h] = h < nh ? od[h] : 0;
         if (d.od[h] > 4) return false;
@@ -873,11 +876,19 @@ extern "C" int scd_adam_step_dev(float* p, const float* g, float* m, float* v, l
 extern "C" int scd_heads_bwd_packed(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
                                     const float* const* w1, const float* const* douts, float dscale, float* packed,
                                     void* dhid, double* acc, void* stream) {
-    SCD_F16_FWD(scd_heads_bwd_packed, hid, N, HW, nh, Hd, od, w1, douts, dscale, packed, dhid, acc, stream);
+    return scd_heads_bwd_packed_split(dtype, hid, N, HW, nh, Hd, od, nh, w1, douts, dscale, packed, dhid, acc, stream);
+}
+
+extern "C" int scd_heads_bwd_packed_split(int dtype, const void* hid, int N, int HW, int nh, int Hd, const int* od,
+                                          int nd, const float* const* w1, const float* const* douts, float dscale,
+                                          float* packed, void* dhid, double* acc, void* stream) {
+    SCD_F16_FWD(scd_heads_bwd_packed_split, hid, N, HW, nh, Hd, od, nd, w1, douts, dscale, packed, dhid, acc, stream);
     HeadsDesc d;
-    if (!make_desc(d, nh, Hd, od) || !packed) return SCD_ERR_ARG;
+    if (!make_desc(d, nh, Hd, od) || !packed || nd < 1 || nd > nh) return SCD_ERR_ARG;
+    d.nd = nd;
+    d.dstride = nd * Hd;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
-    const int cpp = nh * Hd / E;
+    const int cpp = nd * Hd / E;
     if (cpp > 256 || (Hd % E)) return SCD_ERR_ARG;
     for (int h = 0; h < nh; ++h) { d.w1[h] = w1[h]; d.dout[h] = douts[h]; }
     const int accsz = d.nout * Hd + d.nout + nh * Hd;
@@ -902,5 +913,213 @@ extern "C" int scd_heads_bwd_packed(int dtype, const void* hid, int N, int HW, i
                            N, HW, d, (float*)dhid, acc, accsz, PXB);
     else
         return SCD_ERR_ARG;
+    SCD_RETURN_LAUNCH();
+}
+
+// ---------------------------------------------------------------- CenterNet heads: sparse-gradient backward
+// The regression / offset heads (centerNetOffset.py:106-110) are trained only through L1LossMask on
+// gather(head, inds) (centerNetOffset.py:199-214, regression.py:37-44): their output gradient is zero except at
+// the <= K gathered pixels per image.  For those heads the tail backward, the 3x3 weight gradient and the 3x3
+// input gradient reduce to sums over that pixel set (slots s = b*K + k; the first slot naming a pixel carries it,
+// repeats carry nothing, so a pixel named twice is counted once with its summed gradient):
+//   dhid_s[s][c]         = relu'(hid) * sum_o W1[o][c] g[o]           (heads [nd, nh), c over their channels)
+//   xcol[s][ci*9 + t]    = feat[p + d_t][ci]                           (im2col of the slot's pixel)
+//   dW0 = dhid_s^T xcol, and dX[q] += sum_{t : q - d_t active} C[slot(q - d_t)][ci*9 + t], C = dhid_s W0^T
+// The dense heads [0, nd) keep the dense tail (scd_heads_bwd_packed_split) and GEMMs over their channels only.
+// slotmap (pixel -> slot, -1 elsewhere) and ownermap (q -> first (slot, tap) reaching q, INT_MAX elsewhere) are
+// persistent int32 maps over the N*H*W pixels; the kernels below leave them as they found them.
+namespace {
+constexpr int SP_SPB = 8;                   // slots per workgroup of the sparse tail
+
+template <typename T>
+__global__ __launch_bounds__(256) void heads_sparse_bwd_kernel(const T* hid, const T* feat, int N, int H, int W, int Cin,
+                                                               HeadsDesc d, float dscale, const long* inds, int K,
+                                                               T* dhid_s, T* xcol, double* acc, int accsz,
+                                                               int* slotmap, int* ownermap) {
+    const int HW = H * W;
+    const int Cs = (d.nh - d.nd) * d.Hd;
+    const int tid = threadIdx.x;
+    const int c = tid;                                  // sparse-head channel of this thread
+    const bool cok = c < Cs;
+    const int h = cok ? d.nd + c / d.Hd : d.nd;
+    const int j = cok ? c - (h - d.nd) * d.Hd : 0;
+    const int od = d.od[h];
+    float w[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) w[o] = (cok && o < od) ? d.w1[h][o * d.Hd + j] : 0.f;
+    float a_dw1[4] = {0.f, 0.f, 0.f, 0.f}, a_db1[4] = {0.f, 0.f, 0.f, 0.f}, a_db0 = 0.f;
+    const int S = N * K;
+    const int s0 = blockIdx.x * SP_SPB;
+    const int KC = Cin * 9;
+    for (int s = s0; s < min(S, s0 + SP_SPB); ++s) {
+        const int b = s / K, k = s - (s / K) * K;
+        const long ind = inds[s];
+        bool active = ind >= 0 && ind < HW;
+        for (int k2 = 0; k2 < k && active; ++k2) active = inds[(long)b * K + k2] != ind;
+        const int q0 = active ? (int)ind : 0;
+        const int y = q0 / W, x = q0 - (q0 / W) * W;
+        const long p = (long)b * HW + q0;
+        float r = 0.f;
+        if (active && cok) {
+            const float hv = to_f<T>(hid[p * d.hstride + d.nd * d.Hd + c]);
+            float g[4];
+#pragma unroll
+            for (int o = 0; o < 4; ++o) g[o] = o < od ? d.dout[h][((long)b * od + o) * HW + q0] * dscale : 0.f;
+            const float sacc = g[0] * w[0] + g[1] * w[1] + g[2] * w[2] + g[3] * w[3];
+            r = hv > 0.f ? sacc : 0.f;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) { a_dw1[o] += g[o] * hv; a_db1[o] += g[o]; }
+            a_db0 += r;
+        }
+        if (cok) dhid_s[(long)s * Cs + c] = from_f<T>(r);
+        if (active && tid == 0) {
+            slotmap[p] = s;
+            for (int t = 0; t < 9; ++t) {
+                const int qy = y + t / 3 - 1, qx = x + t % 3 - 1;
+                if ((unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W)
+                    atomicMin(ownermap + (long)b * HW + qy * W + qx, s * 9 + t);
+            }
+        }
+        // im2col row of the slot (its pixel's 3x3 x Cin patch, zeros outside the image), ci-major, tap-minor
+        for (int i = tid; i < KC; i += blockDim.x) {
+            const int ci = i / 9, t = i - (i / 9) * 9;
+            const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+            const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+            xcol[(long)s * KC + i] = in ? feat[(((long)b * H + iy) * W + ix) * Cin + ci] : from_f<T>(0.f);
+        }
+    }
+    // weight / bias partials of the sparse heads (same accumulator layout as heads_bwd_kernel)
+    if (cok) {
+        double* dst = acc + (size_t)(blockIdx.x % SCD_STAT_REPLICAS) * accsz;
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+            if (o < od) atomic_add_f64(dst + (d.orow[h] + o) * d.Hd + j, (double)a_dw1[o]);
+        atomic_add_f64(dst + d.nout * d.Hd + d.nout + h * d.Hd + j, (double)a_db0);
+        if (j == 0)
+#pragma unroll
+            for (int o = 0; o < 4; ++o)
+                if (o < od) atomic_add_f64(dst + d.nout * d.Hd + d.orow[h] + o, (double)a_db1[o]);
+    }
+}
+
+// dX[q] += the sparse heads' input-gradient at the pixels q their slots reach; one workgroup per slot, one
+// thread per input channel; q is handled by the first (slot, tap) reaching it (ownermap), which sums the
+// contributions of every active neighbour in tap order.  With bn_y: the following BN+ReLU layer's backward sums
+// (scd_conv_gemm_bnbwd's epilogue over the dense part) get the change of each rewritten value.
+template <typename T>
+__global__ __launch_bounds__(256) void heads_sparse_fixup_kernel(T* dx, const T* cols, int N, int H, int W, int Cin,
+                                                                 const long* inds, int K, const int* slotmap,
+                                                                 int* ownermap, const T* bny, const float* mean,
+                                                                 const float* invstd, const float* rsc,
+                                                                 const float* rsh, double* stats) {
+    const int HW = H * W;
+    const int s = blockIdx.x;
+    const int b = s / K;
+    const long ind = inds[s];
+    if (ind < 0 || ind >= HW) return;
+    const long p = (long)b * HW + ind;
+    if (slotmap[p] != s) return;                       // a repeat of an earlier slot's pixel
+    const int y = (int)ind / W, x = (int)ind - ((int)ind / W) * W;
+    const int ci = threadIdx.x;
+    const bool cok = ci < Cin;
+    const int KC = Cin * 9;
+    float bm = 0.f, bi = 0.f, bs = 0.f, bh = 0.f;
+    if (bny && cok) { bm = mean[ci]; bi = invstd[ci]; bs = rsc[ci]; bh = rsh[ci]; }
+    float dsum = 0.f, dsq = 0.f;
+    for (int t = 0; t < 9; ++t) {
+        const int qy = y + t / 3 - 1, qx = x + t % 3 - 1;
+        if ((unsigned)qy >= (unsigned)H || (unsigned)qx >= (unsigned)W) continue;
+        const long qi = (long)b * HW + qy * W + qx;
+        const int own = ownermap[qi];
+        __syncthreads();                                // every thread has read the owner before it is reset
+        if (own != s * 9 + t) continue;
+        if (threadIdx.x == 0) ownermap[qi] = 0x7fffffff;
+        if (!cok) continue;
+        float corr = 0.f;
+        for (int t2 = 0; t2 < 9; ++t2) {
+            const int py = qy - (t2 / 3 - 1), px = qx - (t2 % 3 - 1);
+            if ((unsigned)py >= (unsigned)H || (unsigned)px >= (unsigned)W) continue;
+            const int s2 = slotmap[(long)b * HW + py * W + px];
+            if (s2 >= 0) corr += to_f<T>(cols[(long)s2 * KC + ci * 9 + t2]);
+        }
+        T* dp = dx + qi * Cin + ci;
+        const T old = *dp;
+        const T nv = from_f<T>(to_f<T>(old) + corr);
+        *dp = nv;
+        if (bny) {
+            const float yv = to_f<T>(bny[qi * Cin + ci]);
+            const float dd = yv * bs + bh > 0.f ? to_f<T>(nv) - to_f<T>(old) : 0.f;
+            dsum += dd;
+            dsq += dd * (yv - bm) * bi;
+        }
+    }
+    if (bny && cok) {
+        const int rep = s % SCD_STAT_REPLICAS;
+        atomic_add_f64(stats + ((long)rep * 2 + 0) * Cin + ci, (double)dsum);
+        atomic_add_f64(stats + ((long)rep * 2 + 1) * Cin + ci, (double)dsq);
+    }
+}
+
+__global__ void heads_sparse_reset_kernel(const long* inds, int S, int K, int HW, int* slotmap) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const long ind = inds[s];
+    if (ind < 0 || ind >= HW) return;
+    const long p = (long)(s / K) * HW + ind;
+    if (slotmap[p] == s) slotmap[p] = -1;
+}
+
+}  // namespace
+
+extern "C" int scd_heads_sparse_bwd(int dtype, const void* hid, const void* feat, int N, int H, int W, int Cin, int nh,
+                                    int Hd, const int* od, int nd, const float* const* w1, const float* const* douts,
+                                    float dscale, const long* inds, int K, void* dhid_s, void* xcol, double* acc,
+                                    int* slotmap, int* ownermap, void* stream) {
+    SCD_F16_FWD(scd_heads_sparse_bwd, hid, feat, N, H, W, Cin, nh, Hd, od, nd, w1, douts, dscale, inds, K, dhid_s, xcol,
+                acc, slotmap, ownermap, stream);
+    HeadsDesc d;
+    if (!make_desc(d, nh, Hd, od) || nd < 0 || nd >= nh || K < 1 || (nh - nd) * Hd > 256) return SCD_ERR_ARG;
+    if ((long)N * K * 9 * 9 >= (1L << 31) || (long)N * H * W * nh * Hd >= (1L << 31)) return SCD_ERR_ARG;
+    d.nd = nd;
+    for (int h = 0; h < nh; ++h) { d.w1[h] = w1[h]; d.dout[h] = douts[h]; }
+    const int accsz = d.nout * Hd + d.nout + nh * Hd;
+    const int blocks = cdiv((long)N * K, SP_SPB);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == SCD_DT_BF16)
+        hipLaunchKernelGGL(heads_sparse_bwd_kernel<__bf16>, dim3(blocks), dim3(256), 0, st, (const __bf16*)hid,
+                           (const __bf16*)feat, N, H, W, Cin, d, dscale, inds, K, (__bf16*)dhid_s, (__bf16*)xcol, acc,
+                           accsz, slotmap, ownermap);
+    else if (dtype == SCD_DT_F32)
+        hipLaunchKernelGGL(heads_sparse_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)hid,
+                           (const float*)feat, N, H, W, Cin, d, dscale, inds, K, (float*)dhid_s, (float*)xcol, acc,
+                           accsz, slotmap, ownermap);
+    else
+        return SCD_ERR_ARG;
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_heads_sparse_fixup(int dtype, void* dx, const void* cols, int N, int H, int W, int Cin,
+                                      const long* inds, int K, int* slotmap, int* ownermap, const void* bn_y,
+                                      const float* mean, const float* invstd, const float* relu_scale,
+                                      const float* relu_shift, double* bn_stats, void* stream) {
+    SCD_F16_FWD(scd_heads_sparse_fixup, dx, cols, N, H, W, Cin, inds, K, slotmap, ownermap, bn_y, mean, invstd,
+                relu_scale, relu_shift, bn_stats, stream);
+    if (Cin < 1 || Cin > 256 || K < 1) return SCD_ERR_ARG;
+    if (bn_y && !(mean && invstd && relu_scale && relu_shift && bn_stats)) return SCD_ERR_ARG;
+    const int S = N * K;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == SCD_DT_BF16)
+        hipLaunchKernelGGL(heads_sparse_fixup_kernel<__bf16>, dim3(S), dim3(256), 0, st, (__bf16*)dx,
+                           (const __bf16*)cols, N, H, W, Cin, inds, K, slotmap, ownermap, (const __bf16*)bn_y, mean,
+                           invstd, relu_scale, relu_shift, bn_stats);
+    else if (dtype == SCD_DT_F32)
+        hipLaunchKernelGGL(heads_sparse_fixup_kernel<float>, dim3(S), dim3(256), 0, st, (float*)dx, (const float*)cols,
+                           N, H, W, Cin, inds, K, slotmap, ownermap, (const float*)bn_y, mean, invstd, relu_scale,
+                           relu_shift, bn_stats);
+    else
+        return SCD_ERR_ARG;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(heads_sparse_reset_kernel, dim3(cdiv(S, 256)), dim3(256), 0, st, inds, S, K, H * W, slotmap);
     SCD_RETURN_LAUNCH();
 }

@@ -34,6 +34,9 @@
 #define scd_heads_bwd_accsize scd_heads_bwd_accsize__f16
 #define scd_heads_bwd scd_heads_bwd__f16
 #define scd_heads_bwd_packed scd_heads_bwd_packed__f16
+#define scd_heads_bwd_packed_split scd_heads_bwd_packed_split__f16
+#define scd_heads_sparse_bwd scd_heads_sparse_bwd__f16
+#define scd_heads_sparse_fixup scd_heads_sparse_fixup__f16
 #define scd_heads_bwd_weight_finalize scd_heads_bwd_weight_finalize__f16
 #define scd_adam_step scd_adam_step__f16
 #define scd_adam_step_dev scd_adam_step_dev__f16
@@ -74,6 +77,9 @@ SCD_F16_DECL(scd_stem_pool_bwd_bn)
 SCD_F16_DECL(scd_heads_fwd)
 SCD_F16_DECL(scd_heads_bwd)
 SCD_F16_DECL(scd_heads_bwd_packed)
+SCD_F16_DECL(scd_heads_bwd_packed_split)
+SCD_F16_DECL(scd_heads_sparse_bwd)
+SCD_F16_DECL(scd_heads_sparse_fixup)
 SCD_F16_DECL(scd_stem_conv_fwd)
 SCD_F16_DECL(scd_stem_conv_wgrad)
 SCD_F16_DECL(scd_pad_channels)

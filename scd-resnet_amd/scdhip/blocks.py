@@ -333,6 +333,9 @@ class HeadsFn(torch.autograd.Function):
         S = ops.begin_loss_scale(feat.dtype)
         dptrs = ops.L.ptr_array([d.data_ptr() for d in douts])
         odarr = ops.L.int_array(od)
+        nd = HeadsFn._dense_prefix(douts, Hd, Cin)
+        if nd < nh:
+            return HeadsFn._backward_sparse(ctx, douts, dptrs, odarr, nd, S)
         dhid = torch.empty_like(hid)
         acc = ops.persistent_zeros(heads[0][2].weight, "_scd_heads_acc",
                                    ops.L.lib().scd_heads_bwd_accsize(nh, Hd, odarr) // 8, torch.float64)
@@ -350,6 +353,78 @@ class HeadsFn(torch.autograd.Function):
         fuse = ctx.prod is not None and feat.dtype in ops.HALF
         dfeat = ops.conv_dgrad(dhid, ops.pack_concat(w0s, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1,
                                bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
+        if fuse:
+            ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
+        grads_ready(*[m for h in heads for m in h if isinstance(m, torch.nn.Module)])
+        return dfeat, None, None
+
+    @staticmethod
+    def _dense_prefix(douts, Hd, Cin):
+        """Number of leading heads that need the dense backward: the rest must carry the loss's sparse-support
+        certificate (one index tensor for all of them; ops.certify_sparse_grad)."""
+        nh = len(douts)
+        if nh < 2 or Cin > 256:
+            return nh
+        certs = [ops.sparse_grad_inds(d) for d in douts]
+        nd = nh
+        while nd > 1 and certs[nd - 1] is not None and certs[nd - 1] is certs[-1]:
+            nd -= 1
+        return nd if (nh - nd) * Hd <= 256 else nh
+
+    @staticmethod
+    def _backward_sparse(ctx, douts, dptrs, odarr, nd, S):
+        """Heads [0, nd): the dense tail backward and 3x3 GEMMs over their nd*Hd hidden channels.  Heads [nd, nh):
+        their output gradient lives on the certified pixels inds[b][k] only, so the tail backward, the 3x3 weight
+        gradient (a GEMM over those pixels' im2col rows) and the 3x3 input gradient (a small GEMM then a gather
+        into the dense input gradient) run over that pixel set (scd_heads_sparse_bwd / scd_heads_sparse_fixup)."""
+        feat, hid = ctx.saved_tensors
+        w0s, heads, od, Hd = ctx.w0s, ctx.heads, ctx.od, ctx.Hd
+        N, H, W, Cin = feat.shape
+        nh = len(heads)
+        dev, dt = feat.device, feat.dtype
+        inds = ops.sparse_grad_inds(douts[-1])
+        K = inds.shape[1]
+        Sl = N * K                                     # slots
+        Cs = (nh - nd) * Hd
+        w1s = ops.L.ptr_array([h[2].weight.data_ptr() for h in heads])
+        acc = ops.persistent_zeros(heads[0][2].weight, "_scd_heads_acc",
+                                   ops.L.lib().scd_heads_bwd_accsize(nh, Hd, odarr) // 8, torch.float64)
+        dh_dense = torch.empty(N, H, W, nd * Hd, device=dev, dtype=dt)
+        packed = torch.empty(N * H * W * nd * 4, device=dev)
+        ops.L.call("scd_heads_bwd_packed_split", ops.dt(hid), ops.ptr(hid), N, H * W, nh, Hd, odarr, nd, w1s, dptrs,
+                   float(S), ops.ptr(packed), ops.ptr(dh_dense), ops.ptr(acc), ops.stream())
+        dhid_s = torch.empty(Sl, Cs, device=dev, dtype=dt)
+        xcol = torch.empty(Sl, Cin * 9, device=dev, dtype=dt)
+        slotmap, ownermap = ops.sparse_maps(dev, N * H * W)
+        ops.L.call("scd_heads_sparse_bwd", ops.dt(hid), ops.ptr(hid), ops.ptr(feat), N, H, W, Cin, nh, Hd, odarr, nd,
+                   w1s, dptrs, float(S), ops.ptr(inds), K, ops.ptr(dhid_s), ops.ptr(xcol), ops.ptr(acc),
+                   ops.ptr(slotmap), ops.ptr(ownermap), ops.stream())
+        ops.L.call("scd_heads_bwd_weight_finalize", ops.ptr(acc), nh, Hd, odarr,
+                   ops.L.ptr_array([ops.grad_of(h[2].weight).data_ptr() for h in heads]),
+                   ops.L.ptr_array([ops.grad_of(h[2].bias).data_ptr() for h in heads]),
+                   ops.L.ptr_array([ops.grad_of(h[0].bias).data_ptr() for h in heads]), 1, 1.0 / S, ops.stream())
+        # weight gradients: dense heads over every pixel, sparse heads over the slots' im2col rows (a 1x1 GEMM whose
+        # Cin*9 columns are the OIHW rows of their 3x3 weights)
+        ld = (Cin * 9, 9, 1)
+        ops.conv_wgrad(dh_dense, feat, 3, 3, 1, 1, None, None,
+                       rows=[(i * Hd, (i + 1) * Hd, ops.grad_of(heads[i][0].weight), ld) for i in range(nd)])
+        ops.conv_wgrad(dhid_s.view(1, 1, Sl, Cs), xcol.view(1, 1, Sl, Cin * 9), 1, 1, 1, 0, None, None,
+                       rows=[((i - nd) * Hd, (i - nd + 1) * Hd, ops.grad_of(heads[i][0].weight), (Cin * 9, 1, 1))
+                             for i in range(nd, nh)])
+        # input gradient: dense heads' GEMM (+ the deconv BN's backward sums), then the sparse heads' part
+        fuse = ctx.prod is not None and dt in ops.HALF
+        bn_args = ops.fused_bn_bwd_args(ctx.prod) if fuse else None
+        dfeat = ops.conv_dgrad(dh_dense, ops.pack_concat(w0s[:nd], dt, 1), Cin, H, W, 3, 3, 1, 1, bn_bwd=bn_args)
+        wt_s = ops.pack_concat(w0s[nd:], dt, 1).view(Cin * 9, Cs)     # [ci][tap][c] rows: W0^T of the sparse heads
+        cols = ops.conv_fwd(dhid_s.view(1, 1, Sl, Cs), wt_s, Cin * 9, 1, 1, 1, 0)
+        if fuse:
+            st, ybn, bstats = bn_args
+            bn_ptrs = (ops.ptr(ybn), ops.ptr(st.mean), ops.ptr(st.invstd), ops.ptr(st.scale), ops.ptr(st.shift),
+                       ops.ptr(bstats))
+        else:
+            bn_ptrs = (None,) * 6
+        ops.L.call("scd_heads_sparse_fixup", ops.dt(dfeat), ops.ptr(dfeat), ops.ptr(cols), N, H, W, Cin, ops.ptr(inds),
+                   K, ops.ptr(slotmap), ops.ptr(ownermap), *bn_ptrs, ops.stream())
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
         grads_ready(*[m for h in heads for m in h if isinstance(m, torch.nn.Module)])

@@ -84,6 +84,9 @@ SIGNATURES = {
     "scd_heads_bwd": (I, [I, P, I, I, I, I, IP, PP, PP, P, P, P]),
     "scd_heads_bwd_packed": (I, [I, P, I, I, I, I, IP, PP, PP, F, P, P, P, P]),
     "scd_heads_bwd_weight_finalize": (I, [P, I, I, IP, PP, PP, PP, I, F, P]),
+    "scd_heads_bwd_packed_split": (I, [I, P, I, I, I, I, IP, I, PP, PP, F, P, P, P, P]),
+    "scd_heads_sparse_bwd": (I, [I, P, P, I, I, I, I, I, I, IP, I, PP, PP, F, P, I, P, P, P, P, P, P]),
+    "scd_heads_sparse_fixup": (I, [I, P, P, I, I, I, I, P, I, P, P, P, P, P, P, P, P, P]),
     "scd_focal_fwd": (I, [P, P, L, P, P, P]),
     "scd_l1_gather_fwd": (I, [P, I, I, I, P, P, P, I, I, I, P, P, P]),
     "scd_centernet_loss_finalize": (I, [P, I, P, I, P, P, P, P]),

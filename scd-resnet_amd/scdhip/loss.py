@@ -47,6 +47,8 @@ class CenterNetLossFn(torch.autograd.Function):
         L.call("scd_centernet_loss_finalize", ops.ptr(facc), 1, ops.ptr(lacc), 2, wts, ops.ptr(out),
                ops.ptr(factors), s)
         ctx.save_for_backward(g_heat, g_regr, g_off, factors)
+        ctx.inds = inds
+        ops.clear_sparse_grads()          # a new loss: earlier certificates are consumed or stale
         loss = out[0:1]
         stats = out[1:4]
         ctx.mark_non_differentiable(stats)
@@ -59,6 +61,8 @@ class CenterNetLossFn(torch.autograd.Function):
         s = ops.stream()
         for i, g in enumerate((g_heat, g_regr, g_off)):
             L.call("scd_scale_by_device", ops.ptr(g), g.numel(), ops.ptr(factors), i, ops.ptr(gl), s)
+        # the L1 terms reach the size / offset outputs only at the gathered pixels (g_regr, g_off share one buffer)
+        ops.certify_sparse_grad(g_regr, ctx.inds)
         return g_heat, g_regr, g_off, None, None, None, None, None, None
 
 

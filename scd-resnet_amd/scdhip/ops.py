@@ -547,6 +547,60 @@ def clear_bn_fusion():
     _BN_PRODUCER.clear()
 
 
+# ------------------------------------------------------------------ sparse head-output gradients
+#
+# CenterNetLoss trains the regression / offset heads through L1LossMask on gather(head, inds) only
+# (centerNetOffset.py:199-214): the gradient it hands back for those outputs is zero outside the gathered pixels.
+# CenterNetLossFn.backward certifies that here (the gradient buffer, its version, the index tensor); HeadsFn.backward
+# then runs those heads' backward over the certified pixels (scd_heads_sparse_bwd / _fixup) instead of dense GEMMs.
+# The entry holds the buffer, so its storage cannot be reused while registered; a gradient that autograd summed,
+# copied or that was modified in place (other storage / version) does not match and takes the dense path.
+
+class SparseHeads:
+    enabled = os.environ.get("SCD_SPARSE_HEADS", "1") != "0"
+
+
+_SPARSE_GRAD = {}
+
+
+def certify_sparse_grad(buf, inds):
+    """`buf` (and its views) is zero outside the pixels inds[b][k] of each image (inds: (N, K) int64)."""
+    if SparseHeads.enabled:
+        _SPARSE_GRAD[buf.untyped_storage().data_ptr()] = (buf, buf._version, inds)
+
+
+def clear_sparse_grads():
+    _SPARSE_GRAD.clear()
+
+
+def sparse_grad_inds(g):
+    """The certified index tensor of gradient `g`, or None."""
+    if g is None or not _SPARSE_GRAD:
+        return None
+    e = _SPARSE_GRAD.get(g.untyped_storage().data_ptr())
+    if e is None:
+        return None
+    buf, ver, inds = e
+    if buf._version != ver or g._version != ver:
+        return None
+    return inds
+
+
+_SPARSE_MAPS = {}
+
+
+def sparse_maps(dev, npix):
+    """Persistent pixel maps of the sparse heads backward (slot map -1, owner map INT_MAX; the kernels restore
+    them after every use)."""
+    key = (str(dev), npix)
+    m = _SPARSE_MAPS.get(key)
+    if m is None:
+        m = (torch.full((npix,), -1, dtype=torch.int32, device=dev),
+             torch.full((npix,), 0x7fffffff, dtype=torch.int32, device=dev))
+        _SPARSE_MAPS[key] = m
+    return m
+
+
 # ------------------------------------------------------------------ weight gradients on a side stream
 #
 # Inside a backward pass the weight-gradient GEMMs (+ their split reductions) only feed the optimizer (and
