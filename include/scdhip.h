@@ -106,7 +106,8 @@ int scd_wgrad_reduce_rows(const float* ws, int nsplit, int Cg, int T, int Ci, in
 
 /* Pack an fp32 (A, B, T) weight (OIHW / IOHW flattening) into the GEMM operand layout:
  * mode 0: out[row_off + a][t*B + b] = w[a][b][t]; mode 1: out[row_off + b][t*A + a] = w[a][b][t];
- * rows are ldp elements long (zero padded). */
+ * rows are ldp elements long (zero padded).  mode 2 (tap-major transpose): out[t*B + b][row_off + a] = w[a][b][t],
+ * T*B rows of ldp elements of which only [row_off, row_off + A) are written (one slice of a concatenation). */
 int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp,
                     int row_off, void* stream);
 
@@ -121,7 +122,8 @@ int scd_pad_channels(int dtype, const void* src, long rows, int C, int Cp, void*
  * mode 0: out[row_off + a][t*B + b] = w[a][b][t], count = A * ldp (k >= T*B zero-filled);
  * mode 1: out[b][t*a_tot + a_off + a] = w[a][b][t] (a slice of a concatenated operand when a_tot > A),
  * transposed through LDS in tiles of 64 a x max(1, 64/T) b (T <= 64), one 4096-element unit per tile:
- * count = 4096 * ceil(A/64) * ceil(B / max(1, 64/T)).  Every start (and total) is a multiple of 4096.
+ * count = 4096 * ceil(A/64) * ceil(B / max(1, 64/T)); mode 2: out[t*B + b][a_off + a] = w[a][b][t] (ldp = a_tot),
+ * count = A * B * T.  Every start (and total) is a multiple of 4096.
  * Replaces one scd_pack_weight launch per conv and direction. */
 typedef struct scd_pack_desc {
     const float* w;
@@ -245,10 +247,10 @@ int scd_heads_bwd_packed_split(int dtype, const void* hid, int N, int HW, int nh
  * regression / offset terminals under L1LossMask(gather(out, inds), ..., mask) (centerNetOffset.py:199-214,
  * regression.py:37-44; utility.py:76-85 gather).  Slot s = b*K + k; the first slot naming a pixel is active.
  * scd_heads_sparse_bwd: dhid_s[s][(nh-nd)*Hd] = relu'(hid) * W1^T g (zero rows for inactive slots),
- * xcol[s][Cin*9] = the slot pixel's 3x3 patch of feat (ci-major, tap-minor: an OIHW weight-gradient row), the
+ * xcol[s][t*Cin + ci] = the slot pixel's 3x3 patch of feat (tap-major; zeros outside the image), the
  * heads' dW1/db1/db0 into acc (scd_heads_bwd_weight_finalize), slotmap[pixel] = s, ownermap[q] = min(s*9 + t)
  * over the (slot, tap) pairs reaching q.  scd_heads_sparse_fixup: dx[q] += sum over taps t of
- * cols[slot(q - d_t)][ci*9 + t] (cols = dhid_s x W0^T, the 3x3 conv's transposed weight as a [Cin*9][Cs] GEMM
+ * cols[slot(q - d_t)][t*Cin + ci] (cols = dhid_s x W0^T, the 3x3 conv's weight packed tap-major as a [9*Cin][Cs] GEMM
  * operand) at every reached q, with the following BN+ReLU layer's backward sums corrected when bn_y != NULL
  * (scd_conv_gemm_bnbwd's definition); both maps are restored (slotmap = -1, ownermap = INT_MAX: persistent
  * int32[N*H*W] buffers initialised once).  (nh-nd)*Hd <= 256, Cin <= 256. */

@@ -10,7 +10,7 @@ namespace {
 // ---------------------------------------------------------------- weight packing
 template <typename T>
 __global__ void pack_weight_kernel(const float* w, T* out, int A, int B, int Tt, int mode, int ldp, int row_off) {
-    const int rows = mode == 0 ? A : B;
+    const int rows = mode == 0 ? A : mode == 1 ? B : Tt * B;
     const unsigned total = (unsigned)rows * ldp;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
         const int r = (int)(i / (unsigned)ldp);
@@ -19,9 +19,14 @@ __global__ void pack_weight_kernel(const float* w, T* out, int A, int B, int Tt,
         if (mode == 0) {        // out[a][t*B+b] = w[a][b][t]
             const int t = k / B, b = k - (k / B) * B;
             if (t < Tt) v = w[((long)r * B + b) * Tt + t];
-        } else {                // out[b][t*A+a] = w[a][b][t]
+        } else if (mode == 1) { // out[b][t*A+a] = w[a][b][t]
             const int t = k / A, a = k - (k / A) * A;
             if (t < Tt) v = w[((long)a * B + r) * Tt + t];
+        } else {                // out[t*B+b][a] = w[a][b][t]: columns k >= A belong to other operands (row_off = a offset)
+            if (k >= A) continue;
+            const int t = r / B, b = r - (r / B) * B;
+            out[(long)r * ldp + row_off + k] = from_f<T>(w[((long)k * B + b) * Tt + t]);
+            continue;
         }
         out[(long)(row_off + r) * ldp + k] = from_f<T>(v);
     }
@@ -70,7 +75,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
         return;
     }
     // 32-bit index math (a descriptor holds < 2^31 elements; 64-bit divides dominated this kernel)
-    const unsigned count = q.mode == 0 ? (unsigned)q.A * q.ldp : (unsigned)q.B * q.T * q.A;
+    const unsigned count = q.mode == 0 ? (unsigned)q.A * q.ldp : (unsigned)q.B * q.T * q.A;   // mode 1 / 2: B x T x A
     const unsigned base = (unsigned)(e0 - q.start);
     const unsigned ldp = q.ldp, B = q.B, Tt = q.T, A = q.A, TA = Tt * A;
 #pragma unroll 4
@@ -84,11 +89,17 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
             const unsigned t = k / B, b = k - t * B;
             v = t < Tt ? q.w[(r * B + b) * Tt + t] : 0.f;
             o = (q.row_off + r) * ldp + k;
-        } else {                      // out[b][t*a_tot + a_off + a] = w[a][b][t]  (B x T x A elements)
+        } else if (q.mode == 1) {     // out[b][t*a_tot + a_off + a] = w[a][b][t]  (B x T x A elements)
             const unsigned r = i / TA, rem = i - r * TA;
             const unsigned t = rem / A, a = rem - t * A;
             v = q.w[(a * B + r) * Tt + t];
             o = r * ldp + t * q.a_tot + q.a_off + a;
+        } else {                      // out[t*B + b][a_off + a] = w[a][b][t]  (T x B x A elements, ldp = a_tot)
+            const unsigned BA = B * A;
+            const unsigned t = i / BA, rem = i - t * BA;
+            const unsigned b = rem / A, a = rem - b * A;
+            v = q.w[(a * B + b) * Tt + t];
+            o = (t * B + b) * ldp + q.a_off + a;
         }
         if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
         else ((float*)q.out)[o] = v;
@@ -923,8 +934,8 @@ extern "C" int scd_heads_bwd_packed_split(int dtype, const void* hid, int N, int
 // input gradient reduce to sums over that pixel set (slots s = b*K + k; the first slot naming a pixel carries it,
 // repeats carry nothing, so a pixel named twice is counted once with its summed gradient):
 //   dhid_s[s][c]         = relu'(hid) * sum_o W1[o][c] g[o]           (heads [nd, nh), c over their channels)
-//   xcol[s][ci*9 + t]    = feat[p + d_t][ci]                           (im2col of the slot's pixel)
-//   dW0 = dhid_s^T xcol, and dX[q] += sum_{t : q - d_t active} C[slot(q - d_t)][ci*9 + t], C = dhid_s W0^T
+//   xcol[s][t*Cin + ci]  = feat[p + d_t][ci]                           (im2col of the slot's pixel, tap-major)
+//   dW0 = dhid_s^T xcol, and dX[q] += sum_{t : q - d_t active} C[slot(q - d_t)][t*Cin + ci], C = dhid_s W0^T
 // The dense heads [0, nd) keep the dense tail (scd_heads_bwd_packed_split) and GEMMs over their channels only.
 // slotmap (pixel -> slot, -1 elsewhere) and ownermap (q -> first (slot, tap) reaching q, INT_MAX elsewhere) are
 // persistent int32 maps over the N*H*W pixels; the kernels below leave them as they found them.
@@ -950,12 +961,22 @@ __global__ __launch_bounds__(256) void heads_sparse_bwd_kernel(const T* hid, con
     float a_dw1[4] = {0.f, 0.f, 0.f, 0.f}, a_db1[4] = {0.f, 0.f, 0.f, 0.f}, a_db0 = 0.f;
     const int S = N * K;
     const int s0 = blockIdx.x * SP_SPB;
-    const int KC = Cin * 9;
-    for (int s = s0; s < min(S, s0 + SP_SPB); ++s) {
-        const int b = s / K, k = s - (s / K) * K;
+    const int ns = min(S, s0 + SP_SPB) - s0;
+    // which of the workgroup's slots repeat an earlier slot's pixel of the same image (all pairs in parallel)
+    __shared__ int dup[SP_SPB];
+    if (tid < SP_SPB) dup[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < ns * K; i += blockDim.x) {
+        const int jj = i / K, k2 = i - (i / K) * K;
+        const int s = s0 + jj, k = s - (s / K) * K;
+        if (k2 < k && inds[s - k + k2] == inds[s]) dup[jj] = 1;
+    }
+    __syncthreads();
+    for (int jj = 0; jj < ns; ++jj) {
+        const int s = s0 + jj;
+        const int b = s / K;
         const long ind = inds[s];
-        bool active = ind >= 0 && ind < HW;
-        for (int k2 = 0; k2 < k && active; ++k2) active = inds[(long)b * K + k2] != ind;
+        const bool active = ind >= 0 && ind < HW && !dup[jj];
         const int q0 = active ? (int)ind : 0;
         const int y = q0 / W, x = q0 - (q0 / W) * W;
         const long p = (long)b * HW + q0;
@@ -972,20 +993,23 @@ __global__ __launch_bounds__(256) void heads_sparse_bwd_kernel(const T* hid, con
             a_db0 += r;
         }
         if (cok) dhid_s[(long)s * Cs + c] = from_f<T>(r);
-        if (active && tid == 0) {
-            slotmap[p] = s;
-            for (int t = 0; t < 9; ++t) {
-                const int qy = y + t / 3 - 1, qx = x + t % 3 - 1;
-                if ((unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W)
-                    atomicMin(ownermap + (long)b * HW + qy * W + qx, s * 9 + t);
-            }
+        if (active && tid < 9) {
+            if (tid == 0) slotmap[p] = s;
+            const int qy = y + tid / 3 - 1, qx = x + tid % 3 - 1;
+            if ((unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W)
+                atomicMin(ownermap + (long)b * HW + qy * W + qx, s * 9 + tid);
         }
-        // im2col row of the slot (its pixel's 3x3 x Cin patch, zeros outside the image), ci-major, tap-minor
-        for (int i = tid; i < KC; i += blockDim.x) {
-            const int ci = i / 9, t = i - (i / 9) * 9;
-            const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
-            const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-            xcol[(long)s * KC + i] = in ? feat[(((long)b * H + iy) * W + ix) * Cin + ci] : from_f<T>(0.f);
+        // im2col row of the slot, tap-major (xcol[s][t*Cin + ci]; zeros outside the image): coalesced rows of feat
+        for (int ci = tid; ci < Cin; ci += blockDim.x) {
+            T v[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+                const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+                v[t] = in ? feat[(((long)b * H + iy) * W + ix) * Cin + ci] : from_f<T>(0.f);
+            }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) xcol[(long)s * 9 * Cin + t * Cin + ci] = v[t];
         }
     }
     // weight / bias partials of the sparse heads (same accumulator layout as heads_bwd_kernel)
@@ -1004,8 +1028,9 @@ __global__ __launch_bounds__(256) void heads_sparse_bwd_kernel(const T* hid, con
 
 // dX[q] += the sparse heads' input-gradient at the pixels q their slots reach; one workgroup per slot, one
 // thread per input channel; q is handled by the first (slot, tap) reaching it (ownermap), which sums the
-// contributions of every active neighbour in tap order.  With bn_y: the following BN+ReLU layer's backward sums
-// (scd_conv_gemm_bnbwd's epilogue over the dense part) get the change of each rewritten value.
+// contributions of every active neighbour in tap order (cols[s][t*Cin + ci], tap-major).  The slot maps of the
+// 5x5 neighbourhood and the owners of the 3x3 reach are read once into LDS.  With bn_y: the following BN+ReLU
+// layer's backward sums (scd_conv_gemm_bnbwd's epilogue over the dense part) get the change of each rewritten value.
 template <typename T>
 __global__ __launch_bounds__(256) void heads_sparse_fixup_kernel(T* dx, const T* cols, int N, int H, int W, int Cin,
                                                                  const long* inds, int K, const int* slotmap,
@@ -1020,43 +1045,50 @@ __global__ __launch_bounds__(256) void heads_sparse_fixup_kernel(T* dx, const T*
     const long p = (long)b * HW + ind;
     if (slotmap[p] != s) return;                       // a repeat of an earlier slot's pixel
     const int y = (int)ind / W, x = (int)ind - ((int)ind / W) * W;
-    const int ci = threadIdx.x;
-    const bool cok = ci < Cin;
-    const int KC = Cin * 9;
-    float bm = 0.f, bi = 0.f, bs = 0.f, bh = 0.f;
-    if (bny && cok) { bm = mean[ci]; bi = invstd[ci]; bs = rsc[ci]; bh = rsh[ci]; }
-    float dsum = 0.f, dsq = 0.f;
-    for (int t = 0; t < 9; ++t) {
+    const int tid = threadIdx.x;
+    __shared__ int nb[25], own[9];
+    if (tid < 25) {
+        const int py = y + tid / 5 - 2, px = x + tid % 5 - 2;
+        nb[tid] = ((unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W) ? slotmap[(long)b * HW + py * W + px] : -1;
+    } else if (tid >= 32 && tid < 41) {
+        const int t = tid - 32;
         const int qy = y + t / 3 - 1, qx = x + t % 3 - 1;
-        if ((unsigned)qy >= (unsigned)H || (unsigned)qx >= (unsigned)W) continue;
-        const long qi = (long)b * HW + qy * W + qx;
-        const int own = ownermap[qi];
-        __syncthreads();                                // every thread has read the owner before it is reset
-        if (own != s * 9 + t) continue;
-        if (threadIdx.x == 0) ownermap[qi] = 0x7fffffff;
-        if (!cok) continue;
-        float corr = 0.f;
-        for (int t2 = 0; t2 < 9; ++t2) {
-            const int py = qy - (t2 / 3 - 1), px = qx - (t2 % 3 - 1);
-            if ((unsigned)py >= (unsigned)H || (unsigned)px >= (unsigned)W) continue;
-            const int s2 = slotmap[(long)b * HW + py * W + px];
-            if (s2 >= 0) corr += to_f<T>(cols[(long)s2 * KC + ci * 9 + t2]);
-        }
-        T* dp = dx + qi * Cin + ci;
-        const T old = *dp;
-        const T nv = from_f<T>(to_f<T>(old) + corr);
-        *dp = nv;
-        if (bny) {
-            const float yv = to_f<T>(bny[qi * Cin + ci]);
-            const float dd = yv * bs + bh > 0.f ? to_f<T>(nv) - to_f<T>(old) : 0.f;
-            dsum += dd;
-            dsq += dd * (yv - bm) * bi;
-        }
+        own[t] = ((unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W) ? ownermap[(long)b * HW + qy * W + qx] : -1;
     }
-    if (bny && cok) {
-        const int rep = s % SCD_STAT_REPLICAS;
-        atomic_add_f64(stats + ((long)rep * 2 + 0) * Cin + ci, (double)dsum);
-        atomic_add_f64(stats + ((long)rep * 2 + 1) * Cin + ci, (double)dsq);
+    __syncthreads();
+    if (tid < 9 && own[tid] == s * 9 + tid)          // restore the owner map (every read above is done)
+        ownermap[(long)b * HW + (y + tid / 3 - 1) * W + x + tid % 3 - 1] = 0x7fffffff;
+    const long KC = 9L * Cin;
+    for (int ci = tid; ci < Cin; ci += blockDim.x) {
+        float bm = 0.f, bi = 0.f, bs = 0.f, bh = 0.f;
+        if (bny) { bm = mean[ci]; bi = invstd[ci]; bs = rsc[ci]; bh = rsh[ci]; }
+        float dsum = 0.f, dsq = 0.f;
+        for (int t = 0; t < 9; ++t) {
+            if (own[t] != s * 9 + t) continue;
+            const int oy = t / 3 - 1, ox = t % 3 - 1;    // q - p
+            float corr = 0.f;
+#pragma unroll
+            for (int t2 = 0; t2 < 9; ++t2) {
+                const int s2 = nb[(oy - (t2 / 3 - 1) + 2) * 5 + ox - (t2 % 3 - 1) + 2];
+                if (s2 >= 0) corr += to_f<T>(cols[(long)s2 * KC + t2 * Cin + ci]);
+            }
+            const long qi = p + oy * W + ox;
+            T* dp = dx + qi * Cin + ci;
+            const T old = *dp;
+            const T nv = from_f<T>(to_f<T>(old) + corr);
+            *dp = nv;
+            if (bny) {
+                const float yv = to_f<T>(bny[qi * Cin + ci]);
+                const float dd = yv * bs + bh > 0.f ? to_f<T>(nv) - to_f<T>(old) : 0.f;
+                dsum += dd;
+                dsq += dd * (yv - bm) * bi;
+            }
+        }
+        if (bny) {
+            const int rep = s % SCD_STAT_REPLICAS;
+            atomic_add_f64(stats + ((long)rep * 2 + 0) * Cin + ci, (double)dsum);
+            atomic_add_f64(stats + ((long)rep * 2 + 1) * Cin + ci, (double)dsq);
+        }
     }
 }
 
@@ -1104,7 +1136,7 @@ extern "C" int scd_heads_sparse_fixup(int dtype, void* dx, const void* cols, int
                                       const float* relu_shift, double* bn_stats, void* stream) {
     SCD_F16_FWD(scd_heads_sparse_fixup, dx, cols, N, H, W, Cin, inds, K, slotmap, ownermap, bn_y, mean, invstd,
                 relu_scale, relu_shift, bn_stats, stream);
-    if (Cin < 1 || Cin > 256 || K < 1) return SCD_ERR_ARG;
+    if (Cin < 1 || K < 1) return SCD_ERR_ARG;
     if (bn_y && !(mean && invstd && relu_scale && relu_shift && bn_stats)) return SCD_ERR_ARG;
     const int S = N * K;
     hipStream_t st = (hipStream_t)stream;

@@ -13,6 +13,8 @@ Parameter gradients are accumulated straight into ``param.grad`` (created on dem
 with FlatAdam/FlatDDP they are views of one flat buffer), so the Functions return None
 for parameter inputs.  Activations between Functions are NHWC in the model's compute dtype.
 """
+import os
+
 import torch
 
 from . import ops
@@ -283,6 +285,9 @@ class ConvBNFn(torch.autograd.Function):
         return dx, None, None, None, None
 
 
+_HEADS_WGRAD_LATE = os.environ.get("SCD_HEADS_WGRAD_LATE", "1") == "1"
+
+
 class HeadsFn(torch.autograd.Function):
     """All CenterNet terminals (Conv2d 3x3 +bias -> ReLU -> Conv2d 1x1 +bias) fused:
     hidden = relu(conv3x3(feat, W0cat) + b0cat) with N = sum of hidden widths, then the
@@ -406,17 +411,23 @@ class HeadsFn(torch.autograd.Function):
         # weight gradients: dense heads over every pixel, sparse heads over the slots' im2col rows (a 1x1 GEMM whose
         # Cin*9 columns are the OIHW rows of their 3x3 weights)
         ld = (Cin * 9, 9, 1)
-        ops.conv_wgrad(dh_dense, feat, 3, 3, 1, 1, None, None,
-                       rows=[(i * Hd, (i + 1) * Hd, ops.grad_of(heads[i][0].weight), ld) for i in range(nd)])
-        ops.conv_wgrad(dhid_s.view(1, 1, Sl, Cs), xcol.view(1, 1, Sl, Cin * 9), 1, 1, 1, 0, None, None,
-                       rows=[((i - nd) * Hd, (i - nd + 1) * Hd, ops.grad_of(heads[i][0].weight), (Cin * 9, 1, 1))
-                             for i in range(nd, nh)])
+
+        def wgrads():
+            ops.conv_wgrad(dh_dense, feat, 3, 3, 1, 1, None, None,
+                           rows=[(i * Hd, (i + 1) * Hd, ops.grad_of(heads[i][0].weight), ld) for i in range(nd)])
+            # (a 1x1 GEMM over the slots; its 9*Cin columns are reduced as 9 taps x Cin into the OIHW rows)
+            ops.conv_wgrad(dhid_s.view(1, 1, Sl, Cs), xcol.view(1, 1, Sl, 9 * Cin), 1, 1, 1, 0, None, None,
+                           rows=[((i - nd) * Hd, (i - nd + 1) * Hd, ops.grad_of(heads[i][0].weight), ld)
+                                 for i in range(nd, nh)], red_taps=9)
+        late = _HEADS_WGRAD_LATE
+        if not late:
+            wgrads()
         # input gradient: dense heads' GEMM (+ the deconv BN's backward sums), then the sparse heads' part
         fuse = ctx.prod is not None and dt in ops.HALF
         bn_args = ops.fused_bn_bwd_args(ctx.prod) if fuse else None
         dfeat = ops.conv_dgrad(dh_dense, ops.pack_concat(w0s[:nd], dt, 1), Cin, H, W, 3, 3, 1, 1, bn_bwd=bn_args)
-        wt_s = ops.pack_concat(w0s[nd:], dt, 1).view(Cin * 9, Cs)     # [ci][tap][c] rows: W0^T of the sparse heads
-        cols = ops.conv_fwd(dhid_s.view(1, 1, Sl, Cs), wt_s, Cin * 9, 1, 1, 1, 0)
+        wt_s = ops.pack_concat(w0s[nd:], dt, 2)          # [tap][ci][c] rows: W0^T of the sparse heads, tap-major
+        cols = ops.conv_fwd(dhid_s.view(1, 1, Sl, Cs), wt_s, 9 * Cin, 1, 1, 1, 0)
         if fuse:
             st, ybn, bstats = bn_args
             bn_ptrs = (ops.ptr(ybn), ops.ptr(st.mean), ops.ptr(st.invstd), ops.ptr(st.scale), ops.ptr(st.shift),
@@ -425,6 +436,8 @@ class HeadsFn(torch.autograd.Function):
             bn_ptrs = (None,) * 6
         ops.L.call("scd_heads_sparse_fixup", ops.dt(dfeat), ops.ptr(dfeat), ops.ptr(cols), N, H, W, Cin, ops.ptr(inds),
                    K, ops.ptr(slotmap), ops.ptr(ownermap), *bn_ptrs, ops.stream())
+        if late:
+            wgrads()             # side stream ordered after the input gradient: it overlaps the deconv backward
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
         grads_ready(*[m for h in heads for m in h if isinstance(m, torch.nn.Module)])

@@ -290,6 +290,8 @@ class PackPlan:
                         descs.append(d)
                         if mode == 0:
                             start += (A * ldp + 4095) // 4096 * 4096      # whole workgroup units per descriptor
+                        elif mode == 2:
+                            start += (A * B * T + 4095) // 4096 * 4096
                         else:
                             # one 4096-element unit per 64 x max(1, 64 // T) transpose tile (scd_pack_desc)
                             bb = max(1, 64 // T)
@@ -338,6 +340,14 @@ def pack_concat(ws, dtype, mode):
         for w in ws:
             parts.append((w, 0, T * B, off, 0, 0))
             pack_weight(w, dtype, 0, out=out, row_off=off, _cache=False)
+            off += w.shape[0]
+    elif mode == 2:
+        # [taps][B][A_tot]: the transposed weight with tap-major rows (scd_heads_sparse_fixup's operand)
+        out = torch.empty(T * B, A_tot, dtype=dtype, device=ws[0].device)
+        parts, off = [], 0
+        for w in ws:
+            parts.append((w, 2, A_tot, 0, off, A_tot))
+            L.call("scd_pack_weight", _DT[dtype], ptr(w), ptr(out), w.shape[0], B, T, 2, A_tot, off, stream())
             off += w.shape[0]
     else:
         cat = torch.cat(list(ws), 0)
@@ -442,9 +452,11 @@ def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, sta
         L.call("scd_conv_gemm_bnbwd", dt(x), ptr(x), ptr(wpack), ptr(y), N, Hi, Wi, Ci, Ho, Wo, Co, in_stride,
                out_stride, wpack.shape[1], len(phases), arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
                ptr(st.shift), ptr(bstats), stream())
+        flush_deferred_wgrads()
         return y
     L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
            in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr, stream())
+    flush_deferred_wgrads()
     return y
 
 
@@ -661,6 +673,7 @@ def _new_side_stream(idx):
 
 def join_side_streams():
     """Make every device's compute stream wait for its side stream (end of backward)."""
+    flush_deferred_wgrads()
     for idx, s in _Side.streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
     _Side.joined_task.clear()
@@ -669,6 +682,7 @@ def join_side_streams():
 def side_stream_for_comm(dev):
     """For a collective launched during backward: the side stream (if any), first ordered after the compute
     stream, so that a collective issued from it sees every gradient written on either stream so far."""
+    flush_deferred_wgrads()
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _Side.streams.get(idx)
     if s is None or _graph_task() == -1:
@@ -677,17 +691,38 @@ def side_stream_for_comm(dev):
     return s
 
 
-def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None):
+# SCD_WGRAD_DEFER=1: a weight gradient issued during backward is queued and put on the side stream right after the
+# next input-gradient GEMM of the compute stream (flushed before any collective and at the end of backward), so it
+# overlaps that layer's BN backward and the next layer instead of competing with the GEMM for every CU.
+_WGRAD_DEFER = os.environ.get("SCD_WGRAD_DEFER", "0") == "1"
+_DEFERRED = []
+
+
+def flush_deferred_wgrads():
+    while _DEFERRED:
+        _DEFERRED.pop(0)()
+
+
+def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None, red_taps=1):
+    if _WGRAD_DEFER and g.is_cuda and _Side.enabled and _graph_task() != -1:
+        side_stream(g.device)             # registers the end-of-backward join (which flushes the queue)
+        _DEFERRED.append(lambda: _conv_wgrad_side(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows,
+                                                  red_taps))
+        return
+    _conv_wgrad_side(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows, red_taps)
+
+
+def _conv_wgrad_side(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None, red_taps=1):
     side = side_stream(g.device) if g.is_cuda else None
     if side is None:
-        return _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows)
+        return _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows, red_taps)
     with torch.cuda.stream(side):
-        _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows)
+        _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows, red_taps)
     g.record_stream(side)
     x.record_stream(side)
 
 
-def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None):
+def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None, red_taps=1):
     """Weight gradient of the gather-GEMM: dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= sum_pix g[pix,r] x[gather,ci].
 
     g: (N,Ho,Wo,Cg) NHWC output-gradient; x: (N,Hi,Wi,Ci) NHWC input; taps gather
@@ -705,10 +740,13 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
            stream())
     if rows is None:
         rows = [(0, Cg, dst, ld)]
-    cv = Ci if cvalid is None else cvalid
+    # red_taps: read the T*Ci workspace columns as red_taps taps of T*Ci/red_taps channels (a 1x1 GEMM over
+    # im2col rows, whose columns are the taps of a wider convolution)
+    Tr, Cr = T * red_taps, Ci // red_taps
+    cv = Cr if cvalid is None else cvalid
     for i in range(0, len(rows), 4):      # up to four row slices per reduce launch
         part = rows[i:i + 4]
-        L.call("scd_wgrad_reduce_rows", ptr(ws), ns, Cg, T, Ci, len(part), L.int_array([r[0] for r in part]),
+        L.call("scd_wgrad_reduce_rows", ptr(ws), ns, Cg, Tr, Cr, len(part), L.int_array([r[0] for r in part]),
                L.int_array([r[1] for r in part]), L.long_array([r[3][0] for r in part]),
                L.long_array([r[3][1] for r in part]), L.long_array([r[3][2] for r in part]),
                L.ptr_array([ptr(r[2]) for r in part]), cv, int(accumulate), grad_alpha(g), stream())

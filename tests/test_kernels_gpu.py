@@ -429,8 +429,9 @@ def test_adam_device_state_matches_torch():
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_batched_pack_matches_single(dtype):
-    """PackPlan's one-launch batched packing (mode 0 rows, mode 1 LDS-tiled transposes, concatenated head
-    operands) reproduces the per-weight scd_pack_weight layouts bit for bit."""
+    """PackPlan's one-launch batched packing (mode 0 rows, mode 1 LDS-tiled transposes, mode 2 tap-major
+    transposes, concatenated head operands) reproduces the per-weight scd_pack_weight layouts bit for bit, and
+    mode 2 is out[t*B + b][a] = w[a][b][t]."""
     from scdhip import ops
     g = torch.Generator().manual_seed(12)
     shapes = [(64, 64, 3, 3), (128, 64, 3, 3), (128, 64, 1, 1), (512, 256, 3, 3), (256, 256, 4, 4), (64, 1, 7, 7),
@@ -440,7 +441,8 @@ def test_batched_pack_matches_single(dtype):
     plan = ops.PackPlan()
     ops.pack_begin(plan)                       # first step: records and packs on demand
     first = [ops.pack_weight(w, dtype, m) for w in ws for m in (0, 1)]
-    first += [ops.pack_concat(heads, dtype, m) for m in (0, 1)]
+    first += [ops.pack_concat(heads, dtype, m) for m in (0, 1, 2)]
+    first += [ops.pack_concat(heads[1:], dtype, 2)]
     first = [f.clone() for f in first]
     ops.pack_end()
     # scribble over the cached operands, then repack everything in one batched launch
@@ -448,11 +450,15 @@ def test_batched_pack_matches_single(dtype):
         e[0].fill_(float("nan"))
     ops.pack_begin(plan)
     again = [ops.pack_weight(w, dtype, m) for w in ws for m in (0, 1)]
-    again += [ops.pack_concat(heads, dtype, m) for m in (0, 1)]
+    again += [ops.pack_concat(heads, dtype, m) for m in (0, 1, 2)]
+    again += [ops.pack_concat(heads[1:], dtype, 2)]
     torch.cuda.synchronize()
     ops.pack_end()
     for a, b in zip(first, again):
         assert torch.equal(a, b)
+    cat = torch.cat([h.detach() for h in heads[1:]], 0)                     # (A=256, B=256, 3, 3)
+    want = cat.reshape(256, 256, 9).permute(2, 1, 0).reshape(9 * 256, 256).to(dtype)
+    assert torch.equal(first[-1], want)
 
 
 def _pp_taken(N, phases, Cout):
