@@ -101,6 +101,25 @@ def train_gflop_per_img(model, S):
     return 3.0 * tot / 1e9
 
 
+def sparse_heads_saved_gflop(model, S, ys):
+    """Per image: the dense 3x3 dgrad + wgrad FLOPs of the size / offset terminals (centerNetOffset.py:106-110) that
+    the sparse-support backward does not execute, minus what it runs instead (2 GEMMs of slots x 128 x 9*Cin per
+    head); 0 when the path is switched off (SCD_SPARSE_HEADS=0)."""
+    from scdhip import ops
+    if not ops.SparseHeads.enabled:
+        return 0.0
+    K = ys[3].shape[1]
+    h = S // 4
+    saved = 0.0
+    for name in ("regr", "offset"):
+        m = getattr(model, name, None)
+        if m is None:
+            continue
+        co, ci, kh, kw = m[0].weight.shape
+        saved += 2 * 2.0 * co * ci * kh * kw * (h * h - K)
+    return saved / 1e9
+
+
 def pmc_traffic(kernel, batch, dtype):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/r<N>_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
@@ -362,8 +381,12 @@ def main():
         core = model.module if hasattr(model, "module") else model
         gflop = TRAIN_GFLOP_PER_IMG if (args.model == "centerOffsetRes10" and S == 512) else \
             train_gflop_per_img(core, S)
-        step_frac = value * gflop / 1e3 / (world * (PEAK_F32_TFLOPS if dtype == torch.float32
-                                                    else PEAK_BF16_TFLOPS))
+        # the size / offset heads' backward runs over the loss's gathered pixels (scdhip.blocks.HeadsFn sparse
+        # path): their dense 3x3 dgrad + wgrad FLOPs are not executed, a [slots x Cs] x [Cs x 9 Cin] GEMM pair is
+        gsaved = sparse_heads_saved_gflop(core, S, ys) if args.model.startswith("centerOffset") else 0.0
+        executed = gflop - gsaved
+        peak = world * (PEAK_F32_TFLOPS if dtype == torch.float32 else PEAK_BF16_TFLOPS)
+        step_frac = value * executed / 1e3 / peak
         line = {
             "metric": "512x512 images/sec training, centerOffsetRes10, at 1/2/4/8 MI355X" if (
                 args.model == "centerOffsetRes10" and S == 512) else "%dx%d images/sec training, %s" % (S, S, args.model),
@@ -375,10 +398,12 @@ def main():
                                    "SCD tiles" % (args.model, S, S), "model": args.model, "global_batch": B * world,
                        "step_issue": "hip graph replay" if graph is not None else "eager launches",
                        "per_gpu_batch": B, "seq_len": None, "parallelism": "dp%d" % world,
-                       "image_size": S, "train_gflop_per_img": round(gflop, 3)},
+                       "image_size": S, "train_gflop_per_img": round(gflop, 3),
+                       "executed_gflop_per_img": round(executed, 3)},
             "roofline": roof,
             **extra,
             "step_mfma_frac": round(step_frac, 4),
+            "step_mfma_frac_dense_equiv": round(value * gflop / 1e3 / peak, 4),
             "final_loss": round(final_loss, 5),
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -5,6 +5,10 @@
 
 #include "scd_common.h"
 
+#ifndef BN_BWD_U
+#define BN_BWD_U 2
+#endif
+
 namespace {
 
 // sum replicas into replica 0 and zero the others (buffers are persistent: the consumer re-zeroes)
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const
                                                             const float* mean, const float* invstd, int C, int ld,
                                                             unsigned rows, unsigned rows_per_block, double* stats) {
     constexpr int E = Vec16<T>::N;
-    constexpr int U = 4;
+    constexpr int U = BN_BWD_U;
     constexpr int nt = 256;
     const int cpr = C / E;                     // chunks per row of this channel slice (divides 256)
     const int rpi = nt / cpr;                  // row lanes
@@ -167,26 +171,32 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const
             q[e] += dz * (yv[e] - mu[e]) * is[e];
         }
     };
+    // raw 16-B vectors (kept packed until used: fewer VGPRs, see bn_bwd_apply_kernel)
+    auto acc_raw = [&](const uint4& rd, const uint4& ry, const uint4& rm) {
+        float d[E], yv[E], mk[E];
+        Vec16<T>::load(&rd, d);
+        Vec16<T>::load(&ry, yv);
+        if (mask) Vec16<T>::load(&rm, mk);
+        acc(d, yv, mk);
+    };
     unsigned r = r0 + rsub;
     for (; r + (U - 1) * rpi < r1; r += U * rpi) {
-        float d[U][E], yv[U][E], mk[U][E];
+        uint4 rd[U], ry[U], rm[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const unsigned i = (r + u * rpi) * (unsigned)ld + ch * E;
-            Vec16<T>::load(dout + i, d[u]);
-            Vec16<T>::load(y + i, yv[u]);
-            if (mask) Vec16<T>::load(mask + i, mk[u]);
+            rd[u] = *(const uint4*)(dout + i);
+            ry[u] = *(const uint4*)(y + i);
+            rm[u] = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc(d[u], yv[u], mk[u]);
+        for (int u = 0; u < U; ++u) acc_raw(rd[u], ry[u], rm[u]);
     }
     for (; r < r1; r += rpi) {
-        float d[E], yv[E], mk[E];
         const unsigned i = r * (unsigned)ld + ch * E;
-        Vec16<T>::load(dout + i, d);
-        Vec16<T>::load(y + i, yv);
-        if (mask) Vec16<T>::load(mask + i, mk);
-        acc(d, yv, mk);
+        const uint4 rd = *(const uint4*)(dout + i), ry = *(const uint4*)(y + i);
+        const uint4 rm = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
+        acc_raw(rd, ry, rm);
     }
     // red[stat][rsub][channel]
 #pragma unroll
@@ -233,8 +243,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const 
                                                            const float* rsh, const float* coef, int C, unsigned nvec,
                                                            T* dy, T* dz_out) {
     constexpr int E = Vec16<T>::N;
-    constexpr int U = 4;
-    // fixed channel chunk per thread (see bn_apply_kernel): coefficients in registers; U vectors in flight
+    // BN_BWD_U vectors in flight, kept packed (16 B each) until used: <= 88 VGPRs, so the kernel's waves fit beside
+    // a one-workgroup-per-CU GEMM of the weight-gradient stream (2 x 212 of the 512 VGPRs per lane) instead of
+    // waiting for its workgroups to retire
+    constexpr int U = BN_BWD_U;
+    // fixed channel chunk per thread (see bn_apply_kernel): coefficients in registers
     const unsigned cpr = (unsigned)C / E;
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned stride = gridDim.x * blockDim.x;
@@ -248,8 +261,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const 
 #pragma unroll
         for (int e = 0; e < E; ++e) { ka[e] = 0.f; kb[e] = 0.f; }
     }
-    // d <- dz (masked gradient), yv <- dy
-    auto body = [&](float* d, float* yv, const float* mk) {
+    // raw 16-B vectors -> dz (masked gradient) and dy, stored
+    auto body = [&](size_t i, const uint4& rd, const uint4& ry, const uint4& rm) {
+        float d[E], yv[E], mk[E];
+        Vec16<T>::load(&rd, d);
+        Vec16<T>::load(&ry, yv);
+        if (mask) Vec16<T>::load(&rm, mk);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
@@ -257,34 +274,27 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const 
             d[e] = dz;
             yv[e] = ca[e] * dz + cb[e] * yv[e] + cc[e];
         }
+        Vec16<T>::store(dy + i, yv);
+        if (dz_out) Vec16<T>::store(dz_out + i, d);
     };
     unsigned v = v0;
     for (; v + (U - 1) * stride < nvec; v += U * stride) {
-        float d[U][E], yv[U][E], mk[U][E];
+        uint4 rd[U], ry[U], rm[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t i = (size_t)(v + u * stride) * E;
-            Vec16<T>::load(dout + i, d[u]);
-            Vec16<T>::load(y + i, yv[u]);
-            if (mask) Vec16<T>::load(mask + i, mk[u]);
+            rd[u] = *(const uint4*)(dout + i);
+            ry[u] = *(const uint4*)(y + i);
+            rm[u] = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const size_t i = (size_t)(v + u * stride) * E;
-            body(d[u], yv[u], mk[u]);
-            Vec16<T>::store(dy + i, yv[u]);
-            if (dz_out) Vec16<T>::store(dz_out + i, d[u]);
-        }
+        for (int u = 0; u < U; ++u) body((size_t)(v + u * stride) * E, rd[u], ry[u], rm[u]);
     }
     for (; v < nvec; v += stride) {
         const size_t i = (size_t)v * E;
-        float d[E], yv[E], mk[E];
-        Vec16<T>::load(dout + i, d);
-        Vec16<T>::load(y + i, yv);
-        if (mask) Vec16<T>::load(mask + i, mk);
-        body(d, yv, mk);
-        Vec16<T>::store(dy + i, yv);
-        if (dz_out) Vec16<T>::store(dz_out + i, d);
+        const uint4 rd = *(const uint4*)(dout + i), ry = *(const uint4*)(y + i);
+        const uint4 rm = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
+        body(i, rd, ry, rm);
     }
 }
 

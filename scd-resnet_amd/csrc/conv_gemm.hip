@@ -3163,6 +3163,14 @@ static bool wgrad_use_pp(int dtype, long M, int Cg, int KK) {
     return mode && dtype == SCD_DT_BF16 && Cg >= 128 && Cg % 128 == 0 && KK >= 128 && M >= 8 * 1024;
 }
 
+// SCD_WGRAD_LDS_PAD=<bytes>: extra dynamic LDS per workgroup of the register-staged weight-gradient kernel, so fewer
+// of its workgroups share a CU with the critical chain's kernels (experiment; 0 = off)
+static int wgrad_lds_pad() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("SCD_WGRAD_LDS_PAD"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
 static bool wgrad_fastx() {
     static int mode = -2;
     if (mode == -2) { const char* e = getenv("SCD_WGRAD_FASTX"); mode = e ? atoi(e) : 1; }
@@ -3351,26 +3359,27 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     } else if (dtype == SCD_DT_BF16 || dtype == SCD_DT_F32) {
         // fast addressing when a stage of KP pixels stays inside one image and one row block
         const int KP = dtype == SCD_DT_BF16 ? 64 : 32;
+        const int lpad = wgrad_lds_pad();
         const bool fastok = wgrad_fastx() && ((long)Ho * Wo) % KP == 0 && chunk % KP == 0;
         const int fx = !fastok ? 0 : (Wo % KP == 0 ? 1 : (KP % Wo == 0 ? 2 : 0));
         // (the 128 x 128 tile has registers for FASTX 1 only)
         if (dtype == SCD_DT_BF16) {
             if (Cg <= 64) {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
-                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), lpad, st, p);
+                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), lpad, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), lpad, st, p);
             } else {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), lpad, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), lpad, st, p);
             }
         } else {
             if (Cg <= 64) {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 1>), grid, dim3(256), 0, st, p);
-                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 2>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 0>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 1>), grid, dim3(256), lpad, st, p);
+                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 2>), grid, dim3(256), lpad, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 0>), grid, dim3(256), lpad, st, p);
             } else {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 1>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 0>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 1>), grid, dim3(256), lpad, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 0>), grid, dim3(256), lpad, st, p);
             }
         }
     } else {
