@@ -273,6 +273,20 @@ int scd_l1_gather_fwd(const float* feat, int N, int C, int HW, const int64_t* in
  * l1_acc after reading them (persistent accumulators: no memset before the next loss). */
 int scd_centernet_loss_finalize(double* focal_acc, int nfocal, double* l1_acc, int nl1,
                                 const float* l1_weights, float* out, float* factors, void* stream);
+/* CenterNetLoss (centerNetOffset.py:182-217) in two launches: the focal loss + gradient on the heatmap logits (as
+ * scd_focal_fwd) with the zero fill of the size / offset gradient buffer (g_off must follow g_regr in memory), then
+ * one workgroup for both masked L1 terms (regr: target channels toff_r.., off: toff_o.., as scd_l1_gather_fwd) and
+ * the finalize (as scd_centernet_loss_finalize with nfocal = 1, nl1 = 2: out = [loss, focal, size, offset],
+ * factors = the three backward scales; focal_acc re-zeroed).  scd_centernet_loss_bwd_scale: g_heat *= factors[0]*go;
+ * g_regr / g_off (zero except at the gathered pixels) scaled by factors[1] / factors[2]*go at those pixels only,
+ * each once. */
+int scd_centernet_loss_fwd(const float* heat, const float* gt, long n_heat, const float* regr, int Cr, const float* off,
+                           int Co, int N, int HW, const int64_t* inds, const uint8_t* mask, const float* target, int K,
+                           int tstride, int toff_r, int toff_o, const float* l1_weights, float* g_heat, float* g_regr,
+                           float* g_off, double* focal_acc, float* out, float* factors, void* stream);
+int scd_centernet_loss_bwd_scale(float* g_heat, long n_heat, int N, int HW, const int64_t* inds, int K, float* g_regr,
+                                 int Cr, float* g_off, int Co, const float* factors, const float* go, void* stream);
+
 /* g[i] *= factors[idx] * go[0]  (in place) */
 int scd_scale_by_device(float* g, long n, const float* factors, int idx, const float* go, void* stream);
 

@@ -122,6 +122,134 @@ __global__ void scale_by_device_kernel(float* g, long n, const float* factors, i
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) g[i] *= f;
 }
 
+// ---------------------------------------------------------------- CenterNetLoss in two launches
+// (centerNetOffset.py:182-217): (A) focal loss + gradient on the heatmap and the zero fill of the size / offset
+// gradient buffer (both element-wise over the batch); (B) one workgroup: the two masked L1 terms on the gathered
+// size / offset values (gradient +-1 added at the gathered pixels: integer-valued, so exact in any order), then the
+// finalize of loss_finalize_kernel (focal replicas + L1 sums -> loss, stats, backward factors).
+__global__ void centernet_loss_a_kernel(const float* x, const float* gt, long n, float* g, double* acc, float* gz,
+                                        long nz) {
+    float posl = 0.f, negl = 0.f, npos = 0.f;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float xi = x[i], t = gt[i];
+        const float p = 1.f / (1.f + expf(-xi));
+        const bool pass = (p >= 1e-4f) && (p <= 1.f - 1e-4f);
+        const float pc = fminf(fmaxf(p, 1e-4f), 1.f - 1e-4f);
+        float dterm = 0.f;
+        if (t == 1.f) {
+            const float om = 1.f - pc;
+            const float lg = logf(pc);
+            posl += lg * (om * om);
+            npos += 1.f;
+            dterm = om * om / pc - 2.f * om * lg;
+        } else if (t < 1.f) {
+            const float om = 1.f - t;
+            const float w = (om * om) * (om * om);
+            const float l1m = logf(1.f - pc);
+            negl += l1m * (pc * pc) * w;
+            dterm = w * (-(pc * pc) / (1.f - pc) + 2.f * pc * l1m);
+        }
+        g[i] = pass ? dterm * p * (1.f - p) : 0.f;
+    }
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nz; i += stride) gz[i] = 0.f;
+    __shared__ double red[3][4];
+    double a = wave_sum_d((double)posl), b = wave_sum_d((double)negl), c = wave_sum_d((double)npos);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { red[0][w] = a; red[1][w] = b; red[2][w] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double* dst = acc + (long)(blockIdx.x % SCD_STAT_REPLICAS) * FOCAL_ACC;
+        const int nw = blockDim.x / 64;
+        double s0 = 0, s1 = 0, s2 = 0;
+        for (int k = 0; k < nw; ++k) { s0 += red[0][k]; s1 += red[1][k]; s2 += red[2][k]; }
+        atomic_add_f64(dst + 0, s0);
+        atomic_add_f64(dst + 1, s1);
+        atomic_add_f64(dst + 2, s2);
+    }
+}
+
+struct L1Term {
+    const float* feat;
+    float* g;
+    int C, toff;
+};
+
+__global__ __launch_bounds__(256) void centernet_loss_b_kernel(int N, int HW, const int64_t* inds, const uint8_t* mask,
+                                                               const float* target, int K, int tstride, L1Term t0,
+                                                               L1Term t1, double* facc, LossFin w, float* out,
+                                                               float* factors) {
+    float s[2] = {0.f, 0.f}, cnt = 0.f;
+    for (int i = threadIdx.x; i < N * K; i += blockDim.x) {
+        if (!mask[i]) continue;
+        cnt += 1.f;
+        const int n = i / K;
+        const long ind = inds[i];
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+            const L1Term& t = l ? t1 : t0;
+            for (int c = 0; c < t.C; ++c) {
+                const long fi = ((long)n * t.C + c) * HW + ind;
+                const float d = t.feat[fi] - target[(long)i * tstride + t.toff + c];
+                s[l] += fabsf(d);
+                const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+                if (sg != 0.f) atomic_add_f32(t.g + fi, sg);
+            }
+        }
+    }
+    __shared__ double red[3][4];
+    const double a = wave_sum_d((double)s[0]), b = wave_sum_d((double)s[1]), c = wave_sum_d((double)cnt);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) { red[0][wv] = a; red[1][wv] = b; red[2][wv] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double ls[2] = {0.0, 0.0}, lc = 0.0;
+        for (int k = 0; k < (int)(blockDim.x / 64); ++k) { ls[0] += red[0][k]; ls[1] += red[1][k]; lc += red[2][k]; }
+        double pl = 0, nl = 0, np = 0;
+        for (int r = 0; r < SCD_STAT_REPLICAS; ++r) {
+            const double* q = facc + (long)r * FOCAL_ACC;
+            pl += q[0]; nl += q[1]; np += q[2];
+        }
+        // focal.py:47-51: no positives -> -negL ; else -(posL+negL)/#pos; regression.py:37-44: sum|d| / (#mask + 1e-4)
+        const float posl = (float)pl, negl = (float)nl, npos = (float)np;
+        const float v = np == 0.0 ? -negl : -(posl + negl) / npos;
+        out[1] = v;
+        factors[0] = np == 0.0 ? -1.f : -1.f / npos;
+        double total = v;
+        for (int l = 0; l < 2; ++l) {
+            const float vl = w.l1w[l] * ((float)ls[l] / ((float)lc + 1e-4f));
+            out[2 + l] = vl;
+            factors[1 + l] = w.l1w[l] / ((float)lc + 1e-4f);
+            total += vl;
+        }
+        out[0] = (float)total;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SCD_STAT_REPLICAS * FOCAL_ACC; i += blockDim.x) facc[i] = 0.0;
+}
+
+// backward: g_heat *= factors[0] * go (dense); the size / offset gradients are zero except at the gathered pixels,
+// so only those are scaled (factors[1], factors[2]), each pixel once (its first slot in the image)
+__global__ void centernet_loss_scale_kernel(float* gh, long nh, int N, int HW, const int64_t* inds, int K, float* g0,
+                                            int C0, float* g1, int C1, const float* factors, const float* go) {
+    const float gs = go ? go[0] : 1.f;
+    const float f0 = factors[0] * gs;
+    const long stride = (long)gridDim.x * blockDim.x;
+    const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    for (long i = t0; i < nh; i += stride) gh[i] *= f0;
+    const float f1 = factors[1] * gs, f2 = factors[2] * gs;
+    for (long s = t0; s < (long)N * K; s += stride) {
+        const int n = (int)(s / K), k = (int)(s - (long)n * K);
+        const int64_t ind = inds[s];
+        if (ind < 0 || ind >= HW) continue;
+        bool first = true;
+        for (int k2 = 0; k2 < k; ++k2) first &= inds[(long)n * K + k2] != ind;
+        if (!first) continue;
+        for (int c = 0; c < C0; ++c) g0[((long)n * C0 + c) * HW + ind] *= f1;
+        for (int c = 0; c < C1; ++c) g1[((long)n * C1 + c) * HW + ind] *= f2;
+    }
+}
+
 // ---------------------------------------------------------------- decode
 // t[n][i] = sigmoid(x) kept where it equals its 3x3 (k x k) max (pad -inf), else 0
 __global__ void decode_nms_kernel(const float* heat, int N, int H, int W, int k, float* t) {
@@ -280,6 +408,34 @@ extern "C" int scd_centernet_loss_finalize(double* focal_acc, int nfocal, double
     for (int i = 0; i < 8; ++i) w.l1w[i] = i < nl1 ? l1_weights[i] : 0.f;
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, focal_acc, nfocal, l1_acc, nl1, w,
                        out, factors);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_centernet_loss_fwd(const float* heat, const float* gt, long n_heat, const float* regr, int Cr,
+                                      const float* off, int Co, int N, int HW, const int64_t* inds, const uint8_t* mask,
+                                      const float* target, int K, int tstride, int toff_r, int toff_o,
+                                      const float* l1_weights, float* g_heat, float* g_regr, float* g_off,
+                                      double* focal_acc, float* out, float* factors, void* stream) {
+    if (n_heat < 1 || K < 1 || N < 1 || g_off != g_regr + (long)N * Cr * HW) return SCD_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const long nz = (long)N * (Cr + Co) * HW;
+    hipLaunchKernelGGL(centernet_loss_a_kernel, dim3(ew_blocks(std::max(n_heat, nz))), dim3(256), 0, st, heat, gt, n_heat,
+                       g_heat, focal_acc, g_regr, nz);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    LossFin w;
+    for (int i = 0; i < 8; ++i) w.l1w[i] = i < 2 ? l1_weights[i] : 0.f;
+    L1Term t0{regr, g_regr, Cr, toff_r}, t1{off, g_off, Co, toff_o};
+    hipLaunchKernelGGL(centernet_loss_b_kernel, dim3(1), dim3(256), 0, st, N, HW, inds, mask, target, K, tstride, t0, t1,
+                       focal_acc, w, out, factors);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_centernet_loss_bwd_scale(float* g_heat, long n_heat, int N, int HW, const int64_t* inds, int K,
+                                            float* g_regr, int Cr, float* g_off, int Co, const float* factors,
+                                            const float* go, void* stream) {
+    hipLaunchKernelGGL(centernet_loss_scale_kernel, dim3(ew_blocks(n_heat)), dim3(256), 0, (hipStream_t)stream, g_heat,
+                       n_heat, N, HW, inds, K, g_regr, Cr, g_off, Co, factors, go);
     SCD_RETURN_LAUNCH();
 }
 

@@ -91,6 +91,8 @@ SIGNATURES = {
     "scd_l1_gather_fwd": (I, [P, I, I, I, P, P, P, I, I, I, P, P, P]),
     "scd_centernet_loss_finalize": (I, [P, I, P, I, P, P, P, P]),
     "scd_scale_by_device": (I, [P, L, P, I, P, P]),
+    "scd_centernet_loss_fwd": (I, [P, P, L, P, I, P, I, I, I, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P]),
+    "scd_centernet_loss_bwd_scale": (I, [P, L, I, I, P, I, P, I, P, I, P, P, P]),
     "scd_decode_workspace": (c_size_t, [I, I]),
     "scd_decode_topk": (I, [P, I, I, I, I, P, I, P, I, P, P, P, P, P, P, P, P]),
     "scd_augment_workspace": (c_size_t, [I]),

@@ -31,21 +31,16 @@ class CenterNetLossFn(torch.autograd.Function):
         s = ops.stream()
         g_heat = torch.empty_like(heat)
         facc = _acc_buffer(dev, "focal", L.STAT_REPLICAS * 4)
-        L.call("scd_focal_fwd", ops.ptr(heat), ops.ptr(gt_heat), heat.numel(), ops.ptr(g_heat), ops.ptr(facc), s)
-        lacc = _acc_buffer(dev, "l1", 4)
-        # one zero fill for both scattered L1 gradients
-        g_both = torch.zeros(regr.numel() + off.numel(), dtype=regr.dtype, device=dev)
+        # one buffer for both scattered L1 gradients (zero-filled by the first launch)
+        g_both = torch.empty(regr.numel() + off.numel(), dtype=regr.dtype, device=dev)
         g_regr = g_both[:regr.numel()].view(regr.shape)
         g_off = g_both[regr.numel():].view(off.shape)
-        L.call("scd_l1_gather_fwd", ops.ptr(regr), N, regr.shape[1], HW, ops.ptr(inds), ops.ptr(mask_u8),
-               ops.ptr(regr_t), K, regr_t.shape[2], 2, ops.ptr(g_regr), ops.ptr(lacc), s)
-        L.call("scd_l1_gather_fwd", ops.ptr(off), N, off.shape[1], HW, ops.ptr(inds), ops.ptr(mask_u8),
-               ops.ptr(regr_t), K, regr_t.shape[2], 0, ops.ptr(g_off), ops.ptr(lacc[2:]), s)
         out = torch.empty(4, device=dev)
         factors = torch.empty(3, device=dev)
-        wts = (ctypes_float2(wr, wo))
-        L.call("scd_centernet_loss_finalize", ops.ptr(facc), 1, ops.ptr(lacc), 2, wts, ops.ptr(out),
-               ops.ptr(factors), s)
+        L.call("scd_centernet_loss_fwd", ops.ptr(heat), ops.ptr(gt_heat), heat.numel(), ops.ptr(regr), regr.shape[1],
+               ops.ptr(off), off.shape[1], N, HW, ops.ptr(inds), ops.ptr(mask_u8), ops.ptr(regr_t), K,
+               regr_t.shape[2], 2, 0, ctypes_float2(wr, wo), ops.ptr(g_heat), ops.ptr(g_regr), ops.ptr(g_off),
+               ops.ptr(facc), ops.ptr(out), ops.ptr(factors), s)
         ctx.save_for_backward(g_heat, g_regr, g_off, factors)
         ctx.inds = inds
         ops.clear_sparse_grads()          # a new loss: earlier certificates are consumed or stale
@@ -58,9 +53,10 @@ class CenterNetLossFn(torch.autograd.Function):
     def backward(ctx, gl, gstats):
         g_heat, g_regr, g_off, factors = ctx.saved_tensors
         gl = gl.contiguous() if gl is not None else torch.ones(1, device=g_heat.device)
-        s = ops.stream()
-        for i, g in enumerate((g_heat, g_regr, g_off)):
-            L.call("scd_scale_by_device", ops.ptr(g), g.numel(), ops.ptr(factors), i, ops.ptr(gl), s)
+        N, Cr, H, W = g_regr.shape
+        L.call("scd_centernet_loss_bwd_scale", ops.ptr(g_heat), g_heat.numel(), N, H * W, ops.ptr(ctx.inds),
+               ctx.inds.shape[1], ops.ptr(g_regr), Cr, ops.ptr(g_off), g_off.shape[1], ops.ptr(factors), ops.ptr(gl),
+               ops.stream())
         # the L1 terms reach the size / offset outputs only at the gathered pixels (g_regr, g_off share one buffer)
         ops.certify_sparse_grad(g_regr, ctx.inds)
         return g_heat, g_regr, g_off, None, None, None, None, None, None
