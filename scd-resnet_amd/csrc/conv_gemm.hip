@@ -3216,6 +3216,15 @@ static long wgrad_ns_model(long M, long tiles, int slots, int kp, double stage_u
     return best;
 }
 
+// SCD_WGRAD_MAXPX=<pixels>: at most this many pixels per split (shorter-lived weight-gradient workgroups, so the
+// side stream frees CUs for the critical chain sooner; more fp32 slab traffic).  0 = the cost model alone.
+static long wgrad_min_splits(long M, long ns_max) {
+    static long v = -1;
+    if (v < 0) { const char* e = getenv("SCD_WGRAD_MAXPX"); v = e ? atol(e) : 0; }
+    if (v <= 0) return 0;
+    return std::min(ns_max, (cdiv(M, v) + 7) / 8 * 8L);
+}
+
 static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
     const int win = wgrad_pp2_win(Cg);
     const long tiles = (long)(Cg / win) * cdiv(KK, 256);
@@ -3225,7 +3234,8 @@ static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
         // one workgroup per CU; a 64-pixel stage ~ 2*win*256*64 flop at ~4.3 TF/s per CU; slab win x 256 fp32
         const double stage_us = 2.0 * win * 256 * 64 / 4.3e6;
         const double epi_us = 4.0 * win * 256 / (5.0e6 / 256);
-        return (int)wgrad_ns_model(M, tiles, 256, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem));
+        const long ns = wgrad_ns_model(M, tiles, 256, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem));
+        return (int)std::max(ns, wgrad_min_splits(M, std::min(cap_px, cap_mem)));
     }
     // about two rounds of one-per-CU workgroups over the channel windows, whole XCD groups, >= 2048 pixels
     // per split, fp32 slabs capped at 256 MB
@@ -3267,7 +3277,9 @@ extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
         const double epi_us = 4.0 * tm * tn / (5.0e6 / slots);
         const long cap_px = std::max(8L, M / 1024 / 8 * 8);
         const long cap_mem = std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * T * Ci) / 8 * 8);
-        return (int)wgrad_ns_model(M, tiles, slots, KP, stage_us, epi_us, 4.0 * Cg * T * Ci, std::min(cap_px, cap_mem));
+        const long ns = wgrad_ns_model(M, tiles, slots, KP, stage_us, epi_us, 4.0 * Cg * T * Ci,
+                                       std::min(cap_px, cap_mem));
+        return (int)std::max(ns, wgrad_min_splits(M, std::min(cap_px, cap_mem)));
     }
     long ns = std::max(1L, std::min((ring ? 1024L : 1024L) / std::max(1L, tiles), M / 1024));
     ns = std::max(1L, std::min(ns, (256L << 20) / std::max(1L, 4L * Cg * T * Ci)));
