@@ -36,6 +36,10 @@
 #ifndef H384_SCHED
 #define H384_SCHED 0  // heads384 DMA order: 0 = P1 {A0, B part 1}, 1 = P1 {B part 1}, P2 {A0, B part 2}
 #endif
+#ifndef WGRAD_OCC
+#define WGRAD_OCC 2   // register-staged weight-gradient kernel: workgroups per CU the registers are budgeted for
+                      // (3 leaves VGPRs for BN kernels beside it: measured -5%, the kernel itself slows down)
+#endif
 #ifndef H384_EPI
 #define H384_EPI 1    // heads384 epilogue: 0 = hidden tile staged in LDS (16-B stores, tails from the staged rows),
                       // 1 = from the accumulators (tails as 16x16x16 MFMAs on the same registers, 16-B stores of
@@ -1908,7 +1912,7 @@ __device__ __forceinline__ int wswz(int row, int byte, int stride) {
 // of the per-row decomposition (the generic path is VALU-issue-bound: ~250 address instructions per stage
 // against 32 MFMAs per wave).
 template <typename T, int BM, int BN, int FASTX>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
+__global__ __launch_bounds__(256, WGRAD_OCC) void conv_wgrad_kernel(WgradParams p) {
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;
     constexpr int KP = ESZ == 2 ? 64 : 32;               // pixels per stage (2 bf16 MFMA k-steps)
@@ -3187,6 +3191,8 @@ static bool wgrad_use_pp(int dtype, long M, int Cg, int KK) {
     static int mode = -2;
     // opt-in (SCD_WGRAD_PP=1): correct, but measured 10-40% slower than conv_wgrad_kernel at every Res10 shape
     if (mode == -2) { const char* e = getenv("SCD_WGRAD_PP"); mode = e ? atoi(e) : 0; }
+    // mode 2: only 128-channel weight gradients over >= 256 K pixels (the heatmap head's 3x3 weight)
+    if (mode == 2) return dtype == SCD_DT_BF16 && Cg == 128 && KK >= 1024 && M >= 256 * 1024;
     return mode && dtype == SCD_DT_BF16 && Cg >= 128 && Cg % 128 == 0 && KK >= 128 && M >= 8 * 1024;
 }
 
