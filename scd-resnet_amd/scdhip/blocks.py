@@ -79,11 +79,24 @@ class StemFn(torch.autograd.Function):
             ctx.st = st
             return out
         direct = ops.stem_direct_ok(x, dtype) and ref_geom
+        ctx.t1 = False
         if direct:
             # direct 7x7/s2 conv: the tap tile is built in LDS from the input patch (no column tensor)
             x = _c(x)
-            y = ops.stem_conv_fwd(x, ops.pack_weight(conv.weight, dtype, 0, ldp=64), stats=stats)
+            wpk = ops.pack_weight(conv.weight, dtype, 0, ldp=64)
+            y = ops.stem_conv_fwd(x, wpk, stats=stats)
             cols = x
+            side = ops.forward_side_stream(x.device) if (training and dtype == torch.bfloat16 and ops.StemT1.enabled
+                                                         and not torch.cuda.is_current_stream_capturing()) else None
+            if side is not None:
+                # the weight gradient's Gram matrix of the input, off the critical path
+                with torch.cuda.stream(side):
+                    ctx.G = ops.stem_gram(x, wpk, None)
+                    ctx.g_event = torch.cuda.Event()
+                    ctx.g_event.record(side)
+                x.record_stream(side)
+                ctx.G.record_stream(torch.cuda.current_stream())
+                ctx.wpk, ctx.t1 = wpk, True
         else:
             cols = ops.im2col_stem(x, dtype, kh=conv.weight.shape[2], kw=conv.weight.shape[3],
                                    stride=conv.stride[0], pad=conv.padding[0])
@@ -105,9 +118,14 @@ class StemFn(torch.autograd.Function):
             return None, None, None, None, None
         cols, y, am = ctx.saved_tensors
         if ctx.direct:
-            # pool/ReLU backward + BN reduction in one pass; the BN apply runs inside the weight gradient
+            # pool/ReLU backward + BN reduction in one pass; the BN apply runs inside the weight gradient, or (T1)
+            # folds into the Gram matrix algebra
             dz, coef = ops.stem_pool_bwd_bn(bn, _c(dout), am, y, st)
-            ops.stem_conv_wgrad(dz, cols, ops.grad_of(conv.weight), ybn=y, coef=coef)
+            if ctx.t1:
+                ops.stem_wgrad_t1(dz, cols, ops.grad_of(conv.weight), ctx.G, ctx.g_event, ctx.wpk, coef)
+                ctx.G = ctx.g_event = ctx.wpk = None
+            else:
+                ops.stem_conv_wgrad(dz, cols, ops.grad_of(conv.weight), ybn=y, coef=coef)
         else:
             dz = ops.stem_pool_bwd(_c(dout), am, y, st)
             dy = ops.bn_backward(bn, st, dz, y)

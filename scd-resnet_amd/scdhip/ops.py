@@ -941,6 +941,42 @@ def stem_pool_fwd(y, st):
     return out, am
 
 
+class StemT1:
+    """Stem weight gradient without the BN-apply pass over the activation (bf16, direct stem): dW = a*T1 + b*W G +
+    c*s with T1 = sum dz col^T from the masked pool gradient and the input only, and the im2col Gram matrix G
+    (ones column: s) computed during the forward on the side stream (residuals.py:209-216 backward; the algebra
+    of scd_stem_wgrad_combine).  Opt-in (SCD_STEM_T1=1): measured -2% in the step (4,880 vs 4,973 img/s: the Gram
+    kernel on the side stream slows the forward's GEMMs more than the cheaper weight gradient saves); the default
+    fuses the BN apply into the weight-gradient GEMM."""
+    enabled = os.environ.get("SCD_STEM_T1", "0") == "1"
+
+
+def forward_side_stream(dev):
+    """The side stream for work issued during a forward pass (ordered after the current stream)."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if not _Side.enabled:
+        return None
+    s = _Side.streams.get(idx)
+    if s is None:
+        s = _new_side_stream(idx)
+        _Side.streams[idx] = s
+    s.wait_stream(torch.cuda.current_stream(idx))
+    return s
+
+
+def stem_wgrad_t1(dz, x, dst, G, g_event, wpk, coef):
+    """dst (+)= a*T1 + b*W G + c*s (StemT1): T1 from the masked pool gradient dz, G from stem_gram (its producer's
+    event), wpk the packed bf16 weight the forward used, coef the BN backward coefficients (a, b, c)."""
+    N, _, H, W = x.shape
+    Ho, Wo = dz.shape[1], dz.shape[2]
+    ns = L.lib().scd_stem_conv_wgrad_nsplit(N * Ho * Wo)
+    ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=dz.device)
+    L.call("scd_stem_conv_wgrad", dt(dz), ptr(dz), 0, 0, ptr(x), ptr(ws), ns, N, H, W, Ho, Wo, stream())
+    if g_event is not None:
+        torch.cuda.current_stream().wait_event(g_event)
+    L.call("scd_stem_wgrad_combine", ptr(ws), ns, ptr(coef), ptr(G), ptr(wpk), ptr(dst), 1, stream())
+
+
 def stem_pool_bwd_bn(bn, dout, am, y, st):
     """MaxPool/ReLU backward of the stem fused with its BN backward reduction; returns (dz, coef):
     dgamma/dbeta are accumulated, coef = the apply coefficients for dy = a*dz + b*y + c."""

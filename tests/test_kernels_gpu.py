@@ -288,6 +288,34 @@ def test_stem_fused_backward_matches_unfused():
     assert rel_err(dwb, dwa) < 2e-2
 
 
+def test_stem_wgrad_t1_matches_fused_apply():
+    """Stem weight gradient as a*T1 + b*W G + c*s (T1 = dz col^T, G = the input's im2col Gram matrix; opt-in ops.StemT1)
+    against the weight-gradient GEMM with the BN backward apply fused (same dz, same coefficients): the two differ
+    only by the bf16 rounding of y inside the apply (b*y term), 2e-2 relative."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(2, 1, 512, 512, generator=g).to(DEV)
+    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).to(DEV)
+    bn = torch.nn.BatchNorm2d(64).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_()
+    wpk = ops.pack_weight(w, torch.bfloat16, 0, ldp=64)
+    stats = ops.new_stats(64, DEV)
+    y = ops.stem_conv_fwd(x, wpk, stats=stats)
+    st = ops.bn_finalize(bn, stats, 64, y.numel() // 64)
+    out, am = ops.stem_pool_fwd(y, st)
+    dout = torch.randn(out.shape, generator=g).to(DEV, torch.bfloat16)
+    dz, coef = ops.stem_pool_bwd_bn(bn, dout, am, y, st)
+    dwa = torch.zeros_like(w)
+    ops.stem_conv_wgrad(dz, x, dwa, ybn=y, coef=coef)
+    G = ops.stem_gram(x, wpk, None)
+    dwb = torch.zeros_like(w)
+    ops.stem_wgrad_t1(dz, x, dwb, G, None, wpk, coef)
+    torch.cuda.synchronize()
+    assert rel_err(dwb, dwa) < 2e-2
+
+
 @pytest.mark.parametrize("shape", [(2, 512, 512), (3, 384, 256)])
 def test_stem_without_full_res_activation(shape):
     """Stem from the Gram matrix and the pooled side (scd_stem_gram / _fused_fwd / _wgrad_pooled / _combine):

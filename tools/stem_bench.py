@@ -57,6 +57,7 @@ def main():
     rep("stem_pool_bwd_bn", timed(lambda: ops.stem_pool_bwd_bn(bn, dout, am, y, st), a.reps))
     dz, coef = ops.stem_pool_bwd_bn(bn, dout, am, y, st)
     rep("stem_conv_wgrad (+BN apply)", timed(lambda: ops.stem_conv_wgrad(dz, x, dw, ybn=y, coef=coef), a.reps))
+    rep("stem_conv_wgrad (dz only: T1)", timed(lambda: ops.stem_conv_wgrad(dz, x, dw), a.reps))
     # without it
     ns = L.lib().scd_stem_conv_wgrad_nsplit(M)
     ws = torch.empty(ns * 4096, device=dev)
@@ -73,7 +74,7 @@ def main():
         256, 256, 128, 128, ops.stream()), a.reps))
     rep("stem_fused_bwd (all)", timed(lambda: ops.stem_fused_bwd(bn, st, dout, am2, yam2, x, G, wpk, dw), a.reps))
     old = rows[0][1] + rows[1][1] + rows[2][1] + rows[3][1]
-    new = rows[5][1] + rows[6][1] + rows[8][1]
+    new = rows[6][1] + rows[7][1] + rows[9][1]
     print("chain with activation %.1f us, without %.1f us" % (old, new))
 
 
