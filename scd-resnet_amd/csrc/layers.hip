@@ -940,7 +940,7 @@ extern "C" int scd_heads_bwd_packed_split(int dtype, const void* hid, int N, int
 // slotmap (pixel -> slot, -1 elsewhere) and ownermap (q -> first (slot, tap) reaching q, INT_MAX elsewhere) are
 // persistent int32 maps over the N*H*W pixels; the kernels below leave them as they found them.
 namespace {
-constexpr int SP_SPB = 8;                   // slots per workgroup of the sparse tail
+constexpr int SP_SPB = 2;                   // slots per workgroup of the sparse tail
 
 template <typename T>
 __global__ __launch_bounds__(256) void heads_sparse_bwd_kernel(const T* hid, const T* feat, int N, int H, int W, int Cin,

@@ -169,13 +169,15 @@ __global__ void centernet_loss_a_kernel(const float* x, const float* gt, long n,
     }
 }
 
+static_assert(SCD_STAT_REPLICAS == 64, "centernet_loss_b_kernel sums the focal replicas with one wave");
+
 struct L1Term {
     const float* feat;
     float* g;
     int C, toff;
 };
 
-__global__ __launch_bounds__(256) void centernet_loss_b_kernel(int N, int HW, const int64_t* inds, const uint8_t* mask,
+__global__ __launch_bounds__(1024) void centernet_loss_b_kernel(int N, int HW, const int64_t* inds, const uint8_t* mask,
                                                                const float* target, int K, int tstride, L1Term t0,
                                                                L1Term t1, double* facc, LossFin w, float* out,
                                                                float* factors) {
@@ -197,19 +199,21 @@ __global__ __launch_bounds__(256) void centernet_loss_b_kernel(int N, int HW, co
             }
         }
     }
-    __shared__ double red[3][4];
+    __shared__ double red[3][16], frd[3];
     const double a = wave_sum_d((double)s[0]), b = wave_sum_d((double)s[1]), c = wave_sum_d((double)cnt);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0) { red[0][wv] = a; red[1][wv] = b; red[2][wv] = c; }
+    if (wv == 0) {
+        // the focal replicas: one lane each (SCD_STAT_REPLICAS == 64), summed across the wave
+        const double* q = facc + (long)lane * FOCAL_ACC;
+        const double pl = wave_sum_d(q[0]), nl = wave_sum_d(q[1]), np = wave_sum_d(q[2]);
+        if (lane == 0) { frd[0] = pl; frd[1] = nl; frd[2] = np; }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         double ls[2] = {0.0, 0.0}, lc = 0.0;
         for (int k = 0; k < (int)(blockDim.x / 64); ++k) { ls[0] += red[0][k]; ls[1] += red[1][k]; lc += red[2][k]; }
-        double pl = 0, nl = 0, np = 0;
-        for (int r = 0; r < SCD_STAT_REPLICAS; ++r) {
-            const double* q = facc + (long)r * FOCAL_ACC;
-            pl += q[0]; nl += q[1]; np += q[2];
-        }
+        const double pl = frd[0], nl = frd[1], np = frd[2];
         // focal.py:47-51: no positives -> -negL ; else -(posL+negL)/#pos; regression.py:37-44: sum|d| / (#mask + 1e-4)
         const float posl = (float)pl, negl = (float)nl, npos = (float)np;
         const float v = np == 0.0 ? -negl : -(posl + negl) / npos;
@@ -426,7 +430,7 @@ extern "C" int scd_centernet_loss_fwd(const float* heat, const float* gt, long n
     LossFin w;
     for (int i = 0; i < 8; ++i) w.l1w[i] = i < 2 ? l1_weights[i] : 0.f;
     L1Term t0{regr, g_regr, Cr, toff_r}, t1{off, g_off, Co, toff_o};
-    hipLaunchKernelGGL(centernet_loss_b_kernel, dim3(1), dim3(256), 0, st, N, HW, inds, mask, target, K, tstride, t0, t1,
+    hipLaunchKernelGGL(centernet_loss_b_kernel, dim3(1), dim3(1024), 0, st, N, HW, inds, mask, target, K, tstride, t0, t1,
                        focal_acc, w, out, factors);
     SCD_RETURN_LAUNCH();
 }
