@@ -297,8 +297,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     }
 }
 
-template <typename T, int BM, int BN, bool HEADS, bool BNB = false>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
+// KS = 2: intra-workgroup split K for grids of about one tile per CU (layer4 at 512 px, long K): two groups of
+// four waves each run the 128x128 tile over one half of the K stages in their own double-buffered LDS
+// stages (8 waves per CU instead of 4, no partial sums through HBM); group 1 hands its accumulators to group
+// 0 through LDS and exits (S_BARRIER then waits on the surviving waves only), group 0 runs the epilogue.
+template <typename T, int BM, int BN, bool HEADS, bool BNB = false, int KS = 1>
+__global__ __launch_bounds__(256 * KS, 2 / KS) void conv_gemm_kernel(GemmParams p) {
+    static_assert(KS == 1 || KS == 2, "split K by 1 or 2");
     constexpr int ESZ = sizeof(T);
     constexpr int EPC = 16 / ESZ;       // elements per 16-B chunk
     constexpr int BK = 128 / ESZ;       // K elements per stage
@@ -308,10 +313,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
     constexpr int STAGE = (BM + BN) * 128;
     constexpr int EROW = 64 * ESZ + 16; // epilogue staging row (64 channels + pad)
     constexpr int EPI = 4 * 64 * EROW;
-    constexpr int SMEM = (2 * STAGE > EPI + 2048) ? 2 * STAGE : EPI + 2048;
+    constexpr int SMEM1 = (KS * 2 * STAGE > EPI + 2048) ? KS * 2 * STAGE : EPI + 2048;
+    constexpr int SMEM = (KS > 1 && SMEM1 < 4 * 64 * 64 * 4) ? 4 * 64 * 64 * 4 : SMEM1;
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
-    const int tid = threadIdx.x;
+    const int grp = KS == 1 ? 0 : (int)(threadIdx.x >> 8);
+    const int tid = threadIdx.x & 255;
+    char* const gsm = smem + grp * 2 * STAGE;     // this group's two operand stages
     // XCD-aware bijective remap: blocks that share an A (pixel) tile run on one XCD's L2
     int bid;
     {
@@ -357,6 +365,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
     }
     const int cpt = p.Ci / BK;            // K stages per tap
     const int KT = ph.ntaps * cpt;
+    const int KTg = (KT + KS - 1) / KS;   // stages per group (both groups run KTg, so barriers pair up)
+    const int kb = grp * KTg;
+    const int ke = min(KT, kb + KTg);
     const int st_off = swz(srow, cch);    // (srow + 32i) & 7 == srow & 7
 
     // raw buffer loads: out-of-range lanes use an offset past num_records and read zeros
@@ -365,8 +376,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
     auto gload = [&](int kt_req, uint4 (&ra)[ACH], uint4 (&rb)[BCH]) {
         // stages past the end are issued with out-of-range offsets (no traffic, no branch)
-        const bool live = kt_req < KT;
-        const int kt = min(kt_req, KT - 1);
+        const bool live = kb + kt_req < ke;
+        const int kt = max(0, min(kb + kt_req, ke - 1));
         const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
         int c0 = chunk * BK + cch * EPC;
         int dh = ph.dh[tap], dw = ph.dw[tap], wt = ph.wt[tap];
@@ -382,7 +393,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
         }
     };
     auto lstore = [&](int buf, const uint4 (&ra)[ACH], const uint4 (&rb)[BCH]) {
-        char* As = smem + buf * STAGE;
+        char* As = gsm + buf * STAGE;
         char* Bs = As + BM * 128;
 #pragma unroll
         for (int i = 0; i < ACH; ++i) *(uint4*)(As + st_off + 32 * 128 * i) = ra[i];
@@ -405,7 +416,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
         for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     auto compute = [&](int buf) {
-        const char* As = smem + buf * STAGE;
+        const char* As = gsm + buf * STAGE;
         const char* Bs = As + BM * 128;
         if constexpr (ESZ == 2) {
 #pragma unroll
@@ -462,17 +473,38 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmParams p) {
         gload(1, ra1, rb1);
         lstore(0, ra0, rb0);
         __syncthreads();
-        for (int kt = 0; kt < KT; kt += 2) {
+        for (int kt = 0; kt < KTg; kt += 2) {
             gload(kt + 2, ra0, rb0);
             compute(0);
             lstore(1, ra1, rb1);
             __syncthreads();
-            if (kt + 1 >= KT) break;
+            if (kt + 1 >= KTg) break;
             gload(kt + 3, ra1, rb1);
             compute(1);
             lstore(0, ra0, rb0);
             __syncthreads();
         }
+    }
+    if constexpr (KS == 2) {
+        // group 1's accumulators -> group 0 through LDS ([wave][register][lane] floats: conflict-free)
+        float* xs = (float*)smem + (wave * 64) * 64 + lane;
+        if (grp == 1) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xs[(a * 16 + b * 4 + r) * 64] = acc[a][b][r];
+        }
+        __syncthreads();
+        if (grp == 1) return;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[a][b][r] += xs[(a * 16 + b * 4 + r) * 64];
+        __syncthreads();
     }
 
     gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
@@ -2851,7 +2883,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int 
 }
 
 template <typename T, int BM, int BN>
-int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st) {
+int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st, int ks = 1) {
+    if constexpr (sizeof(T) == 2 && BM == 128 && BN == 128) {
+        if (ks == 2 && !p.head_on) {
+            if (p.bnbwd) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false, true, 2>), dim3(Mtot_tiles), dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false, false, 2>), dim3(Mtot_tiles), dim3(512), 0, st, p);
+            SCD_RETURN_LAUNCH();
+        }
+    }
     if (p.head_on) {
         if constexpr (BN == 128) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, true>), dim3(Mtot_tiles), dim3(256), 0, st, p);
         else return SCD_ERR_ARG;
@@ -2868,6 +2907,17 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st) {
 
 // Kernel choice: the LDS-DMA ring kernel (256x128, bf16) for large outputs, the register-staged
 // 128x128 kernel otherwise, 256x64 for narrow outputs (Co <= 64).  SCD_GEMM_RING=0/1 forces it off/on.
+// Intra-workgroup split K of the register-staged 128x128 kernel (SCD_GEMM_KSPLIT: 0 off, 1 auto = grids of at
+// most 1.5 tiles per CU with >= 16 K stages, 2 always where it applies)
+static int ksplit_mode() {
+    static int mode = -1;
+    if (mode < 0) {
+        const char* e = getenv("SCD_GEMM_KSPLIT");
+        mode = e ? atoi(e) : 1;
+    }
+    return mode;
+}
+
 static int ring_mode() {
     static int mode = -2;
     if (mode == -2) {
@@ -3096,8 +3146,17 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         else hipLaunchKernelGGL((conv_gemm_ring_kernel<false>), dim3(tiles), dim3(512), 0, st, p);
         SCD_RETURN_LAUNCH();
     }
-    if (dtype == SCD_DT_BF16)
-        return narrow ? launch_gemm<__bf16, 256, 64>(p, tiles, st) : launch_gemm<__bf16, 128, 128>(p, tiles, st);
+    if (dtype == SCD_DT_BF16) {
+        if (narrow) return launch_gemm<__bf16, 256, 64>(p, tiles, st);
+        int ks = 1;
+        const int km = ksplit_mode();
+        if (km && !p.head_on) {
+            int kt = 0;
+            for (int i = 0; i < nphase; ++i) kt = std::max(kt, phases[i].ntaps * (p.Ci / 64));
+            if (km == 2 || (kt >= 16 && 2 * (long)tiles <= 3L * num_cus())) ks = 2;
+        }
+        return launch_gemm<__bf16, 128, 128>(p, tiles, st, ks);
+    }
     if (dtype == SCD_DT_F32)
         return narrow ? launch_gemm<float, 256, 64>(p, tiles, st) : launch_gemm<float, 128, 128>(p, tiles, st);
     return SCD_ERR_ARG;

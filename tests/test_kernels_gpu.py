@@ -36,6 +36,8 @@ CONV_CASES = [  # N, Cin, H, W, Cout, k, stride, pad
     (1, 256, 8, 8, 512, 3, 2, 1),
     (4, 128, 32, 32, 256, 3, 1, 1),     # large enough for the LDS-DMA ring kernels by default
     (3, 64, 41, 37, 192, 3, 2, 1),      # ragged pixels / channels on the ring kernels
+    (2, 192, 11, 13, 256, 3, 1, 1),     # 27 K stages (odd) over the intra-workgroup split-K kernel, ragged M
+    (4, 512, 16, 16, 512, 3, 1, 1),     # layer4 conv2 shape at batch 4: split K, 72 stages
 ]
 
 
