@@ -136,10 +136,11 @@ def pmc_traffic(kernel, batch, dtype):
     return None, None
 
 
-def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2)):
+def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2), kept_px=None):
     """The dominant kernel: the fused head GEMM (conv3x3 M=B*(S/4)^2, N=3*128, K=9*256, + bias/ReLU
     + the three 1x1 tails in the epilogue), timed live by HIP events on its launch stream around
-    every launch inside the timed steps (scdhip.ops.LaunchTimer)."""
+    every launch inside the timed steps (scdhip.ops.LaunchTimer).  kept_px: the size / offset heads' hidden
+    channels are stored at that many pixels only (the loss's gathered pixels; scd_conv_gemm_heads_keep)."""
     from scdhip import ops
     r = ops.LaunchTimer.mean_ms("heads_gemm")
     if r is None:
@@ -149,7 +150,8 @@ def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2)):
     ct = hd * len(ods)
     flops = 2.0 * M * (ct * 9 * cin + hd * sum(ods))
     esz = 4 if dtype_name == "fp32" else 2
-    algo_bytes = M * cin * esz + M * ct * esz + M * sum(ods) * 4 + ct * 9 * cin * esz
+    hid_bytes = M * ct * esz if kept_px is None else M * hd * esz + min(M, kept_px) * (ct - hd) * esz
+    algo_bytes = M * cin * esz + hid_bytes + M * sum(ods) * 4 + ct * 9 * cin * esz
     achieved = flops / (ms * 1e-3) / 1e12
     peak = PEAK_F32_TFLOPS if dtype_name == "fp32" else PEAK_BF16_TFLOPS      # dense fp16 = dense bf16 MFMA rate
     kernel = "conv_gemm_kernel<f32,128,128,heads>" if dtype_name == "fp32" else HEADS_KERNEL
@@ -311,8 +313,12 @@ def main():
         inds = torch.randint(0, H * H, (B, 30), generator=g) * mask
         ys = [heat.to(dev), mask.to(dev), regr.to(dev), inds.to(dev)]
 
+    prepare = getattr(lossfn, "prepare", None)       # CenterNetLoss: tells the heads where the loss will gather
+
     def train_step():
         opt.zero_grad()
+        if prepare is not None:
+            prepare(ys)
         loss, _ = lossfn(model(x, decode=False), ys)
         loss = loss.mean()
         loss.backward()
@@ -372,7 +378,15 @@ def main():
         # the fused CenterNet head GEMM (HeadsFn) is the dominant kernel of the centerOffset* plugins only
         extra = {}
         if args.model.startswith("centerOffset"):
-            roof = heads_gemm_roofline(B, args.dtype, S)
+            kept = None
+            if prepare is not None and ops.SparseHeads.enabled and ops._KEEP_MAPS:
+                # distinct gathered pixels: where the size / offset hidden channels were stored
+                Hh = S // 4
+                base = torch.arange(B, device=ys[3].device)[:, None] * (Hh * Hh)
+                kept = int(torch.unique(ys[3].long() + base).numel())
+            roof = heads_gemm_roofline(B, args.dtype, S, kept_px=kept)
+            if roof is not None:
+                roof["hidden_kept_px"] = kept
         elif args.model.startswith("cornerNet"):
             extra = cornernet_rooflines(B, args.dtype, S)
             roof = extra.pop("roofline", None)

@@ -78,6 +78,13 @@ int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void* y, int N,
 int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void* hid, const float* bias, int N, int H,
                         int W, int Ci, int nh, const int* od, const float* const* w1, const float* const* b1,
                         float* const* outs, void* stream);
+/* As scd_conv_gemm_heads, with hidden channels >= keep_cols (a multiple of 128) stored only at the pixels where
+ * keep[n*H*W + p] != 0 (keep = NULL: all): the size / offset heads' hidden activations are read back by their sparse
+ * backward at the loss's gathered pixels only (centerNetOffset.py:199-214), so the forward skips 2/3 of the
+ * 403 MB hidden store at B = 32.  Outputs outs[h] are complete either way. */
+int scd_conv_gemm_heads_keep(int dtype, const void* x, const void* w, void* hid, const float* bias, int N, int H,
+                             int W, int Ci, int nh, const int* od, const float* const* w1, const float* const* b1,
+                             float* const* outs, const unsigned char* keep, int keep_cols, void* stream);
 
 /* Weight-gradient of the gather-GEMM (split-K over pixels on MFMA, fp32 partial slabs):
  * ws[z, co, t*Ci+ci] = sum_{pix in split z} g[pix, co] * x[gather(pix, t), ci]
@@ -286,6 +293,12 @@ int scd_centernet_loss_fwd(const float* heat, const float* gt, long n_heat, cons
                            float* g_off, double* focal_acc, float* out, float* factors, void* stream);
 int scd_centernet_loss_bwd_scale(float* g_heat, long n_heat, int N, int HW, const int64_t* inds, int K, float* g_regr,
                                  int Cr, float* g_off, int Co, const float* factors, const float* go, void* stream);
+
+/* Keep map for scd_conv_gemm_heads_keep from the loss targets' gather indices inds (N,K) int64 (the `inds` target of
+ * CenterNetLoss, centerNetOffset.py:199-214): keep[n*HW + inds[n][k]] = 1 for every slot, after clearing the pixels
+ * the previous call set (prev: nprev >= N*K int64, -1-filled on first use, updated in place; keep zero-filled on
+ * first use).  One workgroup. */
+int scd_heads_keep_map(const int64_t* inds, int N, int K, int HW, int64_t* prev, int nprev, uint8_t* keep, void* stream);
 
 /* g[i] *= factors[idx] * go[0]  (in place) */
 int scd_scale_by_device(float* g, long n, const float* factors, int idx, const float* go, void* stream);

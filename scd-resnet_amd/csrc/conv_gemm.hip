@@ -79,6 +79,9 @@ struct GemmParams {
     const float* bn_invstd;
     const float* bn_rsc;
     const float* bn_rsh;
+    // heads384 (scd_conv_gemm_heads_keep): hidden channels >= hid_cols stored only where hid_keep[pixel] != 0
+    const unsigned char* hid_keep;
+    int hid_cols;
 };
 
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
@@ -1444,6 +1447,14 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
             // blocks in pairs (b, b+1): after the tails, v_permlane16_swap trades the odd rows' block-b halves for
             // the even rows' block-(b+1) halves, so every lane holds 8 consecutive channels (16-B stores: even rows
             // channels 16b + 4lg .., odd rows 16(b+1) + 4(lg-1) ..; 64 contiguous bytes per pixel and instruction)
+            // hidden channels >= hid_cols are stored only at the pixels the keep map names (the size / offset heads'
+            // sparse backward reads them there only; HeadsFn recomputes the whole tensor for any other backward)
+            unsigned keep = 0;
+    #pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const int m = mt * BM + 96 * grp + 16 * a + l16;
+                if (!p.hid_keep || (m < M && p.hid_keep[m])) keep |= 1u << a;
+            }
     #pragma unroll
             for (int b = 0; b < NB; b += 2) {
                 hx4 whi[2], wlo[2];
@@ -1489,7 +1500,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                     }
                     const int m = mt * BM + 96 * grp + 16 * a + l16;
                     if constexpr (!(H384_ABL & 64))
-                        if (m < M) *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
+                        if (m < M && (colst < p.hid_cols || ((keep >> a) & 1u))) *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
                 }
             }
 #if H384_PERSIST
@@ -3170,6 +3181,7 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.is = in_stride; p.os = out_stride; p.wrow = wrow; p.relu = relu; p.accumulate = accumulate;
     p.head_on = 0;
     p.bnbwd = 0; p.bny = nullptr; p.bn_mean = p.bn_invstd = p.bn_rsc = p.bn_rsh = nullptr;
+    p.hid_keep = nullptr; p.hid_cols = 1 << 30;
     {
         static int dbg = -1;
         if (dbg < 0) { const char* e = getenv("SCD_GEMM_DEBUG"); dbg = e ? atoi(e) : 0; }
@@ -3215,9 +3227,18 @@ extern "C" int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void
                                    int H, int W, int Ci, int nh, const int* od, const float* const* w1,
                                    const float* const* b1, float* const* outs, void* stream) {
     SCD_F16_FWD(scd_conv_gemm_heads, x, w, hid, bias, N, H, W, Ci, nh, od, w1, b1, outs, stream);
-    if (nh < 1 || nh > 4) return SCD_ERR_ARG;
+    return scd_conv_gemm_heads_keep(dtype, x, w, hid, bias, N, H, W, Ci, nh, od, w1, b1, outs, nullptr, 0, stream);
+}
+
+extern "C" int scd_conv_gemm_heads_keep(int dtype, const void* x, const void* w, void* hid, const float* bias, int N,
+                                        int H, int W, int Ci, int nh, const int* od, const float* const* w1,
+                                        const float* const* b1, float* const* outs, const unsigned char* keep,
+                                        int keep_cols, void* stream) {
+    SCD_F16_FWD(scd_conv_gemm_heads_keep, x, w, hid, bias, N, H, W, Ci, nh, od, w1, b1, outs, keep, keep_cols, stream);
+    if (nh < 1 || nh > 4 || (keep && (keep_cols < 0 || keep_cols % 128))) return SCD_ERR_ARG;
     GemmParams p;
     fill_params(p, x, w, hid, bias, nullptr, N, H, W, Ci, H, W, nh * 128, 1, 1, 9 * Ci, 1, 0);
+    if (keep) { p.hid_keep = keep; p.hid_cols = keep_cols; }
     p.head_on = 1;
     for (int h = 0; h < nh; ++h) {
         if (od[h] < 1 || od[h] > 4) return SCD_ERR_ARG;

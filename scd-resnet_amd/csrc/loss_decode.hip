@@ -443,6 +443,34 @@ extern "C" int scd_centernet_loss_bwd_scale(float* g_heat, long n_heat, int N, i
     SCD_RETURN_LAUNCH();
 }
 
+// Keep map of the pixels a CenterNet loss gathers (inds[n][k], all K slots): one workgroup, the previous call's
+// pixels (prev, flattened n*HW + p; -1 = none) cleared first, then the new ones set and remembered, so the persistent
+// map needs no full-size memset per step.
+__global__ __launch_bounds__(1024) void heads_keep_map_kernel(const int64_t* inds, int N, int K, int HW, int64_t* prev,
+                                                              int nprev, uint8_t* keep) {
+    for (int i = threadIdx.x; i < nprev; i += blockDim.x) {
+        const int64_t q = prev[i];
+        if (q >= 0) keep[q] = 0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < N * K; i += blockDim.x) {
+        const int n = i / K;
+        const int64_t v = inds[i];
+        const int64_t q = (v >= 0 && v < HW) ? (int64_t)n * HW + v : -1;
+        if (q >= 0) keep[q] = 1;
+        prev[i] = q;
+    }
+    for (int i = N * K + threadIdx.x; i < nprev; i += blockDim.x) prev[i] = -1;
+}
+
+extern "C" int scd_heads_keep_map(const int64_t* inds, int N, int K, int HW, int64_t* prev, int nprev, uint8_t* keep,
+                                  void* stream) {
+    if (N < 1 || K < 1 || HW < 1 || nprev < N * K) return SCD_ERR_ARG;
+    hipLaunchKernelGGL(heads_keep_map_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, inds, N, K, HW, prev, nprev,
+                       keep);
+    SCD_RETURN_LAUNCH();
+}
+
 extern "C" int scd_scale_by_device(float* g, long n, const float* factors, int idx, const float* go, void* stream) {
     hipLaunchKernelGGL(scale_by_device_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, g, n, factors, idx,
                        go);

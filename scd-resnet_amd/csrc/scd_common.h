@@ -12,6 +12,7 @@
 #define scd_conv_gemm scd_conv_gemm__f16
 #define scd_conv_gemm_bnbwd scd_conv_gemm_bnbwd__f16
 #define scd_conv_gemm_heads scd_conv_gemm_heads__f16
+#define scd_conv_gemm_heads_keep scd_conv_gemm_heads_keep__f16
 #define scd_conv_wgrad_workspace scd_conv_wgrad_workspace__f16
 #define scd_conv_wgrad_nsplit2 scd_conv_wgrad_nsplit2__f16
 #define scd_conv_wgrad_nsplit scd_conv_wgrad_nsplit__f16
@@ -62,6 +63,7 @@
 SCD_F16_DECL(scd_conv_gemm)
 SCD_F16_DECL(scd_conv_gemm_bnbwd)
 SCD_F16_DECL(scd_conv_gemm_heads)
+SCD_F16_DECL(scd_conv_gemm_heads_keep)
 SCD_F16_DECL(scd_conv_wgrad_nsplit2)
 SCD_F16_DECL(scd_conv_wgrad_nsplit)
 SCD_F16_DECL(scd_conv_wgrad)

@@ -77,6 +77,11 @@ class CenterNetLoss(torch.nn.Module):
         self.focal = focal
         self.regression = regression
 
+    def prepare(self, targets):
+        """Called by the training step before the model forward: the heads' forward then keeps the size / offset
+        hidden activations only where this loss will gather them (targets[3] = inds; ops.hint_sparse_support)."""
+        ops.hint_sparse_support(targets[3])
+
     def forward(self, outs, targets):
         if self.focal is not focalLoss or self.regression is not L1LossMask:
             raise NotImplementedError("only focalLoss + L1LossMask run on the fused HIP loss")

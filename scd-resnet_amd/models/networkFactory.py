@@ -239,6 +239,9 @@ class NetworkFactory(object):
         self.model.eval()
 
     def _passParams(self, xs, ys, **kwargs):
+        prepare = getattr(self.loss, "prepare", None)     # CenterNetLoss: the heads keep what the loss gathers
+        if prepare is not None and torch.is_grad_enabled():
+            prepare(ys)
         preds = self.model(*xs, **kwargs)
         return self.loss(preds, ys)
 

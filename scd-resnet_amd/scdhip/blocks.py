@@ -325,13 +325,27 @@ class HeadsFn(torch.autograd.Function):
         b1s = ops.L.ptr_array([h[2].bias.data_ptr() for h in heads])
         optrs = ops.L.ptr_array([o.data_ptr() for o in outs])
         odarr = ops.L.int_array(od)
+        hint = ops.take_sparse_hint()
+        ctx.keep = None
         if Hd == 128 and len(heads) <= 4 and max(od) <= 4:
             # tails fused into the GEMM epilogue (one launch, hidden tensor read once)
             hid = torch.empty(N, H, W, Ct, device=feat.device, dtype=feat.dtype)
+            keep = None
+            if (hint is not None and len(heads) >= 2 and Cin <= 256 and (len(heads) - 1) * Hd <= 256
+                    and hint.dim() == 2 and hint.shape[0] == N):
+                # the loss gathers the size / offset outputs at `hint` only: their hidden channels are stored there
+                keep = ops.heads_keep_map(hint, N, H * W)
+                ctx.keep = (hint, hint._version)
+            args = (ops.dt(feat), ops.ptr(feat), ops.ptr(wp), ops.ptr(hid), ops.ptr(b0), N, H, W, Cin, len(heads),
+                    odarr, w1s, b1s)
             t0 = ops.LaunchTimer.record("heads_gemm")
-            ops.L.call("scd_conv_gemm_heads", ops.dt(feat), ops.ptr(feat), ops.ptr(wp), ops.ptr(hid), ops.ptr(b0),
-                       N, H, W, Cin, len(heads), odarr, w1s, b1s, optrs, ops.stream())
+            ops.L.call("scd_conv_gemm_heads_keep", *args, optrs, ops.ptr(keep) if keep is not None else None, Hd,
+                       ops.stream())
             ops.LaunchTimer.close("heads_gemm", t0)
+            if keep is not None:
+                # everything needed to store the whole hidden tensor again (a dense backward after all)
+                scratch = [torch.empty_like(o) for o in outs]
+                ctx.refill = (args, ops.L.ptr_array([o.data_ptr() for o in scratch]), wp, b0, scratch)
         else:
             hid = ops.conv_fwd(feat, wp, Ct, 3, 3, 1, 1, bias=b0, relu=True)
             ops.L.call("scd_heads_fwd", ops.dt(hid), ops.ptr(hid), N, H * W, len(heads), Hd, odarr, w1s, b1s, optrs,
@@ -357,6 +371,13 @@ class HeadsFn(torch.autograd.Function):
         dptrs = ops.L.ptr_array([d.data_ptr() for d in douts])
         odarr = ops.L.int_array(od)
         nd = HeadsFn._dense_prefix(douts, Hd, Cin)
+        if ctx.keep is not None:
+            inds = ops.sparse_grad_inds(douts[-1]) if nd == 1 else None
+            if inds is None or inds is not ctx.keep[0] or inds._version != ctx.keep[1]:
+                # the forward kept the size / offset hidden channels at other pixels only: store them all
+                args, optrs, _, _, _ = ctx.refill
+                ops.L.call("scd_conv_gemm_heads_keep", *args, optrs, None, 0, ops.stream())
+            ctx.refill = None
         if nd < nh:
             return HeadsFn._backward_sparse(ctx, douts, dptrs, odarr, nd, S)
         dhid = torch.empty_like(hid)

@@ -50,6 +50,7 @@ LP = ctypes.POINTER(c_long)
 SIGNATURES = {
     "scd_conv_gemm": (I, [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P]),
     "scd_conv_gemm_heads": (I, [I, P, P, P, P, I, I, I, I, I, IP, PP, PP, PP, P]),
+    "scd_conv_gemm_heads_keep": (I, [I, P, P, P, P, I, I, I, I, I, IP, PP, PP, PP, P, I, P]),
     "scd_conv_gemm_bnbwd": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P, P, P, P,
                                 P, P, P]),
     "scd_conv_wgrad_workspace": (c_size_t, [I, I, I, I]),
@@ -91,6 +92,7 @@ SIGNATURES = {
     "scd_l1_gather_fwd": (I, [P, I, I, I, P, P, P, I, I, I, P, P, P]),
     "scd_centernet_loss_finalize": (I, [P, I, P, I, P, P, P, P]),
     "scd_scale_by_device": (I, [P, L, P, I, P, P]),
+    "scd_heads_keep_map": (I, [P, I, I, I, P, I, P, P]),
     "scd_centernet_loss_fwd": (I, [P, P, L, P, I, P, I, I, I, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P]),
     "scd_centernet_loss_bwd_scale": (I, [P, L, I, I, P, I, P, I, P, I, P, P, P]),
     "scd_decode_workspace": (c_size_t, [I, I]),

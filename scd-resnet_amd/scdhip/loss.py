@@ -25,7 +25,7 @@ class CenterNetLossFn(torch.autograd.Function):
         dev = heat.device
         mask_u8 = mask.contiguous()
         mask_u8 = mask_u8.view(torch.uint8) if mask_u8.dtype == torch.bool else mask_u8.to(torch.uint8)
-        inds = inds.to(torch.int64).contiguous()
+        inds = ops.hinted_inds(inds)
         regr_t = regr_t.float().contiguous()
         gt_heat = gt_heat.float().contiguous()
         s = ops.stream()

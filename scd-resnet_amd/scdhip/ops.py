@@ -598,6 +598,54 @@ def sparse_grad_inds(g):
     return inds
 
 
+_HEADS_HINT = [None]
+_KEEP_MAPS = {}
+
+
+def hint_sparse_support(inds):
+    """The gather indices (N, K) of the loss that will consume the next heads forward (CenterNetLoss.prepare,
+    called by the training step before the model): that forward then stores the size / offset heads' hidden
+    activations at those pixels only -- their sparse backward reads nothing else, and HeadsFn recomputes the whole
+    tensor if the backward turns out dense.  One-shot: taken by the next HeadsFn.forward."""
+    if SparseHeads.enabled and inds is not None:
+        conv = inds.to(torch.int64).contiguous()
+        _HEADS_HINT[0] = (inds, inds._version, conv)
+
+
+def take_sparse_hint():
+    h = _HEADS_HINT[0]
+    _HEADS_HINT[0] = None
+    _LAST_HINT[0] = h
+    return h[2] if h is not None else None
+
+
+def hinted_inds(inds):
+    """inds as int64 contiguous: the very tensor the hint converted when `inds` is the hinted one (so HeadsFn can
+    tell by identity that the loss gathers where its forward kept the hidden activations)."""
+    h = _HEADS_HINT[0] if _HEADS_HINT[0] is not None else _LAST_HINT[0]
+    if h is not None and h[0] is inds and h[1] == inds._version:
+        return h[2]
+    return inds.to(torch.int64).contiguous()
+
+
+_LAST_HINT = [None]
+
+
+def heads_keep_map(inds, N, HW):
+    """Persistent uint8 map (N*HW) of inds' pixels for scd_conv_gemm_heads_keep (scd_heads_keep_map clears the
+    previous call's pixels itself)."""
+    K = inds.shape[1]
+    key = (str(inds.device), N * HW, K)
+    e = _KEEP_MAPS.get(key)
+    if e is None:
+        e = (torch.zeros(N * HW, dtype=torch.uint8, device=inds.device),
+             torch.full((N * K,), -1, dtype=torch.int64, device=inds.device))
+        _KEEP_MAPS[key] = e
+    keep, prev = e
+    L.call("scd_heads_keep_map", ptr(inds), N, K, HW, ptr(prev), prev.numel(), ptr(keep), stream())
+    return keep
+
+
 _SPARSE_MAPS = {}
 
 

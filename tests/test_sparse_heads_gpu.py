@@ -30,12 +30,14 @@ def _targets(B, Hh, K, dev, seed):
     return [heat.to(dev), mask.to(dev), regr.to(dev), inds.to(dev)]
 
 
-def _grads(model, lossfn, x, ys, sparse):
+def _grads(model, lossfn, x, ys, sparse, hint=None):
     from scdhip import ops
     prev = ops.SparseHeads.enabled
     ops.SparseHeads.enabled = sparse
     try:
         model.zero_grad(set_to_none=False)
+        if hint is not None:
+            lossfn.prepare(hint)
         loss, _ = lossfn(model(x, decode=False), ys)
         loss.mean().backward()
         torch.cuda.synchronize()
@@ -126,3 +128,50 @@ def test_sparse_path_taken_and_maps_restored():
     assert taken == [1]
     slotmap, ownermap = ops.sparse_maps(dev, 2 * 32 * 32)
     assert (slotmap == -1).all() and (ownermap == 0x7fffffff).all()
+
+
+@pytest.mark.parametrize("B,S", [(4, 256), (8, 512)])
+def test_heads_keep_map_gradients_identical(B, S):
+    """CenterNetLoss.prepare before the forward: the heads GEMM stores the size / offset hidden channels only at the
+    gathered pixels (scd_conv_gemm_heads_keep) and the sparse backward reads nothing else, so loss and every
+    gradient are bit-identical to the run without the hint; the keep map names exactly the gathered pixels."""
+    from scdhip import ops
+    plugin, model, x, ys = _setup(torch.bfloat16, B, S)
+    state = {k: v.clone() for k, v in model.state_dict().items()}
+    ga, la = _grads(model, plugin.loss, x, ys, True)
+    model.load_state_dict(state)
+    gb, lb = _grads(model, plugin.loss, x, ys, True, hint=ys)
+    assert la == lb
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), n
+    HW = (S // 4) ** 2
+    keep = ops._KEEP_MAPS[(str(x.device), B * HW, ys[3].shape[1])][0].view(B, HW)
+    ref = torch.zeros(B, HW, dtype=torch.uint8, device=x.device).scatter_(1, ys[3], 1)
+    assert torch.equal(keep, ref)
+
+
+def test_heads_keep_map_fallbacks():
+    """A hint that does not match the backward's gradients makes HeadsFn store the whole hidden tensor again:
+    (1) the loss gathers at other indices than the hinted ones, (2) a loss without the sparse certificate (dense
+    backward).  Gradients equal the runs without any hint."""
+    plugin, model, x, ys = _setup(torch.bfloat16, 4, 256)
+    state = {k: v.clone() for k, v in model.state_dict().items()}
+    other = list(ys)
+    other[3] = (torch.flip(ys[3], (1,)) + 1) % (64 * 64)
+    ga, _ = _grads(model, plugin.loss, x, other, True)
+    model.load_state_dict(state)
+    gb, _ = _grads(model, plugin.loss, x, other, True, hint=ys)
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), n
+
+    def dense_loss(outs, ys_):
+        o = outs[0]
+        return (o["heatmap"].float().square().mean() + o["regr"].float().square().mean()
+                + o["offset"].float().square().mean()).reshape(1), None
+    dense_loss.prepare = plugin.loss.prepare
+    model.load_state_dict(state)
+    gc, _ = _grads(model, dense_loss, x, ys, True)
+    model.load_state_dict(state)
+    gd, _ = _grads(model, dense_loss, x, ys, True, hint=ys)
+    for n in gc:
+        assert torch.equal(gc[n], gd[n]), n
