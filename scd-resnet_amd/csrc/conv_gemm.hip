@@ -46,6 +46,13 @@
                       // 64-B row pieces after v_permlane16_swap), 2 = tails as 1, hidden rows staged in LDS and stored
                       // whole (less write traffic: measured 0.81 vs 0.785 ms)
 #endif
+#ifndef H384_ACP
+#define H384_ACP 0    // heads384 input-gather LDS-DMA cache policy (aux bits; 2 = nt: the gathered rows, re-read only
+                      // within a tile's nine taps, go first when L2 evicts, the weights every round re-reads stay)
+#endif
+#ifndef H384_HCP
+#define H384_HCP 0    // heads384 hidden stores: 0 = plain, 16 = sc1 buffer stores (written through, dropped from L2)
+#endif
 #ifndef SCD_ABM
 #define SCD_ABM 0     // halo kernel ablation bitmask: 1 no MFMA, 2 no loop DMA, 4 no loop fragment reads, 8 no loop barriers
 #endif
@@ -1283,6 +1290,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     const int KT = ph.ntaps * cpt;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+    // hidden output [M][384] bf16 (< 2^31 bytes: checked by the launcher)
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.y, (short)0, 0x7fffffff, 0x00020000);
+    (void)yrs;
 
     struct StageArgs { int live, tap, adelta, bdelta; };
     auto stage_args = [&](int kt_req) {
@@ -1297,7 +1307,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     };
     auto issue_a = [&](const StageArgs& g, char* buf, int j) {
         const bool ok = g.live && ((a_mask[j] >> g.tap) & 1u);
-        dma16(xrs, buf + (96 * grp + 32 * j + 8 * wc) * 128, sel_off(ok, a_base[j] + g.adelta));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(buf + (96 * grp + 32 * j + 8 * wc) * 128), 16,
+                                                 sel_off(ok, a_base[j] + g.adelta), 0, 0, H384_ACP);
     };
     auto issue_b = [&](const StageArgs& g, char* buf, int part) {
         char* Bs = buf + BM * 128;
@@ -1500,7 +1511,14 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                     }
                     const int m = mt * BM + 96 * grp + 16 * a + l16;
                     if constexpr (!(H384_ABL & 64))
-                        if (m < M && (colst < p.hid_cols || ((keep >> a) & 1u))) *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
+                        if (m < M && (colst < p.hid_cols || ((keep >> a) & 1u))) {
+                            if constexpr (H384_HCP == 0) *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
+                            else {
+                                typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+                                const u32x4 sv = {st.x, st.y, st.z, st.w};
+                                __builtin_amdgcn_raw_buffer_store_b128(sv, yrs, (m * BN + colst) * 2, 0, H384_HCP);
+                            }
+                        }
                 }
             }
 #if H384_PERSIST
@@ -3037,6 +3055,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         // the three 128-wide CenterNet heads: one 192 x 384 tile per 192 pixels, tails fused
         const long wb = (long)p.Co * p.wrow * esz;
         if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
+        if (H384_HCP && Mtot * p.Co * esz >= (1L << 31) - 64) return SCD_ERR_ARG;   // 32-bit hidden store offsets
         p.xbytes = (int)xb;
         p.wbytes = (int)wb;
         p.ntn = 1;

@@ -276,7 +276,10 @@ def test_cornernet_b32_bf16_config3(monkeypatch):
             sc = _bn(F.conv2d(xi, mod.shortcutConv.weight), mod.shortcutBn)
             r = F.relu(mg + sc)
             ref = F.relu(_bn(F.conv2d(r, mod.lastConv.conv.weight, padding=1), mod.lastConv.bn))
-            check("cornerpool %d%d" % dirs, _nchw(out), ref, report)
+            # this group rounds to bf16 about 9 times in series (3 weight layers: branch, merge/shortcut, lastConv;
+            # 6 stored values: branch activations, pool sum, merge/shortcut pre-BN, merged r, lastConv pre-BN, output)
+            # against the <= 6 the module bound assumes: scale the bound by 9/6 (measured 0.130 max, 0.012 rms)
+            check("cornerpool %d%d" % dirs, _nchw(out), ref, report, 1.5)
     _print(report)
     losses = _train_steps(m16, plugin, x, ys, 4)
     assert all(math.isfinite(v) for v in losses) and losses[-1] < losses[0], losses
