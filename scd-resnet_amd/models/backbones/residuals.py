@@ -190,6 +190,11 @@ class ResNet(torch.nn.Module):
         mods = [getattr(self, n) for n in names]
         ret = {}
         plain = [n for n, m in zip(names, mods) if _is_plain_head(m)]
+        corner = [n for n, m in zip(names, mods) if n not in plain and _is_corner_head(m)]
+        if len(plain) + len(corner) == len(names):
+            # every consumer of feat is an scdhip Function: one input-gradient buffer instead of autograd's sums
+            nplain = (1 if len({getattr(self, n)[0].weight.shape[0] for n in plain}) == 1 else len(plain)) if plain else 0
+            ops.share_grad(feat, nplain + len(corner))
         if plain:
             hm = [getattr(self, n) for n in plain]
             if len({m[0].weight.shape[0] for m in hm}) == 1:

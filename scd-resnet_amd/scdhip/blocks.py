@@ -394,6 +394,14 @@ class HeadsFn(torch.autograd.Function):
         ld = (Cin * 9, 9, 1)
         rows = [(i * Hd, (i + 1) * Hd, ops.grad_of(h[0].weight), ld) for i, h in enumerate(heads)]
         ops.conv_wgrad(dhid, feat, 3, 3, 1, 1, None, None, rows=rows)
+        slot = ops.shared_grad_slot(feat)
+        if slot is not None:
+            # feat's gradient is shared with other consumers (ops.share_grad): write into / start the one buffer
+            # (no BN-backward sums from this epilogue: they would cover this consumer's part only)
+            dfeat = ops.conv_dgrad(dhid, ops.pack_concat(w0s, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1, out=slot[1],
+                                   accumulate=slot[1] is not None)
+            grads_ready(*[m for h in heads for m in h if isinstance(m, torch.nn.Module)])
+            return ops.shared_grad_out(feat, slot, dfeat if slot[1] is None else None), None, None
         fuse = ctx.prod is not None and feat.dtype in ops.HALF
         dfeat = ops.conv_dgrad(dhid, ops.pack_concat(w0s, feat.dtype, 1), Cin, H, W, 3, 3, 1, 1,
                                bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
@@ -525,7 +533,10 @@ class CornerPoolFn(torch.autograd.Function):
         dys = ops.bn_backward(mod.shortcutBn, sts, dr, ysc, mask=r)
         wsc = mod.shortcutConv.weight
         ops.conv_wgrad(dys, x, 1, 1, 1, 0, ops.grad_of(wsc), _conv_ld(wsc))
-        dx = ops.conv_dgrad(dys, ops.pack_weight(wsc, x.dtype, 1), C, H, W, 1, 1, 1, 0)
+        slot = ops.shared_grad_slot(x)          # x's gradient shared with the other heads (ops.share_grad)
+        prev = slot[1] if slot is not None else None
+        dx = ops.conv_dgrad(dys, ops.pack_weight(wsc, x.dtype, 1), C, H, W, 1, 1, 1, 0, out=prev,
+                            accumulate=prev is not None)
         wm = mod.branchMerge.weight
         ops.conv_wgrad(dym, s, 3, 3, 1, 1, ops.grad_of(wm), _conv_ld(wm))
         Cb = wm.shape[1]
@@ -537,6 +548,8 @@ class CornerPoolFn(torch.autograd.Function):
             ops.conv_dgrad(dy, ops.pack_weight(br.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1, out=dx,
                            accumulate=True)
         grads_ready(mod)
+        if slot is not None:
+            return ops.shared_grad_out(x, slot, dx if prev is None else None), None, None, None
         return dx, None, None, None
 
 

@@ -539,6 +539,47 @@ def fused_bn_bwd_args(prod):
     return (st, y, bn_stats(bn, "bwdf"))
 
 
+# ------------------------------------------------------------------ one input gradient for several consumers
+#
+# A feature map read by several scdhip Functions (the CornerNet feature: the heatmap head and the TL / BR corner
+# pools, cornerNetCPool.py:163-199) would get one input gradient from each, which autograd then sums with
+# elementwise adds (2 x 805 MB of HBM traffic per step at B=32).  share_grad registers the consumers in forward;
+# in backward the first one to run allocates the gradient buffer and returns it, the others accumulate their
+# input-gradient GEMMs into it (accumulate epilogue) and return None (autograd adds nothing for None), so the sum
+# is complete when the producer's backward runs (it waits for every consumer).  A slot never matches a later step:
+# the next registration clears it, and keys carry data pointer, shape and version.
+
+class SharedGrad:
+    enabled = os.environ.get("SCD_SHARED_GRAD", "1") != "0"
+
+
+_SHARED_GRAD = {}
+
+
+def share_grad(t, n):
+    """t feeds n scdhip Functions in this (grad-enabled) forward."""
+    if SharedGrad.enabled and n > 1 and torch.is_grad_enabled() and t.requires_grad:
+        _SHARED_GRAD.clear()
+        _SHARED_GRAD[_tkey(t)] = [n, None]
+
+
+def shared_grad_slot(t):
+    """In a consumer's backward: [remaining consumers, buffer or None] when t's gradient is shared, else None."""
+    return _SHARED_GRAD.get(_tkey(t)) if _SHARED_GRAD else None
+
+
+def shared_grad_out(t, slot, grad):
+    """Record that this consumer has written its part; grad: the buffer it allocated (first consumer) or None.
+    Returns what the consumer's backward hands autograd for t."""
+    first = slot[1] is None
+    if first:
+        slot[1] = grad
+    slot[0] -= 1
+    if slot[0] <= 0:
+        _SHARED_GRAD.pop(_tkey(t), None)
+    return grad if first else None
+
+
 def mark_bn_bwd_fused(bn, grad):
     _BN_FUSED[id(bn)] = _tkey(grad)
 
