@@ -45,6 +45,26 @@ def _train_bn_conv(x, conv, bn, stride, pad, training, timer=None):
     return y, st
 
 
+def _downsample_branch(x, blk, stride, training):
+    """Start a block's downsample branch (conv1x1 + BN statistics, residuals.py:131-134) on the branch stream
+    (ops.branch_begin) so it overlaps the main branch; returns (yd, std, stream) or (None, None, None)."""
+    if blk.downsample is None or not training:
+        return None, None, None
+    bs = ops.branch_begin(x)
+    if bs is None:
+        return None, None, None
+    with torch.cuda.stream(bs):
+        yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], stride, 0, training)
+    return yd, std, bs
+
+
+def _downsample_join(x, blk, stride, training, yd, std, bs):
+    if bs is None:
+        return _train_bn_conv(x, blk.downsample[0], blk.downsample[1], stride, 0, training)
+    ops.branch_join(bs, yd, std.mean, std.invstd, std.scale, std.shift)
+    return yd, std
+
+
 def _dgrad_bn_relu_bwd(dy, wpack_t, C, Hc, Wc, kh, kw, stride, pad, bn, st, y):
     """Input gradient of a conv whose input is a BN+ReLU layer's output (bn, st, pre-BN y), then that layer's
     backward.  In bf16 the dgrad GEMM's epilogue accumulates the BN backward sums (scd_conv_gemm_bnbwd; shapes
@@ -140,12 +160,12 @@ class BasicBlockFn(torch.autograd.Function):
     def forward(ctx, x, w1, blk):
         tr = blk.training
         s = blk.stride
+        yd, std, bs = _downsample_branch(x, blk, s, tr)
         y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, s, 1, tr)
         a1 = ops.bn_apply(y1, st1, True)
         y2, st2 = _train_bn_conv(a1, blk.conv2, blk.bn2, 1, 1, tr)
-        yd, std = None, None
         if blk.downsample is not None:
-            yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], s, 0, tr)
+            yd, std = _downsample_join(x, blk, s, tr, yd, std, bs)
             out = ops.bn_apply(y2, st2, True, res=yd, rst=std)
         else:
             out = ops.bn_apply(y2, st2, True, res=x)
@@ -188,14 +208,14 @@ class BottleneckFn(torch.autograd.Function):
     def forward(ctx, x, w1, blk):
         tr = blk.training
         s = blk.stride
+        yd, std, bs = _downsample_branch(x, blk, s, tr)
         y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, 1, 0, tr)
         a1 = ops.bn_apply(y1, st1, True)
         y2, st2 = _train_bn_conv(a1, blk.conv2, blk.bn2, s, 1, tr)
         a2 = ops.bn_apply(y2, st2, True)
         y3, st3 = _train_bn_conv(a2, blk.conv3, blk.bn3, 1, 0, tr)
-        yd, std = None, None
         if blk.downsample is not None:
-            yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], s, 0, tr)
+            yd, std = _downsample_join(x, blk, s, tr, yd, std, bs)
             out = ops.bn_apply(y3, st3, True, res=yd, rst=std)
         else:
             out = ops.bn_apply(y3, st3, True, res=x)

@@ -539,6 +539,44 @@ def fused_bn_bwd_args(prod):
     return (st, y, bn_stats(bn, "bwdf"))
 
 
+# ------------------------------------------------------------------ independent branches of a block forward
+#
+# The downsample branch of a BasicBlock / Bottleneck (conv1x1 stride s + BN statistics; residuals.py:99-120,
+# 145-165) reads only the block input, so it runs on a second stream at the compute stream's priority while the
+# main branch's first convolutions run.  Opt-in (SCD_BRANCH_STREAM=1): measured neutral to -1.5% (Res10 B=32
+# 4,930-4,950 vs 5,017 img/s; Res50 1024^2 fp16 409 vs 410), the branch's GEMM takes CUs from the main one.
+
+class Branch:
+    enabled = os.environ.get("SCD_BRANCH_STREAM", "0") == "1"
+    streams = {}          # (device index, priority) -> stream
+
+
+def branch_begin(x):
+    """A stream ordered after the current one (same priority) for a branch that reads x, or None.  Not with the
+    peer-memory SyncBN: its all-reduce kernels share one mailbox and must not run concurrently (RCCL collectives are
+    serialised on the communicator's stream in host issue order, gloo ones on the host)."""
+    if not Branch.enabled or not x.is_cuda or _BNSync.peer is not None:
+        return None
+    idx = x.device.index if x.device.index is not None else torch.cuda.current_device()
+    cur = torch.cuda.current_stream(idx)
+    key = (idx, cur.priority)
+    s = Branch.streams.get(key)
+    if s is None:
+        s = Branch.streams[key] = torch.cuda.Stream(device=idx, priority=cur.priority)
+    s.wait_stream(cur)
+    x.record_stream(s)
+    return s
+
+
+def branch_join(s, *tensors):
+    """The current stream waits for branch stream s; tensors s allocated are now also used on the current stream."""
+    cur = torch.cuda.current_stream(s.device)
+    cur.wait_stream(s)
+    for t in tensors:
+        if t is not None:
+            t.record_stream(cur)
+
+
 # ------------------------------------------------------------------ one input gradient for several consumers
 #
 # A feature map read by several scdhip Functions (the CornerNet feature: the heatmap head and the TL / BR corner
