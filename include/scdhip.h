@@ -190,6 +190,16 @@ int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* 
                      const float* relu_shift, const float* coef, int C, long total, void* dy, void* dz,
                      void* stream);
 
+/* Two BN layers behind one residual join (BasicBlock bn2 / Bottleneck bn3 + the downsample BN, residuals.py:110-120,
+ * 158-165; CornerPool branchMergeBn + shortcutBn, cornerNetCPool.py:117-122): the same gradient dout and ReLU mask
+ * (mask > 0, required) for both.  scd_bn_bwd_reduce2 = scd_bn_bwd_reduce for (ya, stats_a) and (yb, stats_b) in one
+ * pass; scd_bn_bwd_apply2 = scd_bn_bwd_apply for (ya, coef_a -> dya) and (yb, coef_b -> dyb) in one pass. */
+int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
+                       const float* mean_a, const float* invstd_a, const float* mean_b, const float* invstd_b, int C,
+                       long total, double* stats_a, double* stats_b, void* stream);
+int scd_bn_bwd_apply2(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
+                      const float* coef_a, const float* coef_b, int C, long total, void* dya, void* dyb, void* stream);
+
 /* ---- stem without the full-resolution activation (residuals.py:209-216; bf16, Conv2d(1,64,7,s2,p3)) ----
  * scd_stem_gram: ws[z][64][64] = per-split sums of col col^T over the im2col rows of x (49 taps, tap 49 = 1, so
  * G[k][49] = sum col[k], G[49][49] = pixel count); reduce with scd_wgrad_reduce (Cg 64, T 1, Ci 64) into G fp32.

@@ -298,6 +298,147 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const 
     }
 }
 
+// ---- two BN layers behind one residual join (BasicBlock / Bottleneck bn2|bn3 + downsample BN, residuals.py:
+// 110-120, 158-165; CornerPool branchMergeBn + shortcutBn, cornerNetCPool.py:117-122): both take the same gradient
+// dout through the same ReLU mask, so one pass reads dout and the mask once for both.  Per element and per thread the
+// arithmetic is that of bn_bwd_reduce_kernel / bn_bwd_apply_kernel with a mask (no BN+ReLU recompute).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
+                                                             const float* mean_a, const float* invstd_a,
+                                                             const float* mean_b, const float* invstd_b, int C, int ld,
+                                                             unsigned rows, unsigned rows_per_block, double* stats_a,
+                                                             double* stats_b) {
+    constexpr int E = Vec16<T>::N;
+    constexpr int U = BN_BWD_U;
+    constexpr int nt = 256;
+    const int cpr = C / E;
+    const int rpi = nt / cpr;
+    const int tid = threadIdx.x;
+    const int ch = tid % cpr;
+    const int rsub = tid / cpr;
+    const unsigned r0 = blockIdx.x * rows_per_block;
+    const unsigned r1 = min(rows, r0 + rows_per_block);
+    __shared__ float red[2 * nt * E];
+    float s[E], qa[E], qb[E], mua[E], isa[E], mub[E], isb[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        s[e] = 0.f; qa[e] = 0.f; qb[e] = 0.f;
+        mua[e] = mean_a[ch * E + e]; isa[e] = invstd_a[ch * E + e];
+        mub[e] = mean_b[ch * E + e]; isb[e] = invstd_b[ch * E + e];
+    }
+    auto acc_raw = [&](const uint4& rd, const uint4& rm, const uint4& ra, const uint4& rb) {
+        float d[E], mk[E], va[E], vb[E];
+        Vec16<T>::load(&rd, d);
+        Vec16<T>::load(&rm, mk);
+        Vec16<T>::load(&ra, va);
+        Vec16<T>::load(&rb, vb);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const float dz = !(mk[e] > 0.f) ? 0.f : d[e];
+            s[e] += dz;
+            qa[e] += dz * (va[e] - mua[e]) * isa[e];
+            qb[e] += dz * (vb[e] - mub[e]) * isb[e];
+        }
+    };
+    unsigned r = r0 + rsub;
+    for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+        uint4 rd[U], rm[U], ra[U], rb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned i = (r + u * rpi) * (unsigned)ld + ch * E;
+            rd[u] = *(const uint4*)(dout + i);
+            rm[u] = *(const uint4*)(mask + i);
+            ra[u] = *(const uint4*)(ya + i);
+            rb[u] = *(const uint4*)(yb + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc_raw(rd[u], rm[u], ra[u], rb[u]);
+    }
+    for (; r < r1; r += rpi) {
+        const unsigned i = r * (unsigned)ld + ch * E;
+        acc_raw(*(const uint4*)(dout + i), *(const uint4*)(mask + i), *(const uint4*)(ya + i), *(const uint4*)(yb + i));
+    }
+    const int rep = blockIdx.x % SCD_STAT_REPLICAS;
+    // pass 1: sum dz (both layers) and layer a's sum dz*xhat; pass 2: layer b's
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        red[rsub * C + ch * E + e] = s[e];
+        red[nt * E + rsub * C + ch * E + e] = qa[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += nt) {
+        double ss = 0.0, qq = 0.0;
+        for (int k = 0; k < rpi; ++k) {
+            ss += red[k * C + c];
+            qq += red[nt * E + k * C + c];
+        }
+        atomic_add_f64(stats_a + ((long)rep * 2 + 0) * ld + c, ss);
+        atomic_add_f64(stats_a + ((long)rep * 2 + 1) * ld + c, qq);
+        atomic_add_f64(stats_b + ((long)rep * 2 + 0) * ld + c, ss);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) red[nt * E + rsub * C + ch * E + e] = qb[e];
+    __syncthreads();
+    for (int c = tid; c < C; c += nt) {
+        double qq = 0.0;
+        for (int k = 0; k < rpi; ++k) qq += red[nt * E + k * C + c];
+        atomic_add_f64(stats_b + ((long)rep * 2 + 1) * ld + c, qq);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
+                                                            const float* coef_a, const float* coef_b, int C,
+                                                            unsigned nvec, T* dya, T* dyb) {
+    constexpr int E = Vec16<T>::N;
+    constexpr int U = BN_BWD_U;
+    const unsigned cpr = (unsigned)C / E;
+    const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned stride = gridDim.x * blockDim.x;
+    const int c0 = (int)(v0 % cpr) * E;
+    float aa[E], ab[E], ac[E], ba[E], bb[E], bc[E];
+    load_params<E>(coef_a + c0, aa);
+    load_params<E>(coef_a + C + c0, ab);
+    load_params<E>(coef_a + 2 * C + c0, ac);
+    load_params<E>(coef_b + c0, ba);
+    load_params<E>(coef_b + C + c0, bb);
+    load_params<E>(coef_b + 2 * C + c0, bc);
+    auto body = [&](size_t i, const uint4& rd, const uint4& rm, const uint4& ra, const uint4& rb) {
+        float d[E], mk[E], va[E], vb[E];
+        Vec16<T>::load(&rd, d);
+        Vec16<T>::load(&rm, mk);
+        Vec16<T>::load(&ra, va);
+        Vec16<T>::load(&rb, vb);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const float dz = !(mk[e] > 0.f) ? 0.f : d[e];
+            va[e] = aa[e] * dz + ab[e] * va[e] + ac[e];
+            vb[e] = ba[e] * dz + bb[e] * vb[e] + bc[e];
+        }
+        Vec16<T>::store(dya + i, va);
+        Vec16<T>::store(dyb + i, vb);
+    };
+    unsigned v = v0;
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+        uint4 rd[U], rm[U], ra[U], rb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = (size_t)(v + u * stride) * E;
+            rd[u] = *(const uint4*)(dout + i);
+            rm[u] = *(const uint4*)(mask + i);
+            ra[u] = *(const uint4*)(ya + i);
+            rb[u] = *(const uint4*)(yb + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) body((size_t)(v + u * stride) * E, rd[u], rm[u], ra[u], rb[u]);
+    }
+    for (; v < nvec; v += stride) {
+        const size_t i = (size_t)v * E;
+        body(i, *(const uint4*)(dout + i), *(const uint4*)(mask + i), *(const uint4*)(ya + i), *(const uint4*)(yb + i));
+    }
+}
+
 // elementwise BN kernels keep one channel chunk per thread: the grid stride (grid * 256 threads) must be a
 // multiple of the chunks per row cpr, i.e. cpr divides 256 or is a multiple of it (grid a multiple of cpr/256)
 inline bool ew_rows_ok(int cpr) { return cpr > 0 && (256 % cpr == 0 || cpr % 256 == 0); }
@@ -390,6 +531,74 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
         if (e != hipSuccess) return (int)e;
     }
     return 0;
+}
+
+extern "C" int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
+                                  const float* mean_a, const float* invstd_a, const float* mean_b,
+                                  const float* invstd_b, int C, long total, double* stats_a, double* stats_b,
+                                  void* stream) {
+    SCD_F16_FWD(scd_bn_bwd_reduce2, dout, mask, ya, yb, mean_a, invstd_a, mean_b, invstd_b, C, total, stats_a, stats_b,
+                stream);
+    hipStream_t st = (hipStream_t)stream;
+    const int E = dtype == SCD_DT_BF16 ? 8 : 4;
+    if (!dout || !mask || !ya || !yb || C % E) return SCD_ERR_ARG;
+    const long rows = total / C;
+    const int cpr = C / E;
+    if (!ew_rows_ok(cpr) || total >= (1L << 31)) return SCD_ERR_ARG;
+    const int scpr = std::min(cpr, 256), sC = scpr * E;
+    // the same row partition as scd_bn_bwd_reduce (per-thread partial sums identical to two separate passes)
+    static const int gb = resident_grid((const void*)bn_bwd_reduce_kernel<__bf16>, 256);
+    static const int gf = resident_grid((const void*)bn_bwd_reduce_kernel<float>, 256);
+    const long nb = dtype == SCD_DT_BF16 ? gb : gf;
+    const long rpi = 256 / scpr;
+    const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
+    const int blocks = cdiv(rows, rpb);
+    const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
+    for (int c0 = 0; c0 < C; c0 += sC) {
+        const size_t o = (size_t)c0 * esz;
+        const char *d = (const char*)dout + o, *m = (const char*)mask + o, *a = (const char*)ya + o,
+                   *b = (const char*)yb + o;
+        if (dtype == SCD_DT_BF16)
+            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)d,
+                               (const __bf16*)m, (const __bf16*)a, (const __bf16*)b, mean_a + c0, invstd_a + c0,
+                               mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
+                               stats_b + c0);
+        else if (dtype == SCD_DT_F32)
+            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)d,
+                               (const float*)m, (const float*)a, (const float*)b, mean_a + c0, invstd_a + c0,
+                               mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
+                               stats_b + c0);
+        else
+            return SCD_ERR_ARG;
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}
+
+extern "C" int scd_bn_bwd_apply2(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
+                                 const float* coef_a, const float* coef_b, int C, long total, void* dya, void* dyb,
+                                 void* stream) {
+    SCD_F16_FWD(scd_bn_bwd_apply2, dout, mask, ya, yb, coef_a, coef_b, C, total, dya, dyb, stream);
+    hipStream_t st = (hipStream_t)stream;
+    const int E = dtype == SCD_DT_BF16 ? 8 : 4;
+    if (!dout || !mask || !ya || !yb || !dya || !dyb || C % E || !ew_rows_ok(C / E) || total / E >= (1L << 32))
+        return SCD_ERR_ARG;
+    const long nvec = total / E;
+    if (dtype == SCD_DT_BF16) {
+        static const int g = resident_grid((const void*)bn_bwd_apply2_kernel<__bf16>, 256);
+        hipLaunchKernelGGL((bn_bwd_apply2_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 0, st,
+                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)ya, (const __bf16*)yb, coef_a,
+                           coef_b, C, (unsigned)nvec, (__bf16*)dya, (__bf16*)dyb);
+    } else if (dtype == SCD_DT_F32) {
+        static const int g = resident_grid((const void*)bn_bwd_apply2_kernel<float>, 256);
+        hipLaunchKernelGGL((bn_bwd_apply2_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 0, st,
+                           (const float*)dout, (const float*)mask, (const float*)ya, (const float*)yb, coef_a, coef_b,
+                           C, (unsigned)nvec, (float*)dya, (float*)dyb);
+    } else {
+        return SCD_ERR_ARG;
+    }
+    SCD_RETURN_LAUNCH();
 }
 
 extern "C" int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,

@@ -25,6 +25,8 @@
 #define scd_bn_bwd_reduce scd_bn_bwd_reduce__f16
 #define scd_bn_bwd_finalize scd_bn_bwd_finalize__f16
 #define scd_bn_bwd_apply scd_bn_bwd_apply__f16
+#define scd_bn_bwd_reduce2 scd_bn_bwd_reduce2__f16
+#define scd_bn_bwd_apply2 scd_bn_bwd_apply2__f16
 #define scd_pack_weights_batched scd_pack_weights_batched__f16
 #define scd_pack_weight scd_pack_weight__f16
 #define scd_im2col_stem scd_im2col_stem__f16
@@ -70,6 +72,8 @@ SCD_F16_DECL(scd_conv_wgrad)
 SCD_F16_DECL(scd_bn_apply)
 SCD_F16_DECL(scd_bn_bwd_reduce)
 SCD_F16_DECL(scd_bn_bwd_apply)
+SCD_F16_DECL(scd_bn_bwd_reduce2)
+SCD_F16_DECL(scd_bn_bwd_apply2)
 SCD_F16_DECL(scd_pack_weights_batched)
 SCD_F16_DECL(scd_pack_weight)
 SCD_F16_DECL(scd_im2col_stem)

@@ -184,8 +184,7 @@ class BasicBlockFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         C = blk.conv1.weight.shape[0]
         if blk.downsample is not None:
-            dy2 = ops.bn_backward(blk.bn2, st2, dout, y2, mask=out)
-            dyd = ops.bn_backward(blk.downsample[1], std, dout, yd, mask=out)
+            dy2, dyd = ops.bn_backward_pair(blk.bn2, st2, y2, blk.downsample[1], std, yd, dout, out)
             wd = blk.downsample[0].weight
             dx = ops.conv_dgrad(dyd, ops.pack_weight(wd, x.dtype, 1), Cin, H, W, 1, 1, s, 0)
             ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
@@ -234,8 +233,7 @@ class BottleneckFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         P = blk.conv1.weight.shape[0]
         if blk.downsample is not None:
-            dy3 = ops.bn_backward(blk.bn3, st3, dout, y3, mask=out)
-            dyd = ops.bn_backward(blk.downsample[1], std, dout, yd, mask=out)
+            dy3, dyd = ops.bn_backward_pair(blk.bn3, st3, y3, blk.downsample[1], std, yd, dout, out)
             wd = blk.downsample[0].weight
             dx = ops.conv_dgrad(dyd, ops.pack_weight(wd, x.dtype, 1), Cin, H, W, 1, 1, s, 0)
             ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
@@ -549,8 +547,7 @@ class CornerPoolFn(torch.autograd.Function):
         dyl = ops.bn_backward(lc.bn, stl, _c(dout), yl, relu=True)
         ops.conv_wgrad(dyl, r, 3, 3, 1, 1, ops.grad_of(lc.conv.weight), _conv_ld(lc.conv.weight))
         dr = ops.conv_dgrad(dyl, ops.pack_weight(lc.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1)
-        dym = ops.bn_backward(mod.branchMergeBn, stm, dr, ym, mask=r)
-        dys = ops.bn_backward(mod.shortcutBn, sts, dr, ysc, mask=r)
+        dym, dys = ops.bn_backward_pair(mod.branchMergeBn, stm, ym, mod.shortcutBn, sts, ysc, dr, r)
         wsc = mod.shortcutConv.weight
         ops.conv_wgrad(dys, x, 1, 1, 1, 0, ops.grad_of(wsc), _conv_ld(wsc))
         slot = ops.shared_grad_slot(x)          # x's gradient shared with the other heads (ops.share_grad)

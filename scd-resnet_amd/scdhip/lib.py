@@ -78,6 +78,8 @@ SIGNATURES = {
     "scd_bn_bwd_reduce": (I, [I, P, P, P, P, P, P, P, I, L, P, P]),
     "scd_bn_bwd_finalize": (I, [P, I, I, D, P, P, P, P, P, F, P, P]),
     "scd_bn_bwd_apply": (I, [I, P, P, P, P, P, P, I, L, P, P, P]),
+    "scd_bn_bwd_reduce2": (I, [I, P, P, P, P, P, P, P, P, I, L, P, P, P]),
+    "scd_bn_bwd_apply2": (I, [I, P, P, P, P, P, P, I, L, P, P, P]),
     "scd_stem_pool_fwd": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_pool_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_heads_fwd": (I, [I, P, I, I, I, I, IP, PP, PP, PP, P]),

@@ -935,6 +935,30 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None)
     return dy
 
 
+class BNPair:
+    enabled = os.environ.get("SCD_BN_PAIR", "1") != "0"
+
+
+def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
+    """Two BN layers behind one residual join, out = relu(bn_a(y_a) + bn_b(y_b)) (BasicBlock / Bottleneck with a
+    downsample, CornerPool merge + shortcut): their backward from the same dout and ReLU mask (the stored `out`),
+    dout / mask read once per pass (scd_bn_bwd_reduce2 / scd_bn_bwd_apply2).  Returns (dy_a, dy_b), equal to two
+    bn_backward calls."""
+    if not BNPair.enabled:
+        return (bn_backward(bn_a, st_a, dout, y_a, mask=mask), bn_backward(bn_b, st_b, dout, y_b, mask=mask))
+    C = y_a.shape[-1]
+    sa, sb = bn_stats(bn_a, "bwd"), bn_stats(bn_b, "bwd")
+    L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean), ptr(st_a.invstd),
+           ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
+    alpha = grad_alpha(y_a)
+    ca = bn_backward_coef(bn_a, st_a, sa, C, alpha)
+    cb = bn_backward_coef(bn_b, st_b, sb, C, alpha)
+    dya, dyb = torch.empty_like(y_a), torch.empty_like(y_b)
+    L.call("scd_bn_bwd_apply2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(ca), ptr(cb), C, y_a.numel(),
+           ptr(dya), ptr(dyb), stream())
+    return dya, dyb
+
+
 def bn_backward_coef(bn, st, stats, C, alpha=1.0):
     """SyncBN all-reduce of the backward sums, dgamma/dbeta accumulation (times alpha: 1 / the fp16 loss scale)
     and the apply coefficients."""

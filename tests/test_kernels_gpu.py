@@ -658,3 +658,49 @@ def test_wgrad_reduce_rows(ns, Cg, T, Ci):
             want[:, :cvalid] = exp[:, :cvalid] + (want[:, :cvalid] if accumulate else 0)
             err = (d.cpu().double() - want).abs().max().item() / max(1e-6, want.abs().max().item())
             assert err < 1e-5, (a, b, accumulate, err)
+
+
+@pytest.mark.parametrize("dtype,C", [(torch.bfloat16, 128), (torch.bfloat16, 512), (torch.float32, 64)])
+def test_bn_backward_pair_matches_two_passes(dtype, C):
+    """Residual join out = relu(bn_a(y_a) + bn_b(y_b)) (BasicBlock bn2 + downsample BN, residuals.py:110-120; CornerPool
+    merge + shortcut): scd_bn_bwd_reduce2 / scd_bn_bwd_apply2 against two scd_bn_bwd_reduce / scd_bn_bwd_apply passes
+    with the same dout and mask -- BN parameter gradients to fp64-summation-order level (1e-6), input gradients equal
+    up to one rounding of the 16-bit output where a coefficient differs in its last float bit."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(C)
+    N, H, W = 4, 32, 32
+    ya = torch.randn(N, H, W, C, generator=g).to(DEV, dtype)
+    yb = (torch.randn(N, H, W, C, generator=g) * 2 + 0.5).to(DEV, dtype)
+    dout = torch.randn(N, H, W, C, generator=g).to(DEV, dtype)
+    res = {}
+    for pair in (False, True):
+        bns = [torch.nn.BatchNorm2d(C).to(DEV) for _ in range(2)]
+        sts = []
+        for bn, y in zip(bns, (ya, yb)):
+            with torch.no_grad():
+                bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+                bn.bias.copy_(torch.linspace(-0.3, 0.3, C))
+            stats = ops.new_stats(C, DEV)
+            # the forward statistics of y (as the producing GEMM epilogue would accumulate them)
+            yd = y.double().reshape(-1, C)
+            stats[:C] = yd.sum(0)
+            stats[C:2 * C] = (yd * yd).sum(0)
+            sts.append(ops.bn_finalize(bn, stats, C, yd.shape[0]))
+        out = torch.relu(ya.float() * sts[0].scale + sts[0].shift + yb.float() * sts[1].scale + sts[1].shift).to(dtype)
+        old = ops.BNPair.enabled
+        ops.BNPair.enabled = pair
+        try:
+            dya, dyb = ops.bn_backward_pair(bns[0], sts[0], ya, bns[1], sts[1], yb, dout, out)
+        finally:
+            ops.BNPair.enabled = old
+        torch.cuda.synchronize()
+        res[pair] = (dya.float(), dyb.float(), [t.grad.clone() for bn in bns for t in (bn.weight, bn.bias)])
+    (a0, b0, g0), (a1, b1, g1) = res[False], res[True]
+    for x, y in zip(g0, g1):
+        assert rel_err(y, x) < 1e-6
+    ulp = 2.0 ** -7 if dtype == torch.bfloat16 else 1e-6
+    for x, y in ((a0, a1), (b0, b1)):
+        d = (x - y).abs()
+        assert (d <= ulp * x.abs().clamp_min(1e-3) + 1e-6).all(), d.max().item()
+        if dtype != torch.float32:      # fp32 shows every last-bit coefficient difference; 16-bit rounding hides most
+            assert (d > 0).float().mean().item() < 1e-3
