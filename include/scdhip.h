@@ -163,6 +163,9 @@ int scd_stem_conv_wgrad(int dtype, const void* dy, const void* ybn, const float*
 /* ---- training BatchNorm2d (residuals.py:92,95,212,262,306; momentum 0.1, eps 1e-5) ---- */
 /* sum replicas [nrep][2][C] -> [2][C] in place (replica 0); used before a SyncBN all-reduce */
 int scd_stats_collapse(double* stats, int nrep, int C, void* stream);
+/* out[0 .. 2C) = the replica sum of stats, every replica zeroed: two BN layers' sums collapsed side by side into one
+ * staging buffer go through ONE SyncBN all-reduce (networkFactory.py:128-133), then finalize with nrep = 1 */
+int scd_stats_collapse_to(double* stats, int nrep, int C, double* out, void* stream);
 /* mean/var from stats (count rows), running-stat update (unbiased var), scale/shift for apply;
  * stats == NULL: eval mode, normalise with the running statistics (no update) */
 int scd_bn_finalize(double* stats, int nrep, int C, double count, const float* gamma,

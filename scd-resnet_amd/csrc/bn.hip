@@ -23,6 +23,19 @@ __global__ void stats_collapse_kernel(double* stats, int nrep, int n) {
     stats[i] = s;
 }
 
+// SyncBN staging: out[i] = sum of the replicas, every replica zeroed (two layers' sums side by side in one buffer,
+// so one collective reduces both)
+__global__ void stats_collapse_to_kernel(double* stats, int nrep, int n, double* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int r = 0; r < nrep; ++r) {
+        s += stats[(long)r * n + i];
+        stats[(long)r * n + i] = 0.0;
+    }
+    out[i] = s;
+}
+
 // one wave per channel: lane r sums replica r (and zeroes it: persistent, consumer-cleared buffers)
 __device__ __forceinline__ void wave_collect(double* stats, int nrep, int C, int c, double& s, double& q) {
     const int lane = threadIdx.x & 63;
@@ -455,6 +468,14 @@ inline int fin_blocks(int C) { return (C + 3) / 4; }   // 4 waves (channels) per
 extern "C" int scd_stats_collapse(double* stats, int nrep, int C, void* stream) {
     const int n = 2 * C;
     hipLaunchKernelGGL(stats_collapse_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, stats, nrep, n);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_stats_collapse_to(double* stats, int nrep, int C, double* out, void* stream) {
+    const int n = 2 * C;
+    if (!stats || !out || nrep < 1) return SCD_ERR_ARG;
+    hipLaunchKernelGGL(stats_collapse_to_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, stats, nrep, n,
+                       out);
     SCD_RETURN_LAUNCH();
 }
 

@@ -20,6 +20,7 @@
 #define scd_wgrad_reduce scd_wgrad_reduce__f16
 #define scd_wgrad_reduce_rows scd_wgrad_reduce_rows__f16
 #define scd_stats_collapse scd_stats_collapse__f16
+#define scd_stats_collapse_to scd_stats_collapse_to__f16
 #define scd_bn_finalize scd_bn_finalize__f16
 #define scd_bn_apply scd_bn_apply__f16
 #define scd_bn_bwd_reduce scd_bn_bwd_reduce__f16

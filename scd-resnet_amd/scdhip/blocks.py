@@ -31,8 +31,8 @@ def _conv_ld(w):
     return (w.shape[1] * T, T, 1)
 
 
-def _train_bn_conv(x, conv, bn, stride, pad, training, timer=None):
-    """conv (no bias) -> raw y + BN statistics -> BNState.  timer: LaunchTimer name for the GEMM (bench.py)."""
+def _conv_stats(x, conv, bn, stride, pad, training, timer=None):
+    """conv (no bias) -> raw y, with the BN statistics accumulated in the GEMM epilogue (training)."""
     C = conv.weight.shape[0]
     kh, kw = conv.weight.shape[2], conv.weight.shape[3]
     wp = ops.pack_weight(conv.weight, x.dtype, 0)
@@ -41,8 +41,24 @@ def _train_bn_conv(x, conv, bn, stride, pad, training, timer=None):
     y = ops.conv_fwd(x, wp, C, kh, kw, stride, pad, stats=stats)
     if timer:
         ops.LaunchTimer.close(timer, t0)
-    st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
-    return y, st
+    return y, stats
+
+
+def _train_bn_conv(x, conv, bn, stride, pad, training, timer=None):
+    """conv (no bias) -> raw y + BN statistics -> BNState.  timer: LaunchTimer name for the GEMM (bench.py)."""
+    y, stats = _conv_stats(x, conv, bn, stride, pad, training, timer)
+    C = conv.weight.shape[0]
+    return y, ops.bn_finalize(bn, stats, C, y.numel() // C, training)
+
+
+def _conv1_and_downsample(x, blk, conv1, bn1, s1, pad1, sd):
+    """A block's first conv and its downsample conv (both read only the block input; residuals.py:99-120,
+    145-165), then both BN finalizes together: with SyncBN one all-reduce for the two layers."""
+    y1, s1st = _conv_stats(x, conv1, bn1, s1, pad1, True)
+    yd, sdst = _conv_stats(x, blk.downsample[0], blk.downsample[1], sd, 0, True)
+    C1, Cd = conv1.weight.shape[0], blk.downsample[0].weight.shape[0]
+    st1, std = ops.bn_finalize_pair(bn1, s1st, C1, y1.numel() // C1, blk.downsample[1], sdst, Cd, yd.numel() // Cd)
+    return y1, st1, yd, std
 
 
 def _downsample_branch(x, blk, stride, training):
@@ -60,6 +76,8 @@ def _downsample_branch(x, blk, stride, training):
 
 def _downsample_join(x, blk, stride, training, yd, std, bs):
     if bs is None:
+        if yd is not None:                  # computed with conv1 (_conv1_and_downsample)
+            return yd, std
         return _train_bn_conv(x, blk.downsample[0], blk.downsample[1], stride, 0, training)
     ops.branch_join(bs, yd, std.mean, std.invstd, std.scale, std.shift)
     return yd, std
@@ -161,7 +179,10 @@ class BasicBlockFn(torch.autograd.Function):
         tr = blk.training
         s = blk.stride
         yd, std, bs = _downsample_branch(x, blk, s, tr)
-        y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, s, 1, tr)
+        if tr and blk.downsample is not None and bs is None:
+            y1, st1, yd, std = _conv1_and_downsample(x, blk, blk.conv1, blk.bn1, s, 1, s)
+        else:
+            y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, s, 1, tr)
         a1 = ops.bn_apply(y1, st1, True)
         y2, st2 = _train_bn_conv(a1, blk.conv2, blk.bn2, 1, 1, tr)
         if blk.downsample is not None:
@@ -208,7 +229,10 @@ class BottleneckFn(torch.autograd.Function):
         tr = blk.training
         s = blk.stride
         yd, std, bs = _downsample_branch(x, blk, s, tr)
-        y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, 1, 0, tr)
+        if tr and blk.downsample is not None and bs is None:
+            y1, st1, yd, std = _conv1_and_downsample(x, blk, blk.conv1, blk.bn1, 1, 0, s)
+        else:
+            y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, 1, 0, tr)
         a1 = ops.bn_apply(y1, st1, True)
         y2, st2 = _train_bn_conv(a1, blk.conv2, blk.bn2, s, 1, tr)
         a2 = ops.bn_apply(y2, st2, True)
@@ -518,17 +542,31 @@ class CornerPoolFn(torch.autograd.Function):
     def forward(ctx, x, w_anchor, mod, dirs):
         tr = mod.branchMergeBn.training
         b1, b2, lc = mod.branch1, mod.branch2, mod.lastConv
-        y1, st1 = _train_bn_conv(x, b1.conv, b1.bn, 1, 1, tr)
+        if tr:
+            # both branch convs read x: their BN finalizes together (one SyncBN all-reduce for the two)
+            y1, s1 = _conv_stats(x, b1.conv, b1.bn, 1, 1, tr)
+            y2, s2 = _conv_stats(x, b2.conv, b2.bn, 1, 1, tr)
+            C1, C2 = b1.conv.weight.shape[0], b2.conv.weight.shape[0]
+            st1, st2 = ops.bn_finalize_pair(b1.bn, s1, C1, y1.numel() // C1, b2.bn, s2, C2, y2.numel() // C2)
+        else:
+            y1, st1 = _train_bn_conv(x, b1.conv, b1.bn, 1, 1, tr)
+            y2, st2 = _train_bn_conv(x, b2.conv, b2.bn, 1, 1, tr)
         a1 = ops.bn_apply(y1, st1, True)
-        y2, st2 = _train_bn_conv(x, b2.conv, b2.bn, 1, 1, tr)
         a2 = ops.bn_apply(y2, st2, True)
         p1 = ops.cpool_fwd(a1, dirs[0])
         t0 = ops.LaunchTimer.record("cpool_fwd_add")
         s = ops.cpool_fwd(a2, dirs[1], addend=p1)
         ops.LaunchTimer.close("cpool_fwd_add", t0)
         del p1
-        ym, stm = _train_bn_conv(s, mod.branchMerge, mod.branchMergeBn, 1, 1, tr)
-        ysc, sts = _train_bn_conv(x, mod.shortcutConv, mod.shortcutBn, 1, 0, tr)
+        if tr:
+            ym, sm = _conv_stats(s, mod.branchMerge, mod.branchMergeBn, 1, 1, tr)
+            ysc, ss = _conv_stats(x, mod.shortcutConv, mod.shortcutBn, 1, 0, tr)
+            Cm, Cs = mod.branchMerge.weight.shape[0], mod.shortcutConv.weight.shape[0]
+            stm, sts = ops.bn_finalize_pair(mod.branchMergeBn, sm, Cm, ym.numel() // Cm, mod.shortcutBn, ss, Cs,
+                                            ysc.numel() // Cs)
+        else:
+            ym, stm = _train_bn_conv(s, mod.branchMerge, mod.branchMergeBn, 1, 1, tr)
+            ysc, sts = _train_bn_conv(x, mod.shortcutConv, mod.shortcutBn, 1, 0, tr)
         r = ops.bn_apply(ym, stm, True, res=ysc, rst=sts)
         yl, stl = _train_bn_conv(r, lc.conv, lc.bn, 1, 1, tr, timer="cpool_lastconv")
         out = ops.bn_apply(yl, stl, True)

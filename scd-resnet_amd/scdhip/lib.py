@@ -73,6 +73,7 @@ SIGNATURES = {
     "scd_stem_wgrad_pooled": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
     "scd_stem_wgrad_combine": (I, [P, I, P, P, P, P, I, P]),
     "scd_stats_collapse": (I, [P, I, I, P]),
+    "scd_stats_collapse_to": (I, [P, I, I, P, P]),
     "scd_bn_finalize": (I, [P, I, I, D, P, P, P, P, P, F, F, P, P, P, P, P]),
     "scd_bn_apply": (I, [I, P, P, I, L, P, P, P, P, P, I, P]),
     "scd_bn_bwd_reduce": (I, [I, P, P, P, P, P, P, P, I, L, P, P]),

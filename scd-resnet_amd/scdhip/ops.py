@@ -211,6 +211,27 @@ def _allreduce_stats(stats, C):
     return 1
 
 
+def _allreduce_stats_pair(sa, Ca, sb, Cb):
+    """Two BN layers whose sums are ready together (a residual join's pair in backward; a block's bn1 and downsample BN
+    in forward): both collapsed side by side into one staging buffer (scd_stats_collapse_to) and all-reduced ONCE --
+    one small collective on the critical path instead of two.  Returns (stats_a, stats_b, nrep) for the finalize."""
+    if _BNSync.group is None:
+        return sa, sb, L.STAT_REPLICAS
+    n = 2 * (Ca + Cb)
+    if _BNSync.peer is not None and n > _BNSync.peer.cap:
+        _allreduce_stats(sa, Ca)
+        _allreduce_stats(sb, Cb)
+        return sa, sb, 1
+    stage = torch.empty(n, dtype=torch.float64, device=sa.device)
+    L.call("scd_stats_collapse_to", ptr(sa), L.STAT_REPLICAS, Ca, ptr(stage), stream())
+    L.call("scd_stats_collapse_to", ptr(sb), L.STAT_REPLICAS, Cb, ptr(stage[2 * Ca:]), stream())
+    if _BNSync.peer is not None:
+        _BNSync.peer.all_reduce(stage)
+    else:
+        dist.all_reduce(stage, group=_BNSync.group)
+    return stage[:2 * Ca], stage[2 * Ca:], 1
+
+
 def new_stats(C, device):
     return torch.zeros(L.STAT_REPLICAS * 2 * C, dtype=torch.float64, device=device)
 
@@ -895,17 +916,40 @@ def bn_finalize(bn, stats, C, count, training=True):
     st.scale = torch.empty(C, device=dev)
     st.shift = torch.empty(C, device=dev)
     if training:
-        nrep = _allreduce_stats(stats, C)
-        count = count * bn_sync_world()
-        L.call("scd_bn_finalize", ptr(stats), nrep, C, float(count), ptr(bn.weight), ptr(bn.bias),
-               ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.num_batches_tracked), float(bn.momentum),
-               float(bn.eps), ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift), stream())
+        return _bn_finalize_launch(bn, st, stats, _allreduce_stats(stats, C), C, count)
     else:
         L.call("scd_bn_finalize", 0, 0, C, 1.0, ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
                ptr(bn.running_var), 0, 0.0, float(bn.eps), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
                ptr(st.shift), stream())
     st.count = count
     return st
+
+
+def _bn_finalize_launch(bn, st, stats, nrep, C, count):
+    count = count * bn_sync_world()
+    L.call("scd_bn_finalize", ptr(stats), nrep, C, float(count), ptr(bn.weight), ptr(bn.bias),
+           ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.num_batches_tracked), float(bn.momentum),
+           float(bn.eps), ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift), stream())
+    st.count = count
+    return st
+
+
+def _bn_state(C, dev):
+    st = BNState()
+    st.mean = torch.empty(C, device=dev)
+    st.invstd = torch.empty(C, device=dev)
+    st.scale = torch.empty(C, device=dev)
+    st.shift = torch.empty(C, device=dev)
+    return st
+
+
+def bn_finalize_pair(bn_a, stats_a, Ca, count_a, bn_b, stats_b, Cb, count_b):
+    """Training-mode bn_finalize of two layers whose statistics are complete together (a block's bn1 and its
+    downsample BN): with SyncBN one all-reduce for both (_allreduce_stats_pair)."""
+    sa, sb, nrep = _allreduce_stats_pair(stats_a, Ca, stats_b, Cb)
+    st_a = _bn_finalize_launch(bn_a, _bn_state(Ca, bn_a.weight.device), sa, nrep, Ca, count_a)
+    st_b = _bn_finalize_launch(bn_b, _bn_state(Cb, bn_b.weight.device), sb, nrep, Cb, count_b)
+    return st_a, st_b
 
 
 def bn_apply(y, st, relu, res=None, rst=None, out=None):
@@ -951,8 +995,9 @@ def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
     L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean), ptr(st_a.invstd),
            ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
     alpha = grad_alpha(y_a)
-    ca = bn_backward_coef(bn_a, st_a, sa, C, alpha)
-    cb = bn_backward_coef(bn_b, st_b, sb, C, alpha)
+    sa, sb, nrep = _allreduce_stats_pair(sa, C, sb, C)
+    ca = _bn_bwd_finalize_launch(bn_a, st_a, sa, nrep, C, alpha)
+    cb = _bn_bwd_finalize_launch(bn_b, st_b, sb, nrep, C, alpha)
     dya, dyb = torch.empty_like(y_a), torch.empty_like(y_b)
     L.call("scd_bn_bwd_apply2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(ca), ptr(cb), C, y_a.numel(),
            ptr(dya), ptr(dyb), stream())
@@ -962,7 +1007,10 @@ def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
 def bn_backward_coef(bn, st, stats, C, alpha=1.0):
     """SyncBN all-reduce of the backward sums, dgamma/dbeta accumulation (times alpha: 1 / the fp16 loss scale)
     and the apply coefficients."""
-    nrep = _allreduce_stats(stats, C)
+    return _bn_bwd_finalize_launch(bn, st, stats, _allreduce_stats(stats, C), C, alpha)
+
+
+def _bn_bwd_finalize_launch(bn, st, stats, nrep, C, alpha):
     coef = torch.empty(3 * C, device=stats.device)
     L.call("scd_bn_bwd_finalize", ptr(stats), nrep, C, float(st.count), ptr(bn.weight), ptr(st.mean),
            ptr(st.invstd), ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), alpha / bn_sync_world(), ptr(coef),
