@@ -195,7 +195,7 @@ class FlatDDP(torch.nn.Module):
     the first backward only learns which they are (post-accumulate hooks) and launches every bucket
     at the end; from then on those parameters are marked by their post-accumulate hook instead."""
 
-    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_mb=25.0):
+    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_mb=25.0, tail_mb=2.0):
         super(FlatDDP, self).__init__()
         self.module = module
         self.group = process_group
@@ -203,6 +203,10 @@ class FlatDDP(torch.nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.flat = ensure_flat(module.parameters())
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
+        # the last bucket is only complete when the backward ends (stem), so it is never overlapped: keep it to the
+        # parameters of the last few layers (<= tail_mb) and launch the rest of what would have been that bucket as
+        # soon as its own parameters are ready
+        self.tail_elems = max(1, int(tail_mb * (1 << 20) / 4))
         self._queued = False
         self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
         self._engine = set()                  # ids of parameters written by torch's AccumulateGrad
@@ -241,10 +245,32 @@ class FlatDDP(torch.nn.Module):
             members.append(id(p))
         self._buckets.append((lo, hi))
         self._bucket_params.append(members)
+        self._split_tail()
         for b, ms in enumerate(self._bucket_params):
             for pid in ms:
                 self._bucket_of[pid] = b
         self._reset_step()
+
+    def _split_tail(self):
+        """Split the last bucket (launch order) so that its final part holds at most tail_elems of parameters."""
+        lo, hi = self._buckets[-1]
+        members = self._bucket_params[-1]
+        K = len(members)
+        if hi - lo <= self.tail_elems or K < 2:
+            return
+        span = {id(p): (o, o + n) for p, (o, n) in zip(self.flat.params, self.flat.offsets)}
+        # members are in launch order (reverse parameter order): member K-1 sits at lo; the tail is the suffix
+        # members[k:], occupying [lo, end of members[k])
+        if span[members[K - 1]][1] - lo > self.tail_elems:
+            return
+        k = K - 1
+        while k > 1 and span[members[k - 1]][1] - lo <= self.tail_elems:
+            k -= 1
+        split = span[members[k]][1]
+        self._buckets[-1] = (split, hi)
+        self._buckets.append((lo, split))
+        self._bucket_params[-1] = members[:k]
+        self._bucket_params.append(members[k:])
 
     def _reset_step(self):
         self._early = 0

@@ -221,3 +221,32 @@ def test_resume_schedule_pops_past_milestones():
             lr /= rates.pop(0)
             decay.pop(0)
     assert abs(lr - 1e-4) < 1e-15
+
+
+def test_flat_ddp_buckets_keep_a_small_tail():
+    """FlatDDP buckets (reverse parameter order, ~25 MB) tile the flat gradient exactly, and the last bucket -- complete
+    only when the backward ends, so never overlapped with it -- holds at most tail_mb of parameters (Res10: layer2,
+    layer1 and the stem), the rest of what would have been that bucket launching as soon as layer3 is done."""
+    import trainer.model.centerOffsetRes10 as plugin
+    from scdhip import flat as F
+
+    class Buckets(F.FlatDDP):
+        def __init__(self, module, bucket_mb=25.0, tail_mb=2.0):
+            torch.nn.Module.__init__(self)
+            self.module = module
+            self.flat = F.ensure_flat(module.parameters())
+            self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
+            self.tail_elems = int(tail_mb * (1 << 20) / 4)
+            self._build_buckets()
+
+    m = plugin.model(**plugin.modelParams)
+    d = Buckets(m)
+    spans = sorted(d._buckets)
+    assert spans[0][0] == 0 and spans[-1][1] == d.flat.data.numel()
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert sum(len(ms) for ms in d._bucket_params) == len(d.flat.params)
+    lo, hi = d._buckets[-1]
+    assert (hi - lo) * 4 <= 2 << 20
+    names = {id(p): n for n, p in m.named_parameters()}
+    assert names[d._bucket_params[-1][-1]].startswith("preprocess")
+    assert len(d._buckets) >= 3
