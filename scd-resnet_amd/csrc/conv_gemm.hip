@@ -104,6 +104,19 @@ __device__ __forceinline__ f32x4 mfma_16x16x16(hx4 a, hx4 b, f32x4 c) {
 #endif
 }
 
+#ifndef PP_DPP
+#define PP_DPP 1      // ping-pong epilogue: BN sums over the 16 pixel lanes with DPP row ops instead of ds_bpermute
+#endif
+
+// sum over the 16 lanes of a DPP row (every lane gets it): quad butterflies, then the half-row and row mirrors
+__device__ __forceinline__ float row16_sum(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
+    return v;
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
 // Buffer-load offset or an out-of-range one (the load then returns zeros).  The offset is made
@@ -1127,8 +1140,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float s = csum[b][r], q = csq[b][r];
+                if constexpr (PP_DPP) {
+                    s = row16_sum(s);
+                    q = row16_sum(q);
+                } else {
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                    for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                }
                 if (l16 == 0) {
                     const int c = wc * WCOLS + b * 16 + lg * 4 + r;
                     red[(grp * BN + c) * 2 + 0] = s;
