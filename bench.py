@@ -286,7 +286,7 @@ def main():
     opt = FlatAdam(filter(lambda p: p.requires_grad, model.parameters()))
     if world > 1:
         if torch.cuda.device_count() > 1 or share:
-            ops.set_bn_sync(dist.group.WORLD)     # SyncBN rule of networkFactory.py:128
+            ops.set_bn_sync(ops.new_bn_group())   # SyncBN rule of networkFactory.py:128, its own communicator
         model = FlatDDP(model)
     lossfn = plugin.loss
 
@@ -371,6 +371,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
     final_loss = loss.item()
+    local_ms = None
+    if world > 1:
+        # after the timed region: the same steps with every collective off (FlatDDP.local_only), max over ranks --
+        # what the exchange (gradient buckets, SyncBN, buffer broadcast) adds to each rank's step, measured in-run
+        with model.local_only():
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            tl = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+        dist.all_reduce(tl, op=dist.ReduceOp.MAX)
+        local_ms = 1e3 * tl.item() / args.steps
 
     if rank == 0:
         imgs = B * world * args.steps
@@ -420,6 +436,12 @@ def main():
             "step_mfma_frac_dense_equiv": round(value * gflop / 1e3 / peak, 4),
             "final_loss": round(final_loss, 5),
         }
+        if local_ms is not None:
+            # in-run split of the N-rank step: the same per-rank work without any collective (not the driver's
+            # cross-run scaling efficiency, which it computes from the per-N values itself)
+            line["exchange"] = {"ddp_ms_per_step": line["ms_per_step"], "local_ms_per_step": round(local_ms, 3),
+                                "local_over_ddp": round(local_ms / line["ms_per_step"], 4),
+                                "syncbn_group": "own communicator (ops.new_bn_group)"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_baseline_steps)
         print(json.dumps(line), flush=True)

@@ -415,7 +415,9 @@ int scd_masked_l1_fwd(const float* r, const float* t, const uint8_t* mask, long 
  * (scd_peer_ipc_handle: 64 bytes) and maps the others' (scd_peer_ipc_open); scd_peer_allreduce_f64 then writes
  * `data` into every mailbox, flags it with `epoch` (1, 2, 3, ... one per call, the same on every rank), waits for
  * all flags and leaves the rank-ordered sum in `data` (identical bits on every rank).  boxes[r] = rank r's mailbox
- * as mapped in this process.  *err is set (and data left unreduced) if a peer's flag is missing after ~0.5 s.
+ * as mapped in this process.  A late peer is waited for up to timeout_ms (a sleeping one-wave poll); if its flag is
+ * still missing then, *err (device, zero-initialised) receives the failing epoch and data is left unreduced.  The
+ * error is sticky: a call that finds *err != 0 does nothing.  The host reads *err once per step (scdhip/peer.py).
  * The allocation entry points are the only ones in this library that allocate. */
 size_t scd_peer_mailbox_bytes(int R, int cap);
 int scd_peer_alloc(size_t bytes, void** ptr);
@@ -424,7 +426,7 @@ int scd_peer_ipc_handle(void* ptr, void* handle64);
 int scd_peer_ipc_open(const void* handle64, void** ptr);
 int scd_peer_ipc_close(void* ptr);
 int scd_peer_allreduce_f64(double* data, int n, int rank, int R, void* const* boxes, int cap, unsigned long long epoch,
-                           int* err, void* stream);
+                           unsigned long long* err, unsigned timeout_ms, void* stream);
 
 /* A HIP stream restricted to `keep` of every `of` compute units (hipExtStreamCreateWithCUMask, the mask spread
  * evenly over the XCDs); used for the weight-gradient side stream when SCD_SIDE_CUS is set.  No reference

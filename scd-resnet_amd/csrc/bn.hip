@@ -10,6 +10,7 @@
 #endif
 
 namespace {
+SCD_KERNEL_NS_BEGIN
 
 // sum replicas into replica 0 and zero the others (buffers are persistent: the consumer re-zeroes)
 __global__ void stats_collapse_kernel(double* stats, int nrep, int n) {
@@ -463,6 +464,7 @@ inline int ew_grid(int resident, long nvec, int cpr) {
 }
 inline int fin_blocks(int C) { return (C + 3) / 4; }   // 4 waves (channels) per 256-thread block
 
+SCD_KERNEL_NS_END
 }  // namespace
 
 extern "C" int scd_stats_collapse(double* stats, int nrep, int C, void* stream) {

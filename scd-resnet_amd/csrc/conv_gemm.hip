@@ -58,6 +58,7 @@
 #endif
 
 namespace {
+SCD_KERNEL_NS_BEGIN
 
 struct GemmParams {
     const char* x;
@@ -2950,6 +2951,7 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st, int ks = 1) {
     SCD_RETURN_LAUNCH();
 }
 
+SCD_KERNEL_NS_END
 }  // namespace
 
 // Kernel choice: the LDS-DMA ring kernel (256x128, bf16) for large outputs, the register-staged

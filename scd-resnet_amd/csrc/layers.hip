@@ -6,6 +6,7 @@
 #include "scd_common.h"
 
 namespace {
+SCD_KERNEL_NS_BEGIN
 
 // ---------------------------------------------------------------- weight packing
 template <typename T>
@@ -679,6 +680,7 @@ __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, lo
 
 inline int ew_blocks(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + 255) / 256)); }
 
+SCD_KERNEL_NS_END
 }  // namespace
 
 extern "C" int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp, int row_off,
@@ -940,6 +942,7 @@ extern "C" int scd_heads_bwd_packed_split(int dtype, const void* hid, int N, int
 // slotmap (pixel -> slot, -1 elsewhere) and ownermap (q -> first (slot, tap) reaching q, INT_MAX elsewhere) are
 // persistent int32 maps over the N*H*W pixels; the kernels below leave them as they found them.
 namespace {
+SCD_KERNEL_NS_BEGIN
 constexpr int SP_SPB = 2;                   // slots per workgroup of the sparse tail
 
 template <typename T>
@@ -1101,6 +1104,7 @@ __global__ void heads_sparse_reset_kernel(const long* inds, int S, int K, int HW
     if (slotmap[p] == s) slotmap[p] = -1;
 }
 
+SCD_KERNEL_NS_END
 }  // namespace
 
 extern "C" int scd_heads_sparse_bwd(int dtype, const void* hid, const void* feat, int N, int H, int W, int Cin, int nh,

@@ -6,6 +6,7 @@
 #include "scd_common.h"
 
 namespace {
+SCD_KERNEL_NS_BEGIN
 
 __global__ __launch_bounds__(256) void pad_channels_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                            long rows, int cv, int cpv) {
@@ -17,6 +18,7 @@ __global__ __launch_bounds__(256) void pad_channels_kernel(const uint4* __restri
     }
 }
 
+SCD_KERNEL_NS_END
 }  // namespace
 
 extern "C" int scd_pad_channels(int dtype, const void* src, long rows, int C, int Cp, void* dst, void* stream) {

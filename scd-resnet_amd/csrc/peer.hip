@@ -5,7 +5,11 @@
 // mailbox, raises its flag (the call's epoch) in each, waits for all flags in its own mailbox and sums the slots in
 // rank order -- the same bits on every rank.  Slots alternate by epoch parity, so a fast rank's next call never
 // overwrites a slot a slow rank is still summing (a rank can only be one call ahead: it waits for everyone's flag).
-// The wait gives up after ~0.5 s and reports it (*err), so a missing peer cannot hang the GPU.
+// A slow rank is not an error: the wait is bounded only by `timeout_ms` (the host's SCD_PEER_TIMEOUT_S, 120 s by
+// default -- longer than a checkpoint write or a validation pass on one rank), sleeping between polls so it holds one
+// wave.  A peer that never comes (a dead process) ends the wait: the kernel records the failing epoch in *err and
+// leaves `data` unreduced.  The error is sticky: every later call sees *err != 0 and does nothing (no mailbox writes,
+// no waits), so the ranks cannot drift into reading slots of different epochs, and the host raises on its next poll.
 // Mailbox layout: [2 parities][R slots][cap doubles] then [R] 64-bit flags.
 #include <string.h>
 
@@ -24,9 +28,12 @@ __device__ __forceinline__ unsigned long long* flags_of(double* box, int R, int 
 }
 
 __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* data, int n, int rank, int R, Boxes b, int cap,
-                                                             unsigned long long epoch, int* err) {
+                                                             unsigned long long epoch, unsigned long long* err,
+                                                             unsigned long long timeout_ticks) {
     const int tid = threadIdx.x;
     const int par = (int)(epoch & 1ull);
+    // sticky failure: an earlier call timed out, every later call is a no-op
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;
     // 1. this rank's vector into slot `rank` of every mailbox (remote stores over xGMI for the peers)
     for (int p = 0; p < R; ++p) {
         double* dst = b.box[p] + ((size_t)par * R + rank) * cap;
@@ -43,17 +50,20 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* data, int n
     if (tid < R) {
         unsigned long long* f = flags_of(b.box[rank], R, cap) + tid;
         const unsigned long long t0 = wall_clock64();
+        unsigned polls = 0;
         while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-            if (wall_clock64() - t0 > 50000000ull) {             // ~0.5 s at the 100 MHz constant clock
+            if (wall_clock64() - t0 > timeout_ticks) {           // wall_clock64: 100 MHz constant clock
                 timed_out = 1;
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            // tight polling for the common microsecond-scale skew, then back off (a rank seconds late)
+            if (++polls < 4096) __builtin_amdgcn_s_sleep(2);
+            else __builtin_amdgcn_s_sleep(127);
         }
     }
     __syncthreads();
     if (timed_out) {
-        if (tid == 0) *err = 1;
+        if (tid == 0) atomicCAS(err, 0ull, epoch);             // the first failing epoch
         return;
     }
     __threadfence_system();
@@ -96,12 +106,13 @@ extern "C" int scd_peer_ipc_open(const void* handle64, void** ptr) {
 extern "C" int scd_peer_ipc_close(void* ptr) { return ptr ? (int)hipIpcCloseMemHandle(ptr) : 0; }
 
 extern "C" int scd_peer_allreduce_f64(double* data, int n, int rank, int R, void* const* boxes, int cap,
-                                      unsigned long long epoch, int* err, void* stream) {
+                                      unsigned long long epoch, unsigned long long* err, unsigned timeout_ms,
+                                      void* stream) {
     if (!data || !boxes || !err || R < 1 || R > PEER_MAX || rank < 0 || rank >= R || n < 0 || n > cap || epoch == 0)
         return SCD_ERR_ARG;
     Boxes b;
     for (int i = 0; i < PEER_MAX; ++i) b.box[i] = i < R ? (double*)boxes[i] : nullptr;
     hipLaunchKernelGGL(peer_allreduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, data, n, rank, R, b, cap,
-                       epoch, err);
+                       epoch, err, (unsigned long long)timeout_ms * 100000ull);
     SCD_RETURN_LAUNCH();
 }

@@ -59,6 +59,17 @@
 
 #include "../../include/scdhip.h"
 
+// The fp16 build's kernels sit in an inline namespace `f16` inside each file's anonymous namespace, so their symbol
+// names (and the rocprofv3 kernel names) differ from the bf16 build's even where a kernel is not templated on the
+// 16-bit type (tools/prof_summary.py labels them by it).
+#ifdef SCD_F16_BUILD
+#define SCD_KERNEL_NS_BEGIN inline namespace f16 {
+#define SCD_KERNEL_NS_END }
+#else
+#define SCD_KERNEL_NS_BEGIN
+#define SCD_KERNEL_NS_END
+#endif
+
 #ifdef SCD_F16_BUILD
 #define SCD_F16_FWD(fn, ...) ((void)0)
 #else

@@ -11,6 +11,7 @@
 #include "scd_common.h"
 
 namespace {
+SCD_KERNEL_NS_BEGIN
 
 constexpr int KS = 7, KK = 49, SP = 2, PD = 3, CO = 64;
 
@@ -792,6 +793,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_combine_kernel(const float* __
     }
 }
 
+SCD_KERNEL_NS_END
 }  // namespace
 
 extern "C" int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H,

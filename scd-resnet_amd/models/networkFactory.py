@@ -154,7 +154,9 @@ class NetworkFactory(object):
         torch.cuda.set_stream(torch.cuda.Stream(device=self.device, priority=-10))
         self.cuda()
         if distributed and self.GPUCOUNT > 1 and dist.get_world_size() > 1:
-            ops.set_bn_sync(dist.group.WORLD)       # SyncBatchNorm semantics (networkFactory.py:128-133)
+            # SyncBatchNorm semantics (networkFactory.py:128-133) on a group of its own: its critical-path all-reduces
+            # must not queue behind FlatDDP's gradient buckets on WORLD's RCCL stream (ops.new_bn_group)
+            ops.set_bn_sync(ops.new_bn_group())
         self.model = FlatDDP(self.model)
         if defaultConfig.stepGraph and not (distributed and dist.get_world_size() > 1):
             self.stepGraph = StepGraph(self._trainStep, optimizer=self.optimizer, warmup=2)

@@ -14,6 +14,7 @@
   joins every bucket; BN buffers are broadcast from rank 0 before each forward (DDP
   broadcast_buffers=True, coalesced per dtype); state_dict keys keep the ``module.`` prefix.
 """
+import contextlib
 import weakref
 
 import torch
@@ -112,6 +113,10 @@ class FlatAdam(torch.optim.Optimizer):
         """Write the param group's lr to the device state if setLearningRate changed it (a captured step graph
         calls this before each replay; the eager step does it itself)."""
         lr = self.param_groups[0]["lr"]
+        # never recorded into a step graph: a captured fill would write this lr back on every replay, after the
+        # replay-time sync (ADVICE r2 graph.py:66)
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return
         if self._hyper is not None and lr != self._dev_lr:
             self._hyper[0].fill_(lr)
             self._dev_lr = lr
@@ -195,11 +200,15 @@ class FlatDDP(torch.nn.Module):
     the first backward only learns which they are (post-accumulate hooks) and launches every bucket
     at the end; from then on those parameters are marked by their post-accumulate hook instead."""
 
-    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_mb=25.0, tail_mb=2.0):
+    def __init__(self, module, process_group=None, broadcast_buffers=True, bucket_mb=25.0, tail_mb=2.0,
+                 force_collectives=False):
         super(FlatDDP, self).__init__()
         self.module = module
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # force_collectives: run the whole exchange (hooks, bucket all-reduces from the side stream, waits, buffer
+        # broadcasts) even in a world of one -- the RCCL path's test on a one-GPU box (tests/test_ddp_gpu.py)
+        self._comm = dist.is_initialized() and (self.world > 1 or force_collectives)
         self.broadcast_buffers = broadcast_buffers
         self.flat = ensure_flat(module.parameters())
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) / 4))
@@ -214,7 +223,7 @@ class FlatDDP(torch.nn.Module):
         self.early_launches = 0               # buckets launched from inside backward, last backward
         self._build_buckets()
         self._hooks = []
-        if self.world > 1:
+        if self._comm:
             for m in module.modules():
                 if any(p.requires_grad for p in m.parameters()):
                     self._hooks.append(m.register_forward_pre_hook(self._pre_hook))
@@ -315,6 +324,8 @@ class FlatDDP(torch.nn.Module):
         self._launch_ready()
 
     def _written(self, modules):
+        if not self._comm:
+            return
         for m in modules:
             for p in m.parameters():
                 if id(p) not in self._engine:
@@ -322,13 +333,15 @@ class FlatDDP(torch.nn.Module):
         self._launch_ready()
 
     def _acc_hook(self, p):
+        if not self._comm:
+            return
         self._engine.add(id(p))
         if self._learned:
             self._mark(id(p))
             self._launch_ready()
 
     def _pre_hook(self, module, args):
-        if not (self.training and torch.is_grad_enabled()):
+        if not (self._comm and self.training and torch.is_grad_enabled()):
             return None
         for a in args:
             if torch.is_tensor(a) and a.requires_grad:
@@ -350,7 +363,7 @@ class FlatDDP(torch.nn.Module):
 
     def _allreduce_grads(self):
         self._queued = False
-        if self.world == 1:
+        if not self._comm:
             return
         if self.flat.grad.is_cuda:
             # every gradient written on scdhip's side stream is ordered before the remaining buckets
@@ -365,14 +378,32 @@ class FlatDDP(torch.nn.Module):
                 self.flat.grad[lo:hi].div_(self.world)
         self._learned = True
         self._reset_step()
+        if self.flat.grad.is_cuda:
+            from . import ops
+            ops.bn_sync_poll()                      # peer-memory SyncBN: raise on a failed call (non-blocking)
+
+    @contextlib.contextmanager
+    def local_only(self):
+        """Steps inside run this rank's shard with no collective at all (no gradient buckets, no buffer broadcast, no
+        SyncBN): bench.py times them beside the data-parallel steps to separate the exchange's cost from the
+        per-GPU work.  The replicas diverge meanwhile; broadcast the parameters again before training on."""
+        from . import ops
+        was = self._comm
+        self._comm = False
+        try:
+            with ops.bn_sync_suspended():
+                yield
+        finally:
+            self._comm = was
+            self._reset_step()
 
     def forward(self, *args, **kwargs):
-        if self.world > 1 and self.broadcast_buffers and self.training:
+        if self._comm and self.broadcast_buffers and self.training:
             self._sync_buffers()
-        if self.world > 1:
+        if self._comm:
             self._reset_step()
         out = self.module(*args, **kwargs)
-        if not torch.is_grad_enabled() or self.world == 1:
+        if not torch.is_grad_enabled() or not self._comm:
             return out
         # route every differentiable output tensor through the end-of-backward hook
         flat, spec = _flatten(out)

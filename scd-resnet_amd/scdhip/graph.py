@@ -68,6 +68,8 @@ class StepGraph:
             self.static_args = tuple(_clone(a) for a in args)
         else:
             self.static_args = ()
+        if self.optimizer is not None:
+            self.optimizer.sync_lr()        # the lr is device state the captured Adam reads; set it outside capture
         torch.cuda.synchronize()
         host_step = getattr(self.optimizer, "_step", None)
         for _ in range(self.copies):

@@ -124,7 +124,7 @@ SIGNATURES = {
     "scd_peer_ipc_handle": (I, [P, P]),
     "scd_peer_ipc_open": (I, [P, PP]),
     "scd_peer_ipc_close": (I, [P]),
-    "scd_peer_allreduce_f64": (I, [P, I, I, I, PP, I, ctypes.c_ulonglong, P, P]),
+    "scd_peer_allreduce_f64": (I, [P, I, I, I, PP, I, ctypes.c_ulonglong, P, ctypes.c_uint, P]),
     "scd_stream_create_cumask": (I, [I, I, PP]),
     "scd_stream_destroy": (I, [P]),
     "scd_event_create": (I, [PP]),

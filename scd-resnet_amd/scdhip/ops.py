@@ -4,6 +4,7 @@ Layouts: activations NHWC (channels innermost) in the compute dtype (fp32 parity
 bf16 performance mode); weights, grads, BN parameters fp32 in the reference layout.
 Every wrapper enqueues on torch's current HIP stream and never synchronises.
 """
+import contextlib
 import ctypes
 import math
 import os
@@ -176,9 +177,19 @@ class _BNSync:
     peer = None           # scdhip.peer.PeerAllReduce when the peer-memory path is on
 
 
+def new_bn_group():
+    """A process group of every rank, for the SyncBN statistics only (networkFactory.py:128-134 runs SyncBatchNorm
+    and DDP as independent collectives).  With the nccl backend (RCCL) each group owns its communicator and its
+    stream, so a critical-path SyncBN all-reduce issued from the compute stream never queues behind a gradient
+    bucket that FlatDDP issued on WORLD from the weight-gradient side stream.  Collective: every rank calls it,
+    once, before FlatDDP is built."""
+    return dist.new_group(ranks=list(range(dist.get_world_size())))
+
+
 def set_bn_sync(group, peer=None):
-    """Enable global-batch BN statistics (SyncBatchNorm, networkFactory.py:128-133).  peer=True (or
-    SCD_SYNCBN_PEER=1) all-reduces them over peer memory (scdhip/peer.py) instead of through torch.distributed."""
+    """Enable global-batch BN statistics (SyncBatchNorm, networkFactory.py:128-133) over `group` (use
+    new_bn_group(), not WORLD, beside FlatDDP).  peer=True (or SCD_SYNCBN_PEER=1) all-reduces them over peer memory
+    (scdhip/peer.py) instead of through torch.distributed."""
     if _BNSync.peer is not None:
         _BNSync.peer.close()
         _BNSync.peer = None
@@ -193,6 +204,27 @@ def set_bn_sync(group, peer=None):
 
 def bn_sync_peer():
     return _BNSync.peer
+
+
+@contextlib.contextmanager
+def bn_sync_suspended():
+    """Local BN statistics inside (FlatDDP.local_only); the group and the peer mailboxes are kept."""
+    saved = (_BNSync.group, _BNSync.world, _BNSync.peer)
+    _BNSync.group, _BNSync.world, _BNSync.peer = None, 1, None
+    try:
+        yield
+    finally:
+        _BNSync.group, _BNSync.world, _BNSync.peer = saved
+
+
+def bn_sync_group():
+    return _BNSync.group
+
+
+def bn_sync_poll():
+    """Once per step: raise if a peer-memory SyncBN call has failed (non-blocking, scdhip/peer.py)."""
+    if _BNSync.peer is not None:
+        _BNSync.peer.poll()
 
 
 def bn_sync_world():
@@ -603,10 +635,13 @@ def branch_join(s, *tensors):
 # A feature map read by several scdhip Functions (the CornerNet feature: the heatmap head and the TL / BR corner
 # pools, cornerNetCPool.py:163-199) would get one input gradient from each, which autograd then sums with
 # elementwise adds (2 x 805 MB of HBM traffic per step at B=32).  share_grad registers the consumers in forward;
-# in backward the first one to run allocates the gradient buffer and returns it, the others accumulate their
-# input-gradient GEMMs into it (accumulate epilogue) and return None (autograd adds nothing for None), so the sum
-# is complete when the producer's backward runs (it waits for every consumer).  A slot never matches a later step:
-# the next registration clears it, and keys carry data pointer, shape and version.
+# in backward the first one to run allocates the gradient buffer, the others accumulate their input-gradient GEMMs
+# into it (accumulate epilogue); every consumer but the LAST returns None (autograd adds nothing for None) and the
+# last returns the finished sum, so autograd never holds a partial buffer that a later consumer still adds into (an
+# extra non-scdhip consumer of the feature -- another loss term, a hook -- is summed with the complete gradient,
+# ADVICE r2 ops.py:630).  A consumer registered in forward whose backward never runs would leave the sum unreturned:
+# the end-of-backward check raises instead of dropping it.  A slot never matches a later step: the next
+# registration clears it, and keys carry data pointer, shape and version.
 
 class SharedGrad:
     enabled = os.environ.get("SCD_SHARED_GRAD", "1") != "0"
@@ -627,16 +662,25 @@ def shared_grad_slot(t):
     return _SHARED_GRAD.get(_tkey(t)) if _SHARED_GRAD else None
 
 
+def _shared_grad_check(key, slot):
+    if slot[0] > 0 and _SHARED_GRAD.get(key) is slot:
+        _SHARED_GRAD.pop(key, None)
+        raise RuntimeError("scdhip: %d consumer(s) of a shared feature gradient never ran backward; the partial sum "
+                           "was not handed to autograd (ops.share_grad)" % slot[0])
+
+
 def shared_grad_out(t, slot, grad):
     """Record that this consumer has written its part; grad: the buffer it allocated (first consumer) or None.
-    Returns what the consumer's backward hands autograd for t."""
-    first = slot[1] is None
-    if first:
+    Returns what the consumer's backward hands autograd for t: the complete sum from the last consumer, else None."""
+    key = _tkey(t)
+    if slot[1] is None:
         slot[1] = grad
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _shared_grad_check(key, slot))
     slot[0] -= 1
     if slot[0] <= 0:
-        _SHARED_GRAD.pop(_tkey(t), None)
-    return grad if first else None
+        _SHARED_GRAD.pop(key, None)
+        return slot[1]
+    return None
 
 
 def mark_bn_bwd_fused(bn, grad):

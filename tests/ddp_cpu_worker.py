@@ -127,12 +127,35 @@ def check(rank, world, bucket_mb):
             assert torch.allclose(p.grad, expected[k], atol=1e-6), (k, p.grad, expected[k])
 
 
+def check_bn_group(rank, world):
+    """SyncBN statistics get a process group of their own (ops.new_bn_group), distinct from the WORLD group FlatDDP
+    all-reduces gradient buckets on: with RCCL every group has its own communicator and stream, so the critical-path
+    statistics never queue behind a bucket (networkFactory.py:128-134)."""
+    from scdhip import ops
+    g = ops.new_bn_group()
+    ops.set_bn_sync(g)
+    try:
+        assert ops.bn_sync_group() is g
+        assert g is not dist.group.WORLD and g != dist.distributed_c10d._get_default_group()
+        assert dist.get_world_size(g) == world and dist.get_rank(g) == rank
+        ddp = FlatDDP(Toy())
+        assert ddp.group is None or ddp.group is dist.group.WORLD
+        assert ops.bn_sync_group() is not (ddp.group or dist.distributed_c10d._get_default_group())
+        assert ops.bn_sync_world() == world
+        t = torch.full((4,), float(rank + 1), dtype=torch.float64)
+        dist.all_reduce(t, group=g)
+        assert torch.all(t == world * (world + 1) / 2)
+    finally:
+        ops.set_bn_sync(None)
+
+
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     for bucket_mb in (25.0, 1e-5):                     # one bucket / one bucket per parameter
         check(rank, world, bucket_mb)
     check_early_buckets(rank, world)
+    check_bn_group(rank, world)
     dist.barrier()
     dist.destroy_process_group()
     print("OK rank", rank)

@@ -26,7 +26,7 @@ def main():
     m = plugin.model(**plugin.modelParams)
     m.load_state_dict(O.hash_weights(entries))
     m = m.cuda().train().set_compute_dtype(torch.float32)
-    ops.set_bn_sync(dist.group.WORLD)          # SCD_SYNCBN_PEER=1: statistics over peer memory (scdhip/peer.py)
+    ops.set_bn_sync(ops.new_bn_group())        # SCD_SYNCBN_PEER=1: statistics over peer memory (scdhip/peer.py)
     peer = ops.bn_sync_peer()
     assert (peer is not None) == (os.environ.get("SCD_SYNCBN_PEER") == "1")
     if peer is not None:

@@ -196,3 +196,33 @@ def test_integration_md_binding_stub_runs():
     x = torch.randn(2, 9, 7, 16, device="cuda")
     y = ns["TopPoolFunction"].apply(x)
     torch.testing.assert_close(y, ops.cpool_fwd(x, 0), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("extra", [False, True])
+def test_shared_feature_gradient_with_extra_consumer(extra):
+    """The backbone feature feeds three scdhip Functions (heatmap head, TL / BR pools) that share one input-gradient
+    buffer (ops.share_grad).  With an extra plain-ATen consumer of the same feature (another loss term) the gradient
+    must still be the full sum: the shared path against the same step with sharing off (autograd sums every
+    consumer's gradient itself).  ADVICE r2 ops.py:630."""
+    from scdhip import ops
+    x = T.batch_inputs(61, 2, 128).to(DEV)
+    ys = [y.to(DEV) for y in T.corner_targets(62, 2, 32)]
+    grads = []
+    for shared in (True, False):
+        ops.SharedGrad.enabled = shared
+        try:
+            m, plugin, _, _ = _model()
+            feat = m.backbone_forward(x)
+            outs = m.heads_forward(feat)
+            loss, _ = plugin.loss([outs], ys)
+            loss = loss.sum()
+            if extra:
+                loss = loss + 1e-3 * (feat.float() * torch.linspace(-1, 1, feat.shape[-1], device=DEV)).square().sum()
+            loss.backward()
+            torch.cuda.synchronize()
+            grads.append({k: p.grad.detach().double().cpu() for k, p in m.named_parameters()})
+        finally:
+            ops.SharedGrad.enabled = True
+    for k, r in grads[1].items():
+        e = ((grads[0][k] - r).norm() / (r.norm() + 1e-30)).item()
+        assert e < 1e-5, (k, e)

@@ -10,20 +10,20 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("peer", [False, True])
-def test_syncbn_ddp_world2_matches_reference(peer):
-    """F7 with the SyncBN statistics through torch.distributed, and (peer) through the peer-memory one-shot
-    all-reduce (scdhip/peer.py: IPC-mapped mailboxes, flag-synchronised kernel) -- same golden vectors."""
+def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2",
-               PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, "scd-resnet_amd")]),
-               SCD_SYNCBN_PEER="1" if peer else "0")
-    worker = os.path.join(REPO, "tests", "ddp_gpu_worker.py")
+    return port
+
+
+def _run(worker, world, **extra):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
+               PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, "scd-resnet_amd")]), **extra)
+    worker = os.path.join(REPO, "tests", worker)
     procs = [subprocess.Popen([sys.executable, worker], env=dict(env, RANK=str(r), LOCAL_RANK="0"),
-                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(2)]
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
     outs = []
     for p in procs:
         try:
@@ -35,6 +35,31 @@ def test_syncbn_ddp_world2_matches_reference(peer):
         outs.append(out.decode()[-3000:])
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o
+    return outs
+
+
+@pytest.mark.parametrize("peer", [False, True])
+def test_syncbn_ddp_world2_matches_reference(peer):
+    """F7 with the SyncBN statistics through torch.distributed, and (peer) through the peer-memory one-shot
+    all-reduce (scdhip/peer.py: IPC-mapped mailboxes, flag-synchronised kernel) -- same golden vectors."""
+    outs = _run("ddp_gpu_worker.py", 2, SCD_SYNCBN_PEER="1" if peer else "0")
+    for o in outs:
         assert "OK rank" in o, o
     if peer:
         print([line for o in outs for line in o.splitlines() if "per call" in line])
+
+
+def test_rccl_world1_flatddp_syncbn():
+    """The nccl (RCCL) backend executed: SyncBN on its own communicator, FlatDDP's AVG buckets from the side stream,
+    async waits -- one step equal to the step without collectives (tests/rccl_gpu_worker.py)."""
+    outs = _run("rccl_gpu_worker.py", 1)
+    assert "OK rccl world1" in outs[0], outs[0]
+    print([line for line in outs[0].splitlines() if "OK rccl" in line])
+
+
+def test_peer_syncbn_late_rank_and_sticky_error():
+    """A rank 2 s late on the host is waited for (no error); a peer missing past the timeout gives a sticky error that
+    poll()/check() raise (tests/peer_gpu_worker.py; ADVICE r2 peer.hip:47)."""
+    outs = _run("peer_gpu_worker.py", 2)
+    for o in outs:
+        assert "OK rank" in o, o

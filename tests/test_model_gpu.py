@@ -124,12 +124,18 @@ def test_f3_train_step(golden):
     opt.step()
     torch.cuda.synchronize()
     np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-4)
+    rel = {}
     for k, p in m.named_parameters():
-        np.testing.assert_allclose(grads[k].double().norm().item(), g["gnorm|" + k], rtol=1e-2, atol=1e-6,
-                                   err_msg=k)
+        ref = float(g["gnorm|" + k])
+        rel[k] = abs(grads[k].double().norm().item() - ref) / max(ref, 1e-6)
         pos = _pos(k, p.numel(), 16)
         np.testing.assert_allclose(p.detach().cpu().reshape(-1)[pos].numpy(), g["psamp|" + k], rtol=1e-4,
                                    atol=2e-5, err_msg=k)
+    worst = sorted(rel.items(), key=lambda kv: -kv[1])[:4]
+    print("F3 worst gradient-norm relative errors:", worst)
+    # fp32 parity mode against the reference's CPU step (summation order differs: MFMA tiles, split-K, fp64 BN
+    # sums); was rtol 1e-2 through round 2
+    assert worst[0][1] < 1e-3, worst
 
 
 def test_bf16_forward_close_to_fp32(f1_outputs):

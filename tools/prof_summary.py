@@ -13,8 +13,15 @@ from collections import defaultdict
 _TY = {"DF16b": "bf16", "DF16_": "f16", "f": "f32"}
 
 
+def _half(name):
+    """The 16-bit type of a kernel that is not templated on it: the fp16 build's kernels live in the inline
+    namespace `f16` (csrc/scd_common.h SCD_KERNEL_NS_BEGIN)."""
+    return "f16" if ("f16::" in name or "_GLOBAL__N_13f16" in name) else "bf16"
+
+
 def short(name):
-    n = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", name)
+    half = _half(name)
+    n = re.sub(r"_ZN12_GLOBAL__N_1(3f16)?\d+", "", name)
     m = re.match(r"(\w+?)I(DF16b|DF16_|f)Li(\d+)ELi(\d+)E(Lb([01])E)?", n)
     if m:
         tail = ""
@@ -24,20 +31,25 @@ def short(name):
     m = re.match(r"(\w+?)I(DF16b|DF16_|f)E", n)
     if m:
         return "%s<%s>" % (m.group(1), _TY[m.group(2)])
-    n = n.replace("(anonymous namespace)::", "")
+    n = n.replace("(anonymous namespace)::", "").replace("f16::", "")
     m = re.search(r"conv_gemm_pp_kernel<(\d+)(, (true|false))?>", n)
     if m:
-        return "conv_gemm_pp_kernel<bf16,256,%s%s>" % (m.group(1), ",heads" if m.group(3) == "true" else "")
+        return "conv_gemm_pp_kernel<%s,256,%s%s>" % (half, m.group(1), ",heads" if m.group(3) == "true" else "")
     m = re.search(r"(conv_gemm_halo_kernel|conv_wgrad_pp_kernel)<([\d, ]+)>", n)
     if m:
         return "%s<%s>" % (m.group(1), m.group(2).replace(" ", ""))
-    m = re.search(r"conv_gemm_ring_kernel(ILb([01])E|<(true|false)>)", n)
+    m = re.search(r"conv_gemm_ring_kernel<(true|false)(, (true|false))?>", n)
     if m:
-        return "conv_gemm_ring_kernel<bf16,256,128%s>" % (",heads" if m.group(2) == "1" or m.group(3) == "true" else "")
+        return "conv_gemm_ring_kernel<%s,256,128%s%s>" % (half, ",heads" if m.group(1) == "true" else "",
+                                                          ",bnbwd" if m.group(3) == "true" else "")
+    m = re.search(r"conv_gemm_pp_kernel<(\d+), (true|false)>", n)
+    if m:
+        return "conv_gemm_pp_kernel<%s,256,%s%s>" % (half, m.group(1), ",heads" if m.group(2) == "true" else "")
     m = re.match(r"(\w+?)ENS_\d+\w*Params", n)         # mangled, non-template kernels of the anonymous namespace
     if m:
-        return m.group(1)
-    return n.split("(")[0][:80]
+        n = m.group(1)
+    n = n.split("(")[0][:80]
+    return n + " [f16]" if half == "f16" and "<" not in n else n
 
 
 def rows_from(path):
