@@ -1965,13 +1965,23 @@ struct WgradParams {
     int dh[SCD_MAX_TAPS], dw[SCD_MAX_TAPS];
 };
 
-// 1-D grid of ntiles * nsplit8 blocks (nsplit8 = nsplit rounded up to 8): block b -> XCD b % 8,
-// split z = 8 * ((b / 8) / ntiles) + b % 8, tile (b / 8) % ntiles.  Returns false for padding blocks.
+// 1-D grid.  nsplit % 8 == 0: ntiles * nsplit blocks, block b -> XCD b % 8, split z = 8 * ((b / 8) / ntiles) + b % 8,
+// tile (b / 8) % ntiles (every tile of split z on one XCD: the tiles re-reading the split's pixel rows share its L2).
+// Otherwise (few splits of many tiles, whose operands sit in L2 / MALL anyway: layer4, deconv1): ntiles * nsplit
+// blocks, tile b % ntiles, split b / ntiles, so one round of workgroups fills every XCD.  Returns false for padding.
 __device__ __forceinline__ bool wgrad_block(const WgradParams& p, int& z, int& mt, int& nt) {
     const int T = p.ntm * p.ntn;
+    int tile;
+    if (p.nsplit & 7) {
+        z = blockIdx.x / T;
+        tile = blockIdx.x - z * T;
+        mt = tile / p.ntn;
+        nt = tile - mt * p.ntn;
+        return z < p.nsplit;
+    }
     const int j = blockIdx.x >> 3;
     z = 8 * (j / T) + (blockIdx.x & 7);
-    const int tile = j - (j / T) * T;
+    tile = j - (j / T) * T;
     mt = tile / p.ntn;
     nt = tile - mt * p.ntn;
     return z < p.nsplit;
@@ -2662,8 +2672,8 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     constexpr int KP = 64, EPC = 8;
     constexpr int QIMG = KP * 64;                     // one G quarter image: 64 px x 64 B
     constexpr int GBYTES = 2 * NQ * QIMG;             // 2 groups x NQ quarters
-    constexpr int WIN = 64 * NQ;                      // channels per window (256 or 192)
-    static_assert(NQ == 3 || NQ == 4, "NQ");
+    constexpr int WIN = 64 * NQ;                      // channels per window (256, 192 or 128)
+    static_assert(NQ >= 2 && NQ <= 4, "NQ");
     constexpr int STAGE = GBYTES + KP * 512;          // + X image
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
@@ -2686,7 +2696,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         const int c = 2 * ((slot >> 1) ^ ((g_r >> 3) & 1)) + (slot & 1);
         g_off = cbase + c * EPC;
     }
-    // X DMA: instruction k = 4*wave + j covers rows 2k, 2k+1; per slot constants (FASTX 1 addressing)
+    // X DMA: instruction k = 4*wave + j covers rows 2k, 2k+1; per slot constants.  A stage is 64 pixels of one
+    // output row (Wo % 64 == 0) or 64 / Wo whole rows (64 % Wo == 0): pixel r of a stage sits at row r / Wo, column
+    // r % Wo from the stage cursor either way (r < Wo in the first case)
     int x_r[4], xA[4], xB[4], xL[4];
     bool x_ok[4];
 #pragma unroll
@@ -2698,11 +2710,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         x_ok[j] = kk < p.KK;
         const int tap = x_ok[j] ? kk / p.Ci : 0;
         const int ci = kk - tap * p.Ci;
+        const int doh = r / p.Wo, dow = r - doh * p.Wo;
         x_r[j] = r;
-        xA[j] = p.dh[tap];
-        xB[j] = p.is * r + p.dw[tap];
+        xA[j] = p.is * doh + p.dh[tap];
+        xB[j] = p.is * dow + p.dw[tap];
         xL[j] = (xA[j] * p.Wi + xB[j]) * p.Ci + ci;
     }
+    const int rows_per_wrap = p.Wo >= KP ? 1 : KP / p.Wo;    // output rows a stage advances when it wraps
     int sn, soh, sow;
     {
         const int HoWo = p.Ho * p.Wo;
@@ -2715,7 +2729,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         sow += KP;
         const bool wrap = sow >= p.Wo;
         sow = wrap ? 0 : sow;
-        soh += wrap ? 1 : 0;
+        soh += wrap ? rows_per_wrap : 0;
         const bool wrap2 = soh >= p.Ho;
         soh = wrap2 ? 0 : soh;
         sn += wrap2 ? 1 : 0;
@@ -2817,7 +2831,10 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         if (grp == 1) bar();
         // schedule (stage t fetches stage t+1 into the other buffer): phase 1: X half 0, phase 2: X half 1,
         // phases 3(-4): the G quarters.  NQ 4: C2 vmcnt(4), L4 vmcnt(4), C4 vmcnt(2);
-        // NQ 3: C1 vmcnt(3), C2 vmcnt(4), L3 vmcnt(3), C3 vmcnt(2)
+        // NQ 3: C1 vmcnt(3), C2 vmcnt(4), L3 vmcnt(3), C3 vmcnt(2);
+        // NQ 2 (128-channel windows: the heatmap head, layer2): phase 1 issues all six DMAs of stage t+1 (X halves,
+        // both G quarters), so they land across both phases; every wave's fragment reads are drained before the
+        // phase-2 barrier (the partner group, one barrier ahead, then overwrites that buffer's G quarters), C2 vmcnt(0)
         for (int t = 0; t < nk; ++t) {
             char* cur = smem + (t & 1) * STAGE;
             char* nxt = smem + ((t & 1) ^ 1) * STAGE;
@@ -2827,6 +2844,15 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
                 bf16x8 (&gf)[2][2] = (q & 1) ? gfy : gfx;
                 if (q == 0) read_x(cur);
                 read_g(cur, q, gf);
+                if constexpr (NQ == 2) {
+                    if (q == 0) { issue_x(k1, nxt, 0); issue_x(k1, nxt, 1); issue_g(k1, nxt, 0); issue_g(k1, nxt, 1); }
+                    if (q == 1) { advance(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+                    bar();
+                    mfma_q(q, gf);
+                    if (q == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    bar();
+                    continue;
+                }
                 if (q < 2) issue_x(k1, nxt, q);
                 if constexpr (NQ == 4) {
                     if (q == 2) { issue_g(k1, nxt, 0); issue_g(k1, nxt, 1); }
@@ -2863,38 +2889,245 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     }
 }
 
-// Split reduction of the weight-gradient slabs (HBM-bound: nsplit slab reads of 4 B per weight).  Every
-// thread owns 4 consecutive fp32 columns of one slab row and keeps 8 independent 16-B slab loads in flight;
-// the summation order is fixed (accumulator j takes slabs j, j+8, ..., then a fixed pairwise tree), so the
-// result does not depend on the launch geometry.
-__device__ __forceinline__ f32x4 wred_sum(const float* src, int n, long zs) {
-    f32x4 a[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    int z = 0;
-    for (; z + 8 <= n; z += 8) {
-        f32x4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = *(const f32x4*)(src + (long)(z + j) * zs);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] += v[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 7; ++j)
-        if (z + j < n) a[j] += *(const f32x4*)(src + (long)(z + j) * zs);
-    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-}
+// -------------------------------------------------------------------------------------
+// 64 -> 64 channel 3x3 stride-1 weight gradient (the layer1 convs of Res10/18/34, residuals.py:84-120; ws[z][co][kk],
+// kk = tap * 64 + ci).  With 64 output-gradient channels every tile of the generic kernels is thin (64 x 256, and
+// 576 = 2.25 tiles of 256 columns: a third of the last tile computes nothing) and each input pixel is fetched once
+// per tap.  Here ONE workgroup computes all 64 x 576 outputs over its pixel range, and a stage of 64 output pixels
+// (part of one output row) stages the input once as a halo of 3 rows x 66 columns (2.6x fewer bytes than the nine
+// shifted copies) plus the 64 x 128 B output gradient, both by LDS-DMA.  The nine taps read the halo at shifted rows
+// with ds_read_b64_tr_b16 (A operand = input columns, B = output-gradient channels, 16x16x32 bf16 MFMA).
+// 8 waves: wave w owns the 16-channel input slice u = w & 3 of every tap (9 column blocks) and the output-gradient
+// channel blocks 2(w >> 2), 2(w >> 2) + 1: 18 accumulators.  Each halo row region is 80 rows apart (bits 0-3 of a
+// row index do not change with the input row), so a wave's 72 fragment reads per stage come from 8 address
+// registers plus immediate offsets (no per-read address VALU).  Stage t+1 is fetched into the other buffer while
+// stage t is computed; one barrier per stage.
+constexpr int L1W_KP = 64;                           // pixels per stage
+constexpr int L1W_HC = L1W_KP + 2;                   // halo columns
+constexpr int L1W_REG = 80;                          // LDS rows per halo row region (66 used)
+constexpr int L1W_DMA_ROWS = 72;                     // rows of a region the DMA fills (whole 8-row instructions)
+constexpr int L1W_HBYTES = 3 * L1W_REG * 128;
+constexpr int L1W_STAGE = L1W_HBYTES + L1W_KP * 128;
+constexpr int L1W_NHDMA = 3 * L1W_DMA_ROWS / 8;     // 27 halo DMA instructions per stage
+// stage buffers: 2 (76 KiB of LDS, so the compute stream's kernels still fit beside it); 3 and 4 (ablation builds 45,
+// 47) measured the same (56-57 us for the Res10 B=32 layer1 gradient: the fill is not what bounds it)
+constexpr int L1W_NBUF = SCD_ABLATE == 45 ? 3 : SCD_ABLATE == 47 ? 4 : 2;
 
-// first pass of a wide reduce: groups of G consecutive slabs summed into the group's first slab, over the
-// 4-column units [e0/4, e0/4 + n4) of each slab (the rows the reduce consumes)
-__global__ __launch_bounds__(256) void wgrad_presum_kernel(float* ws, int nsplit, int G, long zs, long e0, long n4) {
-    const long ngroups = (nsplit + G - 1) / G;
-    const long total = ngroups * n4;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const long g = i / n4, e = i - g * n4;
-        float* base = ws + g * G * zs + e0 + 4 * e;
-        const f32x4 s = wred_sum(base, (int)min((long)G, nsplit - g * G), zs);
-        *(f32x4*)base = s;
+// 128-B rows, two per 256-B bank line: the 32-B unit u of row r is stored at u ^ f(r), so the transposed reads of
+// rows {R..R+3, R+8..R+11} (any R: a tap shifts the base row) hit 8 distinct 32-B bank groups
+__device__ __forceinline__ int l1w_f(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
+__device__ __forceinline__ int l1w_addr(int r, int unit, int pp) { return r * 128 + ((unit ^ l1w_f(r)) << 5) + 8 * pp; }
+
+__global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[L1W_NBUF * L1W_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int u = wave & 3, ch = wave >> 2;
+    const int z = blockIdx.x;
+    const int M = p.N * p.Ho * p.Wo;
+    const int pix0 = min(M, z * p.chunk), pix1 = min(M, pix0 + p.chunk);
+    const int H = p.Ho, W = p.Wo;
+
+    // halo DMA: instruction i = wave + 8 j (i < 27) fills region i / 9, rows 8 (i % 9) .. +7; lane: row + lane / 8,
+    // 16-B slot lane % 8 (source chunk swizzled)
+    int h_dy[4], h_dx[4], h_c8[4];
+    bool h_ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = wave + 8 * j;
+        const int reg = i / 9, col = 8 * (i - reg * 9) + (lane >> 3);
+        const int c = (lane & 7) ^ (l1w_f(col) << 1);
+        h_ok[j] = col < L1W_HC;
+        h_dy[j] = reg - 1;
+        h_dx[j] = col - 1;
+        h_c8[j] = c * 8;
+    }
+    const int g_R = 8 * wave + (lane >> 3);
+    const int g_c8 = ((lane & 7) ^ (l1w_f(g_R) << 1)) * 8;
+
+    int sn, soh, sow;
+    {
+        const int HW = H * W;
+        sn = __builtin_amdgcn_readfirstlane(pix0 / HW);
+        const int rem = pix0 - sn * HW;
+        soh = __builtin_amdgcn_readfirstlane(rem / W);
+        sow = __builtin_amdgcn_readfirstlane(rem - soh * W);
+    }
+    auto advance = [&]() {
+        sow += L1W_KP;
+        const bool wrap = sow >= W;
+        sow = wrap ? 0 : sow;
+        soh += wrap ? 1 : 0;
+        const bool wrap2 = soh >= H;
+        soh = wrap2 ? 0 : soh;
+        sn += wrap2 ? 1 : 0;
+        sn = __builtin_amdgcn_readfirstlane(sn);
+        soh = __builtin_amdgcn_readfirstlane(soh);
+        sow = __builtin_amdgcn_readfirstlane(sow);
+    };
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    auto issue = [&](int k0, char* buf) {
+        const int S = __builtin_amdgcn_readfirstlane(((sn * H + soh) * W + sow) * 64);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = wave + 8 * j;
+            if (i < L1W_NHDMA) {
+                const int reg = i / 9;
+                const bool ok = h_ok[j] & (k0 < pix1) & ((unsigned)(soh + h_dy[j]) < (unsigned)H) &
+                                ((unsigned)(sow + h_dx[j]) < (unsigned)W);
+                dma16_asm(xrs, buf + (reg * L1W_REG + 8 * (i - reg * 9)) * 128,
+                          sel_off(ok, (S + (h_dy[j] * W + h_dx[j]) * 64 + h_c8[j]) * 2));
+            }
+        }
+        dma16_asm(grs, buf + L1W_HBYTES + wave * 1024, sel_off(k0 + g_R < pix1, ((k0 + g_R) * 64 + g_c8) * 2));
+    };
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int q4 = l16 >> 2, pp = l16 & 3;
+    const int r0 = 8 * lg + q4;                      // fragment row of k-step 0 (k-step 1: + 32 rows = + 4096 B)
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    auto trf = [&](const char* lo_addr, const char* hi_addr) {
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo_addr);
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)hi_addr);
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    };
+    // per-lane byte offsets: halo (tap column dw, lo/hi rows) and output gradient (block a; hi = lo + 4 rows)
+    int xo[3][2], go[2];
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) xo[dw][h] = l1w_addr(r0 + dw + 4 * h, u, pp);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) go[a] = L1W_HBYTES + l1w_addr(r0, 2 * ch + a, pp);
+    f32x4 acc[2][9];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[a][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 gf[2], xf[9];
+    auto reads = [&](const char* cur, int s2) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) gf[a] = trf(cur + go[a] + 4096 * s2, cur + go[a] + 4096 * s2 + 512);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int off = (t / 3) * L1W_REG * 128 + 4096 * s2;
+            xf[t] = trf(cur + xo[t % 3][0] + off, cur + xo[t % 3][1] + off);
+        }
+    };
+    auto mfmas = [&]() {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                if constexpr (SCD_ABLATE == 42) {          // ablation: fragment reads kept, no MFMA
+                    asm volatile("" ::"v"(xf[t]), "v"(gf[a]));
+                } else {
+                    acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[t], gf[a], acc[a][t], 0, 0, 0);
+                }
+            }
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();                 // raw: a __syncthreads() fence would drain the stages in flight
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // L1W_NBUF stage buffers: stage t + NBUF - 1 is fetched while stage t is computed.  Every iteration issues a
+    // whole stage -- past the end of the range with out-of-range offsets (zeros into a buffer nobody reads again, no
+    // traffic) -- so the counts are uniform: this wave's DMAs per stage are n = its halo instructions (4 for waves
+    // 0-2, 3 for the rest) + 1, and vmcnt((NBUF - 2) n) retires stage t+1 only.
+    // Two wave groups one barrier apart (waves 4-7 trail): each k-step is a read phase (22 transposed reads, drained
+    // before its barrier) and an MFMA phase, and on every SIMD one group's MFMAs run beside the other's reads.  The
+    // DMA of stage t+3 goes into stage t-1's buffer, whose last reads (both groups' second k-step) were drained before
+    // earlier barriers; stage t+1 is retired before the barrier that opens the leading group's stage t+1 -- by that
+    // group after its last MFMA phase of stage t, by the trailing group after its last read phase (the same barrier
+    // instance for it).  Measured slower than one barrier per stage with every wave reading then computing (60 vs
+    // 57 us for the Res10 B=32 layer1 gradient), so the stagger is ablation build 46 only.
+    const int nk = (pix1 - pix0 + L1W_KP - 1) / L1W_KP;
+    if (nk > 0) {
+        const bool five = wave < L1W_NHDMA - 24;
+        constexpr bool STAGGER = SCD_ABLATE == 46;          // ablation build 46: the two-group stagger
+        const bool lead = !STAGGER || ch == 0;
+        // retire stage t+1, leave stages t+2 .. t+NBUF-1 in flight
+        auto wait_next = [&]() {
+            if constexpr (SCD_ABLATE != 41) {
+                if constexpr (L1W_NBUF == 4) {
+                    if (five) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                } else if constexpr (L1W_NBUF == 3) {
+                    if (five) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+            }
+        };
+#pragma unroll
+        for (int j = 0; j < L1W_NBUF - 1; ++j) {
+            issue(pix0 + j * L1W_KP, smem + j * L1W_STAGE);
+            advance();
+        }
+        if constexpr (L1W_NBUF == 4) {
+            if (five) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else if constexpr (L1W_NBUF == 3) {
+            if (five) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        if (!lead) bar();
+        int b0 = 0;                                   // buffer of stage t
+        for (int t = 0; t < nk; ++t) {
+            const int b3 = b0 == 0 ? L1W_NBUF - 1 : b0 - 1;   // buffer of stage t+NBUF-1 (= that of stage t-1)
+            const char* cur = smem + b0 * L1W_STAGE;
+            if constexpr (SCD_ABLATE != 41) {         // ablation 41: no DMA after the prologue
+                issue(pix0 + (t + L1W_NBUF - 1) * L1W_KP, smem + b3 * L1W_STAGE);
+                advance();
+            }
+            if constexpr (!STAGGER) {
+                reads(cur, 0);
+                mfmas();
+                reads(cur, 1);
+                mfmas();
+                wait_next();
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                bar();
+            } else {
+                reads(cur, 0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                bar();
+                __builtin_amdgcn_s_setprio(1);
+                mfmas();
+                __builtin_amdgcn_s_setprio(0);
+                bar();
+                reads(cur, 1);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (!lead) wait_next();
+                bar();
+                __builtin_amdgcn_s_setprio(1);
+                mfmas();
+                __builtin_amdgcn_s_setprio(0);
+                if (lead) wait_next();
+                bar();
+            }
+            b0 = b0 == L1W_NBUF - 1 ? 0 : b0 + 1;
+        }
+        if (lead && STAGGER) bar();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // fp32 slab: lane holds columns kk .. kk+3 (kk = 64 t + 16 u + 4 lg) of channel 16 (2ch + a) + l16
+    float* ws = p.ws + (long)z * 64 * 576;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int co = 16 * (2 * ch + a) + l16;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            *(f32x4*)(ws + (long)co * 576 + 64 * t + 16 * u + 4 * lg) = acc[a][t];
     }
 }
 
@@ -2906,27 +3139,84 @@ struct WredSlices {
     float* dst[4];
 };
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int nsplit, long zs, int T, int Ci,
-                                                           int cvalid, WredSlices sl, long total4, int accumulate,
-                                                           float alpha) {
-    const int KK = T * Ci;
-    const int KK4 = KK >> 2;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
-        long e = i;
-        int s = 0;
-        while (s < sl.n - 1 && e >= (long)(sl.r1[s] - sl.r0[s]) * KK4) { e -= (long)(sl.r1[s] - sl.r0[s]) * KK4; ++s; }
-        const int r = (int)(e / KK4);
-        const int k = (int)(e - (long)r * KK4) * 4;
-        const f32x4 v = wred_sum(ws + (long)(sl.r0[s] + r) * KK + k, nsplit, zs) * alpha;
-        float* drow = sl.dst[s] + r * sl.ldn[s];
+// Split reduction: block (row, channel chunk) sums the nsplit slabs of its WRED_CB input channels x T taps of one
+// slab row (coalesced 16-B reads, 8 slab loads in flight per thread, fixed summation order) into LDS, then writes the
+// chunk in the destination's order (OIHW: taps fastest) so consecutive lanes store consecutive words.  The earlier
+// form (one thread per 4 slab columns, stores 4 * ldc apart) read the slabs at ~2.2 TB/s behind its scattered
+// stores (tools/wgrad_bench.py: 30 us for the layer4 conv2 gradient, 7 splits).
+constexpr int WRED_CB = 128;                       // widest channel chunk (narrower when there are few rows)
+
+// slab sum over splits g, g + S, g + 2S, ... of one 4-column unit (8 loads in flight), fixed order
+__device__ __forceinline__ f32x4 wred_sum_strided(const float* src, int n, long zs, int g, int S) {
+    f32x4 a[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            // Ci % 4 == 0: the 4 columns share one tap
-            const int t = (k + j) / Ci, c = k + j - t * Ci;
-            if (c >= cvalid) continue;
-            float* d = drow + c * sl.ldc[s] + t * sl.ldt[s];
-            *d = accumulate ? (*d + v[j]) : v[j];
+    for (int j = 0; j < 8; ++j) a[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int z = g;
+    for (; z + 7 * S < n; z += 8 * S) {
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *(const f32x4*)(src + (long)(z + j * S) * zs);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+        if (z + j * S < n) a[j] += *(const f32x4*)(src + (long)(z + j * S) * zs);
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// block (row, channel chunk of cb): S thread groups per 4-column unit each sum every S-th split (S > 1 when the
+// chunk has few units and there are many splits: the 64-row layer1 gradient over 256 splits), the S partials are
+// added in LDS in a fixed order, and the chunk is written in the destination's order
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* ws, int nsplit, long zs, int T, int Ci,
+                                                           int cvalid, WredSlices sl, int ncb, int cb, int S,
+                                                           int accumulate, float alpha) {
+    extern __shared__ float red[];                 // [T][cb + 1], then the S-way partials [S][units] (f32x4)
+    const int tid = threadIdx.x;
+    const int cbk = blockIdx.x % ncb;
+    int rr = blockIdx.x / ncb;
+    int s = 0;
+    while (s < sl.n - 1 && rr >= sl.r1[s] - sl.r0[s]) { rr -= sl.r1[s] - sl.r0[s]; ++s; }
+    const int row = sl.r0[s] + rr;
+    const int c0 = cbk * cb, cn = min(cb, Ci - c0);
+    const int upt = cn >> 2;                       // 4-column units per tap
+    const int units = T * upt;
+    const long KK = (long)T * Ci;
+    const float* src = ws + (long)row * KK + c0;
+    f32x4* part = (f32x4*)(red + ((T * (cb + 1) + 3) & ~3));
+    if (S > 1) {
+        for (int i = tid; i < units * S; i += blockDim.x) {
+            const int u = i % units, g = i / units;
+            const int t = u / upt, j = u - t * upt;
+            part[g * units + u] = wred_sum_strided(src + (long)t * Ci + 4 * j, nsplit, zs, g, S);
         }
+        __syncthreads();
+    }
+    for (int u = tid; u < units; u += blockDim.x) {
+        const int t = u / upt, j = u - t * upt;
+        f32x4 v;
+        if (S > 1) {
+            v = part[u];
+            for (int g = 1; g < S; ++g) v += part[g * units + u];
+        } else {
+            v = wred_sum_strided(src + (long)t * Ci + 4 * j, nsplit, zs, 0, 1);
+        }
+        v *= alpha;
+        float* d = red + t * (cb + 1) + 4 * j;
+        d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+    }
+    __syncthreads();
+    float* drow = sl.dst[s] + rr * sl.ldn[s];
+    const long ldc = sl.ldc[s], ldt = sl.ldt[s];
+    const bool taps_fast = ldt <= ldc;
+    for (int i = tid; i < T * cn; i += blockDim.x) {
+        int c, t;
+        if (taps_fast) { c = i / T; t = i - c * T; }
+        else { t = i / cn; c = i - t * cn; }
+        if (c0 + c >= cvalid) continue;
+        const float v = red[t * (cb + 1) + c];
+        float* d = drow + (c0 + c) * ldc + t * ldt;
+        *d = accumulate ? (*d + v) : v;
     }
 }
 
@@ -3339,11 +3629,28 @@ static void wgrad_tile(int dtype, long M, int Cg, int& tm, int& tn) {
 static bool wgrad_use_pp2(int dtype, long M, int Ho, int Wo, int Cg) {
     static int mode = -2;
     if (mode == -2) { const char* e = getenv("SCD_WGRAD_PP2"); mode = e ? atoi(e) : 1; }
-    return mode && dtype == SCD_DT_BF16 && Cg >= 256 && Wo % 64 == 0 && ((long)Ho * Wo) % 64 == 0 && M >= 64 * 256;
+    // a stage = 64 pixels of one output row, or 64 / Wo whole rows (Wo = 16, 32: layer3/4, deconv1/2)
+    const bool stage_ok = Wo % 64 == 0 || (Wo >= 8 && 64 % Wo == 0);
+    return mode && dtype == SCD_DT_BF16 && Cg >= 128 && stage_ok && ((long)Ho * Wo) % 64 == 0 && M >= 64 * 64;
 }
 
+// the layer1 weight gradient (conv_wgrad_l1_kernel): bf16, 64 -> 64 channels, 3x3 taps, stages inside one row
+static bool wgrad_use_l1(int dtype, long M, int Ho, int Wo, int Cg, int T, int Ci) {
+    static int mode = -2;
+    if (mode == -2) { const char* e = getenv("SCD_WGRAD_L1"); mode = e ? atoi(e) : 1; }
+    return mode && dtype == SCD_DT_BF16 && Cg == 64 && Ci == 64 && T == 9 && Wo % 64 == 0 && M % 64 == 0 &&
+           (long)Ho * Wo * 64 <= (1L << 30) && M >= 64;
+}
+
+// one workgroup per CU over >= 16 stages each
+static int wgrad_l1_nsplit(long M) { return (int)std::max(1L, std::min(256L, M / 64 / 16)); }
+
 // channel window of the ping-pong weight gradient: 256 (NQ 4) or, for widths that are multiples of 192 only, 192
-static int wgrad_pp2_win(int Cg) { return (Cg % 256 != 0 && Cg % 192 == 0) ? 192 : 256; }
+static int wgrad_pp2_win(int Cg) {
+    if (Cg % 256 == 0) return 256;
+    if (Cg % 192 == 0) return 192;
+    return Cg < 256 ? 128 : 256;           // 128: NQ 2 (the heatmap head, layer2); else 256 windows + a remainder
+}
 
 // split count from a wave-quantisation cost model (SCD_WGRAD_NSMODEL=0: the fixed rules below it).  A launch of
 // tiles x ns workgroups runs in ceil(tiles*ns / slots) rounds; a round costs its K stages (stage_us each) plus the
@@ -3356,10 +3663,11 @@ static bool wgrad_nsmodel() {
 }
 
 static long wgrad_ns_model(long M, long tiles, int slots, int kp, double stage_us, double epi_us, double slab_bytes,
-                           long ns_max) {
+                           long ns_max, bool any_ns = false) {
     long best = 8;
     double bt = 1e30;
-    for (long ns = 8; ns <= std::max(8L, ns_max); ns += 8) {
+    const long step = any_ns ? 1 : 8;
+    for (long ns = step; ns <= std::max(8L, ns_max); ns += step) {
         const long stages = cdiv(cdiv(M, ns), (long)kp);
         const long rounds = cdiv(tiles * ns, (long)slots);
         const double t = rounds * (stages * stage_us + epi_us) + ns * slab_bytes / 3.5e6;
@@ -3380,13 +3688,16 @@ static long wgrad_min_splits(long M, long ns_max) {
 static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
     const int win = wgrad_pp2_win(Cg);
     const long tiles = (long)(Cg / win) * cdiv(KK, 256);
-    const long cap_px = std::max(8L, M / 2048 / 8 * 8);
+    // >= 8 stages per split (small layers need many splits to fill the chip: layer3 has 32 K pixels)
+    const long cap_px = std::max(8L, M / 512 / 8 * 8);
     const long cap_mem = std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * KK) / 8 * 8);
     if (wgrad_nsmodel()) {
         // one workgroup per CU; a 64-pixel stage ~ 2*win*256*64 flop at ~4.3 TF/s per CU; slab win x 256 fp32
         const double stage_us = 2.0 * win * 256 * 64 / 4.3e6;
         const double epi_us = 4.0 * win * 256 / (5.0e6 / 256);
-        const long ns = wgrad_ns_model(M, tiles, 256, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem));
+        // many tiles: splits need not come in XCD groups of 8 (wgrad_block's linear map), so one round can be filled
+        const long ns = wgrad_ns_model(M, tiles, 256, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem),
+                                       tiles >= 24);
         return (int)std::max(ns, wgrad_min_splits(M, std::min(cap_px, cap_mem)));
     }
     // about two rounds of one-per-CU workgroups over the channel windows, whole XCD groups, >= 2048 pixels
@@ -3399,6 +3710,7 @@ static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
 
 extern "C" int scd_conv_wgrad_nsplit2(int dtype, long M, int Ho, int Wo, int Cg, int T, int Ci) {
     SCD_F16_FWD(scd_conv_wgrad_nsplit2, M, Ho, Wo, Cg, T, Ci);
+    if (wgrad_use_l1(dtype, M, Ho, Wo, Cg, T, Ci)) return wgrad_l1_nsplit(M);
     if (wgrad_use_pp2(dtype, M, Ho, Wo, Cg)) return wgrad_pp2_nsplit(M, Cg, T * Ci);
     return scd_conv_wgrad_nsplit(dtype, M, Cg, T, Ci);
 }
@@ -3462,18 +3774,28 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     int chunk = cdiv(M, nsplit);
     chunk = (chunk + 63) / 64 * 64;
     p.chunk = chunk;
+    if (wgrad_use_l1(dtype, M, Ho, Wo, Cg, T, Ci) && in_stride == 1 && Hi == Ho && Wi == Wo) {
+        bool std_taps = true;        // taps (t / 3 - 1, t % 3 - 1): the halo row of tap t (conv_wgrad_l1_kernel)
+        for (int t = 0; t < 9; ++t) std_taps &= dh[t] == t / 3 - 1 && dw[t] == t % 3 - 1;
+        if (std_taps) {
+            p.nsplit = nsplit;
+            hipLaunchKernelGGL(conv_wgrad_l1_kernel, dim3(nsplit), dim3(512), 0, (hipStream_t)stream, p);
+            SCD_RETURN_LAUNCH();
+        }
+    }
     if (wgrad_use_pp2(dtype, M, Ho, Wo, Cg) && chunk % 64 == 0) {
         // 256-channel windows on the ping-pong kernel, a remainder on the register-staged one
         hipStream_t st = (hipStream_t)stream;
         p.ntn = cdiv(p.KK, 256);
         p.nsplit = nsplit;
-        const int n8 = (nsplit + 7) / 8 * 8;
+        const int n8 = nsplit;          // whole XCD groups of splits, or the linear map (wgrad_block)
         const int win = wgrad_pp2_win(Cg);
         p.cg0 = 0;
         p.cgn = Cg / win * win;
         p.ntm = Cg / win;
         if (win == 256) hipLaunchKernelGGL((conv_wgrad_pp2_kernel<4>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
-        else hipLaunchKernelGGL((conv_wgrad_pp2_kernel<3>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
+        else if (win == 192) hipLaunchKernelGGL((conv_wgrad_pp2_kernel<3>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
+        else hipLaunchKernelGGL((conv_wgrad_pp2_kernel<2>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || Cg % win == 0) return (int)e;
         p.cg0 = Cg / win * win;
@@ -3482,13 +3804,15 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
         wgrad_tile(dtype, M, p.cgn, BM, BN);
         p.ntm = cdiv(p.cgn, BM);
         p.ntn = cdiv(p.KK, BN);
-        const bool fastok = wgrad_fastx() && ((long)Ho * Wo) % 64 == 0;
+        // stages of one row (FASTX 1, Wo % 64 == 0) or of whole rows (FASTX 2, 64 % Wo == 0; 64 x 256 tile only)
+        const int fx = !(wgrad_fastx() && ((long)Ho * Wo) % 64 == 0) ? 0 : (Wo % 64 == 0 ? 1 : 2);
         dim3 grid(p.ntm * p.ntn * n8);
         if (BM == 64) {
-            if (fastok) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
+            if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
+            else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), 0, st, p);
             else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), 0, st, p);
         } else {
-            if (fastok) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
+            if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
             else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), 0, st, p);
         }
         SCD_RETURN_LAUNCH();
@@ -3516,7 +3840,7 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     p.ntm = cdiv(Cg, BM);
     p.ntn = cdiv(p.KK, BN);
     p.nsplit = nsplit;
-    dim3 grid(p.ntm * p.ntn * ((nsplit + 7) / 8 * 8));
+    dim3 grid(p.ntm * p.ntn * nsplit);
     hipStream_t st = (hipStream_t)stream;
     if (wgrad_use_ring(dtype, M, Cg)) {
         hipLaunchKernelGGL(conv_wgrad_ring_kernel, grid, dim3(512), 0, st, p);
@@ -3555,44 +3879,30 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
 extern "C" int scd_wgrad_reduce_rows(const float* ws, int nsplit, int Cg, int T, int Ci, int nslices, const int* r0,
                                      const int* r1, const long* ld_n, const long* ld_c, const long* ld_t,
                                      float* const* dst, int cvalid, int accumulate, float alpha, void* stream) {
-    if (nslices < 1 || nslices > 4 || nsplit < 1 || Ci % 4 != 0) return SCD_ERR_ARG;
+    if (nslices < 1 || nslices > 4 || nsplit < 1 || Ci % 4 != 0 || T < 1 || T > 64) return SCD_ERR_ARG;
     WredSlices sl;
     sl.n = nslices;
-    int rmin = Cg, rmax = 0;
     long rows = 0;
     for (int s = 0; s < nslices; ++s) {
         if (r0[s] < 0 || r1[s] > Cg || r0[s] >= r1[s] || dst[s] == nullptr) return SCD_ERR_ARG;
         sl.r0[s] = r0[s]; sl.r1[s] = r1[s];
         sl.ldn[s] = ld_n[s]; sl.ldc[s] = ld_c[s]; sl.ldt[s] = ld_t[s];
         sl.dst[s] = dst[s];
-        rmin = std::min(rmin, r0[s]);
-        rmax = std::max(rmax, r1[s]);
         rows += r1[s] - r0[s];
     }
-    hipStream_t st = (hipStream_t)stream;
-    const long KK = (long)T * Ci;
-    const long zs = (long)Cg * KK;
-    const long total4 = rows * KK / 4;
-    int ns = nsplit;
-    long zsr = zs;
-    // one pass keeps >= 8 loads in flight per thread; too few threads for the HBM (small weights, many
-    // splits): first sum groups of G slabs in place, parallel over the groups, over the rows [rmin, rmax)
-    const long want = 128L * 1024;
-    if (nsplit > 16 && total4 < want) {
-        const long ngroups = std::min<long>(cdiv(want, total4), nsplit / 8);
-        const int G = (int)cdiv((long)nsplit, ngroups);
-        const long n4 = (long)(rmax - rmin) * KK / 4;
-        const long tot = (long)((nsplit + G - 1) / G) * n4;
-        hipLaunchKernelGGL(wgrad_presum_kernel, dim3((int)std::min<long>(16384, (tot + 255) / 256)), dim3(256), 0, st,
-                           (float*)ws, nsplit, G, zs, (long)rmin * KK, n4);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return (int)e;
-        ns = (nsplit + G - 1) / G;
-        zsr = zs * G;
-    }
-    const int blocks = (int)std::min<long>(16384, (total4 + 255) / 256);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, ns, zsr, T, Ci, cvalid, sl, total4,
-                       accumulate, alpha);
+    const long zs = (long)Cg * T * Ci;
+    // channel chunk: the widest (<= 128) that still gives >= 1024 workgroups (few rows x many splits, e.g. the
+    // 64-row layer1 gradient over 256 splits, would otherwise leave the reduce latency-bound on 64 workgroups)
+    int cb = WRED_CB;
+    while (cb > 16 && rows * cdiv(Ci, cb) < 512) cb >>= 1;
+    const int ncb = cdiv(Ci, cb);
+    const int units = T * (std::min(cb, Ci) / 4);
+    // split groups per unit: every thread keeps >= 8 slab loads to itself, up to 256 threads per block
+    const int S = std::max(1, std::min(256 / std::max(1, units), nsplit / 8));
+    const int threads = (int)std::min(256L, ((long)units * S + 63) / 64 * 64);
+    const size_t lds = (size_t)((T * (cb + 1) + 3) & ~3) * sizeof(float) + (S > 1 ? (size_t)S * units * 16 : 0);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(rows * ncb)), dim3(threads), lds, (hipStream_t)stream, ws,
+                       nsplit, zs, T, Ci, cvalid, sl, ncb, cb, S, accumulate, alpha);
     SCD_RETURN_LAUNCH();
 }
 

@@ -93,9 +93,31 @@ def test_conv_large_bf16(case, dtype):
     test_conv_fwd_dgrad_wgrad(case, dtype)
 
 
+# weight gradients on the ping-pong kernel with stages of several output rows (Wo = 16, 32: the layer3/4 shapes),
+# the linear split map (split counts not a multiple of 8) and a 192-channel window
+PP2_ROWS_CASES = [
+    (16, 512, 16, 16, 512, 3, 1, 1),      # layer4 conv2, Wo 16
+    (16, 256, 32, 32, 512, 3, 2, 1),      # layer4 conv1 (stride 2)
+    (8, 256, 32, 32, 256, 3, 1, 1),       # layer3 conv2, Wo 32
+    (16, 256, 32, 32, 512, 1, 2, 0),      # layer4 downsample 1x1 s2 (half-empty column tile)
+    (12, 128, 32, 32, 384, 3, 1, 1),      # 192-channel windows, Wo 32
+    (8, 64, 64, 64, 128, 3, 1, 1),        # 128-channel window (NQ 2): layer2 conv2 shape, Wo 64
+    (8, 64, 128, 128, 128, 3, 2, 1),      # NQ 2, stride 2 (layer2 conv1)
+    (16, 128, 32, 32, 128, 3, 1, 1),      # NQ 2, Wo 32
+    (2, 256, 128, 128, 128, 3, 1, 1),     # NQ 2: the heatmap head's 3x3 weight gradient, Wo 128
+    (4, 64, 32, 32, 320, 3, 1, 1),        # 256-channel window + a 64-channel remainder on the register-staged kernel
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", PP2_ROWS_CASES)
+def test_conv_wgrad_pp2_rows(case, dtype):
+    test_conv_fwd_dgrad_wgrad(case, dtype)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", [(2, 128, 5, 7, 64), (1, 256, 8, 8, 256), (2, 64, 16, 16, 128),
-                                  (8, 256, 64, 64, 256)])
+                                  (8, 256, 64, 64, 256), (8, 256, 32, 32, 256), (16, 512, 16, 16, 256)])
 def test_deconv_fwd_dgrad_wgrad(case, dtype):
     from scdhip import ops
     N, Cin, H, W, Cout = case
@@ -582,6 +604,22 @@ def test_conv_h64_bf16(case):
     test_conv_fwd_dgrad_wgrad(case, torch.bfloat16)
 
 
+# the layer1 weight gradient (conv_wgrad_l1_kernel: 64 x 576 per workgroup, halo-staged input): widths 64 (a stage is
+# a whole row, both borders in it), 128, 192 (a middle stage with in-image neighbours on both sides), ragged splits
+L1_WGRAD_CASES = [
+    (3, 64, 64, 64, 64, 3, 1, 1),
+    (4, 64, 128, 128, 64, 3, 1, 1),
+    (2, 64, 32, 192, 64, 3, 1, 1),
+    (1, 64, 7, 64, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", L1_WGRAD_CASES)
+def test_conv_wgrad_layer1(case, dtype):
+    test_conv_fwd_dgrad_wgrad(case, dtype)
+
+
 def test_conv_h64_accumulate_and_bias_relu():
     """Epilogue paths the block code uses on the halo kernel: dgrad += into an existing gradient, and a
     forward with bias + ReLU."""
@@ -627,11 +665,13 @@ def test_augment_tiny_tiles(B, H, W):
         np.testing.assert_allclose(got[b].numpy(), ref.numpy(), rtol=0, atol=2e-5)
 
 
-@pytest.mark.parametrize("ns,Cg,T,Ci", [(1, 64, 9, 64), (7, 64, 9, 64), (17, 64, 1, 64), (56, 384, 9, 256),
-                                        (200, 128, 9, 128), (64, 8, 3, 4)])
-def test_wgrad_reduce_rows(ns, Cg, T, Ci):
-    """scd_wgrad_reduce_rows (split-slab sum into 1..4 OIHW row slices, with and without the in-place group
-    pre-pass) against a float64 sum of the same slabs: fp32 accumulation of ns terms, 1e-5 relative."""
+@pytest.mark.parametrize("ns,Cg,T,Ci,taps_fast", [(1, 64, 9, 64, True), (7, 64, 9, 64, True), (17, 64, 1, 64, True),
+                                                  (56, 384, 9, 256, True), (200, 128, 9, 128, True),
+                                                  (64, 8, 3, 4, True), (9, 32, 16, 260, True), (5, 24, 9, 132, False)])
+def test_wgrad_reduce_rows(ns, Cg, T, Ci, taps_fast):
+    """scd_wgrad_reduce_rows (split-slab sum into 1..4 row slices, per (row, 128-channel chunk) workgroup, written in
+    the destination's order: OIHW with taps fastest, or a [tap][channel] layout) against a float64 sum of the same
+    slabs: fp32 accumulation of ns terms, 1e-5 relative; ragged channel chunks (260 = 2 x 128 + 4)."""
     from scdhip import lib as L
     from scdhip.ops import ptr, stream
     g = torch.Generator().manual_seed(ns * 1000 + Cg)
@@ -642,18 +682,25 @@ def test_wgrad_reduce_rows(ns, Cg, T, Ci):
     slices = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
     cvalid = Ci - 1 if Ci > 4 else Ci
     alpha = 0.5
-    dst = [torch.randn(b - a, Ci, T, generator=g).to(DEV) for a, b in slices]   # OIHW-flattened rows
+    if taps_fast:
+        dst = [torch.randn(b - a, Ci, T, generator=g).to(DEV) for a, b in slices]   # OIHW-flattened rows
+    else:
+        dst = [torch.randn(b - a, T, Ci, generator=g).to(DEV) for a, b in slices]   # [row][tap][channel]
+    ldc, ldt = (T, 1) if taps_fast else (1, Ci)
     before = [d.clone() for d in dst]
     for accumulate in (1, 0):
         d_in = [d.clone() for d in before]
-        wsd = ws.to(DEV)                          # the group pre-pass sums in place
+        wsd = ws.to(DEV)
         L.call("scd_wgrad_reduce_rows", ptr(wsd), ns, Cg, T, Ci, len(slices),
                L.int_array([a for a, _ in slices]), L.int_array([b for _, b in slices]),
-               L.long_array([Ci * T] * len(slices)), L.long_array([T] * len(slices)), L.long_array([1] * len(slices)),
-               L.ptr_array([ptr(d) for d in d_in]), cvalid, accumulate, alpha, stream())
+               L.long_array([Ci * T] * len(slices)), L.long_array([ldc] * len(slices)),
+               L.long_array([ldt] * len(slices)), L.ptr_array([ptr(d) for d in d_in]), cvalid, accumulate, alpha,
+               stream())
         torch.cuda.synchronize()
         for (a, b), d, d0 in zip(slices, d_in, before):
             exp = ref[a:b].view(b - a, T, Ci).permute(0, 2, 1) * alpha      # (rows, Ci, T)
+            if not taps_fast:
+                d, d0 = d.permute(0, 2, 1), d0.permute(0, 2, 1)
             want = d0.cpu().double().clone()
             want[:, :cvalid] = exp[:, :cvalid] + (want[:, :cvalid] if accumulate else 0)
             err = (d.cpu().double() - want).abs().max().item() / max(1e-6, want.abs().max().item())
