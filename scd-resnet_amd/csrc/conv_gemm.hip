@@ -2834,7 +2834,11 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         // NQ 3: C1 vmcnt(3), C2 vmcnt(4), L3 vmcnt(3), C3 vmcnt(2);
         // NQ 2 (128-channel windows: the heatmap head, layer2): phase 1 issues all six DMAs of stage t+1 (X halves,
         // both G quarters), so they land across both phases; every wave's fragment reads are drained before the
-        // phase-2 barrier (the partner group, one barrier ahead, then overwrites that buffer's G quarters), C2 vmcnt(0)
+        // phase-2 barrier (the partner group, one barrier ahead, then overwrites that buffer's G quarters).  Stage t+1
+        // must be retired before the barrier after which group 0 reads it: group 0's post-MFMA barrier of phase 2,
+        // which for group 1 (one barrier behind) is the barrier BEFORE its phase-2 MFMAs -- group 0 waits vmcnt(0)
+        // after its MFMAs, group 1 before that barrier (waiting after it, as group 0 does, let group 0 read group 1's
+        // half of the stage before it had landed: NaN weight gradients, layer2 downsample, cornerNetCPool B=32)
         for (int t = 0; t < nk; ++t) {
             char* cur = smem + (t & 1) * STAGE;
             char* nxt = smem + ((t & 1) ^ 1) * STAGE;
@@ -2846,10 +2850,14 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
                 read_g(cur, q, gf);
                 if constexpr (NQ == 2) {
                     if (q == 0) { issue_x(k1, nxt, 0); issue_x(k1, nxt, 1); issue_g(k1, nxt, 0); issue_g(k1, nxt, 1); }
-                    if (q == 1) { advance(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+                    if (q == 1) {
+                        advance();
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
                     bar();
                     mfma_q(q, gf);
-                    if (q == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (q == 1 && grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     bar();
                     continue;
                 }

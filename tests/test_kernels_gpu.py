@@ -106,6 +106,7 @@ PP2_ROWS_CASES = [
     (16, 128, 32, 32, 128, 3, 1, 1),      # NQ 2, Wo 32
     (2, 256, 128, 128, 128, 3, 1, 1),     # NQ 2: the heatmap head's 3x3 weight gradient, Wo 128
     (4, 64, 32, 32, 320, 3, 1, 1),        # 256-channel window + a 64-channel remainder on the register-staged kernel
+    (32, 64, 128, 128, 128, 1, 2, 0),     # NQ 2, 1x1 stride 2 (layer2 downsample; 256 splits of 8 stages)
 ]
 
 
@@ -113,6 +114,29 @@ PP2_ROWS_CASES = [
 @pytest.mark.parametrize("case", PP2_ROWS_CASES)
 def test_conv_wgrad_pp2_rows(case, dtype):
     test_conv_fwd_dgrad_wgrad(case, dtype)
+
+
+@pytest.mark.parametrize("case", [(32, 64, 128, 128, 128, 1, 2, 0), (4, 256, 128, 128, 128, 3, 1, 1)])
+def test_conv_wgrad_pp2_repeatable(case):
+    """The 128-channel window kernel's stages are filled by both wave groups: the same weight gradient ten times
+    over a workspace that held NaNs must come out bit-identical and finite every time (a group reading the other's
+    half of a stage before it has landed shows as NaN or drift)."""
+    from scdhip import ops
+    N, Cin, H, W, Cout, k, s, p = case
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, H, W, Cin, generator=g).to(DEV, torch.bfloat16)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, Ho, Wo, Cout, generator=g).to(DEV, torch.bfloat16)
+    outs = []
+    for _ in range(10):
+        junk = torch.full((64 << 20,), float("nan"), device=DEV)    # poison the caching allocator's free blocks
+        del junk
+        dw = torch.zeros(Cout, Cin, k, k, device=DEV)
+        ops.conv_wgrad(dy, x, k, k, s, p, dw, (Cin * k * k, k * k, 1), accumulate=False)
+        outs.append(dw)
+    assert torch.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
