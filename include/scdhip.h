@@ -203,27 +203,6 @@ int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask, const void
 int scd_bn_bwd_apply2(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
                       const float* coef_a, const float* coef_b, int C, long total, void* dya, void* dyb, void* stream);
 
-/* ---- stem without the full-resolution activation (residuals.py:209-216; bf16, Conv2d(1,64,7,s2,p3)) ----
- * scd_stem_gram: ws[z][64][64] = per-split sums of col col^T over the im2col rows of x (49 taps, tap 49 = 1, so
- * G[k][49] = sum col[k], G[49][49] = pixel count); reduce with scd_wgrad_reduce (Cg 64, T 1, Ci 64) into G fp32.
- * scd_stem_gram_stats: stats[0][0][co] += sum_k W[co][k] G[k][49], stats[0][1][co] += W[co] G W[co]^T (fp64): the
- * BN batch sums of y = conv(x) (wpk = packed bf16 [64][64] weight) without computing y.
- * scd_stem_fused_fwd: out/argmax/yam (N,Hp,Wp,64) = MaxPool(3,2,1)(relu(y*scale+shift)) with y rounded to bf16 as
- * scd_stem_conv_fwd stores it, its window argmax (0..8) and the bf16 y at the argmax; Hp % 2 == 0, Wp % 32 == 0.
- * scd_stem_wgrad_pooled: ws[z][co][k] = per-split sums of dz[p][co] col[p][k], dz the pool+ReLU gradient built from
- * (dout, argmax, yam); stats[rep][2][64] += [sum dz, sum dz*(y-mean)*invstd] (Wo % 64 == 0).
- * scd_stem_wgrad_combine: dst[co][k] (+)= a sum_z ws + b (W G)[co][k] + c G[k][49] with coef = {a, b, c}[64] of
- * scd_bn_bwd_finalize -- the weight gradient of y = conv(x) under dy = a dz + b y + c.
- * Replace residuals.py:211-214's Conv2d/BatchNorm2d/ReLU/MaxPool2d forward and backward. */
-int scd_stem_gram(const float* x, float* ws, int nsplit, int N, int H, int W, int Ho, int Wo, void* stream);
-int scd_stem_gram_stats(const float* G, const void* wpk, double* stats, void* stream);
-int scd_stem_fused_fwd(const float* x, const void* wpk, const float* scale, const float* shift, void* out,
-                       uint8_t* argmax, void* yam, int N, int H, int W, int Ho, int Wo, int Hp, int Wp, void* stream);
-int scd_stem_wgrad_pooled(const void* dout, const uint8_t* argmax, const void* yam, const float* scale,
-                          const float* shift, const float* mean, const float* invstd, const float* x, float* ws,
-                          double* stats, int nsplit, int N, int H, int W, int Ho, int Wo, int Hp, int Wp, void* stream);
-int scd_stem_wgrad_combine(const float* ws, int nsplit, const float* coef, const float* G, const void* wpk,
-                           float* dst, int accumulate, void* stream);
 
 /* ---- stem BN-apply + ReLU + MaxPool2d(3,2,1) (residuals.py:212-214) ---- */
 /* MaxPool backward + ReLU mask (as scd_stem_pool_bwd) fused with the stem BN backward reduction:
@@ -428,11 +407,6 @@ int scd_peer_ipc_close(void* ptr);
 int scd_peer_allreduce_f64(double* data, int n, int rank, int R, void* const* boxes, int cap, unsigned long long epoch,
                            unsigned long long* err, unsigned timeout_ms, void* stream);
 
-/* A HIP stream restricted to `keep` of every `of` compute units (hipExtStreamCreateWithCUMask, the mask spread
- * evenly over the XCDs); used for the weight-gradient side stream when SCD_SIDE_CUS is set.  No reference
- * counterpart (the reference runs one default stream, networkFactory.py:257-263). */
-int scd_stream_create_cumask(int keep, int of, void** stream);
-int scd_stream_destroy(void* stream);
 
 /* ---- HIP events for live kernel timing (bench.py roofline; scdhip.ops.LaunchTimer) ----
  * scd_event_record stamps the event on `stream`; while the stream is being captured into a graph the record is an

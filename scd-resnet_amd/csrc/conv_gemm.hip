@@ -22,39 +22,8 @@
 #ifndef SCD_ABLATE
 #define SCD_ABLATE 0
 #endif
-#ifndef H384_PRIO
-#define H384_PRIO 0   // heads384 kernel MFMA priority: 0 = s_setprio 1 around each C part, 1 = group 1 static, 2 = none
-#endif
-#ifndef H384_PERSIST
-#define H384_PERSIST 0  // heads384 kernel persistent over tiles, next tile's first stage prefetched under the epilogue
-                        // (SCD_GEMM_HEADS384_GRID workgroups per CU; measured 0.826 vs 0.80 ms one-workgroup-per-tile)
-#endif
-#ifndef H384_ABL
-#define H384_ABL 0    // heads384 timing ablations (wrong results): 1 no MFMA, 2 loop DMAs read nothing, 4 no loop
-                      // fragment reads, 8 no hidden store / tails, 16 no loop barriers, 32 no tails, 64 no hidden store
-#endif
-#ifndef H384_SCHED
-#define H384_SCHED 0  // heads384 DMA order: 0 = P1 {A0, B part 1}, 1 = P1 {B part 1}, P2 {A0, B part 2}
-#endif
 #ifndef WGRAD_OCC
 #define WGRAD_OCC 2   // register-staged weight-gradient kernel: workgroups per CU the registers are budgeted for
-                      // (3 leaves VGPRs for BN kernels beside it: measured -5%, the kernel itself slows down)
-#endif
-#ifndef H384_EPI
-#define H384_EPI 1    // heads384 epilogue: 0 = hidden tile staged in LDS (16-B stores, tails from the staged rows),
-                      // 1 = from the accumulators (tails as 16x16x16 MFMAs on the same registers, 16-B stores of
-                      // 64-B row pieces after v_permlane16_swap), 2 = tails as 1, hidden rows staged in LDS and stored
-                      // whole (less write traffic: measured 0.81 vs 0.785 ms)
-#endif
-#ifndef H384_ACP
-#define H384_ACP 0    // heads384 input-gather LDS-DMA cache policy (aux bits; 2 = nt: the gathered rows, re-read only
-                      // within a tile's nine taps, go first when L2 evicts, the weights every round re-reads stay)
-#endif
-#ifndef H384_HCP
-#define H384_HCP 0    // heads384 hidden stores: 0 = plain, 16 = sc1 buffer stores (written through, dropped from L2)
-#endif
-#ifndef SCD_ABM
-#define SCD_ABM 0     // halo kernel ablation bitmask: 1 no MFMA, 2 no loop DMA, 4 no loop fragment reads, 8 no loop barriers
 #endif
 
 namespace {
@@ -532,113 +501,6 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void conv_gemm_kernel(GemmParams 
     }
 
     gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
-}
-
-// -------------------------------------------------------------------------------------
-// 64 -> 64 channel 3x3 stride-1 convolution (layer1 of the Res10/18/34 stacks, forward and input gradient):
-// persistent halo kernel.  With N = 64 the register-staged 256x64 kernel re-fetches every input pixel once
-// per tap (9x the A bytes through L2 -> VGPR -> LDS) for only 64 output columns, and is bound by that
-// traffic.  Here one workgroup per CU keeps ALL nine taps of the packed weight in LDS (72 KiB, loaded once)
-// and walks a contiguous run of 256-pixel tiles (256 / W full image rows each); a tile's input halo
-// ((256/W + 2) rows x (W + 2) columns x 64 channels, <= 65 KiB) is staged once and the nine taps read it at
-// shifted offsets.  The next tile's halo is fetched into registers while the current one is computed.
-// Same MFMA fragment layout and epilogue as conv_gemm_kernel<bf16,256,64> (the epilogue stages through the
-// halo region after the last fragment read).  Opt-in (SCD_GEMM_H64=1): measured 83 vs 86 us per layer1 conv
-// standalone but 1.5% slower end to end -- one 140 KiB workgroup per CU leaves one wave per SIMD to hide the
-// LDS fragment latency and keeps the side-stream weight gradients off those CUs.
-constexpr int H64_HALO_MAX = 4 * 130 * 128;      // W = 128: 4 halo rows x 130 columns x 128 B
-constexpr int H64_HCH = (H64_HALO_MAX / 16 + 255) / 256;   // halo 16-B chunks per thread (17)
-constexpr int H64_B = 9 * 64 * 128;              // nine taps x 64 co x 64 ci bf16
-
-__global__ __launch_bounds__(256, 1) void conv_gemm_h64_kernel(GemmParams p, int ntiles, int per) {
-    __shared__ __attribute__((aligned(16))) char smem[H64_HALO_MAX + H64_B];
-    char* const Hs = smem;
-    char* const Bs = smem + H64_HALO_MAX;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int l16 = lane & 15, lg = lane >> 4;
-    const scd_gemm_phase& ph = p.ph[0];
-    const int W = p.Wo, TH = 256 / W, HC = W + 2;
-    const int hchunks = (TH + 2) * HC * 8;
-    const int QQ = p.Ho * p.Wo, M = p.N * QQ;
-    const int rows_per_img = p.Ho / TH;
-    const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
-    if (t0 >= t1) return;
-
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
-
-    // all nine taps of the weight: LDS row t*64 + co holds w[co][wt[t]][0..63], chunk-swizzled
-    for (int q = tid; q < 9 * 64 * 8; q += 256) {
-        const int row = q >> 3, c = q & 7, t = row >> 6, co = row & 63;
-        uint4 v = bload(wrs, sel_off(t < ph.ntaps, (co * p.wrow + ph.wt[t] * 64 + c * 8) * 2));
-        *(uint4*)(Bs + swz(row, c)) = v;
-    }
-    // halo of tile t: pixel (hr, hc) = input (oh0 - 1 + hr, hc - 1), 8 chunks of 16 B
-    auto hload = [&](int t, uint4 (&hv)[H64_HCH]) {
-        const int n = t / rows_per_img, oh0 = (t - n * rows_per_img) * TH;
-#pragma unroll
-        for (int i = 0; i < H64_HCH; ++i) {
-            const int q = tid + 256 * i;
-            const int pix = q >> 3, c = q & 7;
-            const int hr = pix / HC, hc = pix - hr * HC;
-            const int ih = oh0 - 1 + hr, iw = hc - 1;
-            const bool ok = q < hchunks && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-            hv[i] = bload(xrs, sel_off(ok, (((n * p.Hi + ih) * p.Wi + iw) * 64 + c * 8) * 2));
-        }
-    };
-    auto hstore = [&](const uint4 (&hv)[H64_HCH]) {
-#pragma unroll
-        for (int i = 0; i < H64_HCH; ++i) {
-            const int q = tid + 256 * i;
-            if (q < hchunks) *(uint4*)(Hs + swz(q >> 3, q & 7)) = hv[i];
-        }
-    };
-    uint4 hv[H64_HCH];
-    hload(t0, hv);
-    hstore(hv);
-    __syncthreads();
-    // per-lane halo row of fragment a at tap offset (0,0): output pixel wave*64 + a*16 + l16 of the tile
-    int hbase[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        const int px = wave * 64 + a * 16 + l16;
-        const int r = px / W, c = px - r * W;
-        hbase[a] = (r + 1) * HC + c + 1;
-    }
-    for (int t = t0; t < t1; ++t) {
-        if (t + 1 < t1) hload(t + 1, hv);
-        f32x4 acc[4][4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        for (int tap = 0; tap < ph.ntaps; ++tap) {
-            const int toff = ph.dh[tap] * HC + ph.dw[tap];
-            const char* Bt = Bs + tap * 64 * 128;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                bf16x8 af[4], bfr[4];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    const int hrow = hbase[a] + toff;
-                    af[a] = *(const bf16x8*)(Hs + hrow * 128 + (((s2 * 4 + lg) ^ (hrow & 7)) << 4));
-                }
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    bfr[b] = *(const bf16x8*)(Bt + (b * 16 + l16) * 128 + (((s2 * 4 + lg) ^ (l16 & 7)) << 4));
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
-            }
-        }
-        __syncthreads();                         // every wave is done with this halo
-        gemm_epilogue<__bf16, 256, 64, 1, false>(p, acc, smem, tid, t, t, 0, M, QQ, ph);
-        __syncthreads();                         // epilogue staging (halo region) consumed
-        if (t + 1 < t1) hstore(hv);
-        __syncthreads();
-    }
 }
 
 // -------------------------------------------------------------------------------------
@@ -1257,10 +1119,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     constexpr int BM = 192, BN = 384, BK = 64, EPC = 8;
     constexpr int NA = 6, NB = 6;                     // 16-row / 16-column blocks per wave
     constexpr int STAGE = (BM + BN) * 128;
-    constexpr int EROW = BN * 2 + 16;
-    constexpr int EPI = BM * EROW;
-    constexpr int SMEM = (H384_EPI == 1 || 2 * STAGE > EPI) ? 2 * STAGE : EPI;     // EPI 0 / 2 stage the hidden tile
-    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1278,7 +1137,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     const int ntiles = (M + BM - 1) / BM;
     const int lrow = lane >> 3;
     const int cch = (lane & 7) ^ lrow;
-    static_assert(!(H384_PERSIST && H384_EPI == 0), "the persistent heads384 kernel needs the register epilogue");
     // A: this lane's DMA rows 96*grp + 32*j + 8*wc + lrow (j = third), byte offset at tap (0,0) + in-image tap mask
     int a_base[3];
     unsigned a_mask[3];
@@ -1309,9 +1167,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     const int KT = ph.ntaps * cpt;
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
-    // hidden output [M][384] bf16 (< 2^31 bytes: checked by the launcher)
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.y, (short)0, 0x7fffffff, 0x00020000);
-    (void)yrs;
 
     struct StageArgs { int live, tap, adelta, bdelta; };
     auto stage_args = [&](int kt_req) {
@@ -1327,7 +1182,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     auto issue_a = [&](const StageArgs& g, char* buf, int j) {
         const bool ok = g.live && ((a_mask[j] >> g.tap) & 1u);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(buf + (96 * grp + 32 * j + 8 * wc) * 128), 16,
-                                                 sel_off(ok, a_base[j] + g.adelta), 0, 0, H384_ACP);
+                                                 sel_off(ok, a_base[j] + g.adelta), 0, 0, 0);
     };
     auto issue_b = [&](const StageArgs& g, char* buf, int part) {
         char* Bs = buf + BM * 128;
@@ -1344,19 +1199,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         issue_a(g0, smem, 1);
         issue_a(g0, smem, 2);
     };
-#if H384_PERSIST
-    // persistent over tiles (SCD_GEMM_HEADS384_GRID workgroups per CU): the next tile's first K-stage is issued
-    // right after this tile's hidden stores, so its DMA latency hides under the tails' LDS exchange and the
-    // output pass (their partials then live in stage buffer 1)
-    if (bid < ntiles && KT > 0) { tile_setup(bid); issue_stage0(); }
-    for (int mt = bid; mt < ntiles; mt += gridDim.x) {
-#else
     {
         const int mt = bid;
         (void)ntiles;
         tile_setup(mt);
         if (KT > 0) issue_stage0();
-#endif
         const int l16 = lane & 15, lg = lane >> 4;
         const int l7 = l16 & 7;
         const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
@@ -1387,16 +1234,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         auto mfma_q = [&](int q) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (H384_PRIO == 0) __builtin_amdgcn_s_setprio(1);
-            if constexpr (H384_ABL & 1) {
-    #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-    #pragma unroll
-                    for (int a = 0; a < 2; ++a) asm volatile("" ::"v"(af[a][s]));
-    #pragma unroll
-                    for (int b = 0; b < NB; ++b) asm volatile("" ::"v"(bfr[b][s]));
-                }
-            } else {
+            __builtin_amdgcn_s_setprio(1);
     #pragma unroll
             for (int s = 0; s < 2; ++s)
     #pragma unroll
@@ -1404,46 +1242,41 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     #pragma unroll
                     for (int b = 0; b < NB; ++b)
                         acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b][s], af[a][s], acc[2 * q + a][b], 0, 0, 0);
-            }
-            if constexpr (H384_PRIO == 0) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
         };
         auto bar = [&]() {
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (!(H384_ABL & 16)) __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
         };
 
         if (KT > 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
-            if constexpr (H384_ABL & 4) { read_b(smem); read_a(smem, 0); }
             if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
-            if constexpr (H384_PRIO == 1) { if (grp == 1) __builtin_amdgcn_s_setprio(1); }
             for (int t = 0; t < KT; ++t) {
                 char* cur = smem + (t & 1) * STAGE;
                 char* nxt = smem + ((t & 1) ^ 1) * STAGE;
-                StageArgs g = stage_args(t + 1);
-                if constexpr (H384_ABL & 2) g.live = 0;
+                const StageArgs g = stage_args(t + 1);
                 // P1
-                if constexpr (!(H384_ABL & 4)) { read_b(cur); read_a(cur, 0); }
-                if constexpr (H384_SCHED == 0) issue_a(g, nxt, 0);
+                read_b(cur);
+                read_a(cur, 0);
+                issue_a(g, nxt, 0);
                 issue_b(g, nxt, 0);
                 bar();
                 mfma_q(0);
-                if constexpr (H384_SCHED == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // A third 1 (P3 of t-1)
-                else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(5)" ::: "memory");     // A third 1 (P3 of t-1)
                 bar();
                 // P2
-                if constexpr (!(H384_ABL & 4)) read_a(cur, 1);
-                if constexpr (H384_SCHED == 1) issue_a(g, nxt, 0);
+                read_a(cur, 1);
                 issue_b(g, nxt, 1);
                 bar();
                 mfma_q(1);
                 asm volatile("s_waitcnt vmcnt(7)" ::: "memory");     // A third 2 of this stage
                 bar();
                 // P3
-                if constexpr (!(H384_ABL & 4)) read_a(cur, 2);
+                read_a(cur, 2);
                 issue_a(g, nxt, 1);
                 issue_a(g, nxt, 2);
                 asm volatile("s_waitcnt vmcnt(2)" ::: "memory");     // next stage: A third 0 and every B row
@@ -1455,7 +1288,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-#if H384_EPI >= 1
         // ---- epilogue from the accumulators.  Lane (l16, lg) of block (a, b) holds hidden channels
         // 96wc + 16b + 4lg .. +3 of pixel 96grp + 16a + l16: after bias + ReLU those 4 bf16 are (1) an 8-B piece of
         // the pixel's NHWC row, stored at once, and (2) exactly the B operand of a 16x16x16 MFMA (B[k = 4lg + j][n =
@@ -1512,14 +1344,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                     for (int e = 0; e < 2; ++e)
     #pragma unroll
                         for (int r = 0; r < 4; ++r) hv[e][r] = (__bf16)fmaxf(acc[a][b + e][r] + bias[e][r], 0.f);
-                    if constexpr (!(H384_ABL & 32)) {
     #pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            tl[a] = mfma_16x16x16(whi[e], hv[e], tl[a]);
-                            tl[a] = mfma_16x16x16(wlo[e], hv[e], tl[a]);
-                        }
+                    for (int e = 0; e < 2; ++e) {
+                        tl[a] = mfma_16x16x16(whi[e], hv[e], tl[a]);
+                        tl[a] = mfma_16x16x16(wlo[e], hv[e], tl[a]);
                     }
-                    if constexpr (H384_EPI != 1) continue;      // EPI 2: the hidden tile leaves through LDS below
                     typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
                     const u32x2 x = __builtin_bit_cast(u32x2, hv[0]), y = __builtin_bit_cast(u32x2, hv[1]);
                     uint4 st;
@@ -1529,23 +1358,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                         st.x = s0[0]; st.y = s1[0]; st.z = s0[1]; st.w = s1[1];
                     }
                     const int m = mt * BM + 96 * grp + 16 * a + l16;
-                    if constexpr (!(H384_ABL & 64))
-                        if (m < M && (colst < p.hid_cols || ((keep >> a) & 1u))) {
-                            if constexpr (H384_HCP == 0) *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
-                            else {
-                                typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-                                const u32x4 sv = {st.x, st.y, st.z, st.w};
-                                __builtin_amdgcn_raw_buffer_store_b128(sv, yrs, (m * BN + colst) * 2, 0, H384_HCP);
-                            }
-                        }
+                    if (m < M && (colst < p.hid_cols || ((keep >> a) & 1u)))
+                        *(uint4*)(p.y + ((long)m * BN + colst) * 2) = st;
                 }
             }
-#if H384_PERSIST
-            if (mt + (int)gridDim.x < ntiles) { tile_setup(mt + gridDim.x); issue_stage0(); }
-#endif
-            if constexpr (!(H384_ABL & 32)) {
+            {
                 // partials [wc][o][pixel of tile]: D[o = 4lg + r][px = l16] of block a
-                float* part = (float*)(smem + (H384_PERSIST ? STAGE : 0));
+                float* part = (float*)smem;
     #pragma unroll
                 for (int a = 0; a < NA; ++a)
     #pragma unroll
@@ -1567,389 +1386,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                     out[((long)n * odh + ob) * QQ + pix] = v + bo;
                 }
             }
-            if constexpr (H384_EPI == 2 && !(H384_ABL & 64)) {
-                // EPI 2: the hidden tile staged in LDS (rows of EROW bytes), then whole 768-B NHWC rows leave as
-                // consecutive 16-B chunks (full 128-B lines instead of 64-B pieces)
-                __syncthreads();                           // tail partials consumed
-    #pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    const int col0 = 96 * wc + 16 * b + 4 * lg;
-                    const float4 bb = *(const float4*)(p.bias + col0);
-                    const float bias[4] = {bb.x, bb.y, bb.z, bb.w};
-    #pragma unroll
-                    for (int a = 0; a < NA; ++a) {
-                        hx4 o;
-    #pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[a][b][r] + bias[r], 0.f);
-                        *(hx4*)(smem + (96 * grp + 16 * a + l16) * EROW + col0 * 2) = o;
-                    }
-                }
-                __syncthreads();
-                for (int idx = tid; idx < BM * 48; idx += 512) {
-                    const int row = idx / 48, ch = idx - (idx / 48) * 48;
-                    const int m = mt * BM + row;
-                    if (m < M) *(uint4*)(p.y + ((long)m * BN + ch * EPC) * 2) = *(const uint4*)(smem + row * EROW + ch * 16);
-                }
-            }
         }
-#else
-        // ---- epilogue: bias + ReLU, the hidden tile staged in LDS
-    #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int col0 = 96 * wc + 16 * b + 4 * lg;
-            const float4 bb = *(const float4*)(p.bias + col0);
-            const float bias[4] = {bb.x, bb.y, bb.z, bb.w};
-    #pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                bf16x4 o;
-    #pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[a][b][r] + bias[r], 0.f);
-                *(bf16x4*)(smem + (96 * grp + 16 * a + l16) * EROW + col0 * 2) = o;
-            }
-        }
-        __syncthreads();
-        if constexpr (H384_ABL & 8) { __syncthreads(); return; }
-        // 1x1 tails as a small MFMA GEMM on the staged hidden tile: out[px][o] = sum_c hid[px][c] * W1[c][o] with the
-        // three heads' 1x1 weights block-diagonal in W1 (o < sum od <= 16 columns, K = 384): 12 k-steps per
-        // 16-pixel block, fp32 weights split into bf16 hi + lo parts (two MFMAs per k-step, ~2^-17 relative weight
-        // error); wave w takes the pixel blocks w and w + 8
-        if constexpr (!(H384_ABL & 32)) {
-            int o = lane & 15;
-            asm volatile("" : "+v"(o));          // tile-invariant setup stays here (not hoisted across the K loop)
-            const int od0 = p.head_od[0], od1 = p.head_od[1], od2 = p.head_od[2];
-            const int hh = o < od0 ? 0 : o < od0 + od1 ? 1 : o < od0 + od1 + od2 ? 2 : -1;
-            const int oo = hh == 0 ? o : hh == 1 ? o - od0 : o - od0 - od1;
-            const int odh = hh == 0 ? od0 : hh == 1 ? od1 : od2;
-            const float* wsel = hh == 0 ? p.head_w[0] : hh == 1 ? p.head_w[1] : p.head_w[2];
-            const float bsel = hh < 0 ? 0.f : (hh == 0 ? p.head_b[0] : hh == 1 ? p.head_b[1] : p.head_b[2])[oo];
-            float* osel = hh == 0 ? p.head_out[0] : hh == 1 ? p.head_out[1] : p.head_out[2];
-            for (int rb = wave; rb < BM / 16; rb += 8) {
-                f32x4 c = (f32x4){0.f, 0.f, 0.f, 0.f};
-                const char* arow = smem + (16 * rb + l16) * EROW + 16 * lg;
-#pragma unroll 4
-                for (int ks = 0; ks < 12; ++ks) {
-                    const int c0 = 32 * ks + 8 * lg;
-                    float w8[8];
-                    if (hh == (c0 >> 7)) {
-                        const float4 u = *(const float4*)(wsel + oo * 128 + (c0 & 127));
-                        const float4 v = *(const float4*)(wsel + oo * 128 + (c0 & 127) + 4);
-                        w8[0] = u.x; w8[1] = u.y; w8[2] = u.z; w8[3] = u.w;
-                        w8[4] = v.x; w8[5] = v.y; w8[6] = v.z; w8[7] = v.w;
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) w8[e] = 0.f;
-                    }
-                    bf16x8 whi, wlo;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        whi[e] = (__bf16)w8[e];
-                        wlo[e] = (__bf16)(w8[e] - (float)whi[e]);
-                    }
-                    const bf16x8 av = *(const bf16x8*)(arow + 64 * ks);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, whi, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, wlo, c, 0, 0, 0);
-                }
-                if (hh >= 0) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int m = mt * BM + 16 * rb + 4 * lg + r;
-                        if (m < M) {
-                            const int n = m / QQ, pix = m - (m / QQ) * QQ;
-                            osel[((long)n * odh + oo) * QQ + pix] = c[r] + bsel;
-                        }
-                    }
-                }
-            }
-        }
-        // hidden activation (NHWC, 384 channels): 48 16-B chunks per pixel row, stored last so that no later load
-        // of the tile (the tails' weights) waits behind these stores in vmcnt order
-        if constexpr (!(H384_ABL & 64))
-        for (int idx = tid; idx < BM * 48; idx += 512) {
-            const int row = idx / 48, ch = idx - (idx / 48) * 48;
-            const int m = mt * BM + row;
-            if (m < M) *(uint4*)(p.y + ((long)m * BN + ch * EPC) * 2) = *(const uint4*)(smem + row * EROW + ch * 16);
-        }
-#endif
         __syncthreads();                 // staging consumed before the next tile's prologue DMA
-    }
-}
-
-// -------------------------------------------------------------------------------------
-// Halo variant of the ping-pong kernel for 3x3 stride-1 convolutions (Conv2d fwd and its dgrad, the
-// head convolution): the 256-pixel tile is a TH x TW block of one image (TW = 32 or 16, TH = 256/TW), the
-// K loop runs channel chunks of 64 (outer) x 9 taps (inner), and each chunk's (TH+2) x (TW+2) input halo is
-// staged in LDS ONCE: all 9 taps read their A fragments from it at a row offset dh*(TW+2)+dw.  Per K-stage
-// the workgroup then moves the BN x 64 weight slab plus 1/9 of a halo (<= 5 KB) instead of BN x 64 + 256 x 64.
-// Phases are N-major: a K-stage has NB phases, phase q multiplies all 8 of the wave's 16-pixel blocks by its
-// 16-channel block q (16 MFMAs), so weight block q of stage t+1 is needed only at phase q of stage t+1 and is
-// fetched at phase q of stage t: ONE weight DMA per wave per phase, a full stage ahead, on two weight buffers.
-// Halo rows of chunk c+1 go out in phase 0 of stages 1..6 of chunk c (dead slots land in a scratch KiB).
-// Waits: every wave keeps the newest NB-1 DMA instructions in flight (vmcnt(NB-1)) before the barrier that
-// opens group 0's next phase (group 0 after its C part, group 1 after its L part).
-template <int BN, int TW>
-__global__ __launch_bounds__(512, 1) void conv_gemm_halo_kernel(GemmParams p) {
-    typedef __bf16 T;
-    constexpr int BM = 256, EPC = 8;
-    constexpr int TH = BM / TW, HW2 = TW + 2;
-    constexpr int HR = (TH + 2) * HW2;               // halo rows
-    constexpr int NK = (HR + 7) / 8;                 // halo DMA wave-instructions per chunk (<= 48)
-    constexpr int HALO = NK * 1024;                  // one halo buffer
-    constexpr int NB = BN / 64, WCOLS = BN / 4;
-    constexpr int BSTAGE = BN * 128;
-    constexpr int DUMMY = 2 * HALO + 2 * BSTAGE;     // 8 x 1 KiB scratch for dead halo slots
-    constexpr int EROW = WCOLS * 2 + 16;
-    constexpr int EPI = 8 * 128 * EROW;
-    constexpr int SMEM = (DUMMY + 8192 > EPI + 4 * BN * 4) ? DUMMY + 8192 : EPI + 4 * BN * 4;
-    static_assert(NK <= 48, "halo");
-    static_assert(SMEM <= 163840, "LDS");
-    __shared__ __attribute__((aligned(16))) char smem[SMEM];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2, wc = wave & 3;
-    int bid;
-    {
-        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
-    }
-    const scd_gemm_phase& ph = p.ph[0];
-    const int H = p.Ho, W = p.Wo;
-    const int mt = bid / p.ntn;
-    const int nt = bid - mt * p.ntn;
-    const int tw_n = W / TW, th_n = (H + TH - 1) / TH;
-    const int img = mt / (tw_n * th_n);
-    const int trem = mt - img * (tw_n * th_n);
-    const int th = trem / tw_n, tw = trem - (trem / tw_n) * tw_n;
-    const int h0 = th * TH, w0 = tw * TW;
-
-    const int lrow = lane >> 3;
-    const int cch = (lane & 7) ^ lrow;
-    // halo slot sl of this thread: instruction k = 8*sl + wave covers halo rows 8k .. 8k+7; the lane fetches
-    // row 8k+lrow (computed per use: a register array indexed by the runtime slot would live in scratch)
-    auto halo_off = [&](int sl) {
-        const int r = 8 * (8 * sl + wave) + lrow;
-        const int hi = r / HW2, hj = r - (r / HW2) * HW2;
-        const int ih = h0 - 1 + hi, iw = w0 - 1 + hj;
-        const bool ok = r < HR && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-        return ok ? (((img * H + ih) * W + iw) * p.Ci + cch * EPC) * 2 : -1;
-    };
-    // weight block q (the 16 channels q of every wave) = LDS rows wc'*WCOLS + 16q + 0..15; this wave fetches
-    // rows wc*WCOLS + 16q + 8*grp + lrow
-    int b_row[NB];
-    bool b_ok[NB];
-#pragma unroll
-    for (int q = 0; q < NB; ++q) {
-        const int nn = nt * BN + wc * WCOLS + 16 * q + 8 * grp + lrow;
-        b_ok[q] = nn < p.Co;
-        b_row[q] = b_ok[q] ? nn : 0;
-    }
-    const int cpt = p.Ci / 64;
-    const int KT = 9 * cpt;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
-    char* const Bbase = smem + 2 * HALO;
-
-    // halo slot `sl` of chunk c into halo buffer (c & 1); live == false -> the scratch KiB, no traffic
-    auto issue_halo = [&](int c, int sl, bool live) {
-        const int off = halo_off(sl);
-        const bool kl = live && (8 * sl + wave) < NK;
-        char* dst = kl ? smem + (c & 1) * HALO + (8 * sl + wave) * 1024 : smem + DUMMY + wave * 1024;
-        dma16(xrs, dst, sel_off(SCD_ABLATE != 7 && kl && off >= 0, off + c * 128));
-    };
-    auto issue_b = [&](int live, int c, int wt, char* buf, int q) {
-        dma16(wrs, buf + (wc * WCOLS + 16 * q + 8 * grp) * 128,
-              sel_off(SCD_ABLATE != 6 && live && b_ok[q], (b_row[q] * p.wrow + wt * p.Ci + c * 64 + cch * EPC) * 2));
-    };
-
-    const int l16 = lane & 15, lg = lane >> 4;
-    const int l7 = l16 & 7;
-    const int co0 = ((0 * 4 + lg) ^ l7) << 4, co1 = ((1 * 4 + lg) ^ l7) << 4;
-    // centre-tap halo row of the pixel this lane feeds in 16-pixel block a
-    int hr0[8];
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-        const int m = 128 * grp + 16 * a + l16;
-        hr0[a] = (m / TW + 1) * HW2 + (m % TW) + 1;
-    }
-    f32x4 acc[8][NB];
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 af[8][2], bx[2], by[2];
-
-    auto read_a = [&](const char* halo, int toff) {
-#pragma unroll
-        for (int a = 0; a < 8; ++a) {
-            const int hr = hr0[a] + toff;
-            const char* row = halo + hr * 128;
-            const int x7 = hr & 7;
-            af[a][0] = *(const bf16x8*)(row + (((0 * 4 + lg) ^ x7) << 4));
-            af[a][1] = *(const bf16x8*)(row + (((1 * 4 + lg) ^ x7) << 4));
-        }
-    };
-    auto read_b = [&](const char* Bs, int q, bf16x8 (&bq)[2]) {
-        const char* row = Bs + (wc * WCOLS + q * 16 + l16) * 128;
-        bq[0] = *(const bf16x8*)(row + co0);
-        bq[1] = *(const bf16x8*)(row + co1);
-    };
-    auto mfma_n = [&](int q, const bf16x8 (&bq)[2]) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (SCD_ABLATE == 1 || (SCD_ABM & 1)) {
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-#pragma unroll
-                for (int a = 0; a < 8; ++a) asm volatile("" ::"v"(af[a][s]));
-                asm volatile("" ::"v"(bq[s]));
-            }
-            return;
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int a = 0; a < 8; ++a)
-                acc[a][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s], af[a][s], acc[a][q], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto bar = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(SCD_ABM & 8)) __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto keep_inflight = [&]() {        // all but the newest NB-1 DMA instructions have landed
-        if constexpr (SCD_ABLATE == 8) return;
-        if constexpr (NB == 4) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    };
-
-    if (cpt > 0) {
-        // prologue: the whole halo of chunk 0 and every weight block of stage 0 (tap 0)
-#pragma unroll
-        for (int sl = 0; sl < 6; ++sl) issue_halo(0, sl, true);
-#pragma unroll
-        for (int q = 0; q < NB; ++q) issue_b(1, 0, ph.wt[0], Bbase, q);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();
-        if constexpr (SCD_ABM & 4) { read_a(smem, 0); read_b(Bbase, 0, bx); read_b(Bbase, 1, by); }
-        if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
-        int c = 0, tp = 0;
-        for (int t = 0; t < KT; ++t) {
-            const char* halo = smem + (c & 1) * HALO;
-            const char* Bcur = Bbase + (t & 1) * BSTAGE;
-            char* Bnxt = Bbase + ((t & 1) ^ 1) * BSTAGE;
-            const int toff = ph.dh[tp] * HW2 + ph.dw[tp];
-            const int ntp = tp == 8 ? 0 : tp + 1, nc = tp == 8 ? c + 1 : c;
-            const int nlive = t + 1 < KT;
-            const int nwt = ph.wt[ntp];
-#pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                bf16x8 (&bq)[2] = (q & 1) ? by : bx;
-                // L part: fragment reads + this phase's DMA (weight block q of stage t+1; phase 0 also a halo slot)
-                if constexpr (!(SCD_ABM & 4)) {
-                    if (q == 0) read_a(halo, toff);
-                    read_b(Bcur, q, bq);
-                }
-                if constexpr (!(SCD_ABM & 2)) {
-                    issue_b(nlive, nc, nwt, Bnxt, q);
-                    if (q == 0) issue_halo(c + 1, tp - 1, tp >= 1 && tp <= 6 && c + 1 < cpt);
-                }
-                if (grp == 1) keep_inflight();
-                bar();
-                // C part
-                mfma_n(q, bq);
-                if (grp == 0) keep_inflight();
-                bar();
-            }
-            tp = ntp;
-            c = nc;
-        }
-        if (grp == 0) bar();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    // ---- epilogue (as conv_gemm_pp_kernel, pixels addressed by tile coordinates)
-    char* ep = smem + wave * 128 * EROW;
-    float csum[NB][4], csq[NB][4];
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
-        float bias[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
-#pragma unroll
-        for (int a = 0; a < 8; ++a) {
-            const int m = 128 * grp + a * 16 + l16;
-            const bool valid = h0 + m / TW < H;
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] = acc[a][b][r] + bias[r];
-                if (p.relu) v[r] = fmaxf(v[r], 0.f);
-                if (valid) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
-            }
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-            bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-            *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    {
-        constexpr int CPR = WCOLS * 2 / 16;
-        for (int idx = lane; idx < 128 * CPR; idx += 64) {
-            const int row = idx / CPR, ch = idx - (idx / CPR) * CPR;
-            const int m = 128 * grp + row;
-            const int oh = h0 + m / TW, ow = w0 + m % TW;
-            const int col = nt * BN + wc * WCOLS + ch * EPC;
-            if (oh >= H || col >= p.Co) continue;
-            T* dst = (T*)(p.y) + ((long)(img * H + oh) * W + ow) * p.Co + col;
-            uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
-            if (p.accumulate) {
-                float a[EPC], o[EPC];
-                Vec16<T>::load(&v, a);
-                Vec16<T>::load(dst, o);
-#pragma unroll
-                for (int e = 0; e < EPC; ++e) a[e] += o[e];
-                Vec16<T>::store(&v, a);
-            }
-            *(uint4*)dst = v;
-        }
-    }
-    if (p.stats) {
-        float* red = (float*)(smem + EPI);
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float s = csum[b][r], q = csq[b][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-                if (l16 == 0) {
-                    const int c = wc * WCOLS + b * 16 + lg * 4 + r;
-                    red[(grp * BN + c) * 2 + 0] = s;
-                    red[(grp * BN + c) * 2 + 1] = q;
-                }
-            }
-        __syncthreads();
-        if (tid < BN) {
-            const int col = nt * BN + tid;
-            if (col < p.Co) {
-                const double s = (double)red[tid * 2] + (double)red[(BN + tid) * 2];
-                const double q = (double)red[tid * 2 + 1] + (double)red[(BN + tid) * 2 + 1];
-                const int rep = (bid % SCD_STAT_REPLICAS);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
-            }
-        }
     }
 }
 
@@ -2270,392 +1708,9 @@ __global__ __launch_bounds__(256, WGRAD_OCC) void conv_wgrad_kernel(WgradParams 
         }
 }
 
-// -------------------------------------------------------------------------------------
-// Large-shape bf16 weight gradient on the LDS-DMA ring: tile 128 (Cg) x 256 (KK), 8 waves (2 x 4,
-// 64x64 each), K = pixels in stages of 64, three 48-KiB ring slots, one raw barrier per stage.
-// Both operands are [pixel][column] rows read with ds_read_b64_tr_b16; the 32-B column pair p of
-// pixel row r is stored at pair p ^ f(r), f(r) = (r & 3) | ((r >> 1) & 4): the 8 rows a half-wave's
-// transposed read touches then sit in 8 different bank groups.  The DMA writes lane-linearly, so
-// each lane fetches the chunk whose swizzled slot it writes.
+// 32-B column-pair swizzle of the transposed-read stage images (conv_wgrad_pp2_kernel): f(r) over rows
+// {r..r+3, r+8..r+11} takes 8 distinct values, so a 32-lane half's ds_read_b64_tr_b16 reads are conflict free
 __device__ __forceinline__ int wr_f(int r) { return (r & 3) | ((r >> 1) & 4); }
-
-__global__ __launch_bounds__(512, 1) void conv_wgrad_ring_kernel(WgradParams p) {
-    constexpr int BM = 128, BN = 256, KP = 64, EPC = 8;
-    constexpr int GROWB = BM * 2, XROWB = BN * 2;          // 256 B, 512 B
-    constexpr int GST = KP * GROWB, STAGE = KP * (GROWB + XROWB);   // 16 KiB, 48 KiB
-    constexpr int NSLOT = 3;
-    __shared__ __attribute__((aligned(16))) char smem[NSLOT * STAGE];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // XCD-aware split placement: every tile of split z runs on XCD z % 8 (blocks are dispatched to XCDs
-    // round-robin on blockIdx), so the tiles re-reading the split's pixel rows share one L2
-    int z, mt, nt;
-    if (!wgrad_block(p, z, mt, nt)) return;
-    const int M = p.N * p.Ho * p.Wo;
-    const int pix0 = z * p.chunk;
-    const int pix1 = min(M, pix0 + p.chunk);
-
-    // G: 16 DMA instructions per stage (4 rows of 256 B each), 2 per wave: rows 8*wave + 4*i + lane/16
-    int g_row[2], g_off[2];
-    bool g_ok[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = 8 * wave + 4 * i + (lane >> 4);
-        const int slot = lane & 15;
-        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);      // chunk this slot holds
-        const int col = mt * BM + c * EPC;
-        g_row[i] = r;
-        g_ok[i] = col < p.Cg;
-        g_off[i] = col;
-    }
-    // X: 32 instructions per stage (2 rows of 512 B each), 4 per wave: rows 8*wave + 2*i + lane/32
-    int x_row[4], x_ci[4], x_dh[4], x_dw[4];
-    bool x_ok[4];
-    int xn[4], xoh[4], xow[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = 8 * wave + 2 * i + (lane >> 5);
-        const int slot = lane & 31;
-        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);
-        const int kk = nt * BN + c * EPC;
-        x_ok[i] = kk < p.KK;
-        const int tap = x_ok[i] ? kk / p.Ci : 0;
-        x_ci[i] = kk - tap * p.Ci;
-        x_dh[i] = p.dh[tap];
-        x_dw[i] = p.dw[tap];
-        x_row[i] = r;
-        const int pix = pix0 + r;
-        const int HoWo = p.Ho * p.Wo;
-        xn[i] = pix / HoWo;
-        const int rem = pix - xn[i] * HoWo;
-        xoh[i] = rem / p.Wo;
-        xow[i] = rem - xoh[i] * p.Wo;
-    }
-    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
-    // stage k (pixels k0 .. k0+63) into ring slot `slot`; always 6 DMA instructions per thread
-    auto issue = [&](int k0, int slot) {
-        char* Gs = smem + slot * STAGE;
-        char* Xs = Gs + GST;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int pix = k0 + g_row[i];
-            dma16_asm(grs, Gs + (8 * wave + 4 * i) * GROWB, sel_off(g_ok[i] && pix < pix1, (pix * p.Cg + g_off[i]) * 2));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int pix = k0 + x_row[i];
-            const int ih = p.is * xoh[i] + x_dh[i], iw = p.is * xow[i] + x_dw[i];
-            const bool ok = x_ok[i] && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-            dma16_asm(xrs, Xs + (8 * wave + 2 * i) * XROWB,
-                  sel_off(ok, (((xn[i] * p.Hi + ih) * p.Wi + iw) * p.Ci + x_ci[i]) * 2));
-        }
-    };
-    auto advance = [&]() {     // every X row advances by KP pixels
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            xow[i] += KP;
-            while (xow[i] >= p.Wo) {
-                xow[i] -= p.Wo;
-                if (++xoh[i] >= p.Ho) { xoh[i] = 0; ++xn[i]; }
-            }
-        }
-    };
-
-    const int wm = wave >> 2, wn = wave & 3;
-    const int l16 = lane & 15, lg = lane >> 4;
-    const int q = l16 >> 2, pp = l16 & 3;
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    const int nk = (pix1 > pix0) ? (pix1 - pix0 + KP - 1) / KP : 0;
-    if (nk > 0) {
-        issue(pix0, 0);
-        advance();
-        issue(pix0 + KP, 1);
-        advance();
-        int slot = 0;
-        for (int it = 0; it < nk; ++it) {
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            issue(pix0 + (it + 2) * KP, slot == 0 ? 2 : slot - 1);
-            advance();
-            const char* Gs = smem + slot * STAGE;
-            const char* Xs = Gs + GST;
-            typedef __attribute__((ext_vector_type(8))) short s16x8;
-            bf16x8 af[2][4], bfr[2][4];
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int r0 = 32 * s + 8 * lg + q;
-                const int f0 = wr_f(r0), f1 = wr_f(r0 + 4);
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    const int cb = (wm * 64 + a * 16 + 4 * pp) * 2;         // byte column in the G row
-                    const int pr = cb >> 5, lo8 = cb & 31;
-                    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(Gs + r0 * GROWB + ((pr ^ f0) << 5) + lo8));
-                    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(Gs + (r0 + 4) * GROWB + ((pr ^ f1) << 5) + lo8));
-                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    af[s][a] = __builtin_bit_cast(bf16x8, v);
-                }
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int cb = (wn * 64 + b * 16 + 4 * pp) * 2;
-                    const int pr = cb >> 5, lo8 = cb & 31;
-                    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(Xs + r0 * XROWB + ((pr ^ f0) << 5) + lo8));
-                    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(Xs + (r0 + 4) * XROWB + ((pr ^ f1) << 5) + lo8));
-                    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    bfr[s][b] = __builtin_bit_cast(bf16x8, v);
-                }
-            }
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s][a], bfr[s][b], acc[a][b], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            slot = slot == 2 ? 0 : slot + 1;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    // ---- epilogue: stage the wave's 64x64 fp32 tile in LDS, then 16-B coalesced slab stores
-    constexpr int EROW = 64 * 4 + 16;
-    float* ep = (float*)(smem + wave * 64 * EROW);
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                ep[((a * 16 + lg * 4 + r) * EROW) / 4 + b * 16 + l16] = acc[a][b][r];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's tile is staged (wave-private)
-    float* ws = p.ws + (long)z * p.Cg * p.KK;
-    const int ch = lane & 15;              // 16-B chunk of a 64-float row
-    const int col = nt * BN + wn * 64 + ch * 4;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int rr = (lane >> 4) + 4 * j;
-        const int row = mt * BM + wm * 64 + rr;
-        if (row < p.Cg && col < p.KK)
-            *(float4*)(ws + (long)row * p.KK + col) = *(const float4*)((const char*)ep + rr * EROW + ch * 16);
-    }
-}
-
-// -------------------------------------------------------------------------------------
-// Ping-pong bf16 weight gradient: tile BMG (output-gradient channels, a column slice starting at gc0) x 256
-// (taps x input channels), K = pixels in stages of 32, four LDS stage slots (stage t+2 is fetched while
-// stage t is computed).  8 waves in two staggered groups of 4 (group g owns BMG/2 channels, wave wc 64
-// columns); a stage is 2 phases (one half of the group's channel blocks each), every phase an L part
-// (ds_read_b64_tr_b16 fragment reads + LDS-DMA issue) and a C part (MFMAs), each closed by s_barrier.  Both
-// stage images are [32 pixels][row] with 32-B column pairs XOR-swizzled by f(r) (conflict-free transposed
-// reads; the DMA is lane-linear, so each lane fetches the chunk its slot holds).  Each wave issues n1 + n2
-// DMA instructions per stage (phase 1: n1, phase 2: n2) and keeps the newest n1 + n2 in flight (group 0
-// after its C2, group 1 after its L2: the barrier that opens group 0's read of the next-but-one stage).
-// The MFMA A operand is the input fragment, so each lane ends with 4 consecutive columns of one channel:
-// the fp32 slab is written with 16-B stores straight from the accumulators.
-template <int BMG>
-__global__ __launch_bounds__(512, 1) void conv_wgrad_pp_kernel(WgradParams p, int gc0) {
-    constexpr int KP = 32, EPC = 8;
-    constexpr int GROWB = BMG * 2, XROWB = 512;
-    constexpr int GST = KP * GROWB, STAGE = GST + KP * XROWB;
-    constexpr int NSLOT = 4;
-    constexpr int MB = BMG / 32;                       // 16-channel blocks per wave (8 or 4)
-    constexpr int GI = KP * GROWB / 1024;              // G DMA instructions per stage (16 or 8)
-    constexpr int GR = 1024 / GROWB;                   // G rows per instruction (2 or 4)
-    constexpr int N1 = BMG == 256 ? 2 : 2, N2 = BMG == 256 ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) char smem[NSLOT * STAGE];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2, wc = wave & 3;
-    int z, mt, nt;
-    if (!wgrad_block(p, z, mt, nt)) return;
-    const int M = p.N * p.Ho * p.Wo;
-    const int pix0 = z * p.chunk;
-    const int pix1 = min(M, pix0 + p.chunk);
-    const int gbase = gc0 + mt * BMG;
-
-    // G DMA: BMG=256: instruction k = 2*wave + j (phase 1); BMG=128: k = wave (phase 2).  Row = GR*k + lane/(64/GR).
-    constexpr int NG = BMG == 256 ? 2 : 1;
-    int g_row[NG], g_col[NG];
-#pragma unroll
-    for (int j = 0; j < NG; ++j) {
-        const int k = NG * wave + j;
-        const int r = GR * k + lane / (64 / GR);
-        const int slot = lane % (64 / GR);
-        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);
-        g_row[j] = r;
-        g_col[j] = gbase + c * EPC;
-    }
-    // X DMA: instruction k = 2*wave + j (16 per stage), rows 2k + lane/32
-    int x_row[2], x_ci[2], x_dh[2], x_dw[2];
-    bool x_ok[2];
-    int xn[2], xoh[2], xow[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int r = 2 * (2 * wave + j) + (lane >> 5);
-        const int slot = lane & 31;
-        const int c = 2 * ((slot >> 1) ^ wr_f(r)) + (slot & 1);
-        const int kk = nt * 256 + c * EPC;
-        x_ok[j] = kk < p.KK;
-        const int tap = x_ok[j] ? kk / p.Ci : 0;
-        x_ci[j] = kk - tap * p.Ci;
-        x_dh[j] = p.dh[tap];
-        x_dw[j] = p.dw[tap];
-        x_row[j] = r;
-        const int pix = pix0 + r;
-        const int HoWo = p.Ho * p.Wo;
-        xn[j] = pix / HoWo;
-        const int rem = pix - xn[j] * HoWo;
-        xoh[j] = rem / p.Wo;
-        xow[j] = rem - xoh[j] * p.Wo;
-    }
-    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, p.gbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
-    auto issue_g = [&](int k0, char* slotp) {
-#pragma unroll
-        for (int j = 0; j < NG; ++j) {
-            const int pix = k0 + g_row[j];
-            dma16_asm(grs, slotp + (GR * (NG * wave + j)) * GROWB, sel_off(pix < pix1, (pix * p.Cg + g_col[j]) * 2));
-        }
-    };
-    auto issue_x = [&](int k0, char* slotp) {
-        char* Xs = slotp + GST;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int pix = k0 + x_row[j];
-            const int ih = p.is * xoh[j] + x_dh[j], iw = p.is * xow[j] + x_dw[j];
-            const bool ok = x_ok[j] && pix < pix1 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-            dma16_asm(xrs, Xs + 2 * (2 * wave + j) * XROWB, sel_off(ok, (((xn[j] * p.Hi + ih) * p.Wi + iw) * p.Ci + x_ci[j]) * 2));
-        }
-    };
-    auto advance = [&]() {     // every X row advances by KP pixels
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            xow[j] += KP;
-            while (xow[j] >= p.Wo) {
-                xow[j] -= p.Wo;
-                if (++xoh[j] >= p.Ho) { xoh[j] = 0; ++xn[j]; }
-            }
-        }
-    };
-    // the stage's DMA for phase ph (0/1): BMG=256: G then X; BMG=128: X then G
-    auto issue_phase = [&](int k0, char* slotp, int ph) {
-        if constexpr (BMG == 256) { if (ph == 0) issue_g(k0, slotp); else issue_x(k0, slotp); }
-        else { if (ph == 0) issue_x(k0, slotp); else issue_g(k0, slotp); }
-    };
-
-    const int l16 = lane & 15, lg = lane >> 4;
-    const int q4 = l16 >> 2, pp = l16 & 3;
-    const int r0 = 8 * lg + q4;
-    const int f0 = wr_f(r0), f1 = wr_f(r0 + 4);
-    f32x4 acc[MB][4];
-#pragma unroll
-    for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    auto trfrag = [&](const char* img, int rowb, int colbyte) {
-        const int pr = colbyte >> 5, lo8 = colbyte & 31;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + r0 * rowb + ((pr ^ f0) << 5) + lo8));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (r0 + 4) * rowb + ((pr ^ f1) << 5) + lo8));
-        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        return __builtin_bit_cast(bf16x8, v);
-    };
-    bf16x8 xf[4], gfa[MB / 2], gfb[MB / 2];
-    auto read_x = [&](const char* slotp) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) xf[b] = trfrag(slotp + GST, XROWB, (wc * 64 + b * 16 + 4 * pp) * 2);
-    };
-    auto read_g = [&](const char* slotp, int h, bf16x8 (&gf)[MB / 2]) {
-#pragma unroll
-        for (int a = 0; a < MB / 2; ++a)
-            gf[a] = trfrag(slotp, GROWB, (grp * (BMG / 2) + (h * (MB / 2) + a) * 16 + 4 * pp) * 2);
-    };
-    auto mfma_h = [&](int h, const bf16x8 (&gf)[MB / 2]) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int a = 0; a < MB / 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                acc[h * (MB / 2) + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[b], gf[a], acc[h * (MB / 2) + a][b], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto bar = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto keep_inflight = [&]() {
-        if constexpr (N1 + N2 == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    };
-
-    const int nk = (pix1 > pix0) ? (pix1 - pix0 + KP - 1) / KP : 0;
-    if (nk > 0) {
-        // prologue: stages 0 and 1, stage 0 landed
-        issue_phase(pix0, smem, 0);
-        issue_phase(pix0, smem, 1);
-        advance();
-        issue_phase(pix0 + KP, smem + STAGE, 0);
-        issue_phase(pix0 + KP, smem + STAGE, 1);
-        advance();
-        keep_inflight();
-        bar();
-        if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
-        for (int it = 0; it < nk; ++it) {
-            const char* cur = smem + (it & 3) * STAGE;
-            char* nx2 = smem + ((it + 2) & 3) * STAGE;
-            const int k2 = pix0 + (it + 2) * KP;
-            // phase 1
-            read_x(cur);
-            read_g(cur, 0, gfa);
-            issue_phase(k2, nx2, 0);
-            bar();
-            mfma_h(0, gfa);
-            bar();
-            // phase 2
-            read_g(cur, 1, gfb);
-            issue_phase(k2, nx2, 1);
-            advance();
-            if (grp == 1) keep_inflight();
-            bar();
-            mfma_h(1, gfb);
-            if (grp == 0) keep_inflight();
-            bar();
-        }
-        if (grp == 0) bar();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    // ---- fp32 partial slab: lane holds columns kk..kk+3 of channel row cg for every (a, b) block
-    float* ws = p.ws + (long)z * p.Cg * p.KK;
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-        const int row = gbase + grp * (BMG / 2) + a * 16 + l16;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int col = nt * 256 + wc * 64 + b * 16 + lg * 4;
-            if (col < p.KK) *(f32x4*)(ws + (long)row * p.KK + col) = acc[a][b];
-        }
-    }
-}
 
 // -------------------------------------------------------------------------------------
 // Ping-pong bf16 weight gradient, 64-pixel stages (the conv_gemm_pp_kernel schedule applied to the
@@ -3283,37 +2338,10 @@ static int pp_mode() {
     return mode;
 }
 
-static int halo_mode() {
-    static int mode = -2;
-    if (mode == -2) {
-        const char* e = getenv("SCD_GEMM_HALO");
-        mode = e ? atoi(e) : 0;     // opt-in: measured 10% slower than the gather ping-pong kernel on the head convs
-    }
-    return mode;
-}
-
-static int h64_mode() {
-    static int mode = -2;
-    if (mode == -2) {
-        const char* e = getenv("SCD_GEMM_H64");
-        mode = e ? atoi(e) : 0;     // opt-in: 3% faster standalone, 1.5% slower in the step
-    }
-    return mode;
-}
-
 static int heads384_mode() {
     static int mode = -2;
     if (mode == -2) {
         const char* e = getenv("SCD_GEMM_HEADS384");
-        mode = e ? atoi(e) : 1;
-    }
-    return mode;
-}
-
-static int heads384_grid() {
-    static int mode = -2;
-    if (mode == -2) {
-        const char* e = getenv("SCD_GEMM_HEADS384_GRID");
         mode = e ? atoi(e) : 1;
     }
     return mode;
@@ -3330,19 +2358,6 @@ static int num_cus() {
     return n;
 }
 
-// conv_gemm_h64_kernel applies: one 3x3 stride-1 phase over whole images, 64 -> 64 channels, 256 % W == 0
-static bool h64_ok(const GemmParams& p, int nphase, const scd_gemm_phase* ph) {
-    if (nphase != 1 || p.Ci != 64 || p.Co != 64 || p.is != 1 || p.os != 1 || p.head_on || p.bnbwd) return false;
-    const scd_gemm_phase& f = ph[0];
-    if (f.ntaps != 9 || f.rho_h || f.rho_w || f.Qh != p.Ho || f.Qw != p.Wo || p.Hi != p.Ho || p.Wi != p.Wo)
-        return false;
-    if (p.Wo < 16 || p.Wo > 128 || 256 % p.Wo || p.Ho % (256 / p.Wo) || p.wrow < 9 * 64) return false;
-    for (int t = 0; t < 9; ++t)
-        if (f.dh[t] < -1 || f.dh[t] > 1 || f.dw[t] < -1 || f.dw[t] > 1 || f.wt[t] < 0 || f.wt[t] > 8) return false;
-    return true;
-}
-
-// BN of the ping-pong kernel for this output width (0 = not applicable)
 static int pp_bn(int dtype, int Co) {
     if (dtype != SCD_DT_BF16 || !pp_mode()) return 0;
     if (Co % 256 == 0) return 256;
@@ -3373,51 +2388,18 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         // the three 128-wide CenterNet heads: one 192 x 384 tile per 192 pixels, tails fused
         const long wb = (long)p.Co * p.wrow * esz;
         if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
-        if (H384_HCP && Mtot * p.Co * esz >= (1L << 31) - 64) return SCD_ERR_ARG;   // 32-bit hidden store offsets
         p.xbytes = (int)xb;
         p.wbytes = (int)wb;
         p.ntn = 1;
         p.ph[0] = phases[0];
         for (int i = 0; i <= SCD_MAX_PHASES; ++i) p.tile_start[i] = 0;
         const int tiles = cdiv(Mtot, 192);
-        const int per = H384_PERSIST ? heads384_grid() : 0;   // 0: one workgroup per tile; k: k per CU, persistent
-        const int grid = per > 0 ? std::min(tiles, per * num_cus()) : tiles;
-        hipLaunchKernelGGL(conv_gemm_heads384_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p);
+        hipLaunchKernelGGL(conv_gemm_heads384_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, p);
         SCD_RETURN_LAUNCH();
     }
     {
         // ping-pong 256 x BN kernel when the grid fills the chip (fused head tails are run as a separate pass)
         const int bn = pp_bn(dtype, p.Co);
-        // halo variant: one 3x3 stride-1 phase over the whole image, width a multiple of 16
-        const scd_gemm_phase& f = phases[0];
-        bool halo = bn && halo_mode() && nphase == 1 && f.ntaps == 9 && p.is == 1 && p.os == 1 && f.rho_h == 0 &&
-                    f.rho_w == 0 && f.Qh == p.Ho && f.Qw == p.Wo && p.Hi == p.Ho && p.Wi == p.Wo && p.Wo % 16 == 0;
-        for (int t = 0; halo && t < 9; ++t)
-            halo = f.dh[t] >= -1 && f.dh[t] <= 1 && f.dw[t] >= -1 && f.dw[t] <= 1;
-        if (halo && !p.bnbwd) {
-            const int TW = p.Wo % 32 == 0 ? 32 : 16, TH = 256 / TW;
-            const long mtiles = (long)p.N * ((p.Ho + TH - 1) / TH) * (p.Wo / TW);
-            if (mtiles * (p.Co / bn) >= 256) {
-                const long wb = (long)p.Co * p.wrow * esz;
-                if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
-                p.xbytes = (int)xb;
-                p.wbytes = (int)wb;
-                p.ntn = p.Co / bn;
-                p.ph[0] = f;
-                const int tiles = (int)(mtiles * p.ntn);
-                hipStream_t st = (hipStream_t)stream;
-                if (bn == 256 && TW == 32) hipLaunchKernelGGL((conv_gemm_halo_kernel<256, 32>), dim3(tiles), dim3(512), 0, st, p);
-                else if (bn == 256) hipLaunchKernelGGL((conv_gemm_halo_kernel<256, 16>), dim3(tiles), dim3(512), 0, st, p);
-                else if (TW == 32) hipLaunchKernelGGL((conv_gemm_halo_kernel<192, 32>), dim3(tiles), dim3(512), 0, st, p);
-                else hipLaunchKernelGGL((conv_gemm_halo_kernel<192, 16>), dim3(tiles), dim3(512), 0, st, p);
-                hipError_t e = hipGetLastError();
-                if (e != hipSuccess || !p.head_on) return (int)e;
-                int nh = 0;
-                while (nh < 4 && p.head_out[nh]) ++nh;
-                return scd_heads_fwd(dtype, p.y, p.N, p.Ho * p.Wo, nh, 128, p.head_od, p.head_w, p.head_b,
-                                     p.head_out, stream);
-            }
-        }
         if (bn && (long)cdiv(Mtot, 256) * (p.Co / bn) >= 256) {
             p.ntn = p.Co / bn;
             int tiles = 0;
@@ -3451,21 +2433,6 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         }
     }
     if (p.bnbwd && dtype != SCD_DT_BF16) return SCD_ERR_ARG;   // BN-backward sums: 16-bit epilogues (caller falls back)
-    if (dtype == SCD_DT_BF16 && h64_mode() && h64_ok(p, nphase, phases)) {
-        p.ntn = 1;
-        p.ph[0] = phases[0];
-        for (int i = 0; i <= SCD_MAX_PHASES; ++i) p.tile_start[i] = 0;
-        const long wb = (long)p.Co * p.wrow * esz;
-        if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
-        p.xbytes = (int)xb;
-        p.wbytes = (int)wb;
-        const int ntiles = (int)((long)p.N * p.Ho * p.Wo / 256);
-        const int grid = min(ntiles, num_cus());
-        const int per = (ntiles + grid - 1) / grid;
-        hipLaunchKernelGGL(conv_gemm_h64_kernel, dim3((ntiles + per - 1) / per), dim3(256), 0, (hipStream_t)stream, p,
-                           ntiles, per);
-        SCD_RETURN_LAUNCH();
-    }
     bool ring = false;
     if (dtype == SCD_DT_BF16 && !narrow) {
         const int rm = ring_mode();
@@ -3591,36 +2558,6 @@ extern "C" size_t scd_conv_wgrad_workspace(int Cg, int T, int Ci, int nsplit) {
     return (size_t)nsplit * Cg * T * Ci * sizeof(float);
 }
 
-// kernel choice for the weight gradient: the ring kernel for bf16 with wide outputs and many pixels
-static bool wgrad_use_ring(int dtype, long M, int Cg) {
-    // measured slower than the register-staged kernel at every Res10 shape (staging-bound at 128x256):
-    // opt-in only (SCD_WGRAD_RING=1)
-    (void)M;
-    if (dtype != SCD_DT_BF16 || Cg <= 64) return false;
-    static int mode = -2;
-    if (mode == -2) { const char* e = getenv("SCD_WGRAD_RING"); mode = e ? atoi(e) : 0; }
-    return mode == 1;
-}
-
-// ping-pong weight gradient (bf16, output-gradient channels a multiple of 128, enough pixels): column
-// slices of 256 (+ one of 128), 256-wide column tiles of taps x channels
-static bool wgrad_use_pp(int dtype, long M, int Cg, int KK) {
-    static int mode = -2;
-    // opt-in (SCD_WGRAD_PP=1): correct, but measured 10-40% slower than conv_wgrad_kernel at every Res10 shape
-    if (mode == -2) { const char* e = getenv("SCD_WGRAD_PP"); mode = e ? atoi(e) : 0; }
-    // mode 2: only 128-channel weight gradients over >= 256 K pixels (the heatmap head's 3x3 weight)
-    if (mode == 2) return dtype == SCD_DT_BF16 && Cg == 128 && KK >= 1024 && M >= 256 * 1024;
-    return mode && dtype == SCD_DT_BF16 && Cg >= 128 && Cg % 128 == 0 && KK >= 128 && M >= 8 * 1024;
-}
-
-// SCD_WGRAD_LDS_PAD=<bytes>: extra dynamic LDS per workgroup of the register-staged weight-gradient kernel, so fewer
-// of its workgroups share a CU with the critical chain's kernels (experiment; 0 = off)
-static int wgrad_lds_pad() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("SCD_WGRAD_LDS_PAD"); v = e ? atoi(e) : 0; }
-    return v;
-}
-
 static bool wgrad_fastx() {
     static int mode = -2;
     if (mode == -2) { const char* e = getenv("SCD_WGRAD_FASTX"); mode = e ? atoi(e) : 1; }
@@ -3628,8 +2565,8 @@ static bool wgrad_fastx() {
 }
 
 static void wgrad_tile(int dtype, long M, int Cg, int& tm, int& tn) {
-    if (wgrad_use_ring(dtype, M, Cg)) { tm = 128; tn = 256; }
-    else if (Cg <= 64) { tm = 64; tn = 256; }
+    (void)dtype; (void)M;
+    if (Cg <= 64) { tm = 64; tn = 256; }
     else { tm = 128; tn = 128; }
 }
 
@@ -3684,15 +2621,6 @@ static long wgrad_ns_model(long M, long tiles, int slots, int kp, double stage_u
     return best;
 }
 
-// SCD_WGRAD_MAXPX=<pixels>: at most this many pixels per split (shorter-lived weight-gradient workgroups, so the
-// side stream frees CUs for the critical chain sooner; more fp32 slab traffic).  0 = the cost model alone.
-static long wgrad_min_splits(long M, long ns_max) {
-    static long v = -1;
-    if (v < 0) { const char* e = getenv("SCD_WGRAD_MAXPX"); v = e ? atol(e) : 0; }
-    if (v <= 0) return 0;
-    return std::min(ns_max, (cdiv(M, v) + 7) / 8 * 8L);
-}
-
 static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
     const int win = wgrad_pp2_win(Cg);
     const long tiles = (long)(Cg / win) * cdiv(KK, 256);
@@ -3706,7 +2634,7 @@ static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
         // many tiles: splits need not come in XCD groups of 8 (wgrad_block's linear map), so one round can be filled
         const long ns = wgrad_ns_model(M, tiles, 256, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem),
                                        tiles >= 24);
-        return (int)std::max(ns, wgrad_min_splits(M, std::min(cap_px, cap_mem)));
+        return (int)ns;
     }
     // about two rounds of one-per-CU workgroups over the channel windows, whole XCD groups, >= 2048 pixels
     // per split, fp32 slabs capped at 256 MB
@@ -3725,22 +2653,11 @@ extern "C" int scd_conv_wgrad_nsplit2(int dtype, long M, int Ho, int Wo, int Cg,
 
 extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
     SCD_F16_FWD(scd_conv_wgrad_nsplit, M, Cg, T, Ci);
-    if (wgrad_use_pp(dtype, M, Cg, T * Ci)) {
-        // about three rounds of one-per-CU workgroups, whole XCD groups of splits, >= 1024 pixels per split,
-        // fp32 slabs capped at 192 MB
-        const long tiles = (long)cdiv(Cg, 256) * cdiv((long)T * Ci, 256);
-        long ns = std::max(8L, (768L / tiles) / 8 * 8);
-        ns = std::min(ns, std::max(8L, M / 1024 / 8 * 8));
-        ns = std::min(ns, std::max(8L, (192L << 20) / std::max(1L, 4L * Cg * T * Ci) / 8 * 8));
-        return (int)ns;
-    }
     int tm, tn;
     wgrad_tile(dtype, M, Cg, tm, tn);
     const long tiles = (long)cdiv(Cg, tm) * cdiv((long)T * Ci, tn);
-    const bool ring = wgrad_use_ring(dtype, M, Cg);
-    // ~4 (ring, one workgroup per CU) / 4 (two per CU) waves of workgroups over 256 CUs, >= 1024 pixels per split,
-    // fp32 slabs capped at 256 MB
-    if (!ring && wgrad_nsmodel() && M >= 8 * 1024) {
+    // ~4 waves of two-per-CU workgroups over 256 CUs, >= 1024 pixels per split, fp32 slabs capped at 256 MB
+    if (wgrad_nsmodel() && M >= 8 * 1024) {
         // 128x128: two workgroups per CU, 64x256: one (register-bound); a stage of KP pixels ~ 2*tm*tn*KP flop
         // at ~2.4 TF/s per CU; slab tm x tn fp32
         const int KP = dtype == SCD_DT_BF16 ? 64 : 32;
@@ -3751,9 +2668,9 @@ extern "C" int scd_conv_wgrad_nsplit(int dtype, long M, int Cg, int T, int Ci) {
         const long cap_mem = std::max(8L, (256L << 20) / std::max(1L, 4L * Cg * T * Ci) / 8 * 8);
         const long ns = wgrad_ns_model(M, tiles, slots, KP, stage_us, epi_us, 4.0 * Cg * T * Ci,
                                        std::min(cap_px, cap_mem));
-        return (int)std::max(ns, wgrad_min_splits(M, std::min(cap_px, cap_mem)));
+        return (int)ns;
     }
-    long ns = std::max(1L, std::min((ring ? 1024L : 1024L) / std::max(1L, tiles), M / 1024));
+    long ns = std::max(1L, std::min(1024L / std::max(1L, tiles), M / 1024));
     ns = std::max(1L, std::min(ns, (256L << 20) / std::max(1L, 4L * Cg * T * Ci)));
     if (ns >= 8) ns = ns / 8 * 8;          // whole XCD groups (see wgrad_block)
     return (int)ns;
@@ -3825,24 +2742,6 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
         }
         SCD_RETURN_LAUNCH();
     }
-    if (wgrad_use_pp(dtype, M, Cg, p.KK)) {
-        hipStream_t st = (hipStream_t)stream;
-        p.ntn = cdiv(p.KK, 256);
-        p.nsplit = nsplit;
-        const int n8 = (nsplit + 7) / 8 * 8;
-        const int nfull = Cg / 256;
-        if (nfull > 0) {
-            p.ntm = nfull;
-            hipLaunchKernelGGL((conv_wgrad_pp_kernel<256>), dim3(p.ntm * p.ntn * n8), dim3(512), 0, st, p, 0);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return (int)e;
-        }
-        if (Cg % 256) {
-            p.ntm = 1;
-            hipLaunchKernelGGL((conv_wgrad_pp_kernel<128>), dim3(p.ntn * n8), dim3(512), 0, st, p, Cg - 128);
-        }
-        SCD_RETURN_LAUNCH();
-    }
     int BM, BN;
     wgrad_tile(dtype, M, Cg, BM, BN);
     p.ntm = cdiv(Cg, BM);
@@ -3850,32 +2749,29 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
     p.nsplit = nsplit;
     dim3 grid(p.ntm * p.ntn * nsplit);
     hipStream_t st = (hipStream_t)stream;
-    if (wgrad_use_ring(dtype, M, Cg)) {
-        hipLaunchKernelGGL(conv_wgrad_ring_kernel, grid, dim3(512), 0, st, p);
-    } else if (dtype == SCD_DT_BF16 || dtype == SCD_DT_F32) {
+    if (dtype == SCD_DT_BF16 || dtype == SCD_DT_F32) {
         // fast addressing when a stage of KP pixels stays inside one image and one row block
         const int KP = dtype == SCD_DT_BF16 ? 64 : 32;
-        const int lpad = wgrad_lds_pad();
         const bool fastok = wgrad_fastx() && ((long)Ho * Wo) % KP == 0 && chunk % KP == 0;
         const int fx = !fastok ? 0 : (Wo % KP == 0 ? 1 : (KP % Wo == 0 ? 2 : 0));
         // (the 128 x 128 tile has registers for FASTX 1 only)
         if (dtype == SCD_DT_BF16) {
             if (Cg <= 64) {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), lpad, st, p);
-                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), lpad, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), lpad, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
+                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), 0, st, p);
             } else {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), lpad, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), lpad, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), 0, st, p);
             }
         } else {
             if (Cg <= 64) {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 1>), grid, dim3(256), lpad, st, p);
-                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 2>), grid, dim3(256), lpad, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 0>), grid, dim3(256), lpad, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 1>), grid, dim3(256), 0, st, p);
+                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 2>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 64, 256, 0>), grid, dim3(256), 0, st, p);
             } else {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 1>), grid, dim3(256), lpad, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 0>), grid, dim3(256), lpad, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 1>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<float, 128, 128, 0>), grid, dim3(256), 0, st, p);
             }
         }
     } else {

@@ -47,11 +47,6 @@
 #define scd_stem_conv_fwd scd_stem_conv_fwd__f16
 #define scd_stem_conv_wgrad_nsplit scd_stem_conv_wgrad_nsplit__f16
 #define scd_stem_conv_wgrad scd_stem_conv_wgrad__f16
-#define scd_stem_gram scd_stem_gram__f16
-#define scd_stem_gram_stats scd_stem_gram_stats__f16
-#define scd_stem_fused_fwd scd_stem_fused_fwd__f16
-#define scd_stem_wgrad_pooled scd_stem_wgrad_pooled__f16
-#define scd_stem_wgrad_combine scd_stem_wgrad_combine__f16
 #define scd_pad_channels scd_pad_channels__f16
 #define __bf16 _Float16
 #define __builtin_amdgcn_mfma_f32_16x16x32_bf16 __builtin_amdgcn_mfma_f32_16x16x32_f16

@@ -40,25 +40,3 @@ extern "C" int scd_event_elapsed_ms(void* start, void* end, float* ms) {
     return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end);
 }
 
-// A stream whose kernels may run only on `keep` of every `of` compute units (hipExtStreamCreateWithCUMask; the
-// CU mask bits are dealt out evenly, so every XCD keeps the same share).  The weight-gradient side stream runs
-// here when SCD_SIDE_CUS is set: its one-workgroup-per-CU GEMMs then never occupy the units the critical
-// input-gradient chain's HBM-bound kernels need.
-extern "C" int scd_stream_create_cumask(int keep, int of, void** stream) {
-    if (!stream || keep < 1 || of < 1 || keep > of) return SCD_ERR_ARG;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return (int)e;
-    hipDeviceProp_t prop;
-    e = hipGetDeviceProperties(&prop, dev);
-    if (e != hipSuccess) return (int)e;
-    const int ncu = prop.multiProcessorCount;
-    uint32_t mask[64] = {0};
-    const int words = (ncu + 31) / 32;
-    if (words > 64) return SCD_ERR_ARG;
-    for (int cu = 0; cu < ncu; ++cu)
-        if ((cu % of) < keep) mask[cu / 32] |= 1u << (cu % 32);
-    return (int)hipExtStreamCreateWithCUMask((hipStream_t*)stream, (uint32_t)words, mask);
-}
-
-extern "C" int scd_stream_destroy(void* stream) { return stream ? (int)hipStreamDestroy((hipStream_t)stream) : 0; }

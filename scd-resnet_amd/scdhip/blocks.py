@@ -61,28 +61,6 @@ def _conv1_and_downsample(x, blk, conv1, bn1, s1, pad1, sd):
     return y1, st1, yd, std
 
 
-def _downsample_branch(x, blk, stride, training):
-    """Start a block's downsample branch (conv1x1 + BN statistics, residuals.py:131-134) on the branch stream
-    (ops.branch_begin) so it overlaps the main branch; returns (yd, std, stream) or (None, None, None)."""
-    if blk.downsample is None or not training:
-        return None, None, None
-    bs = ops.branch_begin(x)
-    if bs is None:
-        return None, None, None
-    with torch.cuda.stream(bs):
-        yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], stride, 0, training)
-    return yd, std, bs
-
-
-def _downsample_join(x, blk, stride, training, yd, std, bs):
-    if bs is None:
-        if yd is not None:                  # computed with conv1 (_conv1_and_downsample)
-            return yd, std
-        return _train_bn_conv(x, blk.downsample[0], blk.downsample[1], stride, 0, training)
-    ops.branch_join(bs, yd, std.mean, std.invstd, std.scale, std.shift)
-    return yd, std
-
-
 def _dgrad_bn_relu_bwd(dy, wpack_t, C, Hc, Wc, kh, kw, stride, pad, bn, st, y):
     """Input gradient of a conv whose input is a BN+ReLU layer's output (bn, st, pre-BN y), then that layer's
     backward.  In bf16 the dgrad GEMM's epilogue accumulates the BN backward sums (scd_conv_gemm_bnbwd; shapes
@@ -103,38 +81,13 @@ class StemFn(torch.autograd.Function):
         C = conv.weight.shape[0]
         stats = ops.bn_stats(bn, "fwd") if training else None
         ref_geom = tuple(conv.weight.shape) == (64, 1, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3
-        ctx.fused = ref_geom and ops.stem_fused_ok(x, dtype)
-        ctx.st, ctx.conv, ctx.bn = None, conv, bn
-        if ctx.fused:
-            # no full-resolution activation: BN statistics from the im2col Gram matrix, conv+BN+ReLU+pool in one pass
-            x = _c(x)
-            wpk = ops.pack_weight(conv.weight, dtype, 0, ldp=64)
-            G = ops.stem_gram(x, wpk, stats) if training else None
-            st = ops.bn_finalize(bn, stats, C, x.shape[0] * ((x.shape[2] - 1) // 2 + 1) * ((x.shape[3] - 1) // 2 + 1),
-                                 training)
-            out, am, yam = ops.stem_fused_fwd(x, wpk, st)
-            ctx.save_for_backward(x, am, yam, G, wpk)
-            ctx.st = st
-            return out
         direct = ops.stem_direct_ok(x, dtype) and ref_geom
-        ctx.t1 = False
         if direct:
             # direct 7x7/s2 conv: the tap tile is built in LDS from the input patch (no column tensor)
             x = _c(x)
             wpk = ops.pack_weight(conv.weight, dtype, 0, ldp=64)
             y = ops.stem_conv_fwd(x, wpk, stats=stats)
             cols = x
-            side = ops.forward_side_stream(x.device) if (training and dtype == torch.bfloat16 and ops.StemT1.enabled
-                                                         and not torch.cuda.is_current_stream_capturing()) else None
-            if side is not None:
-                # the weight gradient's Gram matrix of the input, off the critical path
-                with torch.cuda.stream(side):
-                    ctx.G = ops.stem_gram(x, wpk, None)
-                    ctx.g_event = torch.cuda.Event()
-                    ctx.g_event.record(side)
-                x.record_stream(side)
-                ctx.G.record_stream(torch.cuda.current_stream())
-                ctx.wpk, ctx.t1 = wpk, True
         else:
             cols = ops.im2col_stem(x, dtype, kh=conv.weight.shape[2], kw=conv.weight.shape[3],
                                    stride=conv.stride[0], pad=conv.padding[0])
@@ -149,21 +102,11 @@ class StemFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         conv, bn, st = ctx.conv, ctx.bn, ctx.st
-        if ctx.fused:
-            x, am, yam, G, wpk = ctx.saved_tensors
-            ops.stem_fused_bwd(bn, st, _c(dout), am, yam, x, G, wpk, ops.grad_of(conv.weight))
-            grads_ready(conv, bn)
-            return None, None, None, None, None
         cols, y, am = ctx.saved_tensors
         if ctx.direct:
-            # pool/ReLU backward + BN reduction in one pass; the BN apply runs inside the weight gradient, or (T1)
-            # folds into the Gram matrix algebra
+            # pool/ReLU backward + BN reduction in one pass; the BN apply runs inside the weight gradient
             dz, coef = ops.stem_pool_bwd_bn(bn, _c(dout), am, y, st)
-            if ctx.t1:
-                ops.stem_wgrad_t1(dz, cols, ops.grad_of(conv.weight), ctx.G, ctx.g_event, ctx.wpk, coef)
-                ctx.G = ctx.g_event = ctx.wpk = None
-            else:
-                ops.stem_conv_wgrad(dz, cols, ops.grad_of(conv.weight), ybn=y, coef=coef)
+            ops.stem_conv_wgrad(dz, cols, ops.grad_of(conv.weight), ybn=y, coef=coef)
         else:
             dz = ops.stem_pool_bwd(_c(dout), am, y, st)
             dy = ops.bn_backward(bn, st, dz, y)
@@ -178,15 +121,16 @@ class BasicBlockFn(torch.autograd.Function):
     def forward(ctx, x, w1, blk):
         tr = blk.training
         s = blk.stride
-        yd, std, bs = _downsample_branch(x, blk, s, tr)
-        if tr and blk.downsample is not None and bs is None:
+        yd = std = None
+        if tr and blk.downsample is not None:
             y1, st1, yd, std = _conv1_and_downsample(x, blk, blk.conv1, blk.bn1, s, 1, s)
         else:
             y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, s, 1, tr)
         a1 = ops.bn_apply(y1, st1, True)
         y2, st2 = _train_bn_conv(a1, blk.conv2, blk.bn2, 1, 1, tr)
         if blk.downsample is not None:
-            yd, std = _downsample_join(x, blk, s, tr, yd, std, bs)
+            if yd is None:                      # eval: the downsample conv after the main branch
+                yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], s, 0, tr)
             out = ops.bn_apply(y2, st2, True, res=yd, rst=std)
         else:
             out = ops.bn_apply(y2, st2, True, res=x)
@@ -228,8 +172,8 @@ class BottleneckFn(torch.autograd.Function):
     def forward(ctx, x, w1, blk):
         tr = blk.training
         s = blk.stride
-        yd, std, bs = _downsample_branch(x, blk, s, tr)
-        if tr and blk.downsample is not None and bs is None:
+        yd = std = None
+        if tr and blk.downsample is not None:
             y1, st1, yd, std = _conv1_and_downsample(x, blk, blk.conv1, blk.bn1, 1, 0, s)
         else:
             y1, st1 = _train_bn_conv(x, blk.conv1, blk.bn1, 1, 0, tr)
@@ -238,7 +182,8 @@ class BottleneckFn(torch.autograd.Function):
         a2 = ops.bn_apply(y2, st2, True)
         y3, st3 = _train_bn_conv(a2, blk.conv3, blk.bn3, 1, 0, tr)
         if blk.downsample is not None:
-            yd, std = _downsample_join(x, blk, s, tr, yd, std, bs)
+            if yd is None:                      # eval: the downsample conv after the main branch
+                yd, std = _train_bn_conv(x, blk.downsample[0], blk.downsample[1], s, 0, tr)
             out = ops.bn_apply(y3, st3, True, res=yd, rst=std)
         else:
             out = ops.bn_apply(y3, st3, True, res=x)

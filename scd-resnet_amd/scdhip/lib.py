@@ -67,11 +67,6 @@ SIGNATURES = {
     "scd_stem_conv_wgrad_nsplit": (I, [L]),
     "scd_stem_conv_wgrad": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_pool_bwd_bn": (I, [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),
-    "scd_stem_gram": (I, [P, P, I, I, I, I, I, I, P]),
-    "scd_stem_gram_stats": (I, [P, P, P, P]),
-    "scd_stem_fused_fwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, P]),
-    "scd_stem_wgrad_pooled": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
-    "scd_stem_wgrad_combine": (I, [P, I, P, P, P, P, I, P]),
     "scd_stats_collapse": (I, [P, I, I, P]),
     "scd_stats_collapse_to": (I, [P, I, I, P, P]),
     "scd_bn_finalize": (I, [P, I, I, D, P, P, P, P, P, F, F, P, P, P, P, P]),
@@ -125,8 +120,6 @@ SIGNATURES = {
     "scd_peer_ipc_open": (I, [P, PP]),
     "scd_peer_ipc_close": (I, [P]),
     "scd_peer_allreduce_f64": (I, [P, I, I, I, PP, I, ctypes.c_ulonglong, P, ctypes.c_uint, P]),
-    "scd_stream_create_cumask": (I, [I, I, PP]),
-    "scd_stream_destroy": (I, [P]),
     "scd_event_create": (I, [PP]),
     "scd_event_destroy": (I, [P]),
     "scd_event_record": (I, [P, P]),

@@ -505,11 +505,9 @@ def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, sta
         L.call("scd_conv_gemm_bnbwd", dt(x), ptr(x), ptr(wpack), ptr(y), N, Hi, Wi, Ci, Ho, Wo, Co, in_stride,
                out_stride, wpack.shape[1], len(phases), arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
                ptr(st.shift), ptr(bstats), stream())
-        flush_deferred_wgrads()
         return y
     L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
            in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr, stream())
-    flush_deferred_wgrads()
     return y
 
 
@@ -590,44 +588,6 @@ def fused_bn_bwd_args(prod):
     """bn_bwd argument for a GEMM computing the gradient of prod's output (prod from bn_producer)."""
     bn, st, y = prod
     return (st, y, bn_stats(bn, "bwdf"))
-
-
-# ------------------------------------------------------------------ independent branches of a block forward
-#
-# The downsample branch of a BasicBlock / Bottleneck (conv1x1 stride s + BN statistics; residuals.py:99-120,
-# 145-165) reads only the block input, so it runs on a second stream at the compute stream's priority while the
-# main branch's first convolutions run.  Opt-in (SCD_BRANCH_STREAM=1): measured neutral to -1.5% (Res10 B=32
-# 4,930-4,950 vs 5,017 img/s; Res50 1024^2 fp16 409 vs 410), the branch's GEMM takes CUs from the main one.
-
-class Branch:
-    enabled = os.environ.get("SCD_BRANCH_STREAM", "0") == "1"
-    streams = {}          # (device index, priority) -> stream
-
-
-def branch_begin(x):
-    """A stream ordered after the current one (same priority) for a branch that reads x, or None.  Not with the
-    peer-memory SyncBN: its all-reduce kernels share one mailbox and must not run concurrently (RCCL collectives are
-    serialised on the communicator's stream in host issue order, gloo ones on the host)."""
-    if not Branch.enabled or not x.is_cuda or _BNSync.peer is not None:
-        return None
-    idx = x.device.index if x.device.index is not None else torch.cuda.current_device()
-    cur = torch.cuda.current_stream(idx)
-    key = (idx, cur.priority)
-    s = Branch.streams.get(key)
-    if s is None:
-        s = Branch.streams[key] = torch.cuda.Stream(device=idx, priority=cur.priority)
-    s.wait_stream(cur)
-    x.record_stream(s)
-    return s
-
-
-def branch_join(s, *tensors):
-    """The current stream waits for branch stream s; tensors s allocated are now also used on the current stream."""
-    cur = torch.cuda.current_stream(s.device)
-    cur.wait_stream(s)
-    for t in tensors:
-        if t is not None:
-            t.record_stream(cur)
 
 
 # ------------------------------------------------------------------ one input gradient for several consumers
@@ -850,22 +810,11 @@ def side_stream(dev):
 
 
 def _new_side_stream(idx):
-    """SCD_SIDE_CUS="keep/of" (e.g. "3/4"): the side stream may use only that share of the compute units
-    (scd_stream_create_cumask), so that its one-workgroup-per-CU weight-gradient GEMMs cannot hold every CU
-    while the input-gradient chain's HBM-bound BN kernels wait for a slot."""
-    spec = os.environ.get("SCD_SIDE_CUS", "")
-    if not spec:
-        return torch.cuda.Stream(device=idx, priority=_Side.priority)
-    keep, of = (int(v) for v in spec.split("/"))
-    with torch.cuda.device(idx):
-        h = ctypes.c_void_p()
-        L.call("scd_stream_create_cumask", keep, of, ctypes.byref(h))
-    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+    return torch.cuda.Stream(device=idx, priority=_Side.priority)
 
 
 def join_side_streams():
     """Make every device's compute stream wait for its side stream (end of backward)."""
-    flush_deferred_wgrads()
     for idx, s in _Side.streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
     _Side.joined_task.clear()
@@ -874,7 +823,6 @@ def join_side_streams():
 def side_stream_for_comm(dev):
     """For a collective launched during backward: the side stream (if any), first ordered after the compute
     stream, so that a collective issued from it sees every gradient written on either stream so far."""
-    flush_deferred_wgrads()
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _Side.streams.get(idx)
     if s is None or _graph_task() == -1:
@@ -883,24 +831,7 @@ def side_stream_for_comm(dev):
     return s
 
 
-# SCD_WGRAD_DEFER=1: a weight gradient issued during backward is queued and put on the side stream right after the
-# next input-gradient GEMM of the compute stream (flushed before any collective and at the end of backward), so it
-# overlaps that layer's BN backward and the next layer instead of competing with the GEMM for every CU.
-_WGRAD_DEFER = os.environ.get("SCD_WGRAD_DEFER", "0") == "1"
-_DEFERRED = []
-
-
-def flush_deferred_wgrads():
-    while _DEFERRED:
-        _DEFERRED.pop(0)()
-
-
 def conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None, red_taps=1):
-    if _WGRAD_DEFER and g.is_cuda and _Side.enabled and _graph_task() != -1:
-        side_stream(g.device)             # registers the end-of-backward join (which flushes the queue)
-        _DEFERRED.append(lambda: _conv_wgrad_side(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows,
-                                                  red_taps))
-        return
     _conv_wgrad_side(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows, red_taps)
 
 
@@ -1113,67 +1044,6 @@ def stem_conv_wgrad(dy, x, dst, accumulate=True, ybn=None, coef=None):
            stream())
 
 
-class StemFused:
-    """Stem without the full-resolution activation (stem.hip: Gram statistics, fused conv+BN+ReLU+pool forward,
-    weight gradient from the pooled side).  Opt-in (SCD_STEM_FUSED=1): the kernels are VALU-bound (pool window
-    selects, dz gathers) and measured 0.75 ms against 0.60 ms for the chain that keeps the activation at B=32
-    (profiles/r2_stem_bench.txt)."""
-    enabled = os.environ.get("SCD_STEM_FUSED", "0") == "1"
-
-
-def stem_fused_ok(x, dtype):
-    N, _, H, W = x.shape
-    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    Hp, Wp = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
-    return StemFused.enabled and dtype == torch.bfloat16 and Wo % 64 == 0 and Hp % 2 == 0 and Wp % 32 == 0
-
-
-def _stem_geom(x):
-    N, _, H, W = x.shape
-    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    return N, H, W, Ho, Wo, (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
-
-
-def stem_gram(x, wpk, stats):
-    """G = sum over the stem's im2col rows of col col^T (fp32 [64][64], ones column at tap 49) and, into `stats`
-    (fp64 BN buffer, replica 0), the batch sums of y and y^2 it implies for the packed bf16 weight wpk."""
-    N, H, W, Ho, Wo, _, _ = _stem_geom(x)
-    ns = L.lib().scd_stem_conv_wgrad_nsplit(N * Ho * Wo)
-    ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=x.device)
-    L.call("scd_stem_gram", ptr(x), ptr(ws), ns, N, H, W, Ho, Wo, stream())
-    G = torch.empty(64 * 64, dtype=torch.float32, device=x.device)
-    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(G), 0, 1.0, stream())
-    if stats is not None:
-        L.call("scd_stem_gram_stats", ptr(G), ptr(wpk), ptr(stats), stream())
-    return G
-
-
-def stem_fused_fwd(x, wpk, st):
-    """conv7x7/s2 + BN(st) + ReLU + MaxPool(3,2,1) -> (out (N,Hp,Wp,64) bf16, argmax u8, y at argmax bf16)."""
-    N, H, W, Ho, Wo, Hp, Wp = _stem_geom(x)
-    out = torch.empty(N, Hp, Wp, 64, dtype=torch.bfloat16, device=x.device)
-    am = torch.empty(N, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
-    yam = torch.empty_like(out)
-    L.call("scd_stem_fused_fwd", ptr(x), ptr(wpk), ptr(st.scale), ptr(st.shift), ptr(out), ptr(am), ptr(yam), N, H,
-           W, Ho, Wo, Hp, Wp, stream())
-    return out, am, yam
-
-
-def stem_fused_bwd(bn, st, dout, am, yam, x, G, wpk, dst):
-    """Stem backward from the pooled side: BN backward sums + the dz (x) col GEMM in one pass, SyncBN / finalize,
-    then dst (+)= a * (dz col) + b * W G + c * s."""
-    N, H, W, Ho, Wo, Hp, Wp = _stem_geom(x)
-    ns = L.lib().scd_stem_conv_wgrad_nsplit(N * Ho * Wo)
-    ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=x.device)
-    stats = bn_stats(bn, "bwd")
-    L.call("scd_stem_wgrad_pooled", ptr(dout), ptr(am), ptr(yam), ptr(st.scale), ptr(st.shift), ptr(st.mean),
-           ptr(st.invstd), ptr(x), ptr(ws), ptr(stats), ns, N, H, W, Ho, Wo, Hp, Wp, stream())
-    T1 = torch.empty(64 * 64, dtype=torch.float32, device=x.device)
-    L.call("scd_wgrad_reduce", ptr(ws), ns, 64, 1, 64, 0, 64, 64, 64, 1, 0, ptr(T1), 0, 1.0, stream())
-    coef = bn_backward_coef(bn, st, stats, 64)
-    L.call("scd_stem_wgrad_combine", ptr(T1), 1, ptr(coef), ptr(G), ptr(wpk), ptr(dst), 1, stream())
-
-
 def stem_pool_fwd(y, st):
     N, H, W, C = y.shape
     Ho, Wo = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
@@ -1182,42 +1052,6 @@ def stem_pool_fwd(y, st):
     L.call("scd_stem_pool_fwd", dt(y), ptr(y), ptr(st.scale), ptr(st.shift), ptr(out), ptr(am), N, H, W, C, Ho, Wo,
            stream())
     return out, am
-
-
-class StemT1:
-    """Stem weight gradient without the BN-apply pass over the activation (bf16, direct stem): dW = a*T1 + b*W G +
-    c*s with T1 = sum dz col^T from the masked pool gradient and the input only, and the im2col Gram matrix G
-    (ones column: s) computed during the forward on the side stream (residuals.py:209-216 backward; the algebra
-    of scd_stem_wgrad_combine).  Opt-in (SCD_STEM_T1=1): measured -2% in the step (4,880 vs 4,973 img/s: the Gram
-    kernel on the side stream slows the forward's GEMMs more than the cheaper weight gradient saves); the default
-    fuses the BN apply into the weight-gradient GEMM."""
-    enabled = os.environ.get("SCD_STEM_T1", "0") == "1"
-
-
-def forward_side_stream(dev):
-    """The side stream for work issued during a forward pass (ordered after the current stream)."""
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if not _Side.enabled:
-        return None
-    s = _Side.streams.get(idx)
-    if s is None:
-        s = _new_side_stream(idx)
-        _Side.streams[idx] = s
-    s.wait_stream(torch.cuda.current_stream(idx))
-    return s
-
-
-def stem_wgrad_t1(dz, x, dst, G, g_event, wpk, coef):
-    """dst (+)= a*T1 + b*W G + c*s (StemT1): T1 from the masked pool gradient dz, G from stem_gram (its producer's
-    event), wpk the packed bf16 weight the forward used, coef the BN backward coefficients (a, b, c)."""
-    N, _, H, W = x.shape
-    Ho, Wo = dz.shape[1], dz.shape[2]
-    ns = L.lib().scd_stem_conv_wgrad_nsplit(N * Ho * Wo)
-    ws = torch.empty(ns * 64 * 64, dtype=torch.float32, device=dz.device)
-    L.call("scd_stem_conv_wgrad", dt(dz), ptr(dz), 0, 0, ptr(x), ptr(ws), ns, N, H, W, Ho, Wo, stream())
-    if g_event is not None:
-        torch.cuda.current_stream().wait_event(g_event)
-    L.call("scd_stem_wgrad_combine", ptr(ws), ns, ptr(coef), ptr(G), ptr(wpk), ptr(dst), 1, stream())
 
 
 def stem_pool_bwd_bn(bn, dout, am, y, st):

@@ -336,117 +336,6 @@ def test_stem_fused_backward_matches_unfused():
     assert rel_err(dwb, dwa) < 2e-2
 
 
-def test_stem_wgrad_t1_matches_fused_apply():
-    """Stem weight gradient as a*T1 + b*W G + c*s (T1 = dz col^T, G = the input's im2col Gram matrix; opt-in ops.StemT1)
-    against the weight-gradient GEMM with the BN backward apply fused (same dz, same coefficients): the two differ
-    only by the bf16 rounding of y inside the apply (b*y term), 2e-2 relative."""
-    from scdhip import ops
-    g = torch.Generator().manual_seed(19)
-    x = torch.randn(2, 1, 512, 512, generator=g).to(DEV)
-    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).to(DEV)
-    bn = torch.nn.BatchNorm2d(64).to(DEV)
-    with torch.no_grad():
-        bn.weight.uniform_(0.5, 1.5)
-        bn.bias.normal_()
-    wpk = ops.pack_weight(w, torch.bfloat16, 0, ldp=64)
-    stats = ops.new_stats(64, DEV)
-    y = ops.stem_conv_fwd(x, wpk, stats=stats)
-    st = ops.bn_finalize(bn, stats, 64, y.numel() // 64)
-    out, am = ops.stem_pool_fwd(y, st)
-    dout = torch.randn(out.shape, generator=g).to(DEV, torch.bfloat16)
-    dz, coef = ops.stem_pool_bwd_bn(bn, dout, am, y, st)
-    dwa = torch.zeros_like(w)
-    ops.stem_conv_wgrad(dz, x, dwa, ybn=y, coef=coef)
-    G = ops.stem_gram(x, wpk, None)
-    dwb = torch.zeros_like(w)
-    ops.stem_wgrad_t1(dz, x, dwb, G, None, wpk, coef)
-    torch.cuda.synchronize()
-    assert rel_err(dwb, dwa) < 2e-2
-
-
-@pytest.mark.parametrize("shape", [(2, 512, 512), (3, 384, 256)])
-def test_stem_without_full_res_activation(shape):
-    """Stem from the Gram matrix and the pooled side (scd_stem_gram / _fused_fwd / _wgrad_pooled / _combine):
-    G against float64 im2col; BN statistics, pooled output, argmax and every gradient against the unfused
-    kernel chain (which keeps the 268 MB activation) and against torch fp32 autograd of
-    conv -> BatchNorm2d(train) -> ReLU -> MaxPool2d(3,2,1) on the same bf16-rounded operands."""
-    from scdhip import ops
-    N, H, W = shape
-    g = torch.Generator().manual_seed(21)
-    x = torch.randn(N, 1, H, W, generator=g).bfloat16().float()
-    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).bfloat16().float()
-    xd, wd = x.to(DEV), w.to(DEV)
-    bns = [torch.nn.BatchNorm2d(64).to(DEV) for _ in range(3)]
-    with torch.no_grad():
-        gam, bet = torch.rand(64, generator=g) + 0.5, torch.randn(64, generator=g) * 0.3
-        for b in bns:
-            b.weight.copy_(gam)
-            b.bias.copy_(bet)
-    wpk = ops.pack_weight(wd, torch.bfloat16, 0, ldp=64)
-    # unfused chain
-    stats = ops.new_stats(64, DEV)
-    y = ops.stem_conv_fwd(xd, wpk, stats=stats)
-    M = y.numel() // 64
-    st = ops.bn_finalize(bns[0], stats, 64, M)
-    out, am = ops.stem_pool_fwd(y, st)
-    dout = torch.randn(out.shape, generator=g).to(DEV, torch.bfloat16)
-    dz, coef = ops.stem_pool_bwd_bn(bns[0], dout, am, y, st)
-    dwa = torch.zeros_like(wd)
-    ops.stem_conv_wgrad(dz, xd, dwa, ybn=y, coef=coef)
-    # without the activation
-    ops.StemFused.enabled, was = True, ops.StemFused.enabled
-    try:
-        assert ops.stem_fused_ok(xd, torch.bfloat16)
-    finally:
-        ops.StemFused.enabled = was
-    stats2 = ops.new_stats(64, DEV)
-    G = ops.stem_gram(xd, wpk, stats2)
-    st2 = ops.bn_finalize(bns[1], stats2, 64, M)
-    out2, am2, yam2 = ops.stem_fused_fwd(xd, wpk, st2)
-    dwb = torch.zeros_like(wd)
-    ops.stem_fused_bwd(bns[1], st2, dout, am2, yam2, xd, G, wpk, dwb)
-    torch.cuda.synchronize()
-    # Gram matrix (taps 0..48 and the ones column) against float64 im2col of the bf16 input
-    cols = F.unfold(x.double(), 7, padding=3, stride=2).transpose(1, 2).reshape(-1, 49)
-    cols = torch.cat([cols, torch.ones(cols.shape[0], 1, dtype=torch.float64)], 1)
-    Gr = cols.T @ cols
-    Gd = G.view(64, 64)[:50, :50].double().cpu()
-    assert (Gd - Gr).abs().max().item() < 1e-5 * Gr.abs().max().item()
-    for a, b in ((st.mean, st2.mean), (st.invstd, st2.invstd), (bns[0].running_var, bns[1].running_var)):
-        assert rel_err(b, a) < 1e-5
-    # pooled output / argmax: identical up to the ulp-level scale/shift difference of the two statistics paths
-    assert (out2.float() - out.float()).abs().max().item() <= 2 ** -7 * out.float().abs().max().item()
-    assert (am2 != am).float().mean().item() < 1e-4
-    # the kept pre-BN value is y at the argmax
-    Hp, Wp = out.shape[1], out.shape[2]
-    ii = torch.arange(Hp, device=DEV).view(1, Hp, 1, 1) * 2 - 1 + am2.long() // 3
-    jj = torch.arange(Wp, device=DEV).view(1, 1, Wp, 1) * 2 - 1 + am2.long() % 3
-    nn = torch.arange(N, device=DEV).view(N, 1, 1, 1)
-    cc = torch.arange(64, device=DEV).view(1, 1, 1, 64)
-    yg = y[nn, ii.clamp(0), jj.clamp(0), cc].float()
-    assert ((yam2.float() - yg).abs() <= 2 ** -7 * yg.abs() + 1e-6).all()    # 1 bf16 ulp (conv sum order)
-    for a, b in ((bns[0].weight.grad, bns[1].weight.grad), (bns[0].bias.grad, bns[1].bias.grad)):
-        assert rel_err(b, a) < 1e-3
-    assert rel_err(dwb, dwa) < 1e-2
-    # torch fp32 autograd on the same bf16-rounded operands, with y rounded to bf16 before BN as the bf16 path
-    # stores / pools it (straight-through: the rounding alone moves this dW by ~6.5% normwise, since the BN
-    # backward's a*dz + b*y + c cancels heavily and near-tied pool windows route the gradient differently)
-    wr = w.clone().requires_grad_(True)
-    bnr = torch.nn.BatchNorm2d(64)
-    with torch.no_grad():
-        bnr.weight.copy_(gam)
-        bnr.bias.copy_(bet)
-    yr = F.conv2d(x, wr, stride=2, padding=3)
-    yr = yr + (yr.bfloat16().float() - yr).detach()
-    ref = F.max_pool2d(F.relu(bnr(yr)), 3, 2, 1)
-    (ref * nchw(dout).float()).sum().backward()
-    assert rel_err(nchw(out2), ref.detach()) < TOL[torch.bfloat16]
-    nerr = (dwb.cpu() - wr.grad).norm().item() / wr.grad.norm().item()
-    assert nerr < 1e-2 and rel_err(dwb, wr.grad) < 3e-2, (nerr, rel_err(dwb, wr.grad))
-    assert rel_err(bns[1].weight.grad, bnr.weight.grad) < 1e-2
-    assert rel_err(bns[1].bias.grad, bnr.bias.grad) < 1e-2
-
-
 def test_cpool_fwd_bwd_fp32():
     from scdhip import ops
     g = torch.Generator().manual_seed(5)
@@ -610,10 +499,8 @@ def test_dgrad_with_bn_backward_sums(case):
         assert (a[i] - ref[i]).abs().max().item() <= 1e-4 * ref[i].abs().max().item() + 1e-9, i
 
 
-# 64 -> 64 channel 3x3 stride-1 convs (layer1 shapes): the default 256x64 kernel, and with SCD_GEMM_H64=1 in the
-# environment the opt-in persistent halo kernel (widths 16..128 with 256 % W == 0, 1 to 8 tiles per workgroup;
-# (5, 64, 24, 16) has H % (256 / W) != 0 and always takes the default kernel)
-H64_CASES = [
+# 64 -> 64 channel 3x3 stride-1 convs (layer1 shapes) on every width the Res10/18/34 stacks and ragged sizes give
+LAYER1_CASES = [
     (4, 64, 128, 128, 64, 3, 1, 1),
     (8, 64, 128, 128, 64, 3, 1, 1),
     (3, 64, 64, 64, 64, 3, 1, 1),
@@ -623,8 +510,8 @@ H64_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", H64_CASES)
-def test_conv_h64_bf16(case):
+@pytest.mark.parametrize("case", LAYER1_CASES)
+def test_conv_layer1_bf16(case):
     test_conv_fwd_dgrad_wgrad(case, torch.bfloat16)
 
 
@@ -644,8 +531,8 @@ def test_conv_wgrad_layer1(case, dtype):
     test_conv_fwd_dgrad_wgrad(case, dtype)
 
 
-def test_conv_h64_accumulate_and_bias_relu():
-    """Epilogue paths the block code uses on the halo kernel: dgrad += into an existing gradient, and a
+def test_conv_layer1_accumulate_and_bias_relu():
+    """Epilogue paths the block code uses on the layer1 shapes: dgrad += into an existing gradient, and a
     forward with bias + ReLU."""
     from scdhip import ops
     g = torch.Generator().manual_seed(7)

@@ -1,5 +1,5 @@
-"""Time the stem kernels at the Res10 B=32 512^2 shape: the conv / pool / BN-backward / weight-gradient chain that
-keeps the full-resolution activation against the Gram / fused / pooled-side kernels (stem.hip), HIP events.
+"""Time the stem kernels at the Res10 B=32 512^2 shape: conv (+BN statistics), BN-apply+ReLU+max-pool, pool backward
+(+BN backward sums) and the weight gradient (+BN backward apply) (stem.hip, layers.hip), HIP events.
 
 python tools/stem_bench.py [--reps 20] [--batch 32]
 """
@@ -57,26 +57,7 @@ def main():
     rep("stem_pool_bwd_bn", timed(lambda: ops.stem_pool_bwd_bn(bn, dout, am, y, st), a.reps))
     dz, coef = ops.stem_pool_bwd_bn(bn, dout, am, y, st)
     rep("stem_conv_wgrad (+BN apply)", timed(lambda: ops.stem_conv_wgrad(dz, x, dw, ybn=y, coef=coef), a.reps))
-    rep("stem_conv_wgrad (dz only: T1)", timed(lambda: ops.stem_conv_wgrad(dz, x, dw), a.reps))
-    # without it
-    ns = L.lib().scd_stem_conv_wgrad_nsplit(M)
-    ws = torch.empty(ns * 4096, device=dev)
-    N, H, W = B, 512, 512
-    rep("stem_gram", timed(lambda: L.call("scd_stem_gram", ops.ptr(x), ops.ptr(ws), ns, N, H, W, 256, 256,
-                                          ops.stream()), a.reps))
-    G = ops.stem_gram(x, wpk, None)
-    rep("stem_gram + reduce + stats", timed(lambda: ops.stem_gram(x, wpk, stats), a.reps))
-    rep("stem_fused_fwd", timed(lambda: ops.stem_fused_fwd(x, wpk, st), a.reps))
-    out2, am2, yam2 = ops.stem_fused_fwd(x, wpk, st)
-    rep("stem_wgrad_pooled", timed(lambda: L.call(
-        "scd_stem_wgrad_pooled", ops.ptr(dout), ops.ptr(am2), ops.ptr(yam2), ops.ptr(st.scale), ops.ptr(st.shift),
-        ops.ptr(st.mean), ops.ptr(st.invstd), ops.ptr(x), ops.ptr(ws), ops.ptr(ops.bn_stats(bn, "bwd")), ns, N, H, W,
-        256, 256, 128, 128, ops.stream()), a.reps))
-    rep("stem_fused_bwd (all)", timed(lambda: ops.stem_fused_bwd(bn, st, dout, am2, yam2, x, G, wpk, dw), a.reps))
-    old = rows[0][1] + rows[1][1] + rows[2][1] + rows[3][1]
-    new = rows[6][1] + rows[7][1] + rows[9][1]
-    print("chain with activation %.1f us, without %.1f us" % (old, new))
-
+    print("chain %.1f us" % sum(us for _, us in rows))
 
 if __name__ == "__main__":
     main()
