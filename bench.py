@@ -442,6 +442,10 @@ def main():
             line["exchange"] = {"ddp_ms_per_step": line["ms_per_step"], "local_ms_per_step": round(local_ms, 3),
                                 "local_over_ddp": round(local_ms / line["ms_per_step"], 4),
                                 "syncbn_group": "own communicator (ops.new_bn_group)"}
+            # in-run weak-scaling efficiency: the same per-rank work without any collective over the DDP step (the
+            # driver's own figure comes from its per-N runs)
+            line["weak_scaling_eff"] = round(local_ms / line["ms_per_step"], 4)
+            line["weak_scaling_eff_basis"] = "local_ms_per_step / ddp_ms_per_step, same run"
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_baseline_steps)
         print(json.dumps(line), flush=True)

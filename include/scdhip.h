@@ -362,6 +362,12 @@ int scd_adam_step(float* p, const float* g, float* m, float* v, long n, float lr
  * bias corrections (networkFactory.py:228-234, :273-276). */
 int scd_adam_step_dev(float* p, const float* g, float* m, float* v, long n, double* hyper, float beta1, float beta2,
                       float eps, float gscale, void* stream);
+/* ---- SGD (torch.optim.SGD, networkFactory.py:84-89: momentum 0.9, weight_decay 1e-4) over a flat fp32 buffer ----
+ * hyper = {lr, step} as for scd_adam_step_dev (step advanced on the stream; the momentum buffer `buf` is
+ * initialised to the first step's d = g*gscale + weight_decay*p, as torch clones it).  buf may be NULL when
+ * momentum == 0. */
+int scd_sgd_step_dev(float* p, const float* g, float* buf, long n, double* hyper, float momentum, float dampening,
+                     float weight_decay, int nesterov, float gscale, void* stream);
 
 /* ---- corner pooling (cornerPooling/source/{top,bottom,left,right}Pool.cpp) ----
  * dir: 0 top (max over k>=h), 1 bottom (k<=h), 2 left (k>=w), 3 right (k<=w); NHWC dtype.

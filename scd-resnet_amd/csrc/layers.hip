@@ -678,6 +678,27 @@ __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, lo
     }
 }
 
+// ---------------------------------------------------------------- SGD (torch.optim.SGD, single-tensor form)
+// networkFactory.py:84-89: SGD(lr, momentum 0.9, weight_decay 1e-4).  d = g + wd*p; the momentum buffer starts as a
+// copy of d on the first step (hyper[1] == 1 after the tick), then buf = mom*buf + (1-dampening)*d; the update uses
+// d + mom*buf (nesterov) or buf.  hyper = {lr, step} fp64 in device memory, as for Adam.
+__global__ void sgd_dev_kernel(float* p, const float* g, float* buf, long n, const double* hyper, float mom, float damp,
+                               float wd, int nesterov, float gscale) {
+    const float lr = (float)hyper[0];
+    const bool first = hyper[1] <= 1.0;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float pi = p[i];
+        float d = g[i] * gscale;
+        if (wd != 0.f) d = d + wd * pi;
+        if (mom != 0.f) {
+            const float b = first ? d : buf[i] * mom + (1.f - damp) * d;
+            buf[i] = b;
+            d = nesterov ? d + mom * b : b;
+        }
+        p[i] = pi - lr * d;
+    }
+}
+
 inline int ew_blocks(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + 255) / 256)); }
 
 SCD_KERNEL_NS_END
@@ -883,6 +904,15 @@ extern "C" int scd_adam_step_dev(float* p, const float* g, float* m, float* v, l
     hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
     hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                        (const double*)hyper, beta1, beta2, eps, gscale);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_sgd_step_dev(float* p, const float* g, float* buf, long n, double* hyper, float momentum,
+                                float dampening, float weight_decay, int nesterov, float gscale, void* stream) {
+    if (!hyper || (momentum != 0.f && !buf)) return SCD_ERR_ARG;
+    hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
+    hipLaunchKernelGGL(sgd_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, buf, n,
+                       (const double*)hyper, momentum, dampening, weight_decay, nesterov, gscale);
     SCD_RETURN_LAUNCH();
 }
 

@@ -44,6 +44,7 @@
 #define scd_heads_bwd_weight_finalize scd_heads_bwd_weight_finalize__f16
 #define scd_adam_step scd_adam_step__f16
 #define scd_adam_step_dev scd_adam_step_dev__f16
+#define scd_sgd_step_dev scd_sgd_step_dev__f16
 #define scd_stem_conv_fwd scd_stem_conv_fwd__f16
 #define scd_stem_conv_wgrad_nsplit scd_stem_conv_wgrad_nsplit__f16
 #define scd_stem_conv_wgrad scd_stem_conv_wgrad__f16

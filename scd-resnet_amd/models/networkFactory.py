@@ -10,6 +10,7 @@ execution side:
     SyncBatchNorm -> global-batch statistics all-reduced inside the BN kernels' finalize
     (enabled by the reference rule: more than one GPU on the machine, networkFactory.py:128);
   * torch.optim.Adam -> scdhip.flat.FlatAdam (same defaults: lr 1e-3 until the first decay);
+  * torch.optim.SGD -> scdhip.flat.FlatSGD (momentum 0.9, weight_decay 1e-4, lr = learningRate);
   * batches are moved to this rank's device (the reference datasets pin cuda:0);
   * with ``stepGraph`` (opt-in) a single-process run replays the step as a captured HIP graph after two
     eager steps (scdhip.graph.StepGraph: same kernels, one hipGraphLaunch per step);
@@ -32,7 +33,7 @@ from tqdm import tqdm
 from configuration import defaultConfig
 from logger import Logger, monitorStdOutStream
 from scdhip import ops
-from scdhip.flat import FlatAdam, FlatDDP
+from scdhip.flat import FlatAdam, FlatDDP, FlatSGD
 from scdhip.graph import StepGraph
 
 torch.random.manual_seed(42)
@@ -116,8 +117,12 @@ class NetworkFactory(object):
 
         if defaultConfig.optimizer == "adam":
             self.optimizer = FlatAdam(filter(lambda p: p.requires_grad, self.model.parameters()))
+        elif defaultConfig.optimizer == "sgd":
+            # networkFactory.py:84-89
+            self.optimizer = FlatSGD(filter(lambda p: p.requires_grad, self.model.parameters()),
+                                     lr=defaultConfig.learningRate, momentum=0.9, weight_decay=0.0001)
         else:
-            Logger.err(":: networkFactory.py :: Unsupported Optimizer '{}' on the HIP path (adam)".format(
+            Logger.err(":: networkFactory.py :: Unknown Optimizer '{}', Currently Support 'sgd' or 'adam'".format(
                 defaultConfig.optimizer))
             sys.exit()
         self.device = None

@@ -4,8 +4,9 @@
   buffer and every ``param.grad`` is a view of one flat gradient buffer, so the optimizer
   is a single kernel launch and the DDP all-reduce is one (or a few bucketed) RCCL calls.
 * ``FlatAdam``: torch.optim.Adam semantics (defaults lr=1e-3, betas (0.9,0.999), eps 1e-8,
-  as the reference builds it without an lr, networkFactory.py:79-82) on scd_adam_step;
-  ``param_groups`` keeps the reference's setLearningRate (networkFactory.py:273-276) working.
+  as the reference builds it without an lr, networkFactory.py:79-82) on scd_adam_step_dev;
+  ``FlatSGD``: torch.optim.SGD (momentum 0.9, weight_decay 1e-4 in the reference, networkFactory.py:84-89) on
+  scd_sgd_step_dev; ``param_groups`` keeps the reference's setLearningRate (networkFactory.py:273-276) working.
 * ``FlatDDP``: replaces DistributedDataParallel (networkFactory.py:126-136): gradients are
   averaged across ranks with torch.distributed (RCCL over xGMI on MI355X, gloo in CPU tests)
   in ~25 MB buckets of the flat gradient, each launched asynchronously as soon as the backward
@@ -85,25 +86,28 @@ def ensure_flat(params):
     return FlatParams(params)
 
 
-class FlatAdam(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
-        if weight_decay != 0.0:
-            raise NotImplementedError("weight decay is not used by the reference Adam")
-        super(FlatAdam, self).__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+class _FlatOptimizer(torch.optim.Optimizer):
+    """One launch per step over the flat fp32 buffer (FlatParams); {lr, step} live in device memory (``_hyper``,
+    fp64) so a captured step graph replays with the current learning rate.  ``param_groups`` keeps the
+    reference's setLearningRate working (networkFactory.py:273-276)."""
+
+    def __init__(self, params, defaults):
+        super(_FlatOptimizer, self).__init__(params, defaults)
         self._flat = None
-        self._m = self._v = None
         self._step = 0          # host mirror of the device step counter (state_dict)
-        self._hyper = None      # device {lr, step} fp64, read by scd_adam_step_dev
+        self._hyper = None      # device {lr, step} fp64
         self._dev_lr = None     # the lr last written to _hyper
 
     def _all_params(self):
         return [p for g in self.param_groups for p in g["params"]]
 
+    def _new_state(self, fp):
+        raise NotImplementedError
+
     def flat(self):
         if self._flat is None or not self._flat.valid():
             self._flat = ensure_flat(self._all_params())
-            self._m = torch.zeros_like(self._flat.data)
-            self._v = torch.zeros_like(self._flat.data)
+            self._new_state(self._flat)
             self._hyper = torch.tensor([self.param_groups[0]["lr"], float(self._step)], dtype=torch.float64,
                                        device=self._flat.data.device)
             self._dev_lr = self.param_groups[0]["lr"]
@@ -124,40 +128,97 @@ class FlatAdam(torch.optim.Optimizer):
     def zero_grad(self, set_to_none=False):
         fp = self.flat() if self._all_params()[0].is_cuda else None
         if fp is None:
-            return super(FlatAdam, self).zero_grad(set_to_none=set_to_none)
+            return super(_FlatOptimizer, self).zero_grad(set_to_none=set_to_none)
         fp.rebind_grads()
         fp.grad.zero_()
 
-    @torch.no_grad()
-    def step(self, closure=None):
+    def _begin_step(self):
         from . import ops
         ops.pack_end()          # the packed operands of this step go stale now
         fp = self.flat()
         fp.rebind_grads()
-        g = self.param_groups[0]
         self.sync_lr()
         self._step += 1
-        ops.adam_step_dev(fp.data, fp.grad, self._m, self._v, self._hyper, g["betas"][0], g["betas"][1], g["eps"],
-                          gscale=fp.grad_scale)
-        return None
+        return fp, self.param_groups[0]
 
-    def state_dict(self):
-        return {"step": self._step, "param_groups": [{k: v for k, v in g.items() if k != "params"}
-                                                     for g in self.param_groups],
-                "exp_avg": None if self._m is None else self._m.cpu(),
-                "exp_avg_sq": None if self._v is None else self._v.cpu()}
-
-    def load_state_dict(self, sd):
+    def _load_common(self, sd):
         self._step = sd["step"]
         for g, s in zip(self.param_groups, sd["param_groups"]):
             g.update(s)
         if self._hyper is not None:
             self._hyper.copy_(torch.tensor([self.param_groups[0]["lr"], float(self._step)], dtype=torch.float64))
             self._dev_lr = self.param_groups[0]["lr"]
+
+    def _groups_sd(self):
+        return [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]
+
+
+class FlatAdam(_FlatOptimizer):
+    """torch.optim.Adam (networkFactory.py:79-82: built without an lr, so lr 1e-3, betas (0.9, 0.999), eps 1e-8)
+    on scd_adam_step_dev."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if weight_decay != 0.0:
+            raise NotImplementedError("weight decay is not used by the reference Adam")
+        super(FlatAdam, self).__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._m = self._v = None
+
+    def _new_state(self, fp):
+        self._m = torch.zeros_like(fp.data)
+        self._v = torch.zeros_like(fp.data)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from . import ops
+        fp, g = self._begin_step()
+        ops.adam_step_dev(fp.data, fp.grad, self._m, self._v, self._hyper, g["betas"][0], g["betas"][1], g["eps"],
+                          gscale=fp.grad_scale)
+        return None
+
+    def state_dict(self):
+        return {"step": self._step, "param_groups": self._groups_sd(),
+                "exp_avg": None if self._m is None else self._m.cpu(),
+                "exp_avg_sq": None if self._v is None else self._v.cpu()}
+
+    def load_state_dict(self, sd):
+        self._load_common(sd)
         if sd.get("exp_avg") is not None:
             self.flat()
             self._m.copy_(sd["exp_avg"])
             self._v.copy_(sd["exp_avg_sq"])
+
+
+class FlatSGD(_FlatOptimizer):
+    """torch.optim.SGD (networkFactory.py:84-89: lr = learningRate, momentum 0.9, weight_decay 1e-4) on
+    scd_sgd_step_dev; dampening / nesterov as torch's."""
+
+    def __init__(self, params, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super(FlatSGD, self).__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening,
+                                                   weight_decay=weight_decay, nesterov=nesterov))
+        self._buf = None
+
+    def _new_state(self, fp):
+        self._buf = torch.zeros_like(fp.data) if self.param_groups[0]["momentum"] != 0 else None
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from . import ops
+        fp, g = self._begin_step()
+        ops.sgd_step_dev(fp.data, fp.grad, self._buf, self._hyper, g["momentum"], g["dampening"], g["weight_decay"],
+                         g["nesterov"], gscale=fp.grad_scale)
+        return None
+
+    def state_dict(self):
+        return {"step": self._step, "param_groups": self._groups_sd(),
+                "momentum_buffer": None if self._buf is None else self._buf.cpu()}
+
+    def load_state_dict(self, sd):
+        self._load_common(sd)
+        if sd.get("momentum_buffer") is not None:
+            self.flat()
+            self._buf.copy_(sd["momentum_buffer"])
 
 
 class _EndOfBackward(torch.autograd.Function):

@@ -106,6 +106,7 @@ SIGNATURES = {
     "scd_ceval_summary": (I, [PP, ctypes.POINTER(c_long), L, P, I, P, P, P]),
     "scd_adam_step": (I, [P, P, P, P, L, F, F, F, F, F, F, F, P]),
     "scd_adam_step_dev": (I, [P, P, P, P, L, P, F, F, F, F, P]),
+    "scd_sgd_step_dev": (I, [P, P, P, L, P, F, F, F, I, F, P]),
     "scd_render_center_targets": (I, [P, P, I, I, I, F, P, P, P, P, P]),
     "scd_cpool_fwd": (I, [I, I, P, P, P, I, I, I, I, P]),
     "scd_cpool_bwd": (I, [I, I, P, P, P, I, I, I, I, P]),

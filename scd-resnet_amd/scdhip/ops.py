@@ -1101,6 +1101,13 @@ def adam_step_dev(p, g, m, v, hyper, beta1, beta2, eps, gscale=1.0):
            float(eps), float(gscale), stream())
 
 
+def sgd_step_dev(p, g, buf, hyper, momentum, dampening, weight_decay, nesterov, gscale=1.0):
+    """torch.optim.SGD step over the flat buffer (networkFactory.py:84-89); hyper = {lr, step} fp64 on the device."""
+    _need_gpu(p)
+    L.call("scd_sgd_step_dev", ptr(p), ptr(g), ptr(buf) if buf is not None else None, p.numel(), ptr(hyper),
+           float(momentum), float(dampening), float(weight_decay), int(bool(nesterov)), float(gscale), stream())
+
+
 def decode_topk(heat, offset, regr, K=100):
     """decodeCenterNet core: sigmoid -> 3x3 NMS -> top-K -> gather (centerNetOffset.py:219-251)."""
     _need_gpu(heat)

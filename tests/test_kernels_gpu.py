@@ -392,6 +392,39 @@ def test_adam_device_state_matches_torch():
     np.testing.assert_allclose(p.cpu().numpy(), pt.detach().numpy(), rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("nesterov,damp", [(False, 0.0), (True, 0.0), (False, 0.25)])
+def test_flat_sgd_matches_torch(nesterov, damp):
+    """FlatSGD (scd_sgd_step_dev) against torch.optim.SGD with the reference's settings (networkFactory.py:84-89:
+    momentum 0.9, weight_decay 1e-4): first step clones d into the momentum buffer; an lr change (setLearningRate)
+    between steps is picked up; momentum state survives state_dict round trips."""
+    from scdhip.flat import FlatSGD
+    g = torch.Generator().manual_seed(11)
+    shapes = [(64, 3, 3, 3), (64,), (1000,)]
+    p0 = [torch.randn(*s, generator=g) for s in shapes]
+    pt = [x.clone().requires_grad_(True) for x in p0]
+    opt_t = torch.optim.SGD(pt, lr=2.5e-4, momentum=0.9, weight_decay=1e-4, nesterov=nesterov, dampening=damp)
+    pd = [torch.nn.Parameter(x.clone().to(DEV)) for x in p0]
+    opt = FlatSGD(pd, lr=2.5e-4, momentum=0.9, weight_decay=1e-4, nesterov=nesterov, dampening=damp)
+    for step in range(1, 7):
+        if step == 4:
+            for o in (opt_t, opt):
+                o.param_groups[0]["lr"] = 2.5e-5
+        opt.zero_grad()
+        for a, b in zip(pt, pd):
+            gr = torch.randn(a.shape, generator=g)
+            a.grad = gr.clone()
+            b.grad.copy_(gr.to(DEV))
+        opt_t.step()
+        opt.step()
+        if step == 2:
+            sd = opt.state_dict()
+            opt2 = FlatSGD(pd, lr=2.5e-4, momentum=0.9, weight_decay=1e-4, nesterov=nesterov, dampening=damp)
+            opt2.load_state_dict(sd)
+            opt = opt2
+    for a, b in zip(pt, pd):
+        np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_batched_pack_matches_single(dtype):
     """PackPlan's one-launch batched packing (mode 0 rows, mode 1 LDS-tiled transposes, mode 2 tap-major
