@@ -6,7 +6,14 @@
 #include "scd_common.h"
 
 #ifndef BN_BWD_U
-#define BN_BWD_U 2
+#define BN_BWD_U 1
+#endif
+// Elementwise BN kernels are budgeted for 6 waves per SIMD (<= 80 VGPRs): the weight-gradient stream's ping-pong
+// kernel holds 2 x 216 of the 512 VGPRs per SIMD lane (one 8-wave workgroup per CU), so a wave that needs 88 could
+// not start on any CU until those workgroups retire (in the step the deconv2 BN backward apply then waited out the
+// whole deconv3 weight gradient)
+#ifndef BN_EW_WAVES
+#define BN_EW_WAVES 6
 #endif
 
 namespace {
@@ -95,6 +102,26 @@ __device__ __forceinline__ void load_params(const float* p, float* v) {
     }
 }
 
+// Per-channel parameters of the backward kernels live in LDS and are re-read per vector instead of held in
+// registers (5-6 x E floats per thread otherwise): with <= 80 VGPRs (BN_EW_WAVES) the waves fit beside the
+// weight-gradient stream's one-workgroup-per-CU GEMMs.  The offset is made opaque so the reads stay in the loop.
+__device__ __forceinline__ void stage_params(float* sp, const float* const* src, int nsrc, int C) {
+    for (int i = threadIdx.x; i < nsrc * C; i += blockDim.x) {
+        const int k = i / C;
+        sp[i] = src[k] ? src[k][i - k * C] : 0.f;
+    }
+    __syncthreads();
+}
+template <int E>
+__device__ __forceinline__ void lds_params(const float* sp, int off, float* v) {
+    asm volatile("" : "+v"(off));
+#pragma unroll
+    for (int k = 0; k < E / 4; ++k) {
+        const float4 f = *(const float4*)(sp + off + 4 * k);
+        v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* y, T* out, int C, unsigned nvec, const float* scale,
                                                        const float* shift, const T* res, const float* rscale,
@@ -153,7 +180,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* y, T* out, int C
 // any is used (4 x 3 independent 16-B loads in flight per thread); the block's partials are folded
 // over row lanes in LDS by all threads and added to one fp64 replica slot per channel.
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y,
+__global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y,
                                                             const float* rsc, const float* rsh,
                                                             const float* mean, const float* invstd, int C, int ld,
                                                             unsigned rows, unsigned rows_per_block, double* stats) {
@@ -168,14 +195,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* dout, const
     const unsigned r0 = blockIdx.x * rows_per_block;
     const unsigned r1 = min(rows, r0 + rows_per_block);
     __shared__ float red[2 * nt * E];
-    float s[E], q[E], mu[E], is[E], ka[E], kb[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        s[e] = 0.f; q[e] = 0.f; mu[e] = mean[ch * E + e]; is[e] = invstd[ch * E + e];
-        ka[e] = rsc ? rsc[ch * E + e] : 0.f;
-        kb[e] = rsc ? rsh[ch * E + e] : 0.f;
+    extern __shared__ __attribute__((aligned(16))) float sp[];        // 4 x C floats (dynamic LDS)     // mean, invstd, rsc, rsh
+    {
+        const float* src[4] = {mean, invstd, rsc, rsh};
+        stage_params(sp, src, 4, C);
     }
+    float s[E], q[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { s[e] = 0.f; q[e] = 0.f; }
     auto acc = [&](const float* d, const float* yv, const float* mk) {
+        float mu[E], is[E], ka[E], kb[E];
+        lds_params<E>(sp, ch * E, mu);
+        lds_params<E>(sp, C + ch * E, is);
+        if (rsc) { lds_params<E>(sp, 2 * C + ch * E, ka); lds_params<E>(sp, 3 * C + ch * E, kb); }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             // relu mask: the stored activation (mask) or, for BN+ReLU, the forward's own y*scale+shift > 0
@@ -253,7 +285,7 @@ __global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double co
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* rsc,
+__global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply_kernel(const T* dout, const T* mask, const T* y, const float* rsc,
                                                            const float* rsh, const float* coef, int C, unsigned nvec,
                                                            T* dy, T* dz_out) {
     constexpr int E = Vec16<T>::N;
@@ -266,21 +298,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const 
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned stride = gridDim.x * blockDim.x;
     const int c0 = (int)(v0 % cpr) * E;
-    float ca[E], cb[E], cc[E], ka[E], kb[E];
-    load_params<E>(coef + c0, ca);
-    load_params<E>(coef + C + c0, cb);
-    load_params<E>(coef + 2 * C + c0, cc);
-    if (rsc) { load_params<E>(rsc + c0, ka); load_params<E>(rsh + c0, kb); }
-    else {
-#pragma unroll
-        for (int e = 0; e < E; ++e) { ka[e] = 0.f; kb[e] = 0.f; }
+    extern __shared__ __attribute__((aligned(16))) float sp[];        // 5 x C floats (dynamic LDS)     // coef a, b, c, rsc, rsh
+    {
+        const float* src[5] = {coef, coef + C, coef + 2 * C, rsc, rsh};
+        stage_params(sp, src, 5, C);
     }
     // raw 16-B vectors -> dz (masked gradient) and dy, stored
     auto body = [&](size_t i, const uint4& rd, const uint4& ry, const uint4& rm) {
-        float d[E], yv[E], mk[E];
+        float d[E], yv[E], mk[E], ca[E], cb[E], cc[E], ka[E], kb[E];
         Vec16<T>::load(&rd, d);
         Vec16<T>::load(&ry, yv);
         if (mask) Vec16<T>::load(&rm, mk);
+        lds_params<E>(sp, c0, ca);
+        lds_params<E>(sp, C + c0, cb);
+        lds_params<E>(sp, 2 * C + c0, cc);
+        if (rsc) { lds_params<E>(sp, 3 * C + c0, ka); lds_params<E>(sp, 4 * C + c0, kb); }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
@@ -317,7 +349,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dout, const 
 // dout through the same ReLU mask, so one pass reads dout and the mask once for both.  Per element and per thread the
 // arithmetic is that of bn_bwd_reduce_kernel / bn_bwd_apply_kernel with a mask (no BN+ReLU recompute).
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_reduce2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
+__global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
                                                              const float* mean_a, const float* invstd_a,
                                                              const float* mean_b, const float* invstd_b, int C, int ld,
                                                              unsigned rows, unsigned rows_per_block, double* stats_a,
@@ -333,26 +365,33 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce2_kernel(const T* dout, cons
     const unsigned r0 = blockIdx.x * rows_per_block;
     const unsigned r1 = min(rows, r0 + rows_per_block);
     __shared__ float red[2 * nt * E];
-    float s[E], qa[E], qb[E], mua[E], isa[E], mub[E], isb[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        s[e] = 0.f; qa[e] = 0.f; qb[e] = 0.f;
-        mua[e] = mean_a[ch * E + e]; isa[e] = invstd_a[ch * E + e];
-        mub[e] = mean_b[ch * E + e]; isb[e] = invstd_b[ch * E + e];
+    extern __shared__ __attribute__((aligned(16))) float sp[];        // 4 x C floats (dynamic LDS)     // mean_a, invstd_a, mean_b, invstd_b
+    {
+        const float* src[4] = {mean_a, invstd_a, mean_b, invstd_b};
+        stage_params(sp, src, 4, C);
     }
+    float s[E], qa[E], qb[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { s[e] = 0.f; qa[e] = 0.f; qb[e] = 0.f; }
     auto acc_raw = [&](const uint4& rd, const uint4& rm, const uint4& ra, const uint4& rb) {
-        float d[E], mk[E], va[E], vb[E];
+        float d[E], mk[E], va[E], vb[E], mu[E], is[E];
         Vec16<T>::load(&rd, d);
         Vec16<T>::load(&rm, mk);
         Vec16<T>::load(&ra, va);
         Vec16<T>::load(&rb, vb);
 #pragma unroll
+        for (int e = 0; e < E; ++e) d[e] = !(mk[e] > 0.f) ? 0.f : d[e];
+        lds_params<E>(sp, ch * E, mu);
+        lds_params<E>(sp, C + ch * E, is);
+#pragma unroll
         for (int e = 0; e < E; ++e) {
-            const float dz = !(mk[e] > 0.f) ? 0.f : d[e];
-            s[e] += dz;
-            qa[e] += dz * (va[e] - mua[e]) * isa[e];
-            qb[e] += dz * (vb[e] - mub[e]) * isb[e];
+            s[e] += d[e];
+            qa[e] += d[e] * (va[e] - mu[e]) * is[e];
         }
+        lds_params<E>(sp, 2 * C + ch * E, mu);
+        lds_params<E>(sp, 3 * C + ch * E, is);
+#pragma unroll
+        for (int e = 0; e < E; ++e) qb[e] += d[e] * (vb[e] - mu[e]) * is[e];
     };
     unsigned r = r0 + rsub;
     for (; r + (U - 1) * rpi < r1; r += U * rpi) {
@@ -402,7 +441,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce2_kernel(const T* dout, cons
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
+__global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
                                                             const float* coef_a, const float* coef_b, int C,
                                                             unsigned nvec, T* dya, T* dyb) {
     constexpr int E = Vec16<T>::N;
@@ -411,25 +450,29 @@ __global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const T* dout, const
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned stride = gridDim.x * blockDim.x;
     const int c0 = (int)(v0 % cpr) * E;
-    float aa[E], ab[E], ac[E], ba[E], bb[E], bc[E];
-    load_params<E>(coef_a + c0, aa);
-    load_params<E>(coef_a + C + c0, ab);
-    load_params<E>(coef_a + 2 * C + c0, ac);
-    load_params<E>(coef_b + c0, ba);
-    load_params<E>(coef_b + C + c0, bb);
-    load_params<E>(coef_b + 2 * C + c0, bc);
+    extern __shared__ __attribute__((aligned(16))) float sp[];        // 6 x C floats (dynamic LDS)     // coef_a a, b, c, coef_b a, b, c
+    {
+        const float* src[6] = {coef_a, coef_a + C, coef_a + 2 * C, coef_b, coef_b + C, coef_b + 2 * C};
+        stage_params(sp, src, 6, C);
+    }
     auto body = [&](size_t i, const uint4& rd, const uint4& rm, const uint4& ra, const uint4& rb) {
-        float d[E], mk[E], va[E], vb[E];
+        float d[E], mk[E], va[E], vb[E], k0[E], k1[E], k2[E];
         Vec16<T>::load(&rd, d);
         Vec16<T>::load(&rm, mk);
         Vec16<T>::load(&ra, va);
         Vec16<T>::load(&rb, vb);
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const float dz = !(mk[e] > 0.f) ? 0.f : d[e];
-            va[e] = aa[e] * dz + ab[e] * va[e] + ac[e];
-            vb[e] = ba[e] * dz + bb[e] * vb[e] + bc[e];
-        }
+        for (int e = 0; e < E; ++e) d[e] = !(mk[e] > 0.f) ? 0.f : d[e];
+        lds_params<E>(sp, c0, k0);
+        lds_params<E>(sp, C + c0, k1);
+        lds_params<E>(sp, 2 * C + c0, k2);
+#pragma unroll
+        for (int e = 0; e < E; ++e) va[e] = k0[e] * d[e] + k1[e] * va[e] + k2[e];
+        lds_params<E>(sp, 3 * C + c0, k0);
+        lds_params<E>(sp, 4 * C + c0, k1);
+        lds_params<E>(sp, 5 * C + c0, k2);
+#pragma unroll
+        for (int e = 0; e < E; ++e) vb[e] = k0[e] * d[e] + k1[e] * vb[e] + k2[e];
         Vec16<T>::store(dya + i, va);
         Vec16<T>::store(dyb + i, vb);
     };
@@ -541,11 +584,11 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
         const float* rs = relu_scale ? relu_scale + c0 : nullptr;
         const float* rh = relu_shift ? relu_shift + c0 : nullptr;
         if (dtype == SCD_DT_BF16)
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dz,
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)dz,
                                (const __bf16*)mk, (const __bf16*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
                                (unsigned)rows, (unsigned)rpb, stats + c0);
         else if (dtype == SCD_DT_F32)
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dz,
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const float*)dz,
                                (const float*)mk, (const float*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
                                (unsigned)rows, (unsigned)rpb, stats + c0);
         else
@@ -582,12 +625,12 @@ extern "C" int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask,
         const char *d = (const char*)dout + o, *m = (const char*)mask + o, *a = (const char*)ya + o,
                    *b = (const char*)yb + o;
         if (dtype == SCD_DT_BF16)
-            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)d,
+            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)d,
                                (const __bf16*)m, (const __bf16*)a, (const __bf16*)b, mean_a + c0, invstd_a + c0,
                                mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
                                stats_b + c0);
         else if (dtype == SCD_DT_F32)
-            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)d,
+            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<float>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const float*)d,
                                (const float*)m, (const float*)a, (const float*)b, mean_a + c0, invstd_a + c0,
                                mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
                                stats_b + c0);
@@ -610,12 +653,12 @@ extern "C" int scd_bn_bwd_apply2(int dtype, const void* dout, const void* mask, 
     const long nvec = total / E;
     if (dtype == SCD_DT_BF16) {
         static const int g = resident_grid((const void*)bn_bwd_apply2_kernel<__bf16>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply2_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 0, st,
+        hipLaunchKernelGGL((bn_bwd_apply2_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 6 * C * 4, st,
                            (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)ya, (const __bf16*)yb, coef_a,
                            coef_b, C, (unsigned)nvec, (__bf16*)dya, (__bf16*)dyb);
     } else if (dtype == SCD_DT_F32) {
         static const int g = resident_grid((const void*)bn_bwd_apply2_kernel<float>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply2_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 0, st,
+        hipLaunchKernelGGL((bn_bwd_apply2_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 6 * C * 4, st,
                            (const float*)dout, (const float*)mask, (const float*)ya, (const float*)yb, coef_a, coef_b,
                            C, (unsigned)nvec, (float*)dya, (float*)dyb);
     } else {
@@ -641,14 +684,14 @@ extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, c
         if (C % 8 || !ew_rows_ok(C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
         static const int g = resident_grid((const void*)bn_bwd_apply_kernel<__bf16>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 0, st,
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 5 * C * 4, st,
                            (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, coef, C,
                            (unsigned)nvec, (__bf16*)dy, (__bf16*)dz);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4 || !ew_rows_ok(C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
         static const int g = resident_grid((const void*)bn_bwd_apply_kernel<float>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 0, st, (const float*)dout,
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 5 * C * 4, st, (const float*)dout,
                            (const float*)mask, (const float*)y, relu_scale, relu_shift, coef, C, (unsigned)nvec, (float*)dy,
                            (float*)dz);
     } else {

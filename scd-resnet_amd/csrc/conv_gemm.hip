@@ -530,6 +530,114 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, const char* 
                  : "memory");
 }
 
+// -------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 convolution with 64 input and 64 output channels (ResNet layer1, residuals.py:84-120;
+// forward and input gradient) on whole image rows: tile = 256 output pixels = TR = 256 / WO rows of one image.
+// The tile's input rows plus their one-pixel halo (TR + 2 rows x WO + 2 columns, 64 channels) are DMA'd into
+// LDS once (buffer_load ... lds; columns padded to WH = WO + 8 pixel slots, 16-B chunk c of slot q at c ^ (q & 7),
+// the swizzle applied to the source chunk), and every tap reads its A fragments from that image at a constant
+// displacement: all 9 taps x 2 K-halves are ds_read_b128 with immediate offsets from 6 per-lane base addresses,
+// so the loop has no address arithmetic (the register-staged 256 x 64 kernel spends ~9 VALU per MFMA on it).
+// The 64 x 576 weight operand streams through registers (16-B loads, the tap and channel block in the scalar
+// offset), one tap ahead of the MFMAs.  Wave w computes tile pixels 64w .. 64w+63 x all 64 channels; the shared
+// epilogue (BN sums, accumulate, BN-backward sums) runs on the same accumulator layout.  LDS: 69.6 KB at
+// WO = 128, two workgroups per CU.  FLIP: the input-gradient tap order (dh, dw) = (1 - r, 1 - s).
+template <int WO, bool FLIP, bool BNB>
+__global__ __launch_bounds__(256, 2) void conv_gemm_halo64_kernel(GemmParams p) {
+    typedef __bf16 T;
+    constexpr int TR = 256 / WO;                  // output rows per tile
+    constexpr int WH = WO + 8;                    // halo pixel slots per row (slot = input column + 1)
+    constexpr int HR = TR + 2;                    // halo rows
+    constexpr int ROWB = WH * 128;                // bytes per halo row
+    constexpr int HALO = HR * ROWB;
+    constexpr int EPI = 4 * 64 * (64 * 2 + 16) + 2048;
+    constexpr int SMEM = HALO > EPI ? HALO : EPI;
+    static_assert(WO * TR == 256 && WH % 8 == 0, "tile geometry");
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, lg = lane >> 4;
+    int bid;
+    {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+    }
+    const scd_gemm_phase& ph = p.ph[0];
+    const int QQ = ph.Qh * ph.Qw;
+    const int M = p.N * QQ;
+    const int mt = bid;
+    const int n = (mt * TR) / ph.Qh, row0 = mt * TR - n * ph.Qh;
+
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+
+    // ---- weights of tap 0 (in flight while the halo lands): lane = (co row l16 of block b, K chunk lg)
+    const int wlane = (l16 * p.wrow + lg * 8) * 2;
+    uint4 wb[2][8];
+    auto wload = [&](int buf, int t) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                wb[buf][b * 2 + s] = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wlane, (b * 16 * p.wrow + t * 64 + s * 32) * 2, 0));
+    };
+    wload(0, 0);
+
+    // ---- halo: HR rows x WH/8 groups of 8 pixel slots, one 1-KB DMA per group (lane -> slot lane/8, chunk lane%8)
+    {
+        const int hq = lane >> 3, cs = lane & 7, csrc = cs ^ hq;
+        for (int j = wave; j < HR * (WH / 8); j += 4) {
+            const int hr = j / (WH / 8), g = j - (j / (WH / 8)) * (WH / 8);
+            const int ir = row0 + hr - 1, ic = g * 8 + hq - 1;
+            const bool ok = (unsigned)ir < (unsigned)p.Hi && (unsigned)ic < (unsigned)p.Wi;
+            dma16(xrs, smem + hr * ROWB + g * 8 * 128, sel_off(ok, (((n * p.Hi + ir) * p.Wi + ic) * 64 + csrc * 8) * 2));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- per-lane A addresses: wave w = output row 64w / WO, columns (64w % WO) + 16a + l16; tap column shift dwi
+    const int wr = (wave * 64) / WO, wc = (wave * 64) % WO;
+    int abase[3][2];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int q = wc + l16 + d;
+            abase[d][s] = wr * ROWB + q * 128 + (((s * 4 + lg) ^ (q & 7)) << 4);
+        }
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) wload((t + 1) & 1, t + 1);
+        // keep the next tap's weight loads ahead of this tap's MFMAs (the scheduler would sink them to their use)
+        __builtin_amdgcn_sched_barrier(0);
+        const int r = t / 3, c = t - (t / 3) * 3;
+        const int dhi = FLIP ? 2 - r : r, dwi = FLIP ? 2 - c : c;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 af[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(smem + abase[dwi][s] + dhi * ROWB + a * 16 * 128);
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wb[t & 1][b * 2 + s]),
+                                                                        af[a], acc[a][b], 0, 0, 0);
+        }
+    }
+    __syncthreads();          // halo no longer read: the epilogue stages its tile in the same LDS
+    gemm_epilogue<T, 256, 64, 1, false, BNB>(p, acc, smem, tid, bid, mt, 0, M, QQ, ph);
+}
+
 template <bool HEADS, bool BNB = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
     typedef __bf16 T;
@@ -2365,6 +2473,31 @@ static int pp_bn(int dtype, int Co) {
     return 0;
 }
 
+static int halo64_mode() {
+    // read per launch (not cached): tests switch it to compare with the register-staged kernel bit for bit
+    const char* e = getenv("SCD_GEMM_HALO64");
+    return e ? atoi(e) : 1;
+}
+
+// conv_gemm_halo64_kernel's shapes: one phase of the 9 taps of a 3x3 / stride 1 / pad 1 convolution in the forward
+// order (dh, dw, wt) = (r - 1, s - 1, 3r + s) -> 0, or the input-gradient order (1 - r, 1 - s, 3r + s) -> 1;
+// 64 -> 64 channels, rows of 64 or 128 pixels, whole tiles of 256 pixels.  -1: not this kernel.
+static int halo64_taps(const GemmParams& p, int nphase, const scd_gemm_phase* phases) {
+    if (nphase != 1 || p.Ci != 64 || p.Co != 64 || p.is != 1 || p.os != 1 || p.head_on || p.wrow != 9 * 64) return -1;
+    const scd_gemm_phase& ph = phases[0];
+    if (ph.ntaps != 9 || ph.rho_h || ph.rho_w || ph.Qh != p.Ho || ph.Qw != p.Wo || p.Hi != p.Ho || p.Wi != p.Wo)
+        return -1;
+    if ((p.Wo != 128 && p.Wo != 64) || ph.Qh % (256 / p.Wo)) return -1;
+    int fwd = 1, bwd = 1;
+    for (int t = 0; t < 9; ++t) {
+        const int r = t / 3, c = t % 3;
+        if (ph.wt[t] != t) return -1;
+        fwd &= ph.dh[t] == r - 1 && ph.dw[t] == c - 1;
+        bwd &= ph.dh[t] == 1 - r && ph.dw[t] == 1 - c;
+    }
+    return fwd ? 0 : (bwd ? 1 : -1);
+}
+
 static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm_phase* phases, void* stream) {
     if (nphase < 1 || nphase > SCD_MAX_PHASES) return SCD_ERR_ARG;
     const int BK = dtype == SCD_DT_BF16 ? 64 : 32;
@@ -2433,6 +2566,35 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         }
     }
     if (p.bnbwd && dtype != SCD_DT_BF16) return SCD_ERR_ARG;   // BN-backward sums: 16-bit epilogues (caller falls back)
+    {
+        // 3x3 / s1 / p1, 64 -> 64 channels on whole rows of 64 or 128 pixels: the halo kernel
+        const int flip = halo64_taps(p, nphase, phases);
+        if (dtype == SCD_DT_BF16 && flip >= 0 && halo64_mode()) {
+            p.ntn = 1;
+            p.ph[0] = phases[0];
+            for (int i = 0; i <= SCD_MAX_PHASES; ++i) p.tile_start[i] = 0;
+            const long wb = (long)p.Co * p.wrow * esz;
+            if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
+            p.xbytes = (int)xb;
+            p.wbytes = (int)wb;
+            const int tiles = (int)(Mtot / 256);
+            hipStream_t st = (hipStream_t)stream;
+#define SCD_HALO_LAUNCH(WO)                                                                                          \
+    do {                                                                                                               \
+        if (p.bnbwd) {                                                                                                 \
+            if (flip) hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, true, true>), dim3(tiles), dim3(256), 0, st, p);  \
+            else hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, false, true>), dim3(tiles), dim3(256), 0, st, p);     \
+        } else {                                                                                                       \
+            if (flip) hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, true, false>), dim3(tiles), dim3(256), 0, st, p); \
+            else hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, false, false>), dim3(tiles), dim3(256), 0, st, p);    \
+        }                                                                                                              \
+    } while (0)
+            if (p.Wo == 128) SCD_HALO_LAUNCH(128);
+            else SCD_HALO_LAUNCH(64);
+#undef SCD_HALO_LAUNCH
+            SCD_RETURN_LAUNCH();
+        }
+    }
     bool ring = false;
     if (dtype == SCD_DT_BF16 && !narrow) {
         const int rm = ring_mode();

@@ -564,6 +564,48 @@ def test_conv_wgrad_layer1(case, dtype):
     test_conv_fwd_dgrad_wgrad(case, dtype)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,W", [(4, 128, 128), (3, 64, 64), (2, 32, 128)])
+def test_conv_halo64_matches_register_staged(N, H, W, dtype, monkeypatch):
+    """conv_gemm_halo64_kernel (layer1 3x3 64 -> 64: halo tile in LDS, taps at constant displacements) runs the
+    same MFMA sequence per output as the register-staged 256 x 64 kernel (tap-major, two K halves per tap), so
+    forward, input gradient (+= accumulate), forward BN sums and the BN-backward-sum epilogue are bit-identical."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(71)
+    C = 64
+    x = nhwc(torch.randn(N, C, H, W, generator=g), dtype)
+    w = (torch.randn(C, C, 3, 3, generator=g) / 24).to(DEV)
+    base = nhwc(torch.randn(N, C, H, W, generator=g), dtype)
+    ybn = nhwc(torch.randn(N, C, H, W, generator=g), dtype)
+
+    class St:
+        pass
+    st = St()
+    st.mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    st.invstd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    st.scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    st.shift = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SCD_GEMM_HALO64", mode)
+        wp, wt = ops.pack_weight(w, dtype, 0), ops.pack_weight(w, dtype, 1)
+        stats = torch.zeros(64 * 2 * C, dtype=torch.float64, device=DEV)
+        y = ops.conv_fwd(x, wp, C, 3, 3, 1, 1, stats=stats)
+        dx = base.clone()
+        ops.conv_dgrad(x, wt, C, H, W, 3, 3, 1, 1, out=dx, accumulate=True)
+        bst = torch.zeros(64 * 2 * C, dtype=torch.float64, device=DEV)
+        dxb = ops.conv_dgrad(x, wt, C, H, W, 3, 3, 1, 1, bn_bwd=(st, ybn, bst))
+        torch.cuda.synchronize()
+        outs[mode] = (y, stats.view(64, 2, C).sum(0), dx, dxb, bst.view(64, 2, C).sum(0))
+    for a, b in zip(outs["1"][::2], outs["0"][::2]):
+        assert torch.equal(a, b)
+    for a, b in zip(outs["1"][1::2], outs["0"][1::2]):      # fp64 atomics: replica order may differ
+        assert torch.allclose(a, b, rtol=1e-12, atol=1e-9)
+    xr = nchw(x).float().requires_grad_(True)
+    ref = F.conv2d(xr, w.cpu().to(dtype).float(), padding=1)
+    assert rel_err(nchw(outs["1"][0]), ref) < 1e-2
+
+
 def test_conv_layer1_accumulate_and_bias_relu():
     """Epilogue paths the block code uses on the layer1 shapes: dgrad += into an existing gradient, and a
     forward with bias + ReLU."""
