@@ -531,111 +531,226 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, const char* 
 }
 
 // -------------------------------------------------------------------------------------
-// 3x3 / stride 1 / pad 1 convolution with 64 input and 64 output channels (ResNet layer1, residuals.py:84-120;
-// forward and input gradient) on whole image rows: tile = 256 output pixels = TR = 256 / WO rows of one image.
-// The tile's input rows plus their one-pixel halo (TR + 2 rows x WO + 2 columns, 64 channels) are DMA'd into
-// LDS once (buffer_load ... lds; columns padded to WH = WO + 8 pixel slots, 16-B chunk c of slot q at c ^ (q & 7),
-// the swizzle applied to the source chunk), and every tap reads its A fragments from that image at a constant
-// displacement: all 9 taps x 2 K-halves are ds_read_b128 with immediate offsets from 6 per-lane base addresses,
-// so the loop has no address arithmetic (the register-staged 256 x 64 kernel spends ~9 VALU per MFMA on it).
-// The 64 x 576 weight operand streams through registers (16-B loads, the tap and channel block in the scalar
-// offset), one tap ahead of the MFMAs.  Wave w computes tile pixels 64w .. 64w+63 x all 64 channels; the shared
-// epilogue (BN sums, accumulate, BN-backward sums) runs on the same accumulator layout.  LDS: 69.6 KB at
-// WO = 128, two workgroups per CU.  FLIP: the input-gradient tap order (dh, dw) = (1 - r, 1 - s).
+// 3x3 / stride 1 / pad 1 convolution with 64 input and 64 output channels on whole image rows (ResNet layer1,
+// residuals.py:84-120; forward and input gradient).  A tile is 256 output pixels = TR = 256 / WO rows of one image;
+// the input rows with their one-pixel halo sit in LDS (columns padded to WH = WO + 8 pixel slots, 16-B chunk c of
+// slot q at c ^ (q & 7), the swizzle applied to the DMA's source chunk), so every tap reads its A fragments at a
+// constant displacement from 6 per-lane base addresses: no address arithmetic in the loop (the register-staged
+// 256 x 64 kernel spends ~9 VALU per MFMA on it), and the MFMA order per output is that kernel's (tap-major, two
+// K halves per tap), so the results are bit-identical.  A workgroup runs `run` consecutive tiles of one image
+// (TR output rows each) down the image, so consecutive tiles share two input rows.  LDS holds a ring of 2 TR + 2 input rows: the TR + 2 rows of the current tile and the TR new rows of the
+// next tile, which are DMA'd while the current tile is computed (HBM reads ~1x the input instead of 2x, and the
+// load latency hides behind the MFMAs).  8 waves: wave w computes tile pixels 64 (w & 3) .. +63 x channels
+// 32 (w >> 2) .. +31, its 32 x 576 weight slice held in registers for the whole run (144 VGPRs, loaded once).
+// Epilogue per tile: the accumulators are staged in LDS and the tile -- TR whole rows, one contiguous NHWC block
+// -- leaves as linear 16-B stores (+= when accumulating); BN sums (forward: fp32 accumulators, as the shared
+// epilogue; BNB: the stored gradient against the BN input) are carried in registers across the run and added to
+// the fp64 replicas once per workgroup.
 template <int WO, bool FLIP, bool BNB>
-__global__ __launch_bounds__(256, 2) void conv_gemm_halo64_kernel(GemmParams p) {
+__global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int run) {
     typedef __bf16 T;
     constexpr int TR = 256 / WO;                  // output rows per tile
-    constexpr int WH = WO + 8;                    // halo pixel slots per row (slot = input column + 1)
-    constexpr int HR = TR + 2;                    // halo rows
-    constexpr int ROWB = WH * 128;                // bytes per halo row
-    constexpr int HALO = HR * ROWB;
-    constexpr int EPI = 4 * 64 * (64 * 2 + 16) + 2048;
-    constexpr int SMEM = HALO > EPI ? HALO : EPI;
+    constexpr int WH = WO + 8;                    // pixel slots per ring row (slot = input column + 1)
+    constexpr int ROWB = WH * 128;
+    constexpr int RING = 2 * TR + 2;
+    constexpr int SROW = 64 * 2 + 16;             // staging row: 64 channels + 16 B pad
+    constexpr int STG = 256 * SROW;
     static_assert(WO * TR == 256 && WH % 8 == 0, "tile geometry");
-    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+    __shared__ __attribute__((aligned(16))) char smem[RING * ROWB + STG];
+    char* const stg = smem + RING * ROWB;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, lg = lane >> 4;
-    int bid;
-    {
-        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
-    }
-    const scd_gemm_phase& ph = p.ph[0];
-    const int QQ = ph.Qh * ph.Qw;
-    const int M = p.N * QQ;
-    const int mt = bid;
-    const int n = (mt * TR) / ph.Qh, row0 = mt * TR - n * ph.Qh;
+    const int pw = wave & 3, chh = wave >> 2;
+    const int wr = (64 * pw) / WO, wc = (64 * pw) % WO;
+    const int tpi = p.Ho / TR;                    // tiles per image
+    const int t0 = blockIdx.x * run;
+    const int n = t0 / tpi, r0 = (t0 - n * tpi) * TR;
 
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
 
-    // ---- weights of tap 0 (in flight while the halo lands): lane = (co row l16 of block b, K chunk lg)
-    const int wlane = (l16 * p.wrow + lg * 8) * 2;
-    uint4 wb[2][8];
-    auto wload = [&](int buf, int t) {
+    // ---- input rows -> ring slot (row + 1) % RING; one 1-KB DMA per 8 pixel slots (lane: slot lane/8, chunk lane%8)
+    const int hq = lane >> 3, csrc = (lane & 7) ^ hq;
+    auto dma_rows = [&](int ir0, int nrows) {
+        for (int j = wave; j < nrows * (WH / 8); j += 8) {
+            const int hr = j / (WH / 8), g = j - (j / (WH / 8)) * (WH / 8);
+            const int ir = ir0 + hr, ic = g * 8 + hq - 1;
+            const bool ok = (unsigned)ir < (unsigned)p.Hi && (unsigned)ic < (unsigned)p.Wi;
+            dma16(xrs, smem + ((ir + 1) % RING) * ROWB + g * 8 * 128,
+                  sel_off(ok, (((n * p.Hi + ir) * p.Wi + ic) * 64 + csrc * 8) * 2));
+        }
+    };
+    dma_rows(r0 - 1, TR + 2);
+
+    // ---- this wave's weight slice: co = 32 chh + 16 b + l16, K chunk lg of each (tap, half)
+    uint4 wreg[9][2][2];
+    {
+        const int wl = ((32 * chh + l16) * p.wrow + lg * 8) * 2;
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int t = 0; t < 9; ++t)
 #pragma unroll
             for (int s = 0; s < 2; ++s)
-                wb[buf][b * 2 + s] = __builtin_bit_cast(
-                    uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wlane, (b * 16 * p.wrow + t * 64 + s * 32) * 2, 0));
-    };
-    wload(0, 0);
-
-    // ---- halo: HR rows x WH/8 groups of 8 pixel slots, one 1-KB DMA per group (lane -> slot lane/8, chunk lane%8)
-    {
-        const int hq = lane >> 3, cs = lane & 7, csrc = cs ^ hq;
-        for (int j = wave; j < HR * (WH / 8); j += 4) {
-            const int hr = j / (WH / 8), g = j - (j / (WH / 8)) * (WH / 8);
-            const int ir = row0 + hr - 1, ic = g * 8 + hq - 1;
-            const bool ok = (unsigned)ir < (unsigned)p.Hi && (unsigned)ic < (unsigned)p.Wi;
-            dma16(xrs, smem + hr * ROWB + g * 8 * 128, sel_off(ok, (((n * p.Hi + ir) * p.Wi + ic) * 64 + csrc * 8) * 2));
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    wreg[t][s][b] = bload(wrs, wl + (b * 16 * p.wrow + t * 64 + s * 32) * 2);
+    }
+    // BN-backward epilogue parameters in LDS (the store phase owns fixed 8-channel chunks)
+    __shared__ __attribute__((aligned(16))) float bnpar[BNB ? 4 * 64 : 4];
+    if constexpr (BNB) {
+        if (tid < 256) {
+            const int k = tid >> 6, c = tid & 63;
+            const float* src = k == 0 ? p.bn_mean : k == 1 ? p.bn_invstd : k == 2 ? p.bn_rsc : p.bn_rsh;
+            bnpar[tid] = src[c];
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    // ---- per-lane A addresses: wave w = output row 64w / WO, columns (64w % WO) + 16a + l16; tap column shift dwi
-    const int wr = (wave * 64) / WO, wc = (wave * 64) % WO;
     int abase[3][2];
 #pragma unroll
     for (int d = 0; d < 3; ++d)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int q = wc + l16 + d;
-            abase[d][s] = wr * ROWB + q * 128 + (((s * 4 + lg) ^ (q & 7)) << 4);
+            abase[d][s] = q * 128 + (((s * 4 + lg) ^ (q & 7)) << 4);
         }
+    // the workgroup's BN sums: per tile the waves' partials go to fixed LDS slots ([wave][channel][2]) and threads
+    // 0..127 (channel tid & 63, sum tid >> 6) add them in a fixed order, so the sums are deterministic
+    __shared__ float bnred[8 * 64 * 2];
+    float bnsum = 0.f;
+    const bool fwd_stats = !BNB && p.stats;
+    const int cc = tid & 7;                       // store phase: this thread's 8-channel chunk
 
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
+    for (int i = 0; i < run; ++i) {
+        const int r = r0 + i * TR;
+        if (i + 1 < run) dma_rows(r + TR + 1, TR);            // the next tile's new rows, into free ring slots
+        f32x4 acc[4][2];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        if (t + 1 < 9) wload((t + 1) & 1, t + 1);
-        // keep the next tap's weight loads ahead of this tap's MFMAs (the scheduler would sink them to their use)
-        __builtin_amdgcn_sched_barrier(0);
-        const int r = t / 3, c = t - (t / 3) * 3;
-        const int dhi = FLIP ? 2 - r : r, dwi = FLIP ? 2 - c : c;
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            bf16x8 af[4];
+            for (int b = 0; b < 2; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        int rowoff[3];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(smem + abase[dwi][s] + dhi * ROWB + a * 16 * 128);
+        for (int d = 0; d < 3; ++d) rowoff[d] = ((r + wr + d) % RING) * ROWB;   // input row r + wr + d - 1
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+        for (int t = 0; t < 9; ++t) {
+            const int kr = t / 3, kc = t - (t / 3) * 3;
+            const int dhi = FLIP ? 2 - kr : kr, dwi = FLIP ? 2 - kc : kc;
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wb[t & 1][b * 2 + s]),
-                                                                        af[a], acc[a][b], 0, 0, 0);
+            for (int s = 0; s < 2; ++s) {
+                bf16x8 af[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(smem + rowoff[dhi] + abase[dwi][s] + a * 16 * 128);
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wreg[t][s][b]),
+                                                                            af[a], acc[a][b], 0, 0, 0);
+            }
+        }
+        // stage: lane holds pixel 64pw + 16a + l16, channels 32chh + 16b + 4lg + (0..3)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                bf16x4 o;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q] = (__bf16)acc[a][b][q];
+                *(bf16x4*)(stg + (64 * pw + 16 * a + l16) * SROW + (32 * chh + 16 * b + 4 * lg) * 2) = o;
+            }
+        if (fwd_stats) {
+            // forward BN sums of the fp32 accumulators (as the shared epilogue): over the wave's 4 pixel blocks,
+            // the 16 pixel lanes (DPP row sums), then the 4 pixel-group waves through LDS
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float sv = 0.f, qv = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) { sv += acc[a][b][q]; qv += acc[a][b][q] * acc[a][b][q]; }
+                    sv = row16_sum(sv);
+                    qv = row16_sum(qv);
+                    if (l16 == 0) {
+                        const int c = 32 * chh + 16 * b + 4 * lg + q;
+                        bnred[(pw * 64 + c) * 2] = sv;
+                        bnred[(pw * 64 + c) * 2 + 1] = qv;
+                    }
+                }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // next tile's rows (and the previous stores)
+        __syncthreads();
+        if (fwd_stats && tid < 128) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) bnsum += bnred[(w * 64 + (tid & 63)) * 2 + (tid >> 6)];
+        }
+        // ---- store phase: the tile is rows r .. r+TR-1 of image n, one contiguous 32-KB NHWC block
+        {
+            const long base = ((long)(n * p.Ho + r) * p.Wo) * 64;
+            float bs[8], bq[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { bs[e] = 0.f; bq[e] = 0.f; }
+#pragma unroll(BNB ? 1 : 4)
+            for (int k = 0; k < 4; ++k) {
+                const int j = tid + 512 * k;                    // 16-B chunk of the tile (pixel j / 8, chunk cc)
+                const int px = j >> 3;
+                uint4 v = *(const uint4*)(stg + px * SROW + cc * 16);
+                T* dst = (T*)p.y + base + px * 64 + cc * 8;
+                if (p.accumulate) {
+                    float a8[8], o8[8];
+                    Vec16<T>::load(&v, a8);
+                    Vec16<T>::load(dst, o8);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) a8[e] += o8[e];
+                    Vec16<T>::store(&v, a8);
+                }
+                if constexpr (BNB) {
+                    float d8[8], y8[8];
+                    Vec16<T>::load(&v, d8);
+                    Vec16<T>::load((const T*)p.bny + base + px * 64 + cc * 8, y8);
+                    // parameters re-read from LDS per chunk (an opaque offset keeps them out of the live registers)
+                    int po = cc * 8;
+                    asm volatile("" : "+v"(po));
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) d8[e] = y8[e] * bnpar[128 + po + e] + bnpar[192 + po + e] > 0.f ? d8[e] : 0.f;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        bs[e] += d8[e];
+                        bq[e] += d8[e] * (y8[e] - bnpar[po + e]) * bnpar[64 + po + e];
+                    }
+                }
+                *(uint4*)dst = v;
+            }
+            if constexpr (BNB) {
+                // lanes with equal lane % 8 hold the same channels: fold lane bits 3..5, then the 8 waves via LDS
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+#pragma unroll
+                    for (int o = 8; o < 64; o <<= 1) { bs[e] += __shfl_xor(bs[e], o, 64); bq[e] += __shfl_xor(bq[e], o, 64); }
+                }
+                if (lane < 8) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        bnred[(wave * 64 + cc * 8 + e) * 2] = bs[e];
+                        bnred[(wave * 64 + cc * 8 + e) * 2 + 1] = bq[e];
+                    }
+                }
+            }
+        }
+        __syncthreads();                                         // staging read before the next tile writes it
+        if (BNB && tid < 128) {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) bnsum += bnred[(w * 64 + (tid & 63)) * 2 + (tid >> 6)];
         }
     }
-    __syncthreads();          // halo no longer read: the epilogue stages its tile in the same LDS
-    gemm_epilogue<T, 256, 64, 1, false, BNB>(p, acc, smem, tid, bid, mt, 0, M, QQ, ph);
+
+    // ---- BN sums: once per workgroup into replica blockIdx % SCD_STAT_REPLICAS
+    if ((BNB || p.stats) && tid < 128) {
+        const int rep = blockIdx.x % SCD_STAT_REPLICAS;
+        atomic_add_f64(p.stats + ((long)rep * 2 + (tid >> 6)) * p.Co + (tid & 63), (double)bnsum);
+    }
 }
 
 template <bool HEADS, bool BNB = false>
@@ -2474,12 +2589,13 @@ static int pp_bn(int dtype, int Co) {
 }
 
 static int halo64_mode() {
-    // read per launch (not cached): tests switch it to compare with the register-staged kernel bit for bit
+    // SCD_GEMM_HALO64=0: the register-staged kernel.  Read per launch (not cached): tests switch it to compare the
+    // two bit for bit
     const char* e = getenv("SCD_GEMM_HALO64");
     return e ? atoi(e) : 1;
 }
 
-// conv_gemm_halo64_kernel's shapes: one phase of the 9 taps of a 3x3 / stride 1 / pad 1 convolution in the forward
+// conv_gemm_l1p_kernel's shapes: one phase of the 9 taps of a 3x3 / stride 1 / pad 1 convolution in the forward
 // order (dh, dw, wt) = (r - 1, s - 1, 3r + s) -> 0, or the input-gradient order (1 - r, 1 - s, 3r + s) -> 1;
 // 64 -> 64 channels, rows of 64 or 128 pixels, whole tiles of 256 pixels.  -1: not this kernel.
 static int halo64_taps(const GemmParams& p, int nphase, const scd_gemm_phase* phases) {
@@ -2567,9 +2683,9 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     }
     if (p.bnbwd && dtype != SCD_DT_BF16) return SCD_ERR_ARG;   // BN-backward sums: 16-bit epilogues (caller falls back)
     {
-        // 3x3 / s1 / p1, 64 -> 64 channels on whole rows of 64 or 128 pixels: the halo kernel
+        // 3x3 / s1 / p1, 64 -> 64 channels on whole rows of 64 or 128 pixels: the persistent row-ring kernel
         const int flip = halo64_taps(p, nphase, phases);
-        if (dtype == SCD_DT_BF16 && flip >= 0 && halo64_mode()) {
+        if (dtype == SCD_DT_BF16 && flip >= 0 && halo64_mode() && !p.bias && !p.relu) {
             p.ntn = 1;
             p.ph[0] = phases[0];
             for (int i = 0; i <= SCD_MAX_PHASES; ++i) p.tile_start[i] = 0;
@@ -2579,19 +2695,24 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
             p.wbytes = (int)wb;
             const int tiles = (int)(Mtot / 256);
             hipStream_t st = (hipStream_t)stream;
-#define SCD_HALO_LAUNCH(WO)                                                                                          \
-    do {                                                                                                               \
-        if (p.bnbwd) {                                                                                                 \
-            if (flip) hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, true, true>), dim3(tiles), dim3(256), 0, st, p);  \
-            else hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, false, true>), dim3(tiles), dim3(256), 0, st, p);     \
-        } else {                                                                                                       \
-            if (flip) hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, true, false>), dim3(tiles), dim3(256), 0, st, p); \
-            else hipLaunchKernelGGL((conv_gemm_halo64_kernel<WO, false, false>), dim3(tiles), dim3(256), 0, st, p);    \
-        }                                                                                                              \
+            // `run` tiles per workgroup down one image (about one workgroup per CU)
+            const int tpi = p.Ho / (256 / p.Wo);
+            int run = 1;
+            while (run < 16 && tpi % (2 * run) == 0 && tiles / (2 * run) >= num_cus()) run *= 2;
+            const int grid = tiles / run;
+#define SCD_L1P_LAUNCH(WO)                                                                                              \
+    do {                                                                                                                 \
+        if (p.bnbwd) {                                                                                                   \
+            if (flip) hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, true, true>), dim3(grid), dim3(512), 0, st, p, run);   \
+            else hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, false, true>), dim3(grid), dim3(512), 0, st, p, run);      \
+        } else {                                                                                                         \
+            if (flip) hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, true, false>), dim3(grid), dim3(512), 0, st, p, run);  \
+            else hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, false, false>), dim3(grid), dim3(512), 0, st, p, run);     \
+        }                                                                                                                \
     } while (0)
-            if (p.Wo == 128) SCD_HALO_LAUNCH(128);
-            else SCD_HALO_LAUNCH(64);
-#undef SCD_HALO_LAUNCH
+            if (p.Wo == 128) SCD_L1P_LAUNCH(128);
+            else SCD_L1P_LAUNCH(64);
+#undef SCD_L1P_LAUNCH
             SCD_RETURN_LAUNCH();
         }
     }

@@ -565,11 +565,15 @@ def test_conv_wgrad_layer1(case, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("N,H,W", [(4, 128, 128), (3, 64, 64), (2, 32, 128)])
-def test_conv_halo64_matches_register_staged(N, H, W, dtype, monkeypatch):
-    """conv_gemm_halo64_kernel (layer1 3x3 64 -> 64: halo tile in LDS, taps at constant displacements) runs the
-    same MFMA sequence per output as the register-staged 256 x 64 kernel (tap-major, two K halves per tap), so
-    forward, input gradient (+= accumulate), forward BN sums and the BN-backward-sum epilogue are bit-identical."""
+# (tiles of 256 px >= 2 x CUs give runs of 2..16 tiles per workgroup: the row ring is reused; fewer: one tile each)
+@pytest.mark.parametrize("N,H,W", [(4, 128, 128), (3, 64, 64), (2, 32, 128), (16, 128, 128), (64, 64, 64),
+                                   (32, 128, 128)])
+def test_conv_l1p_matches_register_staged(N, H, W, dtype, monkeypatch):
+    """conv_gemm_l1p_kernel (layer1 3x3 64 -> 64: a persistent ring of input rows in LDS, every tap read at a
+    constant displacement) runs the same MFMA sequence
+    per output as the register-staged 256 x 64 kernel (tap-major, two K halves per tap): forward, input gradient
+    (+= accumulate) and the BN-backward-sum variant's gradient are bit-identical; the BN sums agree to fp32
+    summation-order noise."""
     from scdhip import ops
     g = torch.Generator().manual_seed(71)
     C = 64
@@ -586,7 +590,7 @@ def test_conv_halo64_matches_register_staged(N, H, W, dtype, monkeypatch):
     st.scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
     st.shift = (torch.randn(C, generator=g) * 0.2).to(DEV)
     outs = {}
-    for mode in ("1", "0"):
+    for mode in ("1", "0"):               # persistent row-ring kernel, register-staged kernel
         monkeypatch.setenv("SCD_GEMM_HALO64", mode)
         wp, wt = ops.pack_weight(w, dtype, 0), ops.pack_weight(w, dtype, 1)
         stats = torch.zeros(64 * 2 * C, dtype=torch.float64, device=DEV)
@@ -597,10 +601,12 @@ def test_conv_halo64_matches_register_staged(N, H, W, dtype, monkeypatch):
         dxb = ops.conv_dgrad(x, wt, C, H, W, 3, 3, 1, 1, bn_bwd=(st, ybn, bst))
         torch.cuda.synchronize()
         outs[mode] = (y, stats.view(64, 2, C).sum(0), dx, dxb, bst.view(64, 2, C).sum(0))
-    for a, b in zip(outs["1"][::2], outs["0"][::2]):
-        assert torch.equal(a, b)
-    for a, b in zip(outs["1"][1::2], outs["0"][1::2]):      # fp64 atomics: replica order may differ
-        assert torch.allclose(a, b, rtol=1e-12, atol=1e-9)
+    for m in ("1",):
+        for i in (0, 2, 3):                                  # y, dx (+=), dx of the BN-backward-sum variant
+            assert torch.equal(outs[m][i], outs["0"][i]), (m, i)
+        for i in (1, 4):                                     # BN sums: fp32 partials over other pixel groups
+            d = (outs[m][i] - outs["0"][i]).abs().max().item()
+            assert d <= 1e-5 * outs["0"][i].abs().max().item(), (m, i, d)
     xr = nchw(x).float().requires_grad_(True)
     ref = F.conv2d(xr, w.cpu().to(dtype).float(), padding=1)
     assert rel_err(nchw(outs["1"][0]), ref) < 1e-2

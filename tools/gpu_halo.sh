@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-h}
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "halo64 or layer1 or bn_backward or dgrad_with_bn" > gpurun_out/tk_$TAG.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "l1p or layer1 or bn_backward or dgrad_with_bn" > gpurun_out/tk_$TAG.log 2>&1; rc=$?
 tail -3 gpurun_out/tk_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_ab_lib.sh $TAG libscdhip_base.so libscdhip.so || exit 1
