@@ -159,6 +159,19 @@ int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, doubl
 int scd_stem_conv_wgrad_nsplit(long M);
 int scd_stem_conv_wgrad(int dtype, const void* dy, const void* ybn, const float* coef, const float* x, float* ws,
                         int nsplit, int N, int H, int W, int Ho, int Wo, void* stream);
+/* Stem backward in one pass (residuals.py:209-216 backward, replacing autograd's MaxPool2d / ReLU / BatchNorm2d /
+ * Conv2d backward chain of the stem): from the pooled gradient dout (N,Ho/2,Wo/2,64), its argmax, the pre-BN conv
+ * output y (N,Ho,Wo,64) and the input x (N,1,H,W) fp32, accumulates the BN backward sums (sum dz, sum dz*xhat) into
+ * stats (fp64 replicas, as scd_stem_pool_bwd_bn) and writes tg = [T1 | G] (2 x 64 x 64 fp32: sum dz col^T and the
+ * Gram matrix of the input columns, tap 49 = 1), via ws (scd_stem_bwd_nsplit() x 2 x 64 x 64 floats).
+ * scd_stem_bwd_combine then adds dW = alpha (a T1 + b W G + c s) with (a, b, c) = scd_bn_bwd_finalize's coefficients
+ * and W = the forward's packed bf16 weights (64 x 64) into dst (64,1,7,7). */
+int scd_stem_bwd_nsplit(void);
+int scd_stem_bwd_fused(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
+                       const float* shift, const float* mean, const float* invstd, const float* x, double* stats,
+                       float* ws, int nsplit, float* tg, int N, int H, int W, int Ho, int Wo, void* stream);
+int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk, const float* coef, float* dst, int accumulate,
+                         float alpha, void* stream);
 
 /* ---- training BatchNorm2d (residuals.py:92,95,212,262,306; momentum 0.1, eps 1e-5) ---- */
 /* sum replicas [nrep][2][C] -> [2][C] in place (replica 0); used before a SyncBN all-reduce */

@@ -48,6 +48,9 @@
 #define scd_stem_conv_fwd scd_stem_conv_fwd__f16
 #define scd_stem_conv_wgrad_nsplit scd_stem_conv_wgrad_nsplit__f16
 #define scd_stem_conv_wgrad scd_stem_conv_wgrad__f16
+#define scd_stem_bwd_nsplit scd_stem_bwd_nsplit__f16
+#define scd_stem_bwd_fused scd_stem_bwd_fused__f16
+#define scd_stem_bwd_combine scd_stem_bwd_combine__f16
 #define scd_pad_channels scd_pad_channels__f16
 #define __bf16 _Float16
 #define __builtin_amdgcn_mfma_f32_16x16x32_bf16 __builtin_amdgcn_mfma_f32_16x16x32_f16
@@ -96,6 +99,8 @@ SCD_F16_DECL(scd_heads_sparse_bwd)
 SCD_F16_DECL(scd_heads_sparse_fixup)
 SCD_F16_DECL(scd_stem_conv_fwd)
 SCD_F16_DECL(scd_stem_conv_wgrad)
+SCD_F16_DECL(scd_stem_bwd_fused)
+SCD_F16_DECL(scd_stem_bwd_combine)
 SCD_F16_DECL(scd_pad_channels)
 #define SCD_F16_FWD(fn, ...) \
     do { if (dtype == SCD_DT_F16) return fn##__f16(SCD_DT_BF16, __VA_ARGS__); } while (0)

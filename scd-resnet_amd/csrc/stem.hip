@@ -274,6 +274,248 @@ __global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __re
 }
 
 
+// ---- stem backward in one pass over the pooled gradient (residuals.py:209-216 backward; BN layer :212)
+// With dz = the MaxPool + ReLU gradient at the conv output and the BN backward apply dy = a*dz + b*y + c
+// (scd_bn_bwd_finalize's coefficients, which need the batch sums of dz and dz*xhat first), the weight gradient is
+//     dW = sum_p dy[p] col[p]^T = a * T1 + b * W G + c * s,   T1 = sum_p dz[p] col[p]^T,  G = sum_p col[p] col[p]^T,
+// s = sum_p col[p] (tap 49 of col is 1, so s = G[.][49]).  One pass therefore rebuilds dz per 2x2 conv block from
+// the pooled gradient / argmax / y (as stem_pool_bwd_bn_2x2_kernel), accumulates the BN backward sums, and runs the
+// T1 and G MFMAs on an LDS tile of dz and the [tap][pixel] input columns: dz is never written to HBM and y is read
+// once (the unfused backward wrote dz and read it, and y, again).  Tile = 2 conv rows x 64 columns (32 2x2 blocks
+// x 8 channel chunks = one item per thread).  W G uses the conv's bf16 weights in fp32 (the forward multiplied
+// the same operands), so dW matches the unfused path up to the bf16 rounding of y and dy that it no longer has.
+constexpr int BTW = 64;                              // conv columns per tile (two conv rows per tile)
+constexpr int BPROWS = 9;                            // input rows of a tile: conv rows 2bo, 2bo+1 -> 4bo-3 .. 4bo+5
+constexpr int ONE_TAP = KK;                          // col tap 49 = 1
+
+__global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
+    const __bf16* __restrict__ dout, const uint8_t* __restrict__ argmax, const __bf16* __restrict__ y,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ x, double* __restrict__ stats, float* __restrict__ ws,
+    int H, int W, int Ho, int Wo, int ntiles, int chunk) {
+    constexpr int DT = WPX * DROW;                   // one conv row of dz: [64 px][DROW]
+    constexpr int CT = 64 * 128;                     // one conv row of columns: [64 taps][64 px] bf16
+    __shared__ __attribute__((aligned(16))) char smem[2 * DT + 2 * CT + BPROWS * WPCOLS * 4];
+    char* Ds = smem;
+    char* Cs = smem + 2 * DT;
+    float* patch = (float*)(smem + 2 * DT + 2 * CT);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int q4 = l16 >> 2, pp = l16 & 3;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int Hp = Ho / 2, Wp = Wo / 2;
+    const int gpr = Wo / BTW;                        // column groups per conv row pair
+    const int tpi = Hp * gpr;
+    const int bl = tid >> 3, ch = tid & 7;           // this thread's 2x2 block of the tile and channel chunk
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+    float sc[8], sh[8], mu[8], is[8], s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sc[e] = scale[ch * 8 + e]; sh[e] = shift[ch * 8 + e]; mu[e] = mean[ch * 8 + e]; is[e] = invstd[ch * 8 + e];
+        s1[e] = 0.f; s2[e] = 0.f;
+    }
+    f32x4 acc1[2][2], acc2[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) { acc1[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f}; acc2[a][b] = acc1[a][b]; }
+
+    const int t0 = blockIdx.x * chunk, t1 = min(ntiles, t0 + chunk);
+    // raw operands of one tile, loaded one tile ahead (issued as soon as the previous tile's are consumed)
+    uint4 rd[2][2], ry[2][2];
+    uint2 ra[2][2];
+    float rp[(BPROWS * WPCOLS + 255) / 256];
+    auto load_tile = [&](int t) {
+        const int n = t / tpi, rem = t - (t / tpi) * tpi;
+        const int bo = rem / gpr, jc = rem - (rem / gpr) * gpr;
+        const int w0 = jc * BTW, bc = jc * (BTW / 2) + bl;
+        const bool okh = bo + 1 < Hp, okw = bc + 1 < Wp;
+#pragma unroll
+        for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+            for (int oj = 0; oj < 2; ++oj) {
+                const bool ok = (oi == 0 || okh) && (oj == 0 || okw);
+                const long o = (((long)n * Hp + bo + (ok ? oi : 0)) * Wp + bc + (ok ? oj : 0)) * CO + ch * 8;
+                rd[oi][oj] = *(const uint4*)(dout + o);
+                ra[oi][oj] = ok ? *(const uint2*)(argmax + o) : make_uint2(0xffffffffu, 0xffffffffu);
+            }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                ry[a][b] = *(const uint4*)(y + (((long)n * Ho + 2 * bo + a) * Wo + 2 * bc + b) * CO + ch * 8);
+        const float* xn = x + (size_t)n * H * W;
+        const int ih0 = 4 * bo - PD, iw0 = 2 * w0 - PD;
+#pragma unroll
+        for (int q = 0; q < (BPROWS * WPCOLS + 255) / 256; ++q) {
+            const int i = tid + 256 * q;
+            const int r = i / WPCOLS, c = i - (i / WPCOLS) * WPCOLS;
+            const int ih = ih0 + r, iw = iw0 + c;
+            rp[q] = (i < BPROWS * WPCOLS && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? xn[(size_t)ih * W + iw] : 0.f;
+        }
+    };
+    if (t0 < t1) load_tile(t0);
+    for (int t = t0; t < t1; ++t) {
+        // ---- dz of the 2x2 conv block (2bo + a, 2bc + b), channels 8ch .. 8ch+7
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                float g[8], v[8];
+                Vec16<__bf16>::load(&ry[a][b], v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+                for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+                    for (int oj = 0; oj < 2; ++oj) {
+                        if (oi > a || oj > b) continue;
+                        const unsigned sel = (a - 2 * oi + 1) * 3 + (b - 2 * oj + 1);
+                        float d[8];
+                        Vec16<__bf16>::load(&rd[oi][oj], d);
+                        const unsigned aw[2] = {ra[oi][oj].x, ra[oi][oj].y};
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            if (((aw[e >> 2] >> (8 * (e & 3))) & 0xffu) == sel) g[e] += d[e];
+                    }
+                bf16x8 o8;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    o8[e] = (__bf16)(v[e] * sc[e] + sh[e] > 0.f ? g[e] : 0.f);
+                    const float r = (float)o8[e];
+                    s1[e] += r;
+                    s2[e] += r * (v[e] - mu[e]) * is[e];
+                }
+                *(bf16x8*)(Ds + a * DT + dswz(2 * bl + b, ch * 16)) = o8;
+            }
+#pragma unroll
+        for (int q = 0; q < (BPROWS * WPCOLS + 255) / 256; ++q) {
+            const int i = tid + 256 * q;
+            if (i < BPROWS * WPCOLS) patch[i] = rp[q];
+        }
+        if (t + 1 < t1) load_tile(t + 1);                 // in flight during this tile's column build and MFMAs
+        __syncthreads();
+        // ---- transposed column tiles of both conv rows: thread -> tap k = tid / 4, pixels 16 (tid % 4) .. +15
+        {
+            const int k = tid >> 2, pq = tid & 3;
+            const int kh = k / KS, kw = k - (k / KS) * KS;
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    bf16x8 v;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int px = pq * 16 + h * 8 + e;
+                        v[e] = (__bf16)(k < KK ? patch[(2 * a + kh) * WPCOLS + SP * px + kw] : (k == ONE_TAP ? 1.f : 0.f));
+                    }
+                    *(bf16x8*)(Cs + a * CT + swz128(k, pq * 2 + h)) = v;
+                }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const char* D = Ds + a * DT;
+            const char* C = Cs + a * CT;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int r0 = 32 * s + 8 * lg + q4;
+                bf16x8 tf[2], df[2], gf[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) tf[b] = *(const bf16x8*)(C + swz128(wn * 32 + b * 16 + l16, s * 4 + lg));
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    gf[i] = *(const bf16x8*)(C + swz128(wm * 32 + i * 16 + l16, s * 4 + lg));
+                    const int cb = (wm * 32 + i * 16 + 4 * pp) * 2;
+                    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(D + dswz(r0, cb)));
+                    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(D + dswz(r0 + 4, cb)));
+                    s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    df[i] = __builtin_bit_cast(bf16x8, v8);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) {
+                        acc1[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[b], df[i], acc1[i][b], 0, 0, 0);
+                        acc2[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[b], gf[i], acc2[i][b], 0, 0, 0);
+                    }
+            }
+        }
+        __syncthreads();                             // tiles read before the next tile overwrites them
+    }
+    // ---- partial T1 (channel rows) and G (tap rows) of this split; lane holds columns (taps) wn*32 + b*16 + 4lg ..
+    float* wz = ws + (size_t)blockIdx.x * 2 * CO * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            *(f32x4*)(wz + (wm * 32 + i * 16 + l16) * 64 + wn * 32 + b * 16 + lg * 4) = acc1[i][b];
+            *(f32x4*)(wz + CO * 64 + (wm * 32 + i * 16 + l16) * 64 + wn * 32 + b * 16 + lg * 4) = acc2[i][b];
+        }
+    // ---- BN backward sums: threads with equal tid % 8 hold the same channels
+    float* red = (float*)smem;                        // [2][256][9]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[tid * 9 + e] = s1[e]; red[(256 + tid) * 9 + e] = s2[e]; }
+    __syncthreads();
+    if (tid < 2 * CO) {
+        const int stat = tid / CO, c = tid - (tid / CO) * CO;
+        const int cc = c / 8, e = c - (c / 8) * 8;
+        double acc = 0.0;
+        for (int t = cc; t < 256; t += 8) acc += red[(stat * 256 + t) * 9 + e];
+        atomic_add_f64(stats + ((long)(blockIdx.x % SCD_STAT_REPLICAS) * 2 + stat) * CO + c, acc);
+    }
+}
+
+// sum of the per-split [T1 | G] slabs in a fixed order: workgroup = 32 consecutive elements x 8 split lanes (each
+// summing every 8th split in order), the 8 partials combined in order in fp64
+__global__ __launch_bounds__(256) void stem_bwd_reduce_kernel(const float* __restrict__ ws, int nsplit,
+                                                              float* __restrict__ out) {
+    const int col = threadIdx.x & 31, lane8 = threadIdx.x >> 5;
+    const int i = blockIdx.x * 32 + col;
+    double a = 0.0;
+    int z = lane8;
+    for (; z + 56 < nsplit; z += 64) {               // 8 independent loads in flight, summed in split order
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ws[(size_t)(z + 8 * u) * 2 * CO * 64 + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; z < nsplit; z += 8) a += ws[(size_t)z * 2 * CO * 64 + i];
+    __shared__ double part[8][32];
+    part[lane8][col] = a;
+    __syncthreads();
+    if (lane8 == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += part[k][col];
+        out[i] = (float)t;
+    }
+}
+
+// dst[co][k] (+)= alpha (a[co] T1[co][k] + b[co] (W G)[co][k] + c[co] G[k][49]) for the 49 taps, W = the conv's bf16
+// weights (wpk rows [co][64], taps >= 49 zero); one workgroup per output channel
+__global__ __launch_bounds__(64) void stem_bwd_combine_kernel(const float* __restrict__ tg, const __bf16* __restrict__ wpk,
+                                                              const float* __restrict__ coef, float* __restrict__ dst,
+                                                              int accumulate, float alpha) {
+    const int co = blockIdx.x, k = threadIdx.x;
+    const float* T1 = tg;
+    const float* G = tg + CO * 64;
+    __shared__ float wrow[64];
+    wrow[k] = k < KK ? (float)wpk[co * 64 + k] : 0.f;
+    __syncthreads();
+    if (k >= KK) return;
+    double wg = 0.0;
+    for (int l = 0; l < KK; ++l) wg += (double)wrow[l] * (double)G[l * 64 + k];
+    const double v = (double)coef[co] * T1[co * 64 + k] + (double)coef[CO + co] * wg + (double)coef[2 * CO + co] * G[k * 64 + ONE_TAP];
+    float* d = dst + co * KK + k;
+    *d = (accumulate ? *d : 0.f) + alpha * (float)v;
+}
+
+
 SCD_KERNEL_NS_END
 }  // namespace
 
@@ -308,5 +550,40 @@ extern "C" int scd_stem_conv_wgrad(int dtype, const void* dy, const void* ybn, c
     if (coef && !ybn) return SCD_ERR_ARG;
     hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(nsplit), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dy,
                        (const __bf16*)ybn, coef, x, ws, H, W, Ho, Wo, M, (int)chunk);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_stem_bwd_nsplit(void) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return 2 * cus;
+}
+
+extern "C" int scd_stem_bwd_fused(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
+                                  const float* shift, const float* mean, const float* invstd, const float* x,
+                                  double* stats, float* ws, int nsplit, float* tg, int N, int H, int W, int Ho, int Wo,
+                                  void* stream) {
+    SCD_F16_FWD(scd_stem_bwd_fused, dout, argmax, y, scale, shift, mean, invstd, x, stats, ws, nsplit, tg, N, H, W, Ho,
+                Wo, stream);
+    if (dtype != SCD_DT_BF16 || nsplit < 1 || Wo % BTW || Ho % 2 || Ho != (H + 2 * PD - KS) / SP + 1 ||
+        Wo != (W + 2 * PD - KS) / SP + 1 || (long)N * Ho * Wo * CO >= (1L << 31))
+        return SCD_ERR_ARG;
+    const int ntiles = N * (Ho / 2) * (Wo / BTW);
+    const int chunk = (ntiles + nsplit - 1) / nsplit;
+    const int grid = (ntiles + chunk - 1) / chunk;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(stem_bwd_fused_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)dout, argmax,
+                       (const __bf16*)y, scale, shift, mean, invstd, x, stats, ws, H, W, Ho, Wo, ntiles, chunk);
+    hipLaunchKernelGGL(stem_bwd_reduce_kernel, dim3(2 * CO * 64 / 32), dim3(256), 0, st, (const float*)ws, grid, tg);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk, const float* coef, float* dst,
+                                    int accumulate, float alpha, void* stream) {
+    SCD_F16_FWD(scd_stem_bwd_combine, tg, wpk, coef, dst, accumulate, alpha, stream);
+    if (dtype != SCD_DT_BF16) return SCD_ERR_ARG;
+    hipLaunchKernelGGL(stem_bwd_combine_kernel, dim3(CO), dim3(64), 0, (hipStream_t)stream, tg, (const __bf16*)wpk,
+                       coef, dst, accumulate, alpha);
     SCD_RETURN_LAUNCH();
 }

@@ -25,6 +25,10 @@ def _c(t):
     return t if t is None or t.is_contiguous() else t.contiguous()
 
 
+# stem backward as one pass (ops.stem_backward_fused); SCD_STEM_FUSED_BWD=0: pool backward + fused-apply weight gradient
+_STEM_FUSED_BWD = os.environ.get("SCD_STEM_FUSED_BWD", "1") != "0"
+
+
 def _conv_ld(w):
     """dst strides of an OIHW conv weight (Co, Ci, kh, kw) for scd_wgrad_reduce: [co][ci][tap]."""
     T = w.shape[2] * w.shape[3]
@@ -97,13 +101,17 @@ class StemFn(torch.autograd.Function):
         out, am = ops.stem_pool_fwd(y, st)
         ctx.save_for_backward(cols, y, am)
         ctx.st, ctx.conv, ctx.bn, ctx.direct = st, conv, bn, direct
+        ctx.wpk = wpk if direct else None
         return out
 
     @staticmethod
     def backward(ctx, dout):
         conv, bn, st = ctx.conv, ctx.bn, ctx.st
         cols, y, am = ctx.saved_tensors
-        if ctx.direct:
+        if ctx.direct and _STEM_FUSED_BWD:
+            # pool / ReLU / BN / weight-gradient backward in one pass over the pooled gradient (dz stays on chip)
+            ops.stem_backward_fused(bn, _c(dout), am, y, st, cols, ctx.wpk, ops.grad_of(conv.weight))
+        elif ctx.direct:
             # pool/ReLU backward + BN reduction in one pass; the BN apply runs inside the weight gradient
             dz, coef = ops.stem_pool_bwd_bn(bn, _c(dout), am, y, st)
             ops.stem_conv_wgrad(dz, cols, ops.grad_of(conv.weight), ybn=y, coef=coef)

@@ -1065,6 +1065,22 @@ def stem_pool_bwd_bn(bn, dout, am, y, st):
     return dz, bn_backward_coef(bn, st, stats, C, grad_alpha(y))
 
 
+def stem_backward_fused(bn, dout, am, y, st, x, wpk, dst):
+    """The stem's MaxPool / ReLU / BN / conv weight-gradient backward in one pass (scd_stem_bwd_fused): the BN
+    backward sums (dgamma / dbeta accumulated, SyncBN all-reduce as bn_backward_coef) and dst (64,1,7,7) += the weight
+    gradient a*T1 + b*W G + c*s; the full-resolution dz is never materialised."""
+    N, Ho, Wo, C = y.shape
+    ns = L.lib().scd_stem_bwd_nsplit()
+    ws = torch.empty(ns * 2 * 64 * 64, dtype=torch.float32, device=y.device)
+    tg = torch.empty(2 * 64 * 64, dtype=torch.float32, device=y.device)
+    stats = bn_stats(bn, "bwd")
+    L.call("scd_stem_bwd_fused", dt(y), ptr(dout), ptr(am), ptr(y), ptr(st.scale), ptr(st.shift), ptr(st.mean),
+           ptr(st.invstd), ptr(x), ptr(stats), ptr(ws), ns, ptr(tg), N, x.shape[2], x.shape[3], Ho, Wo, stream())
+    alpha = grad_alpha(y)
+    coef = bn_backward_coef(bn, st, stats, C, alpha)
+    L.call("scd_stem_bwd_combine", dt(y), ptr(tg), ptr(wpk), ptr(coef), ptr(dst), 1, float(alpha), stream())
+
+
 def stem_pool_bwd(dout, am, y, st):
     N, H, W, C = y.shape
     dz = torch.empty_like(y)

@@ -336,6 +336,57 @@ def test_stem_fused_backward_matches_unfused():
     assert rel_err(dwb, dwa) < 2e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(2, 512, 512), (3, 260, 256)])
+def test_stem_one_pass_backward(shape, dtype):
+    """scd_stem_bwd_fused + combine (pool / ReLU / BN backward sums and the weight gradient as a T1 + b W G + c s,
+    dz never stored) against the same backward in float64 from the same 16-bit y, dz, x and weights: the weight
+    gradient within 2e-3 (the unfused kernels round dy to 16 bits: 2e-2), BN parameter gradients as the unfused
+    reduction's (fp32 summation order).  (3, 260, 256): an odd pooled height (the last block row has no pooled row
+    below it)."""
+    from scdhip import ops
+    N, H, W = shape
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(N, 1, H, W, generator=g).to(dtype).float().to(DEV)
+    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).to(dtype).float().to(DEV)
+    bns = [torch.nn.BatchNorm2d(64).to(DEV) for _ in range(2)]
+    with torch.no_grad():
+        bns[0].weight.uniform_(0.5, 1.5)
+        bns[0].bias.normal_()
+    for b in bns[1:]:
+        b.weight.data.copy_(bns[0].weight.data)
+        b.bias.data.copy_(bns[0].bias.data)
+    wpk = ops.pack_weight(w, dtype, 0, ldp=64)
+    stats = ops.new_stats(64, DEV)
+    y = ops.stem_conv_fwd(x, wpk, stats=stats)
+    st = ops.bn_finalize(bns[0], stats, 64, y.numel() // 64)
+    out, am = ops.stem_pool_fwd(y, st)
+    dout = torch.randn(out.shape, generator=g).to(DEV, dtype)
+    # unfused: dz (16-bit), BN backward sums, dy
+    dz = ops.stem_pool_bwd(dout, am, y, st)
+    dy = ops.bn_backward(bns[0], st, dz, y)
+    dwa = torch.zeros_like(w)
+    ops.stem_conv_wgrad(dy, x, dwa)
+    dwb = torch.full_like(w, 0.5)
+    ops.stem_backward_fused(bns[1], dout, am, y, st, x, wpk, dwb)
+    torch.cuda.synchronize()
+    for a, b in ((bns[0].weight.grad, bns[1].weight.grad), (bns[0].bias.grad, bns[1].bias.grad)):
+        assert rel_err(b, a) < 1e-5
+    # float64 backward from the same operands
+    zd = dz.double()
+    yd = y.double()
+    mu, iv = st.mean.double(), st.invstd.double()
+    xh = (yd - mu) * iv
+    cnt = zd.numel() // 64
+    k1 = zd.sum((0, 1, 2)) / cnt
+    k2 = (zd * xh).sum((0, 1, 2)) / cnt
+    dyd = (bns[0].weight.double() * iv) * (zd - k1 - xh * k2)
+    xr = x.double()
+    ref = torch.nn.grad.conv2d_weight(xr, (64, 1, 7, 7), dyd.permute(0, 3, 1, 2), stride=2, padding=3)
+    assert rel_err(dwb - 0.5, ref) < 2e-3
+    assert rel_err(dwa, ref) < 2e-2
+
+
 def test_cpool_fwd_bwd_fp32():
     from scdhip import ops
     g = torch.Generator().manual_seed(5)
