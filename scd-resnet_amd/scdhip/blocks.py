@@ -156,10 +156,10 @@ class BasicBlockFn(torch.autograd.Function):
         s = blk.stride
         N, H, W, Cin = x.shape
         C = blk.conv1.weight.shape[0]
+        dx = dyd = None
         if blk.downsample is not None:
             dy2, dyd = ops.bn_backward_pair(blk.bn2, st2, y2, blk.downsample[1], std, yd, dout, out)
             wd = blk.downsample[0].weight
-            dx = ops.conv_dgrad(dyd, ops.pack_weight(wd, x.dtype, 1), Cin, H, W, 1, 1, s, 0)
             ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
         else:
             dx = torch.empty_like(x)
@@ -170,7 +170,12 @@ class BasicBlockFn(torch.autograd.Function):
                                  blk.bn1, st1, y1)
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 3, 3, s, 1, ops.grad_of(w1), _conv_ld(w1))
-        ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 3, 3, s, 1, out=dx, accumulate=True)
+        dx = ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 3, 3, s, 1, out=dx,
+                            accumulate=dx is not None)
+        if dyd is not None:
+            # the downsample's input gradient last: += over the pixels its 1x1 taps reach only (one in four at stride 2)
+            ops.conv_dgrad(dyd, ops.pack_weight(blk.downsample[0].weight, x.dtype, 1), Cin, H, W, 1, 1, s, 0, out=dx,
+                           accumulate=True)
         grads_ready(blk)
         return dx, None, None
 
@@ -209,10 +214,10 @@ class BottleneckFn(torch.autograd.Function):
         s = blk.stride
         N, H, W, Cin = x.shape
         P = blk.conv1.weight.shape[0]
+        dx = dyd = None
         if blk.downsample is not None:
             dy3, dyd = ops.bn_backward_pair(blk.bn3, st3, y3, blk.downsample[1], std, yd, dout, out)
             wd = blk.downsample[0].weight
-            dx = ops.conv_dgrad(dyd, ops.pack_weight(wd, x.dtype, 1), Cin, H, W, 1, 1, s, 0)
             ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
         else:
             dx = torch.empty_like(x)
@@ -227,7 +232,11 @@ class BottleneckFn(torch.autograd.Function):
                                  blk.bn1, st1, y1)
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 1, 1, 1, 0, ops.grad_of(w1), _conv_ld(w1))
-        ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 1, 1, 1, 0, out=dx, accumulate=True)
+        dx = ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 1, 1, 1, 0, out=dx,
+                            accumulate=dx is not None)
+        if dyd is not None:
+            ops.conv_dgrad(dyd, ops.pack_weight(blk.downsample[0].weight, x.dtype, 1), Cin, H, W, 1, 1, s, 0, out=dx,
+                           accumulate=True)
         grads_ready(blk)
         return dx, None, None
 

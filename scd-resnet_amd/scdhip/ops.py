@@ -528,8 +528,13 @@ def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumula
     N = dy.shape[0]
     if out is None:
         out = torch.empty(N, Hc, Wc, Cin, dtype=dy.dtype, device=dy.device)
-    return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, _dgrad_phases(kh, kw, stride, pad, Hc, Wc),
-                 stats=stats, accumulate=accumulate, bn_bwd=bn_bwd)
+    phases = _dgrad_phases(kh, kw, stride, pad, Hc, Wc)
+    if accumulate:
+        # sub-pixel phases without taps (a 1x1 stride-2 conv reaches one pixel in four) would only add zeros
+        phases = [ph for ph in phases if ph.ntaps > 0]
+        if not phases:
+            return out
+    return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, phases, stats=stats, accumulate=accumulate, bn_bwd=bn_bwd)
 
 
 def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None):
