@@ -120,23 +120,29 @@ def sparse_heads_saved_gflop(model, S, ys):
     return saved / 1e9
 
 
-def pmc_traffic(kernel, batch, dtype):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/r<N>_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this same bench command), or None when none matches this workload."""
+def pmc_traffic(kernel, batch, dtype, model="centerOffsetRes10", S=512):
+    """HBM bytes per launch of `kernel` (a key of the summary, or a substring of one) from the newest committed
+    rocprofv3 PMC summary for this workload (profiles/r<N>_pmc_*.json, written by tools/pmc_summary.py from separate
+    FETCH_SIZE and WRITE_SIZE passes: of this same bench command for Res10, of tools/pmc_kernels.py -- the same kernel
+    on the same shape -- for the other BASELINE configs), or None when none matches."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")),
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_*.json")),
                    key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
-        if d.get("batch") == batch and d.get("dtype") == dtype and kernel in d.get("kernels", {}):
-            return d["kernels"][kernel]["hbm_bytes"], os.path.relpath(f, REPO)
+        if (d.get("batch") != batch or d.get("dtype") != dtype or d.get("model", "centerOffsetRes10") != model
+                or d.get("image_size", 512) != S):
+            continue
+        ks = d.get("kernels", {})
+        hit = kernel if kernel in ks else next((k for k in sorted(ks) if kernel in k), None)
+        if hit is not None:
+            return ks[hit]["hbm_bytes"], os.path.relpath(f, REPO)
     return None, None
 
 
-def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2), kept_px=None):
+def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2), kept_px=None, model="centerOffsetRes10"):
     """The dominant kernel: the fused head GEMM (conv3x3 M=B*(S/4)^2, N=3*128, K=9*256, + bias/ReLU
     + the three 1x1 tails in the epilogue), timed live by HIP events on its launch stream around
     every launch inside the timed steps (scdhip.ops.LaunchTimer).  kept_px: the size / offset heads' hidden
@@ -155,7 +161,10 @@ def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2), ke
     achieved = flops / (ms * 1e-3) / 1e12
     peak = PEAK_F32_TFLOPS if dtype_name == "fp32" else PEAK_BF16_TFLOPS      # dense fp16 = dense bf16 MFMA rate
     kernel = "conv_gemm_kernel<f32,128,128,heads>" if dtype_name == "fp32" else HEADS_KERNEL
-    traffic, src = pmc_traffic(kernel, B, dtype_name) if S == 512 else (None, None)
+    if S == 512:
+        traffic, src = pmc_traffic(kernel, B, dtype_name)
+    else:
+        traffic, src = pmc_traffic("heads384", B, dtype_name, model=model, S=S)
     return {"bound": "mfma", "kernel": kernel, "achieved": round(achieved, 1), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": None if traffic is None else round(traffic), "traffic_source": src,
@@ -221,9 +230,11 @@ def cornernet_rooflines(B, dtype_name, S=512, C=256, Cp=128):
         flops = 2.0 * M * C * 9 * C
         peak = PEAK_BF16_TFLOPS if dtype_name == "bf16" else PEAK_F32_TFLOPS
         achieved = flops / (ms * 1e-3) / 1e12
+        traffic, src = pmc_traffic("conv_gemm_pp_kernel<bf16,256,256>", B, dtype_name, model="cornerNetCPool", S=S)
         out["roofline"] = {"bound": "mfma", "kernel": "conv_gemm_pp_kernel<bf16,256,256> (CornerPool lastConv)"
                            if dtype_name == "bf16" else "conv_gemm_kernel<f32,128,128>", "achieved": round(achieved, 1),
-                           "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                           "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                           "traffic": None if traffic is None else round(traffic), "traffic_source": src,
                            "algorithmic_bytes": 2 * M * C * esz + 9 * C * C * esz, "flop_per_launch": flops,
                            "avg_launch_ms": round(ms, 4), "launches_timed": n}
     r = ops.LaunchTimer.mean_ms("cpool_fwd_add")
@@ -231,9 +242,11 @@ def cornernet_rooflines(B, dtype_name, S=512, C=256, Cp=128):
         ms, n = r
         nbytes = 3 * M * Cp * esz
         gbs = nbytes / (ms * 1e-3) / 1e9
+        traffic, src = pmc_traffic("cpool_fwd", B, dtype_name, model="cornerNetCPool", S=S)
         out["pool_roofline"] = {"bound": "hbm", "kernel": "cpool_fwd_kernel (with addend)", "achieved": round(gbs, 1),
                                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
-                                "traffic": None, "algorithmic_bytes": nbytes, "avg_launch_ms": round(ms, 4),
+                                "traffic": None if traffic is None else round(traffic), "traffic_source": src,
+                                "algorithmic_bytes": nbytes, "avg_launch_ms": round(ms, 4),
                                 "launches_timed": n}
     return out
 
@@ -400,7 +413,7 @@ def main():
                 Hh = S // 4
                 base = torch.arange(B, device=ys[3].device)[:, None] * (Hh * Hh)
                 kept = int(torch.unique(ys[3].long() + base).numel())
-            roof = heads_gemm_roofline(B, args.dtype, S, kept_px=kept)
+            roof = heads_gemm_roofline(B, args.dtype, S, kept_px=kept, model=args.model)
             if roof is not None:
                 roof["hidden_kept_px"] = kept
         elif args.model.startswith("cornerNet"):

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-kernel HBM bytes per launch.
 
 usage: python tools/pmc_summary.py <fetch counter_collection.csv> <write counter_collection.csv> out.json \
-       [batch dtype command]
+       [batch dtype command [model image_size]]
 
 Corrections (MI355X_MICROARCH.md, HBM section): rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
 (derived from TCC_EA0_RDREQ / _WRREQ); on gfx950 FETCH_SIZE counts half the bytes of a wide
@@ -37,6 +37,8 @@ def main():
         out.update({"batch": int(sys.argv[4]), "dtype": sys.argv[5]})
     if len(sys.argv) > 6:
         out["command"] = sys.argv[6]
+    if len(sys.argv) > 8:
+        out.update({"model": sys.argv[7], "image_size": int(sys.argv[8])})
     for k in sorted(set(fetch) | set(write)):
         nf, f = fetch.get(k, (0, 0.0))
         nw, w = write.get(k, (0, 0.0))

@@ -45,7 +45,14 @@ def short(name):
     m = re.search(r"conv_gemm_pp_kernel<(\d+), (true|false)>", n)
     if m:
         return "conv_gemm_pp_kernel<%s,256,%s%s>" % (half, m.group(1), ",heads" if m.group(2) == "true" else "")
+    m = re.search(r"conv_gemm_l1p_kernel<(\d+), (true|false), (true|false)>", n)
+    if m:
+        return "conv_gemm_l1p_kernel<%s,%s%s%s>" % (half, m.group(1), ",dgrad" if m.group(2) == "true" else "",
+                                                   ",bnbwd" if m.group(3) == "true" else "")
     m = re.match(r"(\w+?)ENS_\d+\w*Params", n)         # mangled, non-template kernels of the anonymous namespace
+    if m:
+        n = m.group(1)
+    m = re.match(r"(\w+?_kernel)E(P|i|S)", n)          # mangled kernels with plain pointer / int arguments
     if m:
         n = m.group(1)
     n = n.split("(")[0][:80]
