@@ -66,6 +66,13 @@ int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, const float*
  * relu_scale, relu_shift, ...) adds, without re-reading y (ping-pong bf16 GEMM; other shapes run the GEMM and
  * then scd_bn_bwd_reduce).  Replaces the cuDNN input-gradient + BatchNorm2d backward pair of
  * residuals.py:298-307 / centerNetOffset.py:106-110 followed by residuals.py:306. */
+/* Input gradient of a 3x3 / stride 2 / pad 1 Conv2d (replaces autograd's cuDNN backward-data of a stride-2 conv,
+ * residuals.py:99-103) as ONE forward GEMM: dy (N, Hq, Wq, Cg) gathered at the 2x2 taps (dq, dp) in {0,1}^2, against
+ * w3 = pack mode 3 of the (Cg, Cin, 3, 3) weight (4 Cin rows: the four sub-pixel phases, 4 Cg columns), the phases
+ * stored as pixels of dx (N, 2Hq, 2Wq, Cin) (+= when accumulate).  SCD_ERR_ARG when the ping-pong GEMM kernel does
+ * not take the shape (4 Cin not a multiple of 192 / 256, or fewer than 256 tiles): use scd_conv_gemm then. */
+int scd_conv_dgrad_s2(int dtype, const void* dy, const void* w3, void* dx, int N, int Hq, int Wq, int Cg, int Cin,
+                      int accumulate, void* stream);
 int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void* y, int N, int Hi, int Wi, int Ci, int Ho,
                         int Wo, int Co, int in_stride, int out_stride, int wrow, int nphase,
                         const scd_gemm_phase* phases, const void* bn_y, const float* mean, const float* invstd,
@@ -114,7 +121,9 @@ int scd_wgrad_reduce_rows(const float* ws, int nsplit, int Cg, int T, int Ci, in
 /* Pack an fp32 (A, B, T) weight (OIHW / IOHW flattening) into the GEMM operand layout:
  * mode 0: out[row_off + a][t*B + b] = w[a][b][t]; mode 1: out[row_off + b][t*A + a] = w[a][b][t];
  * rows are ldp elements long (zero padded).  mode 2 (tap-major transpose): out[t*B + b][row_off + a] = w[a][b][t],
- * T*B rows of ldp elements of which only [row_off, row_off + A) are written (one slice of a concatenation). */
+ * T*B rows of ldp elements of which only [row_off, row_off + A) are written (one slice of a concatenation).
+ * mode 3 (T = 9, ldp >= 4A): out[row_off + (2 rh + rw) B + b][(2 dq + dp) A + a] = w[a][b][rh + 1 - 2 dq][rw + 1 - 2 dp]
+ * (zero outside the kernel): the operand of scd_conv_dgrad_s2. */
 int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp,
                     int row_off, void* stream);
 
@@ -130,7 +139,9 @@ int scd_pad_channels(int dtype, const void* src, long rows, int C, int Cp, void*
  * mode 1: out[b][t*a_tot + a_off + a] = w[a][b][t] (a slice of a concatenated operand when a_tot > A),
  * transposed through LDS in tiles of 64 a x max(1, 64/T) b (T <= 64), one 4096-element unit per tile:
  * count = 4096 * ceil(A/64) * ceil(B / max(1, 64/T)); mode 2: out[t*B + b][a_off + a] = w[a][b][t] (ldp = a_tot),
- * count = A * B * T.  Every start (and total) is a multiple of 4096.
+ * count = A * B * T; mode 3 (T = 9, ldp = 4A): out[row_off + (2 rh + rw) B + b][(2 dq + dp) A + a] =
+ * w[a][b][rh + 1 - 2 dq][rw + 1 - 2 dp] (zero outside the 3x3 kernel; scd_conv_dgrad_s2's operand), count = 16 A B.
+ * Every start (and total) is a multiple of 4096.
  * Replaces one scd_pack_weight launch per conv and direction. */
 typedef struct scd_pack_desc {
     const float* w;

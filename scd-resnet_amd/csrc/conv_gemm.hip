@@ -59,6 +59,9 @@ struct GemmParams {
     // heads384 (scd_conv_gemm_heads_keep): hidden channels >= hid_cols stored only where hid_keep[pixel] != 0
     const unsigned char* hid_keep;
     int hid_cols;
+    // scd_conv_dgrad_s2 (ping-pong kernel): GEMM column c = phase * Co/4 + channel is stored at output pixel
+    // (2 oh + phase / 2, 2 ow + phase % 2) of a (2 Ho, 2 Wo, Co/4) tensor
+    int shuf;
 };
 
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
@@ -1207,6 +1210,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             const int qw = rem - qh * ph.Qw;
             const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
             T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+            if (p.shuf) {
+                const int c4 = p.Co >> 2, sp = col / c4;
+                dst = (T*)(p.y) + ((long)(n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 +
+                      (col - sp * c4);
+            }
             uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
             if (p.accumulate) {
                 float a[EPC], o[EPC];
@@ -2769,6 +2777,7 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.head_on = 0;
     p.bnbwd = 0; p.bny = nullptr; p.bn_mean = p.bn_invstd = p.bn_rsc = p.bn_rsh = nullptr;
     p.hid_keep = nullptr; p.hid_cols = 1 << 30;
+    p.shuf = 0;
     {
         static int dbg = -1;
         if (dbg < 0) { const char* e = getenv("SCD_GEMM_DEBUG"); dbg = e ? atoi(e) : 0; }
@@ -2808,6 +2817,25 @@ extern "C" int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void
     if (rc) return rc;
     return scd_bn_bwd_reduce(dtype, y, nullptr, bn_y, relu_scale, relu_shift, mean, invstd, Co, (long)N * Ho * Wo * Co,
                              bn_stats, stream);
+}
+
+extern "C" int scd_conv_dgrad_s2(int dtype, const void* dy, const void* w3, void* dx, int N, int Hq, int Wq, int Cg,
+                                 int Cin, int accumulate, void* stream) {
+    SCD_F16_FWD(scd_conv_dgrad_s2, dy, w3, dx, N, Hq, Wq, Cg, Cin, accumulate, stream);
+    // the input gradient of a 3x3 / stride 2 / pad 1 conv (dy: N x Hq x Wq x Cg -> dx: N x 2Hq x 2Wq x Cin) as a
+    // forward 2x2-tap GEMM over dy whose 4 Cin output columns are the four sub-pixel phases (operand: pack mode 3);
+    // only where the ping-pong kernel takes it (its epilogue stores the phases as pixels)
+    const int Co = 4 * Cin;
+    const long Mtot = (long)N * Hq * Wq;
+    const int bn = pp_bn(dtype, Co);
+    if (!bn || Cin % 8 || (long)cdiv(Mtot, 256) * (Co / bn) < 256) return SCD_ERR_ARG;
+    GemmParams p;
+    fill_params(p, dy, w3, dx, nullptr, nullptr, N, Hq, Wq, Cg, Hq, Wq, Co, 1, 1, 4 * Cg, 0, accumulate);
+    p.shuf = 1;
+    scd_gemm_phase ph;
+    ph.Qh = Hq; ph.Qw = Wq; ph.rho_h = 0; ph.rho_w = 0; ph.ntaps = 4;
+    for (int t = 0; t < 4; ++t) { ph.dh[t] = t >> 1; ph.dw[t] = t & 1; ph.wt[t] = t; }
+    return conv_gemm_launch(dtype, p, 1, &ph, stream);
 }
 
 extern "C" int scd_conv_gemm_heads(int dtype, const void* x, const void* w, void* hid, const float* bias, int N,

@@ -9,8 +9,25 @@ namespace {
 SCD_KERNEL_NS_BEGIN
 
 // ---------------------------------------------------------------- weight packing
+// mode 3 (a 3x3 stride-2 conv's input gradient as a 2x2-tap forward GEMM with the four output phases as channels,
+// scd_conv_dgrad_s2): out[(2 rh + rw) B + b][(2 dq + dp) A + a] = w[a][b][rh + 1 - 2 dq][rw + 1 - 2 dp], 0 where the
+// tap index leaves 0..2
+__device__ __forceinline__ float s2_phase_weight(const float* w, unsigned A, unsigned B, unsigned r, unsigned k) {
+    const unsigned ph = r / B, b = r - ph * B, t = k / A, a = k - t * A;
+    const int kr = (int)(ph >> 1) + 1 - 2 * (int)(t >> 1), ks = (int)(ph & 1) + 1 - 2 * (int)(t & 1);
+    return (kr >= 0 && kr < 3 && ks >= 0 && ks < 3) ? w[(a * B + b) * 9 + kr * 3 + ks] : 0.f;
+}
+
 template <typename T>
 __global__ void pack_weight_kernel(const float* w, T* out, int A, int B, int Tt, int mode, int ldp, int row_off) {
+    if (mode == 3) {
+        const unsigned total = 4u * B * ldp;
+        for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+            const unsigned r = i / (unsigned)ldp, k = i - r * (unsigned)ldp;
+            out[(long)(row_off + r) * ldp + k] = from_f<T>(k < 4u * A ? s2_phase_weight(w, A, B, r, k) : 0.f);
+        }
+        return;
+    }
     const int rows = mode == 0 ? A : mode == 1 ? B : Tt * B;
     const unsigned total = (unsigned)rows * ldp;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -76,6 +93,20 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
         return;
     }
     // 32-bit index math (a descriptor holds < 2^31 elements; 64-bit divides dominated this kernel)
+    if (q.mode == 3) {                // out[row_off + r][k], 4B x ldp elements (ldp = 4A)
+        const unsigned count3 = 4u * q.B * q.ldp, base3 = (unsigned)(e0 - q.start);
+#pragma unroll 4
+        for (int j = 0; j < PACK_UNIT / 256; ++j) {
+            const unsigned i = base3 + threadIdx.x + 256 * j;
+            if (i >= count3) break;
+            const unsigned r = i / (unsigned)q.ldp, k = i - r * (unsigned)q.ldp;
+            const float v = s2_phase_weight(q.w, q.A, q.B, r, k);
+            const unsigned o = (q.row_off + r) * (unsigned)q.ldp + k;
+            if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
+            else ((float*)q.out)[o] = v;
+        }
+        return;
+    }
     const unsigned count = q.mode == 0 ? (unsigned)q.A * q.ldp : (unsigned)q.B * q.T * q.A;   // mode 1 / 2: B x T x A
     const unsigned base = (unsigned)(e0 - q.start);
     const unsigned ldp = q.ldp, B = q.B, Tt = q.T, A = q.A, TA = Tt * A;
@@ -707,7 +738,8 @@ SCD_KERNEL_NS_END
 extern "C" int scd_pack_weight(int dtype, const float* w, void* out, int A, int B, int T, int mode, int ldp, int row_off,
                                void* stream) {
     SCD_F16_FWD(scd_pack_weight, w, out, A, B, T, mode, ldp, row_off, stream);
-    const long total = (long)(mode == 0 ? A : B) * ldp;
+    if (mode == 3 && (T != 9 || ldp < 4 * A)) return SCD_ERR_ARG;
+    const long total = (long)(mode == 0 ? A : mode == 3 ? 4 * B : B) * ldp;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((pack_weight_kernel<__bf16>), dim3(ew_blocks(total)), dim3(256), 0, st, w, (__bf16*)out, A, B,

@@ -49,6 +49,7 @@
 #define scd_stem_conv_wgrad_nsplit scd_stem_conv_wgrad_nsplit__f16
 #define scd_stem_conv_wgrad scd_stem_conv_wgrad__f16
 #define scd_stem_bwd_nsplit scd_stem_bwd_nsplit__f16
+#define scd_conv_dgrad_s2 scd_conv_dgrad_s2__f16
 #define scd_stem_bwd_fused scd_stem_bwd_fused__f16
 #define scd_stem_bwd_combine scd_stem_bwd_combine__f16
 #define scd_pad_channels scd_pad_channels__f16
@@ -100,6 +101,7 @@ SCD_F16_DECL(scd_heads_sparse_fixup)
 SCD_F16_DECL(scd_stem_conv_fwd)
 SCD_F16_DECL(scd_stem_conv_wgrad)
 SCD_F16_DECL(scd_stem_bwd_fused)
+SCD_F16_DECL(scd_conv_dgrad_s2)
 SCD_F16_DECL(scd_stem_bwd_combine)
 SCD_F16_DECL(scd_pad_channels)
 #define SCD_F16_FWD(fn, ...) \

@@ -170,8 +170,7 @@ class BasicBlockFn(torch.autograd.Function):
                                  blk.bn1, st1, y1)
         w1 = blk.conv1.weight
         ops.conv_wgrad(dy1, x, 3, 3, s, 1, ops.grad_of(w1), _conv_ld(w1))
-        dx = ops.conv_dgrad(dy1, ops.pack_weight(w1, x.dtype, 1), Cin, H, W, 3, 3, s, 1, out=dx,
-                            accumulate=dx is not None)
+        dx = ops.conv_dgrad_w(dy1, w1, H, W, s, 1, out=dx, accumulate=dx is not None)
         if dyd is not None:
             # the downsample's input gradient last: += over the pixels its 1x1 taps reach only (one in four at stride 2)
             ops.conv_dgrad(dyd, ops.pack_weight(blk.downsample[0].weight, x.dtype, 1), Cin, H, W, 1, 1, s, 0, out=dx,

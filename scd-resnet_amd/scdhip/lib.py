@@ -67,6 +67,7 @@ SIGNATURES = {
     "scd_stem_conv_wgrad_nsplit": (I, [L]),
     "scd_stem_conv_wgrad": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_bwd_nsplit": (I, []),
+    "scd_conv_dgrad_s2": (I, [I, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_bwd_fused": (I, [I, P, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P]),
     "scd_stem_bwd_combine": (I, [I, P, P, P, P, I, F, P]),
     "scd_stem_pool_bwd_bn": (I, [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),

@@ -343,6 +343,8 @@ class PackPlan:
                         descs.append(d)
                         if mode == 0:
                             start += (A * ldp + 4095) // 4096 * 4096      # whole workgroup units per descriptor
+                        elif mode == 3:
+                            start += (4 * B * ldp + 4095) // 4096 * 4096
                         elif mode == 2:
                             start += (A * B * T + 4095) // 4096 * 4096
                         else:
@@ -429,8 +431,11 @@ def pack_weight(w, dtype, mode, ldp=None, out=None, row_off=0, _cache=True):
         return res
     A, B = w.shape[0], w.shape[1]
     T = w.shape[2] * w.shape[3]
-    rows = A if mode == 0 else B
-    ldp = ldp or T * (B if mode == 0 else A)
+    if mode == 3:          # stride-2 3x3 input gradient as a 2x2-tap GEMM: (4 B) x (4 A), scd_conv_dgrad_s2
+        rows, ldp = 4 * B, ldp or 4 * A
+    else:
+        rows = A if mode == 0 else B
+        ldp = ldp or T * (B if mode == 0 else A)
     if out is None:
         out = torch.empty(rows, ldp, dtype=dtype, device=w.device)
     L.call("scd_pack_weight", _DT[dtype], ptr(w), ptr(out), A, B, T, mode, ldp, row_off, stream())
@@ -535,6 +540,30 @@ def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumula
         if not phases:
             return out
     return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, phases, stats=stats, accumulate=accumulate, bn_bwd=bn_bwd)
+
+
+class DgradS2:
+    enabled = os.environ.get("SCD_DGRAD_S2", "1") != "0"
+
+
+def conv_dgrad_w(dy, w, Hc, Wc, stride, pad, out=None, accumulate=False):
+    """Input gradient of Conv2d(w) from the fp32 weight: a 3x3 / stride 2 / pad 1 conv whose input is exactly twice
+    dy's size runs as one 2x2-tap GEMM with the sub-pixel phases as output channels (scd_conv_dgrad_s2: no
+    one-tap phases of nearly empty tiles) where the ping-pong kernel takes it; everything else as conv_dgrad."""
+    N, Hq, Wq, Cg = dy.shape
+    Cin, kh, kw = w.shape[1], w.shape[2], w.shape[3]
+    if (DgradS2.enabled and dy.dtype in HALF and kh == 3 and kw == 3 and stride == 2 and pad == 1 and Hc == 2 * Hq
+            and Wc == 2 * Wq):
+        if out is None:
+            out = torch.empty(N, Hc, Wc, Cin, dtype=dy.dtype, device=dy.device)
+        rc = L.lib().scd_conv_dgrad_s2(dt(dy), ptr(dy), ptr(pack_weight(w, dy.dtype, 3)), ptr(out), N, Hq, Wq, Cg, Cin,
+                                       int(accumulate), stream())
+        if rc == 0:
+            return out
+        if rc != 9001:
+            L.check(rc, "scd_conv_dgrad_s2")
+    return conv_dgrad(dy, pack_weight(w, dy.dtype, 1), Cin, Hc, Wc, kh, kw, stride, pad, out=out,
+                      accumulate=accumulate)
 
 
 def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None):

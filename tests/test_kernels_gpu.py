@@ -663,6 +663,37 @@ def test_conv_l1p_matches_register_staged(N, H, W, dtype, monkeypatch):
     assert rel_err(nchw(outs["1"][0]), ref) < 1e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,Hq,Cg,Cin,taken", [(32, 64, 128, 64, True), (32, 32, 256, 128, True),
+                                               (4, 16, 512, 256, False), (3, 17, 128, 64, False)])
+def test_conv_dgrad_s2_phase_gemm(N, Hq, Cg, Cin, taken, dtype):
+    """Input gradient of a 3x3 / stride 2 / pad 1 conv as one 2x2-tap GEMM with the four sub-pixel phases as output
+    channels (scd_conv_dgrad_s2, pack mode 3) against torch fp32 and the phase-decomposed gather-GEMM; `taken`:
+    whether the shape goes to the ping-pong kernel (otherwise ops.conv_dgrad_w falls back), plus += accumulation."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(23)
+    dy = torch.randn(N, Cg, Hq, Hq, generator=g).to(dtype).float()
+    w = (torch.randn(Cg, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5).to(dtype).float()
+    base = torch.randn(N, Cin, 2 * Hq, 2 * Hq, generator=g).to(dtype).float()
+    x = torch.zeros(N, Cin, 2 * Hq, 2 * Hq, requires_grad=True)
+    F.conv2d(x, w, stride=2, padding=1).backward(dy)
+    dyd = nhwc(dy, dtype)
+    out = torch.empty(N, 2 * Hq, 2 * Hq, Cin, dtype=dtype, device=DEV)
+    rc = ops.L.lib().scd_conv_dgrad_s2(ops.dt(dyd), ops.ptr(dyd), ops.ptr(ops.pack_weight(w.to(DEV), dtype, 3)),
+                                       ops.ptr(out), N, Hq, Hq, Cg, Cin, 0, ops.stream())
+    assert (rc == 0) == taken and rc in (0, 9001)
+    dx = ops.conv_dgrad_w(dyd, w.to(DEV), 2 * Hq, 2 * Hq, 2, 1)
+    ref_gather = ops.conv_dgrad(dyd, ops.pack_weight(w.to(DEV), dtype, 1), Cin, 2 * Hq, 2 * Hq, 3, 3, 2, 1)
+    acc = nhwc(base, dtype)
+    ops.conv_dgrad_w(dyd, w.to(DEV), 2 * Hq, 2 * Hq, 2, 1, out=acc, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(dx), x.grad) < TOL[dtype]
+    assert rel_err(nchw(dx), nchw(ref_gather)) < TOL[dtype]
+    if taken:
+        assert torch.equal(dx, out)
+    assert rel_err(nchw(acc), base + x.grad) < TOL[dtype]
+
+
 def test_conv_layer1_accumulate_and_bias_relu():
     """Epilogue paths the block code uses on the layer1 shapes: dgrad += into an existing gradient, and a
     forward with bias + ReLU."""
