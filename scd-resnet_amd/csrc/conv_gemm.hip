@@ -2898,8 +2898,14 @@ static bool wgrad_use_l1(int dtype, long M, int Ho, int Wo, int Cg, int T, int C
            (long)Ho * Wo * 64 <= (1L << 30) && M >= 64;
 }
 
-// one workgroup per CU over >= 16 stages each
-static int wgrad_l1_nsplit(long M) { return (int)std::max(1L, std::min(256L, M / 64 / 16)); }
+// >= 16 stages per workgroup, at most 128 workgroups (SCD_WGRAD_L1_NSPLIT): in the step this kernel shares the chip
+// with the compute stream's last layer1 / stem kernels, and half the splits halve its 64 x 576 fp32 slab reduce
+// (measured +1% per step against 256)
+static int wgrad_l1_nsplit(long M) {
+    static long cap = -2;
+    if (cap == -2) { const char* e = getenv("SCD_WGRAD_L1_NSPLIT"); cap = e ? atol(e) : 128; }
+    return (int)std::max(1L, std::min(cap, M / 64 / 16));
+}
 
 // channel window of the ping-pong weight gradient: 256 (NQ 4) or, for widths that are multiples of 192 only, 192
 static int wgrad_pp2_win(int Cg) {
@@ -2910,8 +2916,10 @@ static int wgrad_pp2_win(int Cg) {
 
 // split count from a wave-quantisation cost model (SCD_WGRAD_NSMODEL=0: the fixed rules below it).  A launch of
 // tiles x ns workgroups runs in ceil(tiles*ns / slots) rounds; a round costs its K stages (stage_us each) plus the
-// workgroup's fp32 slab store (epi_us), and every split adds one slab to the reduce (read at ~3.5 TB/s).  Candidates
-// are whole XCD groups (multiples of 8) within the pixel and slab-memory caps.
+// workgroup's fp32 slab store (epi_us), and every split adds one slab to the reduce, priced at 0.8 TB/s
+// (SCD_WGRAD_SLAB_TBPS): the reduce reads ~3.5 TB/s alone but a fraction of that inside the step, beside the compute
+// stream's BN passes; pricing it at 3.5 measured 1% slower per step.  Candidates are whole XCD groups (multiples of
+// 8) within the pixel and slab-memory caps.
 static bool wgrad_nsmodel() {
     static int mode = -2;
     if (mode == -2) { const char* e = getenv("SCD_WGRAD_NSMODEL"); mode = e ? atoi(e) : 1; }
@@ -2920,13 +2928,15 @@ static bool wgrad_nsmodel() {
 
 static long wgrad_ns_model(long M, long tiles, int slots, int kp, double stage_us, double epi_us, double slab_bytes,
                            long ns_max, bool any_ns = false) {
+    static double slab_rate = -1.0;          // bytes/us at which the reduce reads the slabs (SCD_WGRAD_SLAB_TBPS)
+    if (slab_rate < 0) { const char* e = getenv("SCD_WGRAD_SLAB_TBPS"); slab_rate = (e ? atof(e) : 0.8) * 1e6; }
     long best = 8;
     double bt = 1e30;
     const long step = any_ns ? 1 : 8;
     for (long ns = step; ns <= std::max(8L, ns_max); ns += step) {
         const long stages = cdiv(cdiv(M, ns), (long)kp);
         const long rounds = cdiv(tiles * ns, (long)slots);
-        const double t = rounds * (stages * stage_us + epi_us) + ns * slab_bytes / 3.5e6;
+        const double t = rounds * (stages * stage_us + epi_us) + ns * slab_bytes / slab_rate;
         if (t < bt * 0.995) { bt = t; best = ns; }
     }
     return best;

@@ -63,9 +63,10 @@ class FlatParams:
 
     def rebind_grads(self):
         """Re-attach .grad views if something set them to None (e.g. Module.zero_grad())."""
+        gbase = self.grad.data_ptr()
         for p, (o, n) in zip(self.params, self.offsets):
             g = p.grad
-            if g is None or g.data_ptr() != self.grad[o:o + n].data_ptr():
+            if g is None or g.data_ptr() != gbase + 4 * o:
                 if g is not None:
                     self.grad[o:o + n].copy_(g.reshape(-1))
                 else:
@@ -73,7 +74,8 @@ class FlatParams:
                 p.grad = self.grad[o:o + n].view_as(p)
 
     def valid(self):
-        return all(p.data_ptr() == self.data[o:o + n].data_ptr() for p, (o, n) in zip(self.params, self.offsets))
+        base = self.data.data_ptr()
+        return all(p.data_ptr() == base + 4 * o for p, (o, _) in zip(self.params, self.offsets))
 
 
 def ensure_flat(params):

@@ -57,8 +57,14 @@ def dt(t):
         raise RuntimeError("libscdhip: unsupported dtype %s" % t.dtype)
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_device = torch._C._cuda_getDevice
+
+
 def stream():
-    return torch.cuda.current_stream().cuda_stream
+    """torch's current HIP stream on the current device, as a raw handle (the same value as
+    torch.cuda.current_stream().cuda_stream, without building a Stream object: ~10 us less per launch)."""
+    return _raw_stream(_cur_device())
 
 
 def ptr(t):

@@ -825,3 +825,15 @@ def test_bn_backward_pair_matches_two_passes(dtype, C):
         assert (d <= ulp * x.abs().clamp_min(1e-3) + 1e-6).all(), d.max().item()
         if dtype != torch.float32:      # fp32 shows every last-bit coefficient difference; 16-bit rounding hides most
             assert (d > 0).float().mean().item() < 1e-3
+
+
+@pytest.mark.gpu
+def test_raw_stream_handle_follows_torch_current_stream():
+    """ops.stream() (the raw-handle fast path every launch uses) names torch's current stream, inside and outside a
+    stream context."""
+    from scdhip import ops
+    assert ops.stream() == torch.cuda.current_stream().cuda_stream
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        assert ops.stream() == s.cuda_stream == torch.cuda.current_stream().cuda_stream
+    assert ops.stream() == torch.cuda.current_stream().cuda_stream

@@ -1,6 +1,6 @@
 """cProfile of the host side of the Res10 B=32 bf16 training step (what issuing one step costs in Python / ctypes).
 
-python tools/host_profile.py [--steps 20] [--top 40]
+python tools/host_profile.py [--steps 20] [--top 40] [--engine-thread]
 """
 import argparse
 import cProfile
@@ -19,8 +19,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--engine-thread", action="store_true",
+                    help="leave the backward on the autograd engine's device thread (cProfile then sees it as one "
+                         "opaque run_backward call)")
     a = ap.parse_args()
     import importlib
+    if not a.engine_thread:
+        # run the backward's Python Functions on this thread so cProfile attributes their time
+        torch.autograd.set_multithreading_enabled(False)
 
     from scdhip.flat import FlatAdam
     from trainer.dataset.syntheticSCD import SCD
