@@ -1068,7 +1068,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         __builtin_amdgcn_sched_barrier(0);
     };
     // ablations (SCD_GEMM_DEBUG): 3 = no DMA instructions in the loop, 4 = no fragment reads in the loop,
-    // 5 = no barriers in the loop (timing only; 3-5 give wrong results)
+    // 5 = no barriers in the loop, 60 = no output stores, 61 = no epilogue (timing only; 3-5, 60, 61 give wrong
+    // results; tools/pp_probe.py)
     constexpr int dbg = SCD_ABLATE;
     auto bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
@@ -1127,6 +1128,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (dbg == 61) {                 // ablation 61: no epilogue (the accumulators kept live by a test)
+        float s = 0.f;
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+        if (s == 1234.5f) ((float*)p.y)[tid] = s;
+        return;
+    }
 
     // ---- epilogue: bias / relu in registers, BN partial sums, stage the wave's 128 x WCOLS tile, coalesced stores
     char* ep = smem + wave * 128 * EROW;
@@ -1224,7 +1234,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                 for (int e = 0; e < EPC; ++e) a[e] += o[e];
                 Vec16<T>::store(&v, a);
             }
-            *(uint4*)dst = v;
+            if constexpr (dbg == 60) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));   // ablation 60: no stores
+            else *(uint4*)dst = v;
         }
     }
     if (p.stats) {
