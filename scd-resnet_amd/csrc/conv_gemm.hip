@@ -2202,11 +2202,14 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
 // (part of one output row) stages the input once as a halo of 3 rows x 66 columns (2.6x fewer bytes than the nine
 // shifted copies) plus the 64 x 128 B output gradient, both by LDS-DMA.  The nine taps read the halo at shifted rows
 // with ds_read_b64_tr_b16 (A operand = input columns, B = output-gradient channels, 16x16x32 bf16 MFMA).
-// 8 waves: wave w owns the 16-channel input slice u = w & 3 of every tap (9 column blocks) and the output-gradient
-// channel blocks 2(w >> 2), 2(w >> 2) + 1: 18 accumulators.  Each halo row region is 80 rows apart (bits 0-3 of a
-// row index do not change with the input row), so a wave's 72 fragment reads per stage come from 8 address
-// registers plus immediate offsets (no per-read address VALU).  Stage t+1 is fetched into the other buffer while
-// stage t is computed; one barrier per stage.
+// 8 waves: wave w owns the 16-channel input slice u = w & 3 of every tap (9 column blocks) and all four
+// output-gradient channel blocks (36 accumulators), over k-step w >> 2 of each 64-pixel stage: 13 fragment pairs
+// per 36 MFMAs (the earlier split -- two output-gradient blocks, both k-steps -- read 22 pairs per 36 MFMAs, and the
+// fragment reads, not the MFMAs, bounded it: ablation build 42 ran 83.5 of its 99 us).  The two waves of an input
+// slice sum their accumulators through LDS at the end.  Each halo row region is 80 rows apart (bits 0-3 of a row
+// index do not change with the input row), so the fragment reads come from a few address registers plus immediate
+// offsets (no per-read address VALU).  Stage t+1 is fetched into the other buffer while stage t is computed; one
+// barrier per stage.
 constexpr int L1W_KP = 64;                           // pixels per stage
 constexpr int L1W_HC = L1W_KP + 2;                   // halo columns
 constexpr int L1W_REG = 80;                          // LDS rows per halo row region (66 used)
@@ -2227,7 +2230,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
     __shared__ __attribute__((aligned(16))) char smem[L1W_NBUF * L1W_STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int u = wave & 3, ch = wave >> 2;
+    const int u = wave & 3, ks = wave >> 2;         // input slice, k-step of each stage
     const int z = blockIdx.x;
     const int M = p.N * p.Ho * p.Wo;
     const int pix0 = min(M, z * p.chunk), pix1 = min(M, pix0 + p.chunk);
@@ -2299,23 +2302,23 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
         return __builtin_bit_cast(bf16x8, v);
     };
     // per-lane byte offsets: halo (tap column dw, lo/hi rows) and output gradient (block a; hi = lo + 4 rows)
-    int xo[3][2], go[2];
+    int xo[3][2], go[4];
 #pragma unroll
     for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
         for (int h = 0; h < 2; ++h) xo[dw][h] = l1w_addr(r0 + dw + 4 * h, u, pp);
 #pragma unroll
-    for (int a = 0; a < 2; ++a) go[a] = L1W_HBYTES + l1w_addr(r0, 2 * ch + a, pp);
-    f32x4 acc[2][9];
+    for (int a = 0; a < 4; ++a) go[a] = L1W_HBYTES + l1w_addr(r0, a, pp);
+    f32x4 acc[4][9];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[a][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    bf16x8 gf[2], xf[9];
+    bf16x8 gf[4], xf[9];
     auto reads = [&](const char* cur, int s2) {
 #pragma unroll
-        for (int a = 0; a < 2; ++a) gf[a] = trf(cur + go[a] + 4096 * s2, cur + go[a] + 4096 * s2 + 512);
+        for (int a = 0; a < 4; ++a) gf[a] = trf(cur + go[a] + 4096 * s2, cur + go[a] + 4096 * s2 + 512);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int off = (t / 3) * L1W_REG * 128 + 4096 * s2;
@@ -2326,7 +2329,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
 #pragma unroll
         for (int t = 0; t < 9; ++t)
 #pragma unroll
-            for (int a = 0; a < 2; ++a) {
+            for (int a = 0; a < 4; ++a) {
                 if constexpr (SCD_ABLATE == 42) {          // ablation: fragment reads kept, no MFMA
                     asm volatile("" ::"v"(xf[t]), "v"(gf[a]));
                 } else {
@@ -2344,18 +2347,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
     // whole stage -- past the end of the range with out-of-range offsets (zeros into a buffer nobody reads again, no
     // traffic) -- so the counts are uniform: this wave's DMAs per stage are n = its halo instructions (4 for waves
     // 0-2, 3 for the rest) + 1, and vmcnt((NBUF - 2) n) retires stage t+1 only.
-    // Two wave groups one barrier apart (waves 4-7 trail): each k-step is a read phase (22 transposed reads, drained
-    // before its barrier) and an MFMA phase, and on every SIMD one group's MFMAs run beside the other's reads.  The
-    // DMA of stage t+3 goes into stage t-1's buffer, whose last reads (both groups' second k-step) were drained before
-    // earlier barriers; stage t+1 is retired before the barrier that opens the leading group's stage t+1 -- by that
-    // group after its last MFMA phase of stage t, by the trailing group after its last read phase (the same barrier
-    // instance for it).  Measured slower than one barrier per stage with every wave reading then computing (60 vs
-    // 57 us for the Res10 B=32 layer1 gradient), so the stagger is ablation build 46 only.
     const int nk = (pix1 - pix0 + L1W_KP - 1) / L1W_KP;
     if (nk > 0) {
         const bool five = wave < L1W_NHDMA - 24;
-        constexpr bool STAGGER = SCD_ABLATE == 46;          // ablation build 46: the two-group stagger
-        const bool lead = !STAGGER || ch == 0;
         // retire stage t+1, leave stages t+2 .. t+NBUF-1 in flight
         auto wait_next = [&]() {
             if constexpr (SCD_ABLATE != 41) {
@@ -2385,7 +2379,6 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
-        if (!lead) bar();
         int b0 = 0;                                   // buffer of stage t
         for (int t = 0; t < nk; ++t) {
             const int b3 = b0 == 0 ? L1W_NBUF - 1 : b0 - 1;   // buffer of stage t+NBUF-1 (= that of stage t-1)
@@ -2394,42 +2387,45 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
                 issue(pix0 + (t + L1W_NBUF - 1) * L1W_KP, smem + b3 * L1W_STAGE);
                 advance();
             }
-            if constexpr (!STAGGER) {
-                reads(cur, 0);
-                mfmas();
-                reads(cur, 1);
-                mfmas();
-                wait_next();
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                bar();
-            } else {
-                reads(cur, 0);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                bar();
-                __builtin_amdgcn_s_setprio(1);
-                mfmas();
-                __builtin_amdgcn_s_setprio(0);
-                bar();
-                reads(cur, 1);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (!lead) wait_next();
-                bar();
-                __builtin_amdgcn_s_setprio(1);
-                mfmas();
-                __builtin_amdgcn_s_setprio(0);
-                if (lead) wait_next();
-                bar();
-            }
+            reads(cur, ks);
+            mfmas();
+            wait_next();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            bar();
             b0 = b0 == L1W_NBUF - 1 ? 0 : b0 + 1;
         }
-        if (lead && STAGGER) bar();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    // fp32 slab: lane holds columns kk .. kk+3 (kk = 64 t + 16 u + 4 lg) of channel 16 (2ch + a) + l16
+    // the k-step 1 waves hand their sums to the k-step 0 waves of the same input slice through LDS (the stage buffers,
+    // two slices per round: 2 x 36 x 64 x 16 B = 72 KiB), which then write the fp32 slab: lane holds columns
+    // kk .. kk+3 (kk = 64 t + 16 u + 4 lg) of channel 16 a + l16
+    __syncthreads();
+    static_assert(2 * 36 * 64 * 16 <= L1W_NBUF * L1W_STAGE, "reduction buffer");
+    f32x4* xch = (f32x4*)smem;
+#pragma unroll
+    for (int round = 0; round < 2; ++round) {
+        const bool mine = (u >> 1) == round;
+        f32x4* slot = xch + (u & 1) * 36 * 64;
+        if (mine && ks == 1) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) slot[(a * 9 + t) * 64 + lane] = acc[a][t];
+        }
+        __syncthreads();
+        if (mine && ks == 0) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[a][t] += slot[(a * 9 + t) * 64 + lane];
+        }
+        __syncthreads();
+    }
+    if (ks != 0) return;
     float* ws = p.ws + (long)z * 64 * 576;
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const int co = 16 * (2 * ch + a) + l16;
+    for (int a = 0; a < 4; ++a) {
+        const int co = 16 * a + l16;
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             *(f32x4*)(ws + (long)co * 576 + 64 * t + 16 * u + 4 * lg) = acc[a][t];
