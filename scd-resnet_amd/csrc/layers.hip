@@ -230,24 +230,32 @@ __global__ void stem_pool_fwd_kernel(const T* y, const float* scale, const float
             best[e] = -INFINITY; arg[e] = 0;
             sc[e] = scale[ch * E + e]; sh[e] = shift[ch * E + e];
         }
-        for (int di = 0; di < 3; ++di) {
-            const int h = 2 * oh - 1 + di;
-            if ((unsigned)h >= (unsigned)H) continue;
-            for (int dj = 0; dj < 3; ++dj) {
-                const int w = 2 * ow - 1 + dj;
-                if ((unsigned)w >= (unsigned)W) continue;
-                float v[E];
-                Vec16<T>::load(y + (((long)n * H + h) * W + w) * C + ch * E, v);
+        // the 9 window loads from clamped addresses (all in flight at once; taps outside the image never win),
+        // compared in window order as before
+        float v[9][E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const float z = fmaxf(v[e] * sc[e] + sh[e], 0.f);
-                    if (z > best[e]) { best[e] = z; arg[e] = di * 3 + dj; }
-                }
+        for (int d = 0; d < 9; ++d) {
+            const int h = min(max(2 * oh - 1 + d / 3, 0), H - 1), w = min(max(2 * ow - 1 + d % 3, 0), W - 1);
+            Vec16<T>::load(y + (((long)n * H + h) * W + w) * C + ch * E, v[d]);
+        }
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const bool in = (unsigned)(2 * oh - 1 + d / 3) < (unsigned)H && (unsigned)(2 * ow - 1 + d % 3) < (unsigned)W;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float z = in ? fmaxf(v[d][e] * sc[e] + sh[e], 0.f) : -INFINITY;
+                if (z > best[e]) { best[e] = z; arg[e] = d; }
             }
         }
         Vec16<T>::store(out + pix * C + ch * E, best);
+        // the E argmax bytes of this chunk in one store
+        unsigned lo = 0, hi = 0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) argmax[pix * C + ch * E + e] = (uint8_t)arg[e];
+        for (int e = 0; e < E && e < 4; ++e) lo |= (unsigned)arg[e] << (8 * e);
+#pragma unroll
+        for (int e = 4; e < E; ++e) hi |= (unsigned)arg[e] << (8 * (e - 4));
+        if constexpr (E == 8) *(uint2*)(argmax + pix * C + ch * E) = make_uint2(lo, hi);
+        else *(unsigned*)(argmax + pix * C + ch * E) = lo;
     }
 }
 
