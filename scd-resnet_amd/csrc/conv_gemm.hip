@@ -231,9 +231,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float s = csum[b][r], q = csq[b][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                const float s = row16_sum(csum[b][r]), q = row16_sum(csq[b][r]);   // DPP, no LDS permutes
                 if (l16 == 0) {
                     const int c = wn * 64 + b * 16 + lg * 4 + r;
                     red[(wm * BN + c) * 2 + 0] = s;

@@ -17,6 +17,16 @@ constexpr int KS = 7, KK = 49, SP = 2, PD = 3, CO = 64;
 
 __device__ __forceinline__ int swz128(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
+// sum over the 16 lanes of a DPP row (quad butterflies, then the half-row and row mirrors): VALU only, where
+// __shfl_xor costs an LDS permute per step
+__device__ __forceinline__ float stem_row16_sum(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
+    return v;
+}
+
 // ---- forward: one workgroup = 2 output rows x 128 output columns (256 pixels) of one image
 constexpr int FTW = 128, FTH = 2;
 constexpr int PROWS = SP * (FTH - 1) + KS;          // 9 input rows
@@ -46,12 +56,26 @@ __global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const float* __restr
         const int r = i >> 3, c = i & 7;
         *(uint4*)(Bs + swz128(r, c)) = *(const uint4*)(wpk + r * 64 + c * 8);
     }
-    // input patch (zero outside the image)
+    // input patch (zero outside the image): a fixed number of loads per thread from clamped addresses, all in flight
+    // at once (a bounds branch around each load made the compiler wait for every one before the next)
     const float* xn = x + (size_t)n * H * W;
-    for (int i = tid; i < PROWS * PCOLS; i += 256) {
+    constexpr int PN = (PROWS * PCOLS + 255) / 256;
+    float pv[PN];
+#pragma unroll
+    for (int j = 0; j < PN; ++j) {
+        const int i = min(tid + 256 * j, PROWS * PCOLS - 1);
         const int r = i / PCOLS, c = i - (i / PCOLS) * PCOLS;
-        const int ih = ih0 + r, iw = iw0 + c;
-        patch[i] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? xn[(size_t)ih * W + iw] : 0.f;
+        const int ih = min(max(ih0 + r, 0), H - 1), iw = min(max(iw0 + c, 0), W - 1);
+        pv[j] = xn[(size_t)ih * W + iw];
+    }
+#pragma unroll
+    for (int j = 0; j < PN; ++j) {
+        const int i = tid + 256 * j;
+        if (i < PROWS * PCOLS) {
+            const int r = i / PCOLS, c = i - (i / PCOLS) * PCOLS;
+            const int ih = ih0 + r, iw = iw0 + c;
+            patch[i] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? pv[j] : 0.f;
+        }
     }
     __syncthreads();
     // im2col tile: thread -> pixel p = tid, all 64 taps (8 chunks of 8)
@@ -134,9 +158,7 @@ __global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const float* __restr
         for (int b = 0; b < 4; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float s = csum[b][r], q = csq[b][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                const float s = stem_row16_sum(csum[b][r]), q = stem_row16_sum(csq[b][r]);
                 if (l16 == 0) {
                     const int c = b * 16 + lg * 4 + r;
                     red[(wave * CO + c) * 2] = s;
@@ -340,7 +362,8 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                 const bool ok = (oi == 0 || okh) && (oj == 0 || okw);
                 const long o = (((long)n * Hp + bo + (ok ? oi : 0)) * Wp + bc + (ok ? oj : 0)) * CO + ch * 8;
                 rd[oi][oj] = *(const uint4*)(dout + o);
-                ra[oi][oj] = ok ? *(const uint2*)(argmax + o) : make_uint2(0xffffffffu, 0xffffffffu);
+                const uint2 av = *(const uint2*)(argmax + o);        // o is in range either way: no branch
+                ra[oi][oj] = ok ? av : make_uint2(0xffffffffu, 0xffffffffu);
             }
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -352,9 +375,13 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
 #pragma unroll
         for (int q = 0; q < (BPROWS * WPCOLS + 255) / 256; ++q) {
             const int i = tid + 256 * q;
-            const int r = i / WPCOLS, c = i - (i / WPCOLS) * WPCOLS;
+            const int ic = min(i, BPROWS * WPCOLS - 1);
+            const int r = ic / WPCOLS, c = ic - (ic / WPCOLS) * WPCOLS;
             const int ih = ih0 + r, iw = iw0 + c;
-            rp[q] = (i < BPROWS * WPCOLS && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? xn[(size_t)ih * W + iw] : 0.f;
+            // unconditional load from a clamped address, then the select (a load under the bounds test would be a
+            // branch, and the compiler then waits for it before the next one)
+            const float v = xn[(size_t)min(max(ih, 0), H - 1) * W + min(max(iw, 0), W - 1)];
+            rp[q] = (i < BPROWS * WPCOLS && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? v : 0.f;
         }
     };
     if (t0 < t1) load_tile(t0);
