@@ -136,9 +136,14 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
             const unsigned r = i / ldp, k = i - r * ldp;
             const unsigned t = k / B, b = k - t * B;
             bf8 v;
-            const float* src = q.w + (r * B + b) * Tt + t;
+            // unconditional loads (the padding columns t >= T read tap T-1 and are zeroed): a load under the test
+            // would be a branch the compiler waits on
+            const float* src = q.w + (r * B + b) * Tt + min(t, Tt - 1);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = (__bf16)(t < Tt ? src[e * Tt] : 0.f);
+            for (int e = 0; e < 8; ++e) {
+                const float x = src[e * Tt];
+                v[e] = (__bf16)(t < Tt ? x : 0.f);
+            }
             *(bf8*)((__bf16*)q.out + (q.row_off + r) * ldp + k) = v;
         }
         return;
