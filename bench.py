@@ -299,7 +299,7 @@ def main():
     opt = FlatAdam(filter(lambda p: p.requires_grad, model.parameters()))
     if world > 1:
         if torch.cuda.device_count() > 1 or share:
-            ops.set_bn_sync(ops.new_bn_group())   # SyncBN rule of networkFactory.py:128, its own communicator
+            ops.set_bn_sync(ops.syncbn_group())   # SyncBN rule of networkFactory.py:128 (WORLD unless opted out)
         model = FlatDDP(model)
     lossfn = plugin.loss
 
@@ -452,13 +452,15 @@ def main():
         if local_ms is not None:
             # in-run split of the N-rank step: the same per-rank work without any collective (not the driver's
             # cross-run scaling efficiency, which it computes from the per-N values itself)
+            # (the exchange's overhead inside one N-rank run; 1 -> N scaling efficiency is the driver's, from its own
+            # per-N runs, and is not reported here)
+            shared = ops.bn_sync_shares_group(model.group)
             line["exchange"] = {"ddp_ms_per_step": line["ms_per_step"], "local_ms_per_step": round(local_ms, 3),
                                 "local_over_ddp": round(local_ms / line["ms_per_step"], 4),
-                                "syncbn_group": "own communicator (ops.new_bn_group)"}
-            # in-run weak-scaling efficiency: the same per-rank work without any collective over the DDP step (the
-            # driver's own figure comes from its per-N runs)
-            line["weak_scaling_eff"] = round(local_ms / line["ms_per_step"], 4)
-            line["weak_scaling_eff_basis"] = "local_ms_per_step / ddp_ms_per_step, same run"
+                                "syncbn": "peer memory" if ops.bn_sync_peer() is not None else
+                                ("WORLD (shared with the buckets)" if shared else "own communicator")
+                                if ops.bn_sync_group() is not None else "off",
+                                "buckets_overlap_backward": bool(model.overlap_buckets())}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_baseline_steps)
         print(json.dumps(line), flush=True)

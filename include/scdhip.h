@@ -387,9 +387,10 @@ int scd_adam_step(float* p, const float* g, float* m, float* v, long n, float lr
 int scd_adam_step_dev(float* p, const float* g, float* m, float* v, long n, double* hyper, float beta1, float beta2,
                       float eps, float gscale, void* stream);
 /* ---- SGD (torch.optim.SGD, networkFactory.py:84-89: momentum 0.9, weight_decay 1e-4) over a flat fp32 buffer ----
- * hyper = {lr, step} as for scd_adam_step_dev (step advanced on the stream; the momentum buffer `buf` is
- * initialised to the first step's d = g*gscale + weight_decay*p, as torch clones it).  buf may be NULL when
- * momentum == 0. */
+ * hyper = {lr, step, initialised, scratch} (fp64, 4 values): step advanced on the stream as for scd_adam_step_dev;
+ * the momentum buffer `buf` is initialised to this step's d = g*gscale + weight_decay*p (as torch clones it when the
+ * parameter has no momentum_buffer yet) when hyper[2] == 0, and hyper[2] is set to 1 -- a per-buffer flag, so a
+ * buffer rebuilt or reset mid-training starts like torch's, whatever the step.  buf may be NULL when momentum == 0. */
 int scd_sgd_step_dev(float* p, const float* g, float* buf, long n, double* hyper, float momentum, float dampening,
                      float weight_decay, int nesterov, float gscale, void* stream);
 

@@ -105,12 +105,22 @@ __device__ __forceinline__ void load_params(const float* p, float* v) {
 // Per-channel parameters of the backward kernels live in LDS and are re-read per vector instead of held in
 // registers (5-6 x E floats per thread otherwise): with <= 80 VGPRs (BN_EW_WAVES) the waves fit beside the
 // weight-gradient stream's one-workgroup-per-CU GEMMs.  The offset is made opaque so the reads stay in the loop.
-__device__ __forceinline__ void stage_params(float* sp, const float* const* src, int nsrc, int C) {
-    for (int i = threadIdx.x; i < nsrc * C; i += blockDim.x) {
-        const int k = i / C;
-        sp[i] = src[k] ? src[k][i - k * C] : 0.f;
+// Only the channels a block touches are staged (chan_window): at most 256 chunks of E channels, so the dynamic LDS is
+// bounded (<= 6 x 2048 x 4 B for bf16) whatever C is, and the host sizes the grid with that LDS in the occupancy query.
+__device__ __forceinline__ void stage_params(float* sp, const float* const* src, int nsrc, int cb, int W) {
+    for (int i = threadIdx.x; i < nsrc * W; i += blockDim.x) {
+        const int k = i / W;
+        sp[i] = src[k] ? src[k][cb + i - k * W] : 0.f;
     }
     __syncthreads();
+}
+// first channel and width of the channel window of this block's threads in the elementwise kernels (one fixed chunk
+// of E channels per thread, grid stride a multiple of the C/E chunks per row, ew_rows_ok): the whole row when it has
+// <= 256 chunks, else the block's own 256-chunk window
+__device__ __forceinline__ void chan_window(int C, int E, int& cb, int& W) {
+    const unsigned cpr = (unsigned)C / E;
+    cb = cpr > 256u ? (int)((blockIdx.x * 256u) % cpr) * E : 0;
+    W = cpr > 256u ? 256 * E : C;
 }
 template <int E>
 __device__ __forceinline__ void lds_params(const float* sp, int off, float* v) {
@@ -198,7 +208,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T
     extern __shared__ __attribute__((aligned(16))) float sp[];        // 4 x C floats (dynamic LDS)     // mean, invstd, rsc, rsh
     {
         const float* src[4] = {mean, invstd, rsc, rsh};
-        stage_params(sp, src, 4, C);
+        stage_params(sp, src, 4, 0, C);
     }
     float s[E], q[E];
 #pragma unroll
@@ -298,27 +308,30 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply_kernel(const T*
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned stride = gridDim.x * blockDim.x;
     const int c0 = (int)(v0 % cpr) * E;
-    extern __shared__ __attribute__((aligned(16))) float sp[];        // 5 x C floats (dynamic LDS)     // coef a, b, c, rsc, rsh
+    extern __shared__ __attribute__((aligned(16))) float sp[];        // 5 x W floats (dynamic LDS): coef a, b, c, rsc, rsh
+    int cb, W;
+    chan_window(C, E, cb, W);
     {
         const float* src[5] = {coef, coef + C, coef + 2 * C, rsc, rsh};
-        stage_params(sp, src, 5, C);
+        stage_params(sp, src, 5, cb, W);
     }
+    const int cl = c0 - cb;
     // raw 16-B vectors -> dz (masked gradient) and dy, stored
     auto body = [&](size_t i, const uint4& rd, const uint4& ry, const uint4& rm) {
-        float d[E], yv[E], mk[E], ca[E], cb[E], cc[E], ka[E], kb[E];
+        float d[E], yv[E], mk[E], ca[E], cq[E], cc[E], ka[E], kb[E];
         Vec16<T>::load(&rd, d);
         Vec16<T>::load(&ry, yv);
         if (mask) Vec16<T>::load(&rm, mk);
-        lds_params<E>(sp, c0, ca);
-        lds_params<E>(sp, C + c0, cb);
-        lds_params<E>(sp, 2 * C + c0, cc);
-        if (rsc) { lds_params<E>(sp, 3 * C + c0, ka); lds_params<E>(sp, 4 * C + c0, kb); }
+        lds_params<E>(sp, cl, ca);
+        lds_params<E>(sp, W + cl, cq);
+        lds_params<E>(sp, 2 * W + cl, cc);
+        if (rsc) { lds_params<E>(sp, 3 * W + cl, ka); lds_params<E>(sp, 4 * W + cl, kb); }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
             const float dz = off ? 0.f : d[e];
             d[e] = dz;
-            yv[e] = ca[e] * dz + cb[e] * yv[e] + cc[e];
+            yv[e] = ca[e] * dz + cq[e] * yv[e] + cc[e];
         }
         Vec16<T>::store(dy + i, yv);
         if (dz_out) Vec16<T>::store(dz_out + i, d);
@@ -368,7 +381,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const 
     extern __shared__ __attribute__((aligned(16))) float sp[];        // 4 x C floats (dynamic LDS)     // mean_a, invstd_a, mean_b, invstd_b
     {
         const float* src[4] = {mean_a, invstd_a, mean_b, invstd_b};
-        stage_params(sp, src, 4, C);
+        stage_params(sp, src, 4, 0, C);
     }
     float s[E], qa[E], qb[E];
 #pragma unroll
@@ -450,11 +463,14 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply2_kernel(const T
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned stride = gridDim.x * blockDim.x;
     const int c0 = (int)(v0 % cpr) * E;
-    extern __shared__ __attribute__((aligned(16))) float sp[];        // 6 x C floats (dynamic LDS)     // coef_a a, b, c, coef_b a, b, c
+    extern __shared__ __attribute__((aligned(16))) float sp[];        // 6 x W floats (dynamic LDS): coef_a a, b, c, coef_b a, b, c
+    int cb, W;
+    chan_window(C, E, cb, W);
     {
         const float* src[6] = {coef_a, coef_a + C, coef_a + 2 * C, coef_b, coef_b + C, coef_b + 2 * C};
-        stage_params(sp, src, 6, C);
+        stage_params(sp, src, 6, cb, W);
     }
+    const int cl = c0 - cb;
     auto body = [&](size_t i, const uint4& rd, const uint4& rm, const uint4& ra, const uint4& rb) {
         float d[E], mk[E], va[E], vb[E], k0[E], k1[E], k2[E];
         Vec16<T>::load(&rd, d);
@@ -463,14 +479,14 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply2_kernel(const T
         Vec16<T>::load(&rb, vb);
 #pragma unroll
         for (int e = 0; e < E; ++e) d[e] = !(mk[e] > 0.f) ? 0.f : d[e];
-        lds_params<E>(sp, c0, k0);
-        lds_params<E>(sp, C + c0, k1);
-        lds_params<E>(sp, 2 * C + c0, k2);
+        lds_params<E>(sp, cl, k0);
+        lds_params<E>(sp, W + cl, k1);
+        lds_params<E>(sp, 2 * W + cl, k2);
 #pragma unroll
         for (int e = 0; e < E; ++e) va[e] = k0[e] * d[e] + k1[e] * va[e] + k2[e];
-        lds_params<E>(sp, 3 * C + c0, k0);
-        lds_params<E>(sp, 4 * C + c0, k1);
-        lds_params<E>(sp, 5 * C + c0, k2);
+        lds_params<E>(sp, 3 * W + cl, k0);
+        lds_params<E>(sp, 4 * W + cl, k1);
+        lds_params<E>(sp, 5 * W + cl, k2);
 #pragma unroll
         for (int e = 0; e < E; ++e) vb[e] = k0[e] * d[e] + k1[e] * vb[e] + k2[e];
         Vec16<T>::store(dya + i, va);
@@ -506,6 +522,17 @@ inline int ew_grid(int resident, long nvec, int cpr) {
     return (int)g;
 }
 inline int fin_blocks(int C) { return (C + 3) / 4; }   // 4 waves (channels) per 256-thread block
+// dynamic LDS of an elementwise backward kernel staging nsrc per-channel arrays over its channel window (chan_window)
+inline size_t ew_param_lds(int nsrc, int C, int E) { return (size_t)nsrc * std::min(C, 256 * E) * sizeof(float); }
+constexpr size_t EW_LDS_MAX = 64 * 1024;
+// resident blocks of `kernel` with `lds` bytes of dynamic LDS, cached per (kernel slot, window width)
+template <int SLOT>
+inline int ew_resident(const void* kernel, size_t lds) {
+    static int cache[EW_LDS_MAX / 16 + 1] = {0};        // lds is a multiple of 16 B (E >= 4 floats per chunk)
+    const size_t k = std::min<size_t>(lds / 16, EW_LDS_MAX / 16);
+    if (!cache[k]) cache[k] = resident_grid(kernel, 256, lds);
+    return cache[k];
+}
 
 SCD_KERNEL_NS_END
 }  // namespace
@@ -570,9 +597,9 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
     if (!ew_rows_ok(cpr) || total >= (1L << 31)) return SCD_ERR_ARG;
     const int scpr = std::min(cpr, 256), sC = scpr * E;
     // one round of resident blocks (at most), at least 8 rows per row lane
-    static const int gb = resident_grid((const void*)bn_bwd_reduce_kernel<__bf16>, 256);
-    static const int gf = resident_grid((const void*)bn_bwd_reduce_kernel<float>, 256);
-    const long nb = dtype == SCD_DT_BF16 ? gb : gf;
+    const size_t lds = (size_t)4 * sC * sizeof(float);
+    const long nb = dtype == SCD_DT_BF16 ? ew_resident<4>((const void*)bn_bwd_reduce_kernel<__bf16>, lds)
+                                         : ew_resident<5>((const void*)bn_bwd_reduce_kernel<float>, lds);
     const long rpi = 256 / scpr;
     const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
     const int blocks = cdiv(rows, rpb);
@@ -613,9 +640,9 @@ extern "C" int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask,
     if (!ew_rows_ok(cpr) || total >= (1L << 31)) return SCD_ERR_ARG;
     const int scpr = std::min(cpr, 256), sC = scpr * E;
     // the same row partition as scd_bn_bwd_reduce (per-thread partial sums identical to two separate passes)
-    static const int gb = resident_grid((const void*)bn_bwd_reduce_kernel<__bf16>, 256);
-    static const int gf = resident_grid((const void*)bn_bwd_reduce_kernel<float>, 256);
-    const long nb = dtype == SCD_DT_BF16 ? gb : gf;
+    const size_t lds = (size_t)4 * sC * sizeof(float);
+    const long nb = dtype == SCD_DT_BF16 ? ew_resident<4>((const void*)bn_bwd_reduce_kernel<__bf16>, lds)
+                                         : ew_resident<5>((const void*)bn_bwd_reduce_kernel<float>, lds);
     const long rpi = 256 / scpr;
     const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
     const int blocks = cdiv(rows, rpb);
@@ -652,13 +679,17 @@ extern "C" int scd_bn_bwd_apply2(int dtype, const void* dout, const void* mask, 
         return SCD_ERR_ARG;
     const long nvec = total / E;
     if (dtype == SCD_DT_BF16) {
-        static const int g = resident_grid((const void*)bn_bwd_apply2_kernel<__bf16>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply2_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 6 * C * 4, st,
+        const size_t lds = ew_param_lds(6, C, 8);
+        if (lds > EW_LDS_MAX) return SCD_ERR_ARG;
+        const int g = ew_resident<0>((const void*)bn_bwd_apply2_kernel<__bf16>, lds);
+        hipLaunchKernelGGL((bn_bwd_apply2_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), lds, st,
                            (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)ya, (const __bf16*)yb, coef_a,
                            coef_b, C, (unsigned)nvec, (__bf16*)dya, (__bf16*)dyb);
     } else if (dtype == SCD_DT_F32) {
-        static const int g = resident_grid((const void*)bn_bwd_apply2_kernel<float>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply2_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 6 * C * 4, st,
+        const size_t lds = ew_param_lds(6, C, 4);
+        if (lds > EW_LDS_MAX) return SCD_ERR_ARG;
+        const int g = ew_resident<1>((const void*)bn_bwd_apply2_kernel<float>, lds);
+        hipLaunchKernelGGL((bn_bwd_apply2_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), lds, st,
                            (const float*)dout, (const float*)mask, (const float*)ya, (const float*)yb, coef_a, coef_b,
                            C, (unsigned)nvec, (float*)dya, (float*)dyb);
     } else {
@@ -683,15 +714,19 @@ extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, c
     if (dtype == SCD_DT_BF16) {
         if (C % 8 || !ew_rows_ok(C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
-        static const int g = resident_grid((const void*)bn_bwd_apply_kernel<__bf16>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 5 * C * 4, st,
+        const size_t lds = ew_param_lds(5, C, 8);
+        if (lds > EW_LDS_MAX) return SCD_ERR_ARG;
+        const int g = ew_resident<2>((const void*)bn_bwd_apply_kernel<__bf16>, lds);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), lds, st,
                            (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, coef, C,
                            (unsigned)nvec, (__bf16*)dy, (__bf16*)dz);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4 || !ew_rows_ok(C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
-        static const int g = resident_grid((const void*)bn_bwd_apply_kernel<float>, 256);
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), 5 * C * 4, st, (const float*)dout,
+        const size_t lds = ew_param_lds(5, C, 4);
+        if (lds > EW_LDS_MAX) return SCD_ERR_ARG;
+        const int g = ew_resident<3>((const void*)bn_bwd_apply_kernel<float>, lds);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<float>), dim3(ew_grid(g, nvec, C / 4)), dim3(256), lds, st, (const float*)dout,
                            (const float*)mask, (const float*)y, relu_scale, relu_shift, coef, C, (unsigned)nvec, (float*)dy,
                            (float*)dz);
     } else {

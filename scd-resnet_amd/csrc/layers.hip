@@ -757,12 +757,22 @@ __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, lo
 
 // ---------------------------------------------------------------- SGD (torch.optim.SGD, single-tensor form)
 // networkFactory.py:84-89: SGD(lr, momentum 0.9, weight_decay 1e-4).  d = g + wd*p; the momentum buffer starts as a
-// copy of d on the first step (hyper[1] == 1 after the tick), then buf = mom*buf + (1-dampening)*d; the update uses
-// d + mom*buf (nesterov) or buf.  hyper = {lr, step} fp64 in device memory, as for Adam.
+// copy of d on the buffer's first step, then buf = mom*buf + (1-dampening)*d; the update uses d + mom*buf (nesterov) or
+// buf.  hyper = {lr, step, initialised, snapshot} fp64 in device memory: the tick advances the step and moves the
+// buffer's "initialised" flag into the snapshot the update reads (set to 1 for the next step), so a buffer re-created
+// mid-training (flag cleared by the host) starts as torch's does, not from the global step count.
+__global__ void sgd_tick_kernel(double* hyper) {
+    if (threadIdx.x == 0) {
+        hyper[1] = hyper[1] + 1.0;
+        hyper[3] = hyper[2];
+        hyper[2] = 1.0;
+    }
+}
+
 __global__ void sgd_dev_kernel(float* p, const float* g, float* buf, long n, const double* hyper, float mom, float damp,
                                float wd, int nesterov, float gscale) {
     const float lr = (float)hyper[0];
-    const bool first = hyper[1] <= 1.0;
+    const bool first = hyper[3] == 0.0;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const float pi = p[i];
         float d = g[i] * gscale;
@@ -988,7 +998,7 @@ extern "C" int scd_adam_step_dev(float* p, const float* g, float* m, float* v, l
 extern "C" int scd_sgd_step_dev(float* p, const float* g, float* buf, long n, double* hyper, float momentum,
                                 float dampening, float weight_decay, int nesterov, float gscale, void* stream) {
     if (!hyper || (momentum != 0.f && !buf)) return SCD_ERR_ARG;
-    hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
+    hipLaunchKernelGGL(sgd_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
     hipLaunchKernelGGL(sgd_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, buf, n,
                        (const double*)hyper, momentum, dampening, weight_decay, nesterov, gscale);
     SCD_RETURN_LAUNCH();

@@ -7,9 +7,12 @@
 // overwrites a slot a slow rank is still summing (a rank can only be one call ahead: it waits for everyone's flag).
 // A slow rank is not an error: the wait is bounded only by `timeout_ms` (the host's SCD_PEER_TIMEOUT_S, 120 s by
 // default -- longer than a checkpoint write or a validation pass on one rank), sleeping between polls so it holds one
-// wave.  A peer that never comes (a dead process) ends the wait: the kernel records the failing epoch in *err and
-// leaves `data` unreduced.  The error is sticky: every later call sees *err != 0 and does nothing (no mailbox writes,
-// no waits), so the ranks cannot drift into reading slots of different epochs, and the host raises on its next poll.
+// wave.  A peer that never comes (a dead process) ends the wait: the kernel records the failing epoch in *err, fills
+// `data` with NaN (the step's results are visibly wrong rather than silently reduced over this rank only) and writes
+// the POISON flag into its slot of every peer's mailbox, so a peer that is waiting -- or arrives later -- fails at once
+// instead of after a timeout of its own, and poisons its peers in turn.  The error is sticky: every later call sees
+// *err != 0, re-posts the poison, fills its data with NaN and returns without waiting, so the ranks cannot drift into
+// reading slots of different epochs, and the host raises on its next poll.
 // Mailbox layout: [2 parities][R slots][cap doubles] then [R] 64-bit flags.
 #include <string.h>
 
@@ -18,6 +21,7 @@
 namespace {
 
 constexpr int PEER_MAX = 8;
+constexpr unsigned long long POISON = ~0ull;        // a flag no epoch reaches: "this rank has failed"
 
 struct Boxes {
     double* box[PEER_MAX];
@@ -32,8 +36,19 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* data, int n
                                                              unsigned long long timeout_ticks) {
     const int tid = threadIdx.x;
     const int par = (int)(epoch & 1ull);
-    // sticky failure: an earlier call timed out, every later call is a no-op
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) return;
+    // failure path: NaN into the data, the poison flag into every peer's mailbox (remote stores over xGMI)
+    auto fail = [&]() {
+        const double qnan = __builtin_nan("");
+        for (int i = tid; i < n; i += blockDim.x) data[i] = qnan;
+        __threadfence_system();
+        if (tid < R && tid != rank)
+            __hip_atomic_store(flags_of(b.box[tid], R, cap) + rank, POISON, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    // sticky failure: an earlier call failed, every later call fails at once
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull) {
+        fail();
+        return;
+    }
     // 1. this rank's vector into slot `rank` of every mailbox (remote stores over xGMI for the peers)
     for (int p = 0; p < R; ++p) {
         double* dst = b.box[p] + ((size_t)par * R + rank) * cap;
@@ -43,17 +58,23 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* data, int n
     __syncthreads();
     if (tid < R)
         __hip_atomic_store(flags_of(b.box[tid], R, cap) + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    // 2. every rank's flag for this epoch in our own mailbox
-    __shared__ int timed_out;
-    if (tid == 0) timed_out = 0;
+    // 2. every rank's flag for this epoch in our own mailbox (or a peer's poison)
+    __shared__ int failed;
+    if (tid == 0) failed = 0;
     __syncthreads();
     if (tid < R) {
         unsigned long long* f = flags_of(b.box[rank], R, cap) + tid;
         const unsigned long long t0 = wall_clock64();
         unsigned polls = 0;
-        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+        for (;;) {
+            const unsigned long long v = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (v == POISON) {                                   // the peer failed: fail now, do not wait it out
+                failed = 1;
+                break;
+            }
+            if (v >= epoch) break;
             if (wall_clock64() - t0 > timeout_ticks) {           // wall_clock64: 100 MHz constant clock
-                timed_out = 1;
+                failed = 1;
                 break;
             }
             // tight polling for the common microsecond-scale skew, then back off (a rank seconds late)
@@ -62,8 +83,9 @@ __global__ __launch_bounds__(256) void peer_allreduce_kernel(double* data, int n
         }
     }
     __syncthreads();
-    if (timed_out) {
+    if (failed) {
         if (tid == 0) atomicCAS(err, 0ull, epoch);             // the first failing epoch
+        fail();
         return;
     }
     __threadfence_system();

@@ -179,10 +179,10 @@ static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 // Workgroups of `kernel` (blockDim `threads`, no dynamic LDS) resident on the whole device at once:
 // grid-stride HBM kernels launch exactly this many, so every workgroup runs in the first (only) round
 // and the grid never has a partial second round.
-static inline int resident_grid(const void* kernel, int threads) {
+static inline int resident_grid(const void* kernel, int threads, size_t dyn_lds = 0) {
     int dev = 0, cus = 256, per = 1;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || per < 1) per = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, dyn_lds) != hipSuccess || per < 1) per = 1;
     return per * cus;
 }

@@ -106,12 +106,15 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def _new_state(self, fp):
         raise NotImplementedError
 
+    def _hyper_init(self):
+        """The device step state: {lr, step} (FlatSGD adds its buffer's initialised flag)."""
+        return [self.param_groups[0]["lr"], float(self._step)]
+
     def flat(self):
         if self._flat is None or not self._flat.valid():
             self._flat = ensure_flat(self._all_params())
             self._new_state(self._flat)
-            self._hyper = torch.tensor([self.param_groups[0]["lr"], float(self._step)], dtype=torch.float64,
-                                       device=self._flat.data.device)
+            self._hyper = torch.tensor(self._hyper_init(), dtype=torch.float64, device=self._flat.data.device)
             self._dev_lr = self.param_groups[0]["lr"]
         return self._flat
 
@@ -148,7 +151,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
         for g, s in zip(self.param_groups, sd["param_groups"]):
             g.update(s)
         if self._hyper is not None:
-            self._hyper.copy_(torch.tensor([self.param_groups[0]["lr"], float(self._step)], dtype=torch.float64))
+            self._hyper[:2].copy_(torch.tensor([self.param_groups[0]["lr"], float(self._step)], dtype=torch.float64))
             self._dev_lr = self.param_groups[0]["lr"]
 
     def _groups_sd(self):
@@ -202,7 +205,12 @@ class FlatSGD(_FlatOptimizer):
         self._buf = None
 
     def _new_state(self, fp):
+        # a new buffer starts uninitialised: its first update copies d, as torch does for a parameter without a
+        # momentum_buffer (hyper[2], the flag the kernel reads; _hyper_init), whatever the global step
         self._buf = torch.zeros_like(fp.data) if self.param_groups[0]["momentum"] != 0 else None
+
+    def _hyper_init(self):
+        return [self.param_groups[0]["lr"], float(self._step), 0.0, 0.0]
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -217,10 +225,17 @@ class FlatSGD(_FlatOptimizer):
                 "momentum_buffer": None if self._buf is None else self._buf.cpu()}
 
     def load_state_dict(self, sd):
+        buf = sd.get("momentum_buffer")
+        if buf is not None and self.param_groups[0]["momentum"] == 0:
+            raise ValueError("FlatSGD.load_state_dict: the state has a momentum_buffer but this optimizer has "
+                             "momentum 0 (no buffer to load it into)")
         self._load_common(sd)
-        if sd.get("momentum_buffer") is not None:
-            self.flat()
-            self._buf.copy_(sd["momentum_buffer"])
+        self.flat()
+        if buf is not None:
+            self._buf.copy_(buf)
+        elif self._buf is not None:
+            self._buf.zero_()
+        self._hyper[2].fill_(1.0 if buf is not None else 0.0)
 
 
 class _EndOfBackward(torch.autograd.Function):
@@ -351,7 +366,17 @@ class FlatDDP(torch.nn.Module):
         self._works = [None] * len(self._buckets)
         self._next = 0                        # buckets are launched in order: RCCL needs one order on all ranks
 
+    def overlap_buckets(self):
+        """Buckets may be all-reduced from inside the backward unless SyncBN all-reduces its statistics on the same
+        group (ops.syncbn_group's default): on one RCCL communicator a bucket waits for the side stream's weight
+        gradients, and every critical-path SyncBN collective issued after it would wait with it -- then all buckets
+        go at the end of the backward, after the last SyncBN collective."""
+        from . import ops
+        return not ops.bn_sync_shares_group(self.group)
+
     def _launch_ready(self, final=False):
+        if not final and not self.overlap_buckets():
+            return
         while self._next < len(self._buckets) and (final or self._pending[self._next] == 0):
             b = self._next
             lo, hi = self._buckets[b]

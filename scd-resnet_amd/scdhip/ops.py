@@ -192,10 +192,36 @@ def new_bn_group():
     return dist.new_group(ranks=list(range(dist.get_world_size())))
 
 
+def syncbn_group():
+    """The process group for the SyncBN statistics at world > 1 (networkFactory.py:128-133).
+
+    Default: WORLD, the group FlatDDP all-reduces its gradient buckets on -- as the reference's SyncBatchNorm and DDP
+    share the default group.  With RCCL every collective of the rank then runs on one communicator and its one stream,
+    in issue order, so no two communicators' kernels are ever in flight at once (that combination has not
+    run at world >= 2 on RCCL).  The price: a bucket queued on that stream waits for the weight-gradient side stream,
+    and a critical-path SyncBN all-reduce issued after it would wait too -- so FlatDDP launches no bucket during the
+    backward while SyncBN shares its group (FlatDDP.overlap_buckets), and all buckets go at the end of the backward.
+    SCD_SYNCBN_OWN_GROUP=1: a communicator of their own (new_bn_group), buckets overlap the backward.
+    Collective when it creates a group: every rank calls it, once, before FlatDDP is built."""
+    if os.environ.get("SCD_SYNCBN_OWN_GROUP", "0") == "1":
+        return new_bn_group()
+    return dist.group.WORLD
+
+
+def bn_sync_shares_group(group):
+    """True when SyncBN all-reduces its statistics through torch.distributed on `group` (None = WORLD), i.e. on the
+    same communicator and stream as a collective issued on `group` (the peer-memory path uses no collective)."""
+    g = _BNSync.group
+    if g is None or _BNSync.peer is not None:
+        return False
+    world = dist.group.WORLD
+    return (g or world) is (group or world)
+
+
 def set_bn_sync(group, peer=None):
-    """Enable global-batch BN statistics (SyncBatchNorm, networkFactory.py:128-133) over `group` (use
-    new_bn_group(), not WORLD, beside FlatDDP).  peer=True (or SCD_SYNCBN_PEER=1) all-reduces them over peer memory
-    (scdhip/peer.py) instead of through torch.distributed."""
+    """Enable global-batch BN statistics (SyncBatchNorm, networkFactory.py:128-133) over `group` (syncbn_group():
+    WORLD by default).  peer=True (or SCD_SYNCBN_PEER=1) all-reduces them over peer memory (scdhip/peer.py) instead
+    of through torch.distributed."""
     if _BNSync.peer is not None:
         _BNSync.peer.close()
         _BNSync.peer = None

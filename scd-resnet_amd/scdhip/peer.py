@@ -8,9 +8,11 @@ default until an 8-GPU run has compared them.  Single node, <= 8 ranks, eager st
 
 Late ranks: a rank whose host is seconds behind (a checkpoint write, validation, first-step allocation, a GC pause) is
 waited for on the device, up to SCD_PEER_TIMEOUT_S (120 s).  Only a peer that never arrives is an error: the kernel then
-records the failing epoch in a sticky device word (every later call is a no-op, so the ranks cannot drift into slots of
-different epochs), ``poll()`` -- called once per step by FlatDDP at the end of backward -- raises on the first step whose
-copy of that word is non-zero, and ``check()`` raises synchronously.
+records the failing epoch in a sticky device word, fills that call's data with NaN and posts a poison flag into every
+peer's mailbox, so the peers fail at that call too instead of waiting out their own timeout (and poison theirs); every
+later call re-posts the poison and returns NaN at once, so no replica silently continues on statistics reduced over a
+subset of the ranks.  ``poll()`` -- called once per step by FlatDDP at the end of backward -- raises on the first step
+whose copy of the error word is non-zero, and ``check()`` raises synchronously.
 """
 import ctypes
 import os

@@ -56,9 +56,10 @@ class Deep(torch.nn.Module):
         return self.body(self.stem(x))
 
 
-def check_early_buckets(rank, world):
+def check_early_buckets(rank, world, expect_early=True):
     """Buckets are all-reduced from inside backward once the hook kinds are learned, also when the
-    parameter-holding leaves never run forward (the hooks must sit on modules that run)."""
+    parameter-holding leaves never run forward (the hooks must sit on modules that run); with
+    expect_early=False (SyncBN sharing FlatDDP's group) none is, and all still average correctly at the end."""
     torch.manual_seed(5 + rank)
     m = Deep()
     ddp = FlatDDP(m, bucket_mb=1e-5)
@@ -79,9 +80,11 @@ def check_early_buckets(rank, world):
         for k, p in m.named_parameters():
             exp = sum(gr[k] for gr in grads) / world
             assert torch.allclose(p.grad, exp, atol=1e-6), (it, k)
-        if it > 0:
+        if it > 0 and expect_early:
             # 6 body buckets (3 blocks x weight/bias) become ready inside backward; the stem's only at the end
             assert ddp.early_launches >= 6, ddp.early_launches
+        if not expect_early:
+            assert ddp.early_launches == 0 and not ddp.overlap_buckets(), ddp.early_launches
 
 
 def check(rank, world, bucket_mb):
@@ -128,24 +131,37 @@ def check(rank, world, bucket_mb):
 
 
 def check_bn_group(rank, world):
-    """SyncBN statistics get a process group of their own (ops.new_bn_group), distinct from the WORLD group FlatDDP
-    all-reduces gradient buckets on: with RCCL every group has its own communicator and stream, so the critical-path
-    statistics never queue behind a bucket (networkFactory.py:128-134)."""
+    """SyncBN group policy (ops.syncbn_group; ADVICE r3 networkFactory.py:164).  Default: WORLD, shared with FlatDDP's
+    buckets (one RCCL communicator and stream), so FlatDDP launches no bucket inside the backward and every bucket
+    still averages correctly from the end-of-backward callback.  SCD_SYNCBN_OWN_GROUP=1: a group of its own, distinct
+    from WORLD, and the buckets overlap the backward again (networkFactory.py:128-134)."""
     from scdhip import ops
-    g = ops.new_bn_group()
+    os.environ.pop("SCD_SYNCBN_OWN_GROUP", None)
+    g = ops.syncbn_group()
+    assert g is dist.group.WORLD
     ops.set_bn_sync(g)
     try:
+        assert ops.bn_sync_shares_group(None)
+        check_early_buckets(rank, world, expect_early=False)
+    finally:
+        ops.set_bn_sync(None)
+    os.environ["SCD_SYNCBN_OWN_GROUP"] = "1"
+    try:
+        g = ops.syncbn_group()
+        ops.set_bn_sync(g)
         assert ops.bn_sync_group() is g
         assert g is not dist.group.WORLD and g != dist.distributed_c10d._get_default_group()
         assert dist.get_world_size(g) == world and dist.get_rank(g) == rank
         ddp = FlatDDP(Toy())
         assert ddp.group is None or ddp.group is dist.group.WORLD
-        assert ops.bn_sync_group() is not (ddp.group or dist.distributed_c10d._get_default_group())
+        assert not ops.bn_sync_shares_group(ddp.group) and ddp.overlap_buckets()
         assert ops.bn_sync_world() == world
         t = torch.full((4,), float(rank + 1), dtype=torch.float64)
         dist.all_reduce(t, group=g)
         assert torch.all(t == world * (world + 1) / 2)
+        check_early_buckets(rank, world, expect_early=True)
     finally:
+        os.environ.pop("SCD_SYNCBN_OWN_GROUP", None)
         ops.set_bn_sync(None)
 
 

@@ -1,7 +1,9 @@
-"""The RCCL code path at world size 1 (one GPU box): init_process_group("nccl") with device_id, SyncBN statistics on
-their own group (ops.new_bn_group), and one FlatDDP step with every collective forced on -- buckets all-reduced with
-ReduceOp.AVG from the weight-gradient side stream, async work.wait(), the buffer broadcast -- compared with the same
-step without any of it.  Launched by tests/test_ddp_gpu.py with MASTER_ADDR / MASTER_PORT set."""
+"""The RCCL code path at world size 1 (one GPU box): init_process_group("nccl") with device_id, and FlatDDP steps with
+every collective forced on -- buckets all-reduced with ReduceOp.AVG from the weight-gradient side stream, async
+work.wait(), the buffer broadcast -- compared with the same step without any of it, for both SyncBN group policies
+(ops.syncbn_group): WORLD shared with the buckets (the default: every bucket at the end of the backward) and a group of
+its own (SCD_SYNCBN_OWN_GROUP=1: buckets from inside the backward).  Launched by tests/test_ddp_gpu.py with
+MASTER_ADDR / MASTER_PORT set."""
 import os
 import sys
 
@@ -44,31 +46,38 @@ def main():
     ref_m = make()
     ref_loss, ref_g = step(ref_m, ref_m)
 
-    # forced RCCL: SyncBN on its own communicator, FlatDDP buckets on WORLD
-    bn_group = ops.new_bn_group()
-    ops.set_bn_sync(bn_group)
-    assert ops.bn_sync_group() is bn_group and bn_group is not dist.group.WORLD
-    m = make()
-    ddp = FlatDDP(m, force_collectives=True)
-    assert ddp._use_avg and ddp._comm
     worst = 0.0
-    for it in range(2):          # the second backward launches the head bucket from inside backward
-        loss, g = step(ddp, m)
-        assert abs(loss - ref_loss) <= 1e-6 * abs(ref_loss), (it, loss, ref_loss)
-        for k, r in ref_g.items():
-            e = (g[k] - r).norm().item() / max(r.norm().item(), 1e-30)
-            worst = max(worst, e)
-            # the collectives themselves are exact at world 1 (AVG of one rank); what differs is the SyncBN statistics'
-            # replica collapse (sequential fp64) against the local finalize's fp64 wave tree -- rounding only
-            assert e <= 1e-6, (it, k, e)
-        if it == 0:
-            # BN running statistics after one forward each (SyncBN count = local count at world 1)
-            rs = ref_m.state_dict()
-            for k, v in m.state_dict().items():
-                np.testing.assert_allclose(v.double().cpu().numpy(), rs[k].double().cpu().numpy(), rtol=1e-6,
-                                           atol=1e-7, err_msg=k)
-    assert ddp.early_launches >= 1, ddp.early_launches
-    ops.set_bn_sync(None)
+    for policy in ("world", "own"):
+        if policy == "own":
+            os.environ["SCD_SYNCBN_OWN_GROUP"] = "1"
+        bn_group = ops.syncbn_group()
+        os.environ.pop("SCD_SYNCBN_OWN_GROUP", None)
+        ops.set_bn_sync(bn_group)
+        assert ops.bn_sync_group() is bn_group and (bn_group is dist.group.WORLD) == (policy == "world")
+        m = make()
+        ddp = FlatDDP(m, force_collectives=True)
+        assert ddp._use_avg and ddp._comm and ddp.overlap_buckets() == (policy == "own")
+        for it in range(2):          # the second backward launches the head bucket from inside backward (own group)
+            loss, g = step(ddp, m)
+            assert abs(loss - ref_loss) <= 1e-6 * abs(ref_loss), (policy, it, loss, ref_loss)
+            for k, r in ref_g.items():
+                e = (g[k] - r).norm().item() / max(r.norm().item(), 1e-30)
+                worst = max(worst, e)
+                # the collectives themselves are exact at world 1 (AVG of one rank); what differs is the SyncBN
+                # statistics' replica collapse (sequential fp64) against the local finalize's fp64 wave tree --
+                # rounding only
+                assert e <= 1e-6, (policy, it, k, e)
+            if it == 0 and policy == "world":
+                # BN running statistics after one forward each (SyncBN count = local count at world 1)
+                rs = ref_m.state_dict()
+                for k, v in m.state_dict().items():
+                    np.testing.assert_allclose(v.double().cpu().numpy(), rs[k].double().cpu().numpy(), rtol=1e-6,
+                                               atol=1e-7, err_msg=k)
+        if policy == "own":
+            assert ddp.early_launches >= 1, ddp.early_launches
+        else:
+            assert ddp.early_launches == 0, ddp.early_launches
+        ops.set_bn_sync(None)
     dist.destroy_process_group()
     print("OK rccl world1: loss %.6f, worst normwise gradient difference %.2e, %d early bucket launches, %d buckets"
           % (loss, worst, ddp.early_launches, len(ddp._buckets)))

@@ -38,15 +38,16 @@ def _run(worker, world, **extra):
     return outs
 
 
-@pytest.mark.parametrize("peer", [False, True])
-def test_syncbn_ddp_world2_matches_reference(peer):
-    """F7 with the SyncBN statistics through torch.distributed, and (peer) through the peer-memory one-shot
-    all-reduce (scdhip/peer.py: IPC-mapped mailboxes, flag-synchronised kernel) -- same golden vectors."""
-    outs = _run("ddp_gpu_worker.py", 2, SCD_SYNCBN_PEER="1" if peer else "0")
+@pytest.mark.parametrize("world,sync", [(2, "world"), (2, "own"), (2, "peer"), (4, "world"), (4, "peer")])
+def test_syncbn_ddp_matches_reference(world, sync):
+    """F7 (W=2) and F7b (W=4, tests/golden/make_golden_ddp4.py) with the SyncBN statistics through torch.distributed
+    on WORLD beside the buckets (the default), on a group of their own, or through the peer-memory one-shot all-reduce
+    (scdhip/peer.py: IPC-mapped mailboxes, flag-synchronised kernel) -- the reference's golden vectors."""
+    outs = _run("ddp_gpu_worker.py", world, SCD_SYNCBN_PEER="1" if sync == "peer" else "0",
+                SCD_SYNCBN_OWN_GROUP="1" if sync == "own" else "0")
     for o in outs:
         assert "OK rank" in o, o
-    if peer:
-        print([line for o in outs for line in o.splitlines() if "per call" in line])
+    print([line for o in outs for line in o.splitlines() if "per call" in line or "worst" in line])
 
 
 def test_rccl_world1_flatddp_syncbn():

@@ -476,6 +476,38 @@ def test_flat_sgd_matches_torch(nesterov, damp):
         np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().numpy(), rtol=1e-6, atol=1e-7)
 
 
+def test_flat_sgd_buffer_reset_matches_torch():
+    """A momentum buffer re-created mid-training starts as torch's does (clone of d on its first update), also with
+    dampening != 0 where the global step count would give (1-dampening)*d (ADVICE r3 flat.py:219): the state is
+    loaded without a momentum_buffer on both sides after two steps."""
+    from scdhip.flat import FlatSGD
+    g = torch.Generator().manual_seed(13)
+    p0 = [torch.randn(64, 3, 3, 3, generator=g), torch.randn(1000, generator=g)]
+    pt = [x.clone().requires_grad_(True) for x in p0]
+    kw = dict(lr=2.5e-4, momentum=0.9, weight_decay=1e-4, dampening=0.25)
+    opt_t = torch.optim.SGD(pt, **kw)
+    pd = [torch.nn.Parameter(x.clone().to(DEV)) for x in p0]
+    opt = FlatSGD(pd, **kw)
+    for step in range(1, 6):
+        if step == 3:
+            opt_t.state.clear()                         # torch: no momentum_buffer -> the next step clones d
+            sd = opt.state_dict()
+            sd["momentum_buffer"] = None
+            opt.load_state_dict(sd)
+        opt.zero_grad()
+        for a, b in zip(pt, pd):
+            gr = torch.randn(a.shape, generator=g)
+            a.grad = gr.clone()
+            b.grad.copy_(gr.to(DEV))
+        opt_t.step()
+        opt.step()
+    for a, b in zip(pt, pd):
+        np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().numpy(), rtol=1e-6, atol=1e-7)
+    with pytest.raises(ValueError):
+        FlatSGD(pd, lr=1e-3).load_state_dict({"step": 1, "param_groups": [{"lr": 1e-3}],
+                                              "momentum_buffer": torch.zeros(64 * 27 + 1000)})
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_batched_pack_matches_single(dtype):
     """PackPlan's one-launch batched packing (mode 0 rows, mode 1 LDS-tiled transposes, mode 2 tap-major

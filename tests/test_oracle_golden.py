@@ -140,25 +140,29 @@ def test_f6_layer_stats(spec, golden):
         np.testing.assert_allclose(t.reshape(-1)[pos].numpy(), g[name + "|samp"], rtol=1e-4, atol=1e-4)
 
 
-def test_f7_ddp_syncbn(spec, golden):
-    """Global-batch BN == SyncBN; averaging per-shard losses == DDP gradient averaging."""
+@pytest.mark.parametrize("name,world,per,seeds", [("ddp", 2, 2, (8, 9)), ("ddp4", 4, 2, (31, 32))])
+def test_f7_ddp_syncbn(spec, golden, name, world, per, seeds):
+    """Global-batch BN == SyncBN; averaging per-shard losses == DDP gradient averaging (F7 at W=2, F7b at W=4)."""
     entries, topo = spec
-    g = golden("ddp")
+    g = golden(name)
     P, Bf = O.split_state(O.hash_weights(entries))
     P = {k: v.requires_grad_(True) for k, v in P.items()}
-    x = T.batch_inputs(8, 4, 128)
-    ys = T.batch_targets(9, 4, 32)
+    x = T.batch_inputs(seeds[0], world * per, 128)
+    ys = T.batch_targets(seeds[1], world * per, 32)
     outs = O.forward(P, Bf, x, topo)
     losses = []
-    for r in range(2):
-        sl = slice(2 * r, 2 * r + 2)
+    for r in range(world):
+        sl = slice(per * r, per * r + per)
         l, _ = O.centernet_loss({k: v[sl] for k, v in outs.items()}, [y[sl] for y in ys])
         losses.append(l.mean())
-    ((losses[0] + losses[1]) / 2).backward()
-    np.testing.assert_allclose(losses[0].item(), g["loss_r0"], rtol=1e-4)
-    np.testing.assert_allclose(losses[1].item(), g["loss_r1"], rtol=1e-4)
+    (sum(losses) / world).backward()
+    for r in range(world):
+        np.testing.assert_allclose(losses[r].item(), g["loss_r%d" % r], rtol=1e-4)
     for k, v in P.items():
         np.testing.assert_allclose(v.grad.double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7)
+    for k in g.files:
+        if k.startswith("rs|"):
+            np.testing.assert_allclose(Bf[k[3:]].numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
 
 
 # ---------------------------------------------------------------- CornerNet (F5, F8)
