@@ -62,6 +62,8 @@ struct GemmParams {
     // scd_conv_dgrad_s2 (ping-pong kernel): GEMM column c = phase * Co/4 + channel is stored at output pixel
     // (2 oh + phase / 2, 2 ow + phase % 2) of a (2 Ho, 2 Wo, Co/4) tensor
     int shuf;
+    // heads384: K-stage order reversed on every other round of 256 workgroups (kserp = 1; SCD_HEADS_SERP)
+    int kserp;
 };
 
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
@@ -547,17 +549,24 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, const char* 
 // -- leaves as linear 16-B stores (+= when accumulating); BN sums (forward: fp32 accumulators, as the shared
 // epilogue; BNB: the stored gradient against the BN input) are carried in registers across the run and added to
 // the fp64 replicas once per workgroup.
+// Rows of 256 pixels (Res50 layer1 at 1024^2 input, residuals.py:122-165, 357): a tile is one row, and the four ring
+// rows (132 KiB) leave no room for the staging buffer, so the tile is stored straight from the accumulators (8-B
+// stores of the lane's 4 channels; L2 merges a pixel's 128 B): outputs bit-identical.  The BN-backward-sum variant
+// is not built for them (its operand loads in this layout spill registers): scd_conv_gemm_bnbwd then runs this
+// kernel's plain input gradient and the separate scd_bn_bwd_reduce.
 template <int WO, bool FLIP, bool BNB>
 __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int run) {
     typedef __bf16 T;
-    constexpr int TR = 256 / WO;                  // output rows per tile
+    constexpr int TR = WO >= 256 ? 1 : 256 / WO;  // output rows per tile
+    constexpr bool DIRECT = WO == 256;            // no staging buffer: stores from the accumulators
+    static_assert(!(DIRECT && BNB), "256-pixel rows: BN-backward sums by the separate reduction");
     constexpr int WH = WO + 8;                    // pixel slots per ring row (slot = input column + 1)
     constexpr int ROWB = WH * 128;
     constexpr int RING = 2 * TR + 2;
     constexpr int SROW = 64 * 2 + 16;             // staging row: 64 channels + 16 B pad
-    constexpr int STG = 256 * SROW;
+    constexpr int STG = DIRECT ? 0 : 256 * SROW;
     static_assert(WO * TR == 256 && WH % 8 == 0, "tile geometry");
-    __shared__ __attribute__((aligned(16))) char smem[RING * ROWB + STG];
+    __shared__ __attribute__((aligned(16))) char smem[RING * ROWB + (STG ? STG : 16)];
     char* const stg = smem + RING * ROWB;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -651,6 +660,26 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
                                                                             af[a], acc[a][b], 0, 0, 0);
             }
         }
+        if constexpr (DIRECT) {
+            // the tile is row r of image n: lane's pixel 64pw + 16a + l16 is its column; channels 32chh + 16b + 4lg
+            const long base = ((long)(n * p.Ho + r) * p.Wo) * 64;
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    const long off = base + (long)(64 * pw + 16 * a + l16) * 64 + 32 * chh + 16 * b + 4 * lg;
+                    bf16x4 o;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) o[q] = (__bf16)acc[a][b][q];
+                    if (p.accumulate) {
+                        const bf16x4 old4 = *(const bf16x4*)((const T*)p.y + off);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) o[q] = (__bf16)((float)o[q] + (float)old4[q]);
+                    }
+                    *(bf16x4*)((T*)p.y + off) = o;
+                }
+        } else {
         // stage: lane holds pixel 64pw + 16a + l16, channels 32chh + 16b + 4lg + (0..3)
 #pragma unroll
         for (int a = 0; a < 4; ++a)
@@ -662,6 +691,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
                 for (int q = 0; q < 4; ++q) o[q] = (__bf16)acc[a][b][q];
                 *(bf16x4*)(stg + (64 * pw + 16 * a + l16) * SROW + (32 * chh + 16 * b + 4 * lg) * 2) = o;
             }
+        }
         if (fwd_stats) {
             // forward BN sums of the fp32 accumulators (as the shared epilogue): over the wave's 4 pixel blocks,
             // the 16 pixel lanes (DPP row sums), then the 4 pixel-group waves through LDS
@@ -686,6 +716,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
         if (fwd_stats && tid < 128) {
 #pragma unroll
             for (int w = 0; w < 4; ++w) bnsum += bnred[(w * 64 + (tid & 63)) * 2 + (tid >> 6)];
+        }
+        if constexpr (DIRECT) {
+            __syncthreads();                                     // bnred read before the next tile writes it
+            continue;
         }
         // ---- store phase: the tile is rows r .. r+TR-1 of image n, one contiguous 32-KB NHWC block
         {
@@ -1143,37 +1177,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
-    // BN-backward mode: output pixel of each of the lane's 8 rows (-1 past the end)
-    int pix[8];
-    if (p.bnbwd) {
-#pragma unroll
-        for (int a = 0; a < 8; ++a) {
-            const int m = mt * BM + 128 * grp + a * 16 + l16;
-            const int n = m / QQ;
-            const int rem = m - n * QQ;
-            const int qh = rem / ph.Qw, qw = rem - (rem / ph.Qw) * ph.Qw;
-            pix[a] = m < M ? (n * p.Ho + p.os * qh + ph.rho_h) * p.Wo + p.os * qw + ph.rho_w : -1;
-        }
-    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
         float bias[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
-        float bmu[4], bis[4], bsc[4], bsh[4];
-        uint2 yq[8];
-        if (p.bnbwd) {
-            const float4 f0 = *(const float4*)(p.bn_mean + col0), f1 = *(const float4*)(p.bn_invstd + col0);
-            const float4 f2 = *(const float4*)(p.bn_rsc + col0), f3 = *(const float4*)(p.bn_rsh + col0);
-            bmu[0] = f0.x; bmu[1] = f0.y; bmu[2] = f0.z; bmu[3] = f0.w;
-            bis[0] = f1.x; bis[1] = f1.y; bis[2] = f1.z; bis[3] = f1.w;
-            bsc[0] = f2.x; bsc[1] = f2.y; bsc[2] = f2.z; bsc[3] = f2.w;
-            bsh[0] = f3.x; bsh[1] = f3.y; bsh[2] = f3.z; bsh[3] = f3.w;
-#pragma unroll
-            for (int a = 0; a < 8; ++a)
-                yq[a] = pix[a] >= 0 ? *(const uint2*)(p.bny + ((long)pix[a] * p.Co + col0) * 2) : make_uint2(0, 0);
-        }
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
             const int m = mt * BM + 128 * grp + a * 16 + l16;
@@ -1183,21 +1192,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                 v[r] = acc[a][b][r] + bias[r];
                 if (p.relu) v[r] = fmaxf(v[r], 0.f);
             }
-            if (m < M) {
-                if (p.bnbwd) {
-                    const unsigned yw[2] = {yq[a].x, yq[a].y};
+            if (!p.bnbwd && m < M) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float yv = h16_word_half(yw[r >> 1], r & 1);
-                        const float d = (float)(__bf16)v[r];            // the stored gradient
-                        const float dz = yv * bsc[r] + bsh[r] > 0.f ? d : 0.f;
-                        csum[b][r] += dz;
-                        csq[b][r] += dz * (yv - bmu[r]) * bis[r];
-                    }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
-                }
+                for (int r = 0; r < 4; ++r) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
             }
             typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
             bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
@@ -1205,24 +1202,81 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the staged tile is wave-private
-    {
-        constexpr int CPR = WCOLS * 2 / 16;                  // 16-B chunks per staged row (8 or 6)
+    constexpr int CPR = WCOLS * 2 / 16;                      // 16-B chunks per staged row (8 or 6)
+    // output element offset of tile row `row` (< 128 of this group), channel `col` (M-range checked by the caller)
+    auto out_off = [&](int m, int col) -> long {
+        const int n = m / QQ;
+        const int rem = m - n * QQ;
+        const int qh = rem / ph.Qw;
+        const int qw = rem - qh * ph.Qw;
+        const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
+        if (p.shuf) {
+            const int c4 = p.Co >> 2, sp = col / c4;
+            return ((long)(n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 + (col - sp * c4);
+        }
+        return ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+    };
+    // BN-backward mode (scd_conv_gemm_bnbwd: the output is the gradient of a following BN+ReLU layer): its backward
+    // sums come from the stored gradient and the pre-BN activation, read in the store phase as whole 128-B row pieces
+    // (lane: fixed 16-B channel chunk, RPI rows per pass) -- not as 8-B pieces per accumulator fragment
+    constexpr int RPI = 64 / CPR;                            // rows per pass (8, or 10 with 4 lanes idle)
+    const int rsub = lane / CPR, chx = lane - (lane / CPR) * CPR;
+    float bs8[EPC], bq8[EPC];
+    if (p.bnbwd) {
+        const int colb = nt * BN + wc * WCOLS + chx * EPC;
+        const bool cok = rsub < RPI && colb < p.Co;
+        const int cl = cok ? colb : 0;
+        float mu[EPC], is[EPC], sc[EPC], sh[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; e += 4) {
+            const float4 f0 = *(const float4*)(p.bn_mean + cl + e), f1 = *(const float4*)(p.bn_invstd + cl + e);
+            const float4 f2 = *(const float4*)(p.bn_rsc + cl + e), f3 = *(const float4*)(p.bn_rsh + cl + e);
+            mu[e] = f0.x; mu[e + 1] = f0.y; mu[e + 2] = f0.z; mu[e + 3] = f0.w;
+            is[e] = f1.x; is[e + 1] = f1.y; is[e + 2] = f1.z; is[e + 3] = f1.w;
+            sc[e] = f2.x; sc[e + 1] = f2.y; sc[e + 2] = f2.z; sc[e + 3] = f2.w;
+            sh[e] = f3.x; sh[e + 1] = f3.y; sh[e + 2] = f3.z; sh[e + 3] = f3.w;
+        }
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) { bs8[e] = 0.f; bq8[e] = 0.f; }
+        constexpr int NIT = (128 + RPI - 1) / RPI;
+#pragma unroll 4
+        for (int it = 0; it < NIT; ++it) {
+            const int row = it * RPI + rsub;
+            const int m = mt * BM + 128 * grp + row;
+            const bool ok = cok && row < 128 && m < M;
+            // every load from a valid address (row 0 / pixel 0 when masked off): no branch around the loads
+            const long off = out_off(ok ? m : 0, cl);
+            uint4 v = *(const uint4*)(ep + (ok ? row : 0) * EROW + chx * 16);
+            T* dst = (T*)(p.y) + off;
+            if (p.accumulate) {
+                float a8[EPC], o8[EPC];
+                Vec16<T>::load(&v, a8);
+                Vec16<T>::load(dst, o8);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) a8[e] += o8[e];
+                Vec16<T>::store(&v, a8);
+            }
+            float d8[EPC], y8[EPC];
+            Vec16<T>::load(&v, d8);
+            Vec16<T>::load((const T*)p.bny + off, y8);
+            if (ok) {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) {
+                    const float dz = y8[e] * sc[e] + sh[e] > 0.f ? d8[e] : 0.f;
+                    bs8[e] += dz;
+                    bq8[e] += dz * (y8[e] - mu[e]) * is[e];
+                }
+                if constexpr (dbg == 60) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+                else *(uint4*)dst = v;
+            }
+        }
+    } else {
         for (int idx = lane; idx < 128 * CPR; idx += 64) {
             const int row = idx / CPR, ch = idx - (idx / CPR) * CPR;
             const int m = mt * BM + 128 * grp + row;
             const int col = nt * BN + wc * WCOLS + ch * EPC;
             if (m >= M || col >= p.Co) continue;
-            const int n = m / QQ;
-            const int rem = m - n * QQ;
-            const int qh = rem / ph.Qw;
-            const int qw = rem - qh * ph.Qw;
-            const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
-            T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
-            if (p.shuf) {
-                const int c4 = p.Co >> 2, sp = col / c4;
-                dst = (T*)(p.y) + ((long)(n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 +
-                      (col - sp * c4);
-            }
+            T* dst = (T*)(p.y) + out_off(m, col);
             uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
             if (p.accumulate) {
                 float a[EPC], o[EPC];
@@ -1238,24 +1292,43 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     }
     if (p.stats) {
         float* red = (float*)(smem + EPI);    // [2 groups][BN][2]
+        if (p.bnbwd) {
+            // the lanes' partials into the wave's own staging rows (read above, wave-private), then channel c of the
+            // wave summed over its RPI row lanes in a fixed order
+            float* part = (float*)ep;                        // [64 lanes][2 * EPC]
 #pragma unroll
-        for (int b = 0; b < NB; ++b)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float s = csum[b][r], q = csq[b][r];
-                if constexpr (PP_DPP) {
-                    s = row16_sum(s);
-                    q = row16_sum(q);
-                } else {
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+            for (int e = 0; e < EPC; ++e) { part[lane * 2 * EPC + e] = bs8[e]; part[lane * 2 * EPC + EPC + e] = bq8[e]; }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane < WCOLS) {
+                const int cx = lane / EPC, e = lane - (lane / EPC) * EPC;
+                float s = 0.f, q = 0.f;
+                for (int r = 0; r < RPI; ++r) {
+                    s += part[(r * CPR + cx) * 2 * EPC + e];
+                    q += part[(r * CPR + cx) * 2 * EPC + EPC + e];
                 }
-                if (l16 == 0) {
-                    const int c = wc * WCOLS + b * 16 + lg * 4 + r;
-                    red[(grp * BN + c) * 2 + 0] = s;
-                    red[(grp * BN + c) * 2 + 1] = q;
-                }
+                red[(grp * BN + wc * WCOLS + lane) * 2 + 0] = s;
+                red[(grp * BN + wc * WCOLS + lane) * 2 + 1] = q;
             }
+        } else {
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float s = csum[b][r], q = csq[b][r];
+                    if constexpr (PP_DPP) {
+                        s = row16_sum(s);
+                        q = row16_sum(q);
+                    } else {
+#pragma unroll
+                        for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+                    }
+                    if (l16 == 0) {
+                        const int c = wc * WCOLS + b * 16 + lg * 4 + r;
+                        red[(grp * BN + c) * 2 + 0] = s;
+                        red[(grp * BN + c) * 2 + 1] = q;
+                    }
+                }
+        }
         __syncthreads();
         if (tid < BN) {
             const int col = nt * BN + tid;
@@ -1408,11 +1481,18 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
 
+    // Serpentine K order: every workgroup reads the whole 1.77-MB weight operand in K order, and by the time an XCD's
+    // next round of tiles starts, its 4-MB L2 has streamed that round's input rows too, so the first K-stages'
+    // weights are gone again (the ~150 MB of re-fetch in the PMC traffic).  Tiles of odd rounds (256 workgroups per
+    // round, 32 per XCD) walk K backwards, starting on the stages the previous round used last.  The fp32 summation
+    // order of those tiles changes; it is fixed per tile index, so every run gives the same bits.
+    const bool krev = p.kserp && ((blockIdx.x >> 8) & 1);
     struct StageArgs { int live, tap, adelta, bdelta; };
     auto stage_args = [&](int kt_req) {
         StageArgs a;
         a.live = kt_req < KT;
-        const int kt = min(kt_req, KT - 1);
+        int kt = min(kt_req, KT - 1);
+        kt = krev ? KT - 1 - kt : kt;
         const int chunk = kt / ph.ntaps, tap = kt - chunk * ph.ntaps;   // channel chunk outer, taps inner
         a.tap = tap;
         a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * BK) * 2;
@@ -2616,7 +2696,8 @@ static int halo64_taps(const GemmParams& p, int nphase, const scd_gemm_phase* ph
     const scd_gemm_phase& ph = phases[0];
     if (ph.ntaps != 9 || ph.rho_h || ph.rho_w || ph.Qh != p.Ho || ph.Qw != p.Wo || p.Hi != p.Ho || p.Wi != p.Wo)
         return -1;
-    if ((p.Wo != 128 && p.Wo != 64) || ph.Qh % (256 / p.Wo)) return -1;
+    if (p.Wo != 256 && p.Wo != 128 && p.Wo != 64) return -1;
+    if (p.Wo < 256 && ph.Qh % (256 / p.Wo)) return -1;
     int fwd = 1, bwd = 1;
     for (int t = 0; t < 9; ++t) {
         const int r = t / 3, c = t % 3;
@@ -2696,9 +2777,10 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     }
     if (p.bnbwd && dtype != SCD_DT_BF16) return SCD_ERR_ARG;   // BN-backward sums: 16-bit epilogues (caller falls back)
     {
-        // 3x3 / s1 / p1, 64 -> 64 channels on whole rows of 64 or 128 pixels: the persistent row-ring kernel
+        // 3x3 / s1 / p1, 64 -> 64 channels on whole rows of 64, 128 or 256 pixels: the persistent row-ring kernel
         const int flip = halo64_taps(p, nphase, phases);
         if (dtype == SCD_DT_BF16 && flip >= 0 && halo64_mode() && !p.bias && !p.relu) {
+            if (p.Wo == 256 && p.bnbwd) return SCD_ERR_ARG;    // scd_conv_gemm_bnbwd: this kernel + separate reduce
             p.ntn = 1;
             p.ph[0] = phases[0];
             for (int i = 0; i <= SCD_MAX_PHASES; ++i) p.tile_start[i] = 0;
@@ -2709,21 +2791,22 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
             const int tiles = (int)(Mtot / 256);
             hipStream_t st = (hipStream_t)stream;
             // `run` tiles per workgroup down one image (about one workgroup per CU)
-            const int tpi = p.Ho / (256 / p.Wo);
+            const int tpi = p.Wo >= 256 ? p.Ho : p.Ho / (256 / p.Wo);
             int run = 1;
             while (run < 16 && tpi % (2 * run) == 0 && tiles / (2 * run) >= num_cus()) run *= 2;
             const int grid = tiles / run;
 #define SCD_L1P_LAUNCH(WO)                                                                                              \
     do {                                                                                                                 \
-        if (p.bnbwd) {                                                                                                   \
-            if (flip) hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, true, true>), dim3(grid), dim3(512), 0, st, p, run);   \
-            else hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, false, true>), dim3(grid), dim3(512), 0, st, p, run);      \
+        if (WO != 256 && p.bnbwd) {                                                                                      \
+            if (flip) hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, true, WO != 256>), dim3(grid), dim3(512), 0, st, p, run); \
+            else hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, false, WO != 256>), dim3(grid), dim3(512), 0, st, p, run);    \
         } else {                                                                                                         \
             if (flip) hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, true, false>), dim3(grid), dim3(512), 0, st, p, run);  \
             else hipLaunchKernelGGL((conv_gemm_l1p_kernel<WO, false, false>), dim3(grid), dim3(512), 0, st, p, run);     \
         }                                                                                                                \
     } while (0)
-            if (p.Wo == 128) SCD_L1P_LAUNCH(128);
+            if (p.Wo == 256) SCD_L1P_LAUNCH(256);
+            else if (p.Wo == 128) SCD_L1P_LAUNCH(128);
             else SCD_L1P_LAUNCH(64);
 #undef SCD_L1P_LAUNCH
             SCD_RETURN_LAUNCH();
@@ -2783,6 +2866,11 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.bnbwd = 0; p.bny = nullptr; p.bn_mean = p.bn_invstd = p.bn_rsc = p.bn_rsh = nullptr;
     p.hid_keep = nullptr; p.hid_cols = 1 << 30;
     p.shuf = 0;
+    {
+        static int serp = -1;
+        if (serp < 0) { const char* e = getenv("SCD_HEADS_SERP"); serp = e ? atoi(e) : 1; }
+        p.kserp = serp;
+    }
     {
         static int dbg = -1;
         if (dbg < 0) { const char* e = getenv("SCD_GEMM_DEBUG"); dbg = e ? atoi(e) : 0; }

@@ -650,7 +650,7 @@ def test_conv_wgrad_layer1(case, dtype):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 # (tiles of 256 px >= 2 x CUs give runs of 2..16 tiles per workgroup: the row ring is reused; fewer: one tile each)
 @pytest.mark.parametrize("N,H,W", [(4, 128, 128), (3, 64, 64), (2, 32, 128), (16, 128, 128), (64, 64, 64),
-                                   (32, 128, 128)])
+                                   (32, 128, 128), (2, 32, 256), (8, 128, 256)])
 def test_conv_l1p_matches_register_staged(N, H, W, dtype, monkeypatch):
     """conv_gemm_l1p_kernel (layer1 3x3 64 -> 64: a persistent ring of input rows in LDS, every tap read at a
     constant displacement) runs the same MFMA sequence
