@@ -291,6 +291,7 @@ def main():
 
     from scdhip import ops
     from scdhip.flat import FlatAdam, FlatDDP
+    from scdhip.loss import mean_backward
     from trainer.dataset.syntheticSCD import SCD
     plugin = importlib.import_module("trainer.model." + args.model)
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.dtype]
@@ -333,8 +334,7 @@ def main():
         if prepare is not None:
             prepare(ys)
         loss, _ = lossfn(model(x, decode=False), ys)
-        loss = loss.mean()
-        loss.backward()
+        loss = mean_backward(loss)              # loss.mean(); loss.backward()
         opt.step()
         return loss
 

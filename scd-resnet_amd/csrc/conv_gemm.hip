@@ -1177,6 +1177,20 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
+    constexpr int CPR = WCOLS * 2 / 16;                      // 16-B chunks per staged row (8 or 6)
+    // output element offset of tile row `row` (< 128 of this group), channel `col` (M-range checked by the caller)
+    auto out_off = [&](int m, int col) -> long {
+        const int n = m / QQ;
+        const int rem = m - n * QQ;
+        const int qh = rem / ph.Qw;
+        const int qw = rem - qh * ph.Qw;
+        const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
+        if (p.shuf) {
+            const int c4 = p.Co >> 2, sp = col / c4;
+            return ((long)(n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 + (col - sp * c4);
+        }
+        return ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+    };
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
@@ -1202,20 +1216,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the staged tile is wave-private
-    constexpr int CPR = WCOLS * 2 / 16;                      // 16-B chunks per staged row (8 or 6)
-    // output element offset of tile row `row` (< 128 of this group), channel `col` (M-range checked by the caller)
-    auto out_off = [&](int m, int col) -> long {
-        const int n = m / QQ;
-        const int rem = m - n * QQ;
-        const int qh = rem / ph.Qw;
-        const int qw = rem - qh * ph.Qw;
-        const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
-        if (p.shuf) {
-            const int c4 = p.Co >> 2, sp = col / c4;
-            return ((long)(n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 + (col - sp * c4);
-        }
-        return ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
-    };
     // BN-backward mode (scd_conv_gemm_bnbwd: the output is the gradient of a following BN+ReLU layer): its backward
     // sums come from the stored gradient and the pre-BN activation, read in the store phase as whole 128-B row pieces
     // (lane: fixed 16-B channel chunk, RPI rows per pass) -- not as 8-B pieces per accumulator fragment
@@ -2867,9 +2867,9 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.hid_keep = nullptr; p.hid_cols = 1 << 30;
     p.shuf = 0;
     {
-        static int serp = -1;
-        if (serp < 0) { const char* e = getenv("SCD_HEADS_SERP"); serp = e ? atoi(e) : 1; }
-        p.kserp = serp;
+        // read per call (tests switch them to compare the variants)
+        const char* e = getenv("SCD_HEADS_SERP");
+        p.kserp = e ? atoi(e) : 1;
     }
     {
         static int dbg = -1;

@@ -35,6 +35,7 @@ from logger import Logger, monitorStdOutStream
 from scdhip import ops
 from scdhip.flat import FlatAdam, FlatDDP, FlatSGD
 from scdhip.graph import StepGraph
+from scdhip.loss import mean_backward
 
 torch.random.manual_seed(42)
 
@@ -262,8 +263,7 @@ class NetworkFactory(object):
     def _trainStep(self, xs, ys, **kwargs):
         self.optimizer.zero_grad()
         loss, lossStats = self._passParams(xs, ys, decode=False)
-        loss = loss.mean()
-        loss.backward()
+        loss = mean_backward(loss)          # loss.mean(); loss.backward() (scdhip.loss.mean_backward)
         self.optimizer.step()
         return loss, lossStats
 

@@ -14,6 +14,28 @@ from . import lib as L
 from . import ops
 
 
+_ONES = {}
+
+
+def mean_backward(loss):
+    """``loss = loss.mean(); loss.backward()`` of the reference step (networkFactory.py:257-263) without ATen launches
+    when the loss is one element (the fused losses return out[0:1]): the mean is then a view, and the seed gradient a
+    persistent 0-dim one (backward() would fill a fresh ones tensor and MeanBackward divide it by numel: three
+    small kernels on the critical path between the loss and the heads' backward).  Returns the 0-dim mean."""
+    if loss.numel() != 1:
+        m = loss.mean()
+        m.backward()
+        return m
+    m = loss.reshape(())
+    key = (m.device, m.dtype)
+    one = _ONES.get(key)
+    if one is None:
+        one = torch.ones((), dtype=m.dtype, device=m.device)
+        _ONES[key] = one
+    m.backward(one)
+    return m
+
+
 class CenterNetLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, heat, regr, off, gt_heat, mask, regr_t, inds, wr, wo):

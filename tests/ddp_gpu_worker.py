@@ -60,8 +60,10 @@ def main():
             for k, p in m.named_parameters()}
     wk = max(errs, key=errs.get)
     print("rank %d worst gradient-norm relative error %.2e (%s)" % (rank, errs[wk], wk), flush=True)
+    # fp32 parity mode: measured worst 8.5e-5 (W=2) and 9.5e-4 (W=4, the stem BN weight); 1e-2 through round 3
+    rtol = 1e-3 if world == 2 else 2e-3
     for k, p in m.named_parameters():
-        np.testing.assert_allclose(p.grad.double().norm().item(), float(g["gnorm|" + k]), rtol=1e-3, atol=1e-6,
+        np.testing.assert_allclose(p.grad.double().norm().item(), float(g["gnorm|" + k]), rtol=rtol, atol=1e-6,
                                    err_msg=k)
     # a second backward on the same batch launches gradient buckets during backward (FlatDDP learned the
     # hook kinds on the first one): the averaged gradients must not change

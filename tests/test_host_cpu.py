@@ -250,3 +250,19 @@ def test_flat_ddp_buckets_keep_a_small_tail():
     names = {id(p): n for n, p in m.named_parameters()}
     assert names[d._bucket_params[-1][-1]].startswith("preprocess")
     assert len(d._buckets) >= 3
+
+
+def test_mean_backward_matches_mean_then_backward():
+    """scdhip.loss.mean_backward (the step's loss.mean(); loss.backward() without ATen launches for a one-element
+    loss) gives the same value and gradients as the reference's two calls, for one- and many-element losses."""
+    from scdhip.loss import mean_backward
+    for shape in ((1,), (3,)):
+        w1 = torch.arange(1.0, 7.0, requires_grad=True)
+        w2 = w1.detach().clone().requires_grad_(True)
+        l1 = (w1.reshape(3, 2).sum(1) ** 2)[:shape[0]]
+        l2 = (w2.reshape(3, 2).sum(1) ** 2)[:shape[0]]
+        m1 = mean_backward(l1)
+        m2 = l2.mean()
+        m2.backward()
+        assert m1.shape == m2.shape == ()
+        assert torch.equal(m1.detach(), m2.detach()) and torch.equal(w1.grad, w2.grad)

@@ -208,6 +208,47 @@ def test_heads_fused_gemm(N, H, W, dtype):
     assert rel_err(nchw(hid), hid_ref) < TOL[dtype] * 2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_heads_serpentine_k_order(dtype, monkeypatch):
+    """conv_gemm_heads384_kernel walks K backwards on odd rounds of 256 workgroups (SCD_HEADS_SERP, weight reuse in
+    L2): 4 x 128^2 pixels = 342 tiles, so tiles 256.. take the reversed order.  Same hidden activation and head
+    outputs as the forward order up to fp32 summation order, and the same bits on every run."""
+    from scdhip import ops
+    L = ops.L
+    g = torch.Generator().manual_seed(77)
+    N, H, W, Cin, od = 4, 128, 128, 256, [1, 4, 2]
+    xg = nhwc(torch.randn(N, Cin, H, W, generator=g), dtype)
+    w0c = (torch.randn(384, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5).to(DEV)
+    wp = ops.pack_weight(w0c, dtype, 0)
+    b0c = (0.1 * torch.randn(384, generator=g)).to(DEV)
+    w1d = [(torch.randn(o, 128, 1, 1, generator=g) / 128 ** 0.5).to(DEV) for o in od]
+    b1d = [(0.1 * torch.randn(o, generator=g)).to(DEV) for o in od]
+
+    def run(serp):
+        monkeypatch.setenv("SCD_HEADS_SERP", str(serp))
+        outs = [torch.full((N, o, H, W), float("nan"), device=DEV) for o in od]
+        hid = torch.empty(N, H, W, 384, device=DEV, dtype=dtype)
+        L.call("scd_conv_gemm_heads", ops.dt(xg), ops.ptr(xg), ops.ptr(wp), ops.ptr(hid), ops.ptr(b0c), N, H, W,
+               Cin, len(od), L.int_array(od), L.ptr_array([w.data_ptr() for w in w1d]),
+               L.ptr_array([b.data_ptr() for b in b1d]), L.ptr_array([o.data_ptr() for o in outs]), ops.stream())
+        torch.cuda.synchronize()
+        return hid, outs
+
+    h0, o0 = run(0)
+    h1, o1 = run(1)
+    h2, o2 = run(1)
+    assert torch.equal(h1, h2) and all(torch.equal(a, b) for a, b in zip(o1, o2))
+    # workgroups 0..255 keep the forward order: their tiles (XCD-contiguous tile map of the kernel) have the same bits
+    nwg = (N * H * W + 191) // 192
+    q, r = nwg >> 3, nwg & 7
+    fwd_tiles = [(x * (q + 1) if x < r else r * (q + 1) + (x - r) * q) + (b >> 3) for b in range(256) for x in [b & 7]]
+    rows = torch.cat([torch.arange(t * 192, t * 192 + 192) for t in fwd_tiles]).to(DEV)
+    assert torch.equal(h1.view(-1, 384)[rows], h0.view(-1, 384)[rows])
+    assert rel_err(h1, h0) < 1e-2 and not torch.equal(h1, h0)
+    for a, b in zip(o1, o0):
+        assert rel_err(a, b) < 1e-4
+
+
 @pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("HW", [(128, 128), (9, 11)])
