@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 // fp16 compute mode (SCD_DT_F16).  The type-generic sources (conv_gemm, bn, layers, stem, pad) are compiled twice:
 // once as written (16-bit type __bf16, v_mfma_f32_16x16x32_bf16) and once with SCD_F16_BUILD, where the 16-bit type
@@ -11,6 +12,12 @@
 #ifdef SCD_F16_BUILD
 #define scd_conv_gemm scd_conv_gemm__f16
 #define scd_conv_gemm_bnbwd scd_conv_gemm_bnbwd__f16
+#define scd_conv_gemm_fin scd_conv_gemm_fin__f16
+#define scd_conv_gemm_bnbwd_fin scd_conv_gemm_bnbwd_fin__f16
+#define scd_stem_conv_fwd_fin scd_stem_conv_fwd_fin__f16
+#define scd_bn_bwd_reduce_fin scd_bn_bwd_reduce_fin__f16
+#define scd_bn_bwd_reduce2_fin scd_bn_bwd_reduce2_fin__f16
+#define scd_bn_fin_standalone scd_bn_fin_standalone__f16
 #define scd_conv_gemm_heads scd_conv_gemm_heads__f16
 #define scd_conv_gemm_heads_keep scd_conv_gemm_heads_keep__f16
 #define scd_conv_wgrad_workspace scd_conv_wgrad_workspace__f16
@@ -76,6 +83,11 @@
 #define SCD_F16_DECL(fn) extern "C" decltype(fn) fn##__f16;
 SCD_F16_DECL(scd_conv_gemm)
 SCD_F16_DECL(scd_conv_gemm_bnbwd)
+SCD_F16_DECL(scd_conv_gemm_fin)
+SCD_F16_DECL(scd_conv_gemm_bnbwd_fin)
+SCD_F16_DECL(scd_stem_conv_fwd_fin)
+SCD_F16_DECL(scd_bn_bwd_reduce_fin)
+SCD_F16_DECL(scd_bn_bwd_reduce2_fin)
 SCD_F16_DECL(scd_conv_gemm_heads)
 SCD_F16_DECL(scd_conv_gemm_heads_keep)
 SCD_F16_DECL(scd_conv_wgrad_nsplit2)
@@ -173,6 +185,112 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // fp64 atomic add (global_atomic_add_f64 on gfx950)
 __device__ __forceinline__ void atomic_add_f64(double* p, double v) { unsafeAtomicAdd(p, v); }
 __device__ __forceinline__ void atomic_add_f32(float* p, float v) { unsafeAtomicAdd(p, v); }
+
+// ---- BN finalize fused into the statistics producer (scd_bn_fin, include/scdhip.h) ----
+// The descriptor lives in device memory (written once by the caller); the kernels take its pointer plus the
+// statistics buffer they add into, and read the descriptor only in the tail -- so it costs the kernel body one
+// pointer argument, not twenty (kernel arguments are loaded into SGPRs up front: the by-value form spilled SGPRs in
+// the ping-pong GEMM and VGPRs in the BN reduce).
+struct BnFinDev {
+    const scd_bn_fin* f;      // device memory; NULL: the launch does not finalize
+    double* stats;            // the producer's statistics, [rep][2][ld]
+    int ld;
+};
+// replica a workgroup adds its statistics into: the first SCD_FIN_REPLICAS when the launch finalizes them itself
+__device__ __forceinline__ int stat_rep(const BnFinDev& d, int bid) {
+    return d.f ? bid % SCD_FIN_REPLICAS : bid % SCD_STAT_REPLICAS;
+}
+// Called by every remaining thread of every workgroup at its end: true in the last workgroup to arrive, once every
+// other workgroup's statistics atomics are visible (release fence before the count, acquire fence after it).
+__device__ __forceinline__ bool bn_fin_arrive(int* counter) {
+    __shared__ int fin_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) fin_last = atomicAdd(counter, 1) == (int)(gridDim.x * gridDim.y * gridDim.z) - 1;
+    __syncthreads();
+    const bool last = fin_last != 0;
+    if (last) __threadfence();
+    return last;
+}
+// The finalize of one layer by threads 0 .. nact-1 of the last workgroup: the replicas summed in a fixed order
+// (agent-scope loads: they were written by other XCDs' atomics) and re-zeroed, then bn_finalize_kernel's /
+// bn_bwd_finalize_kernel's arithmetic.
+__device__ __forceinline__ void bn_fin_compute(const scd_bn_fin* fp, double* stats, int ld, int nact,
+                                               int nrep = SCD_FIN_REPLICAS) {
+    const int C = fp->C;
+    const int bwd = fp->backward;
+    const double count = fp->count;
+    for (int c = threadIdx.x; c < C; c += nact) {
+        double* p0 = stats + c;
+        double s = 0.0, q = 0.0;
+        // 4 replicas (8 loads) in flight at a time: within the register budget of the BN kernels (BN_EW_WAVES)
+        for (int r0 = 0; r0 < nrep; r0 += 4) {
+            double vs[4], vq[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                vs[r] = __hip_atomic_load(p0 + (long)(2 * (r0 + r)) * ld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                vq[r] = __hip_atomic_load(p0 + (long)(2 * (r0 + r) + 1) * ld, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { s += vs[r]; q += vq[r]; }
+        }
+        for (int r = 0; r < nrep; ++r) {
+            p0[(long)(2 * r) * ld] = 0.0;
+            p0[(long)(2 * r + 1) * ld] = 0.0;
+        }
+        if (!bwd) {
+            const double mean = s / count;
+            double var = q / count - mean * mean;
+            if (var < 0.0) var = 0.0;
+            const float invstd = (float)(1.0 / sqrt(var + (double)fp->eps));
+            const float g = fp->gamma ? fp->gamma[c] : 1.f;
+            const float b = fp->beta ? fp->beta[c] : 0.f;
+            const float sc = g * invstd;
+            fp->mean[c] = (float)mean;
+            fp->invstd[c] = invstd;
+            fp->scale[c] = sc;
+            fp->shift[c] = b - (float)mean * sc;
+            if (fp->running_mean) {
+                const float m = fp->momentum;
+                const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+                fp->running_mean[c] = (1.f - m) * fp->running_mean[c] + m * (float)mean;
+                fp->running_var[c] = (1.f - m) * fp->running_var[c] + m * (float)unbiased;
+            }
+        } else {
+            if (fp->dgamma) fp->dgamma[c] += fp->gscale * (float)q;
+            if (fp->dbeta) fp->dbeta[c] += fp->gscale * (float)s;
+            const float g = fp->gamma ? fp->gamma[c] : 1.f;
+            const float is = fp->invstd[c];
+            const float sc = g * is;
+            const float k1 = (float)(s / count);
+            const float k2 = (float)(q / count);
+            fp->coef[c] = sc;
+            fp->coef[C + c] = -sc * is * k2;
+            fp->coef[2 * C + c] = -sc * k1 + sc * is * k2 * fp->mean[c];
+        }
+    }
+    if (threadIdx.x == 0 && !bwd && fp->num_batches) *fp->num_batches += 1;
+}
+// the tail of a producer (one layer; d1 != NULL: a second layer whose statistics the launch produced too, counted on
+// d0's counter); every remaining thread calls it at the kernel's end
+__device__ __forceinline__ void bn_fin_tail2(const BnFinDev& d0, const BnFinDev* d1, int nact) {
+    if (!d0.f) return;
+    int* counter = d0.f->counter;
+    if (!bn_fin_arrive(counter)) return;
+    bn_fin_compute(d0.f, d0.stats, d0.ld, nact);
+    if (d1 && d1->f) bn_fin_compute(d1->f, d1->stats, d1->ld, nact);
+    if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void bn_fin_tail(const BnFinDev& d, int nact) { bn_fin_tail2(d, nullptr, nact); }
+// host: the kernels' view of a `_fin` entry point's argument (off when fin == NULL)
+static inline BnFinDev bn_fin_dev(const scd_bn_fin* fin_dev, double* stats, int ld) {
+    BnFinDev d;
+    d.f = (fin_dev && stats) ? fin_dev : nullptr;
+    d.stats = stats;
+    d.ld = ld;
+    return d;
+}
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 

@@ -34,7 +34,7 @@ constexpr int PCOLS = SP * (FTW - 1) + KS + 1;      // 262 -> padded to an even 
 
 __global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
                                                             __bf16* __restrict__ y, double* __restrict__ stats,
-                                                            int H, int W, int Ho, int Wo) {
+                                                            int H, int W, int Ho, int Wo, BnFinDev fin) {
     constexpr int AT = FTH * FTW * 128;             // A tile [256 px][64 taps] bf16, 128-B rows
     constexpr int BT = CO * 128;                    // B tile [64 co][64 taps]
     constexpr int EROW = CO * 2 + 16;
@@ -170,11 +170,12 @@ __global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const float* __restr
             double s = 0.0, q = 0.0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) { s += red[(w * CO + tid) * 2]; q += red[(w * CO + tid) * 2 + 1]; }
-            const int rep = bid % SCD_STAT_REPLICAS;
+            const int rep = stat_rep(fin, bid);
             atomic_add_f64(stats + ((long)rep * 2 + 0) * CO + tid, s);
             atomic_add_f64(stats + ((long)rep * 2 + 1) * CO + tid, q);
         }
     }
+    bn_fin_tail(fin, 256);
 }
 
 // ---- weight gradient: ws[z][co][k] = sum over the split's pixels of dy[pix][co] * col[pix][k]
@@ -548,13 +549,18 @@ SCD_KERNEL_NS_END
 
 extern "C" int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H,
                                  int W, int Ho, int Wo, void* stream) {
-    SCD_F16_FWD(scd_stem_conv_fwd, x, wpk, y, stats, N, H, W, Ho, Wo, stream);
+    return scd_stem_conv_fwd_fin(dtype, x, wpk, y, stats, N, H, W, Ho, Wo, nullptr, stream);
+}
+
+extern "C" int scd_stem_conv_fwd_fin(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H,
+                                     int W, int Ho, int Wo, const scd_bn_fin* fin, void* stream) {
+    SCD_F16_FWD(scd_stem_conv_fwd_fin, x, wpk, y, stats, N, H, W, Ho, Wo, fin, stream);
     if (dtype != SCD_DT_BF16 || N <= 0 || Ho != (H + 2 * PD - KS) / SP + 1 || Wo != (W + 2 * PD - KS) / SP + 1 ||
-        Wo % FTW || Ho % FTH)
+        Wo % FTW || Ho % FTH || (fin && !stats))
         return SCD_ERR_ARG;
     const int blocks = N * (Ho / FTH) * (Wo / FTW);
     hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (const __bf16*)wpk,
-                       (__bf16*)y, stats, H, W, Ho, Wo);
+                       (__bf16*)y, stats, H, W, Ho, Wo, bn_fin_dev(fin, stats, CO));
     SCD_RETURN_LAUNCH();
 }
 

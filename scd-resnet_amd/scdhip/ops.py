@@ -8,6 +8,7 @@ import contextlib
 import ctypes
 import math
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -522,7 +523,7 @@ def pad_channels(t, C, Cp, rows):
 
 
 def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, stats=None, relu=False,
-          accumulate=False, bn_bwd=None):
+          accumulate=False, bn_bwd=None, fin=None):
     N, Hi, Wi, Ci = x.shape
     bk = 64 if x.dtype in HALF else 32
     if Ci % bk:
@@ -543,25 +544,32 @@ def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, sta
                out_stride, wpack.shape[1], len(phases), arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
                ptr(st.shift), ptr(bstats), stream())
         return y
+    if fin is not None:
+        # fin: FinForward -- the GEMM's last workgroup finalizes the BN statistics it accumulated
+        L.call("scd_conv_gemm_fin", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo,
+               Co, in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr,
+               fin.ptr(y.numel() // Co), stream())
+        return y
     L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
            in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr, stream())
     return y
 
 
-def conv_fwd(x, wpack, Co, kh, kw, stride, pad, bias=None, stats=None, relu=False, out=None):
-    """Conv2d forward (NHWC); wpack = pack_weight(w, mode=0)."""
+def conv_fwd(x, wpack, Co, kh, kw, stride, pad, bias=None, stats=None, relu=False, out=None, fin=None):
+    """Conv2d forward (NHWC); wpack = pack_weight(w, mode=0).  fin: FinForward of the BN the stats belong to."""
     _need_gpu(x)
     N, H, W, _ = x.shape
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
     if out is None:
         out = torch.empty(N, Ho, Wo, Co, dtype=x.dtype, device=x.device)
-    return _gemm(x, wpack, out, Co, Ho, Wo, stride, 1, _fwd_phase(kh, kw, pad, Ho, Wo), bias, stats, relu)
+    return _gemm(x, wpack, out, Co, Ho, Wo, stride, 1, _fwd_phase(kh, kw, pad, Ho, Wo), bias, stats, relu, fin=fin)
 
 
-def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumulate=False, stats=None, bn_bwd=None):
+def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumulate=False, stats=None, bn_bwd=None,
+               fin=None):
     """Input-gradient of Conv2d (NHWC) as a phase-decomposed gather-GEMM; wpack_t = pack_weight(w, mode=1).
-    Also ConvTranspose2d forward (with the transposed conv's geometry).  bn_bwd: see _gemm."""
+    Also ConvTranspose2d forward (with the transposed conv's geometry).  bn_bwd: see _gemm; fin: FinForward."""
     N = dy.shape[0]
     if out is None:
         out = torch.empty(N, Hc, Wc, Cin, dtype=dy.dtype, device=dy.device)
@@ -571,7 +579,8 @@ def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumula
         phases = [ph for ph in phases if ph.ntaps > 0]
         if not phases:
             return out
-    return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, phases, stats=stats, accumulate=accumulate, bn_bwd=bn_bwd)
+    return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, phases, stats=stats, accumulate=accumulate, bn_bwd=bn_bwd,
+                 fin=fin)
 
 
 class DgradS2:
@@ -598,13 +607,13 @@ def conv_dgrad_w(dy, w, Hc, Wc, stride, pad, out=None, accumulate=False):
                       accumulate=accumulate)
 
 
-def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None):
+def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None, fin=None):
     """ConvTranspose2d(k, stride, pad, output_padding=0) forward; wpack_t = pack_weight(W_t, mode=1)."""
     _need_gpu(x)
     N, H, W, _ = x.shape
     Ho = (H - 1) * stride - 2 * pad + k
     Wo = (W - 1) * stride - 2 * pad + k
-    return conv_dgrad(x, wpack_t, Cout, Ho, Wo, k, k, stride, pad, stats=stats)
+    return conv_dgrad(x, wpack_t, Cout, Ho, Wo, k, k, stride, pad, stats=stats, fin=fin)
 
 
 def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=False, bn_bwd=None):
@@ -966,8 +975,130 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
 # ------------------------------------------------------------------ BatchNorm (training)
 
 class BNState:
-    """Per-call BN quantities kept for backward."""
-    __slots__ = ("mean", "invstd", "scale", "shift", "count")
+    """Per-call BN quantities kept for backward (fin: they live in the module's persistent finalize buffers)."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "count", "fin", "owner", "__weakref__")
+
+    def __init__(self):
+        self.fin = False
+        self.owner = None
+
+
+# ---- BN finalize fused into its statistics producer (scd_bn_fin, include/scdhip.h)
+class BNFinalize:
+    """Training at world 1 (no SyncBN all-reduce between the statistics and their finalize): the producing kernel's
+    last workgroup finalizes (the _fin entry points) instead of a separate ~5-us launch per BN layer and direction.
+    The descriptor the kernels read lives in device memory, written when its fields change (the first step), so the
+    BN quantities it points at are persistent per module: a forward takes them only while no earlier forward's
+    quantities are still referenced by an autograd graph (else it falls back to fresh buffers and the separate
+    finalize).  SCD_BN_FIN_FUSE=0: off."""
+    enabled = os.environ.get("SCD_BN_FIN_FUSE", "1") != "0"
+
+
+class _FinSlot:
+    """One BN module and direction: the arrival counter, the device copy of the descriptor and its last bytes."""
+
+    def __init__(self, dev):
+        n = ctypes.sizeof(L.BnFin)
+        self.counter = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.dbuf = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.last = None
+        self.keep = []
+
+    def write(self, desc):
+        b = bytes(desc)
+        if b != self.last:
+            # rare (first step, a new batch size, a re-created .grad): a stream-ordered copy from pinned memory, kept
+            # alive until it has certainly run
+            host = torch.frombuffer(bytearray(b), dtype=torch.uint8).pin_memory()
+            self.dbuf.copy_(host, non_blocking=True)
+            self.keep = (self.keep + [host])[-4:]
+            self.last = b
+        return self.dbuf.data_ptr()
+
+
+def _fin_slot(bn, which):
+    slot = getattr(bn, "_scd_fin_" + which, None)
+    if slot is None or slot.dbuf.device != bn.weight.device:
+        slot = _FinSlot(bn.weight.device)
+        setattr(bn, "_scd_fin_" + which, slot)
+    return slot
+
+
+def _fin_ok(bn):
+    return (BNFinalize.enabled and bn.training and _BNSync.group is None and bn.weight is not None and
+            bn.weight.is_cuda and bn.momentum is not None)
+
+
+def _fin_release(ref, gen):
+    bn = ref()
+    if bn is not None and getattr(bn, "_scd_fin_busy", 0) == gen:
+        bn._scd_fin_busy = 0
+
+
+def fin_release(*sts):
+    """A Function's backward is done with its BN quantities: the module's persistent finalize buffers may serve the
+    next forward (also released when the BNState is garbage-collected, e.g. after a forward without backward)."""
+    for st in sts:
+        if st is not None and st.fin and st.owner is not None:
+            _fin_release(*st.owner)
+
+
+class FinForward:
+    """The forward finalize of `bn` fused into its statistics producer: ``ptr(count)`` is the scd_bn_fin argument of
+    the producing launch, ``st`` the BN quantities it writes."""
+
+    def __init__(self, bn, C):
+        self.bn, self.C = bn, C
+        buf = getattr(bn, "_scd_fin_st", None)
+        if buf is None or buf.numel() != 7 * C or buf.device != bn.weight.device:
+            buf = torch.empty(7 * C, device=bn.weight.device)     # mean, invstd, scale, shift | backward coef
+            bn._scd_fin_st = buf
+        st = BNState()
+        st.mean, st.invstd, st.scale, st.shift = buf[:C], buf[C:2 * C], buf[2 * C:3 * C], buf[3 * C:4 * C]
+        st.fin = True
+        gen = getattr(bn, "_scd_fin_gen", 0) + 1
+        bn._scd_fin_gen = gen
+        bn._scd_fin_busy = gen
+        st.owner = (weakref.ref(bn), gen)
+        weakref.finalize(st, _fin_release, weakref.ref(bn), gen)
+        self.st = st
+
+    def ptr(self, count):
+        bn, st = self.bn, self.st
+        st.count = count
+        d = L.BnFin()
+        slot = _fin_slot(bn, "fwd")
+        d.counter, d.backward, d.C, d.count = slot.counter.data_ptr(), 0, self.C, float(count)
+        d.gamma, d.beta = ptr(bn.weight), ptr(bn.bias)
+        d.running_mean, d.running_var = ptr(bn.running_mean), ptr(bn.running_var)
+        d.num_batches = ptr(bn.num_batches_tracked)
+        d.momentum, d.eps = float(bn.momentum), float(bn.eps)
+        d.mean, d.invstd, d.scale, d.shift = ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift)
+        return slot.write(d)
+
+
+def fin_forward(bn, C):
+    """A FinForward for a training BN whose statistics producer can finalize them (world 1), else None."""
+    if not _fin_ok(bn) or getattr(bn, "_scd_fin_busy", 0):
+        return None
+    return FinForward(bn, C)
+
+
+def fin_backward(bn, st, C, alpha):
+    """(descriptor pointer, coef) for the backward finalize of `bn` fused into its backward-sum producer, or None:
+    only for BN quantities of a fused forward (persistent buffers; the coefficients go to the same buffer)."""
+    if not (getattr(st, "fin", False) and _fin_ok(bn)):
+        return None
+    coef = bn._scd_fin_st[4 * C:7 * C]
+    d = L.BnFin()
+    slot = _fin_slot(bn, "bwd")
+    d.counter, d.backward, d.C, d.count = slot.counter.data_ptr(), 1, C, float(st.count)
+    d.gamma = ptr(bn.weight)
+    d.mean, d.invstd = ptr(st.mean), ptr(st.invstd)
+    d.dgamma, d.dbeta = ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias))
+    d.gscale = float(alpha)
+    d.coef = ptr(coef)
+    return slot.write(d), coef
 
 
 def bn_finalize(bn, stats, C, count, training=True):
@@ -1031,11 +1162,20 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None)
     stats: the backward sums already accumulated by the producing GEMM (take_bn_bwd_fused)."""
     C = y.shape[-1]
     rsc, rsh = (ptr(st.scale), ptr(st.shift)) if (relu and mask is None) else (0, 0)
+    coef = None
     if stats is None:
         stats = bn_stats(bn, "bwd")
-        L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd), C,
-               y.numel(), ptr(stats), stream())
-    coef = bn_backward_coef(bn, st, stats, C, grad_alpha(y))
+        fin = fin_backward(bn, st, C, grad_alpha(y))
+        if fin is not None:
+            # the reduce's last workgroup finalizes (scd_bn_bwd_reduce_fin): dgamma / dbeta and the coefficients
+            L.call("scd_bn_bwd_reduce_fin", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean),
+                   ptr(st.invstd), C, y.numel(), ptr(stats), fin[0], stream())
+            coef = fin[1]
+        else:
+            L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd),
+                   C, y.numel(), ptr(stats), stream())
+    if coef is None:
+        coef = bn_backward_coef(bn, st, stats, C, grad_alpha(y))
     dy = torch.empty_like(y)
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),
            ptr(dz_out), stream())
@@ -1057,12 +1197,21 @@ def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
         return (bn_backward(bn_a, st_a, dout, y_a, mask=mask), bn_backward(bn_b, st_b, dout, y_b, mask=mask))
     C = y_a.shape[-1]
     sa, sb = bn_stats(bn_a, "bwd"), bn_stats(bn_b, "bwd")
-    L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean), ptr(st_a.invstd),
-           ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
     alpha = grad_alpha(y_a)
-    sa, sb, nrep = _allreduce_stats_pair(sa, C, sb, C)
-    ca = _bn_bwd_finalize_launch(bn_a, st_a, sa, nrep, C, alpha)
-    cb = _bn_bwd_finalize_launch(bn_b, st_b, sb, nrep, C, alpha)
+    fa = fin_backward(bn_a, st_a, C, alpha)
+    fb = fin_backward(bn_b, st_b, C, alpha) if fa is not None else None
+    if fa is not None and fb is not None:
+        # both finalizes by the reduce's last workgroup (scd_bn_bwd_reduce2_fin)
+        L.call("scd_bn_bwd_reduce2_fin", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean),
+               ptr(st_a.invstd), ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), fa[0], fb[0],
+               stream())
+        ca, cb = fa[1], fb[1]
+    else:
+        L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean),
+               ptr(st_a.invstd), ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
+        sa, sb, nrep = _allreduce_stats_pair(sa, C, sb, C)
+        ca = _bn_bwd_finalize_launch(bn_a, st_a, sa, nrep, C, alpha)
+        cb = _bn_bwd_finalize_launch(bn_b, st_b, sb, nrep, C, alpha)
     dya, dyb = torch.empty_like(y_a), torch.empty_like(y_b)
     L.call("scd_bn_bwd_apply2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(ca), ptr(cb), C, y_a.numel(),
            ptr(dya), ptr(dyb), stream())
@@ -1110,12 +1259,17 @@ def stem_direct_ok(x, dtype):
     return dtype in HALF and Wo % 128 == 0 and Ho % 2 == 0
 
 
-def stem_conv_fwd(x, wpk, stats=None):
-    """Conv2d(1,64,7,s2,p3) of NCHW fp32 x -> (N,Ho,Wo,64) bf16 NHWC (+BN sums); wpk = pack_weight(w, bf16, 0, ldp=64)."""
+def stem_conv_fwd(x, wpk, stats=None, fin=None):
+    """Conv2d(1,64,7,s2,p3) of NCHW fp32 x -> (N,Ho,Wo,64) bf16 NHWC (+BN sums); wpk = pack_weight(w, bf16, 0, ldp=64).
+    fin: FinForward of the stem BN (its finalize by the conv's last workgroup)."""
     _need_gpu(x)
     N, _, H, W = x.shape
     Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
     y = torch.empty(N, Ho, Wo, 64, dtype=wpk.dtype, device=x.device)
+    if fin is not None:
+        L.call("scd_stem_conv_fwd_fin", dt(wpk), ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo,
+               fin.ptr(N * Ho * Wo), stream())
+        return y
     L.call("scd_stem_conv_fwd", dt(wpk), ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo, stream())
     return y
 

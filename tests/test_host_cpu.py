@@ -43,6 +43,27 @@ def test_gemm_phase_struct_matches_header():
     assert ctypes.sizeof(L.GemmPhase) == 4 * (5 + 3 * L.MAX_TAPS)
 
 
+def test_bn_fin_struct_matches_header(tmp_path):
+    """ctypes scd_bn_fin (scdhip.lib.BnFin) has the C layout of include/scdhip.h: field offsets and size from a C
+    program compiled against the header with gcc."""
+    import ctypes
+    import subprocess
+
+    import scdhip.lib as L
+    names = [f[0] for f in L.BnFin._fields_]
+    src = tmp_path / "fin.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "scdhip.h"\nint main(void){printf("%zu",'
+                   ' sizeof(scd_bn_fin));' + "".join('printf(" %%zu", offsetof(scd_bn_fin, %s));' % n for n in names)
+                   + "return 0;}\n")
+    exe = tmp_path / "fin"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(L.BnFin)
+    assert vals[1:] == [getattr(L.BnFin, n).offset for n in names]
+    m = re.search(r"#define SCD_FIN_REPLICAS (\d+)", open(HEADER).read())
+    assert int(m.group(1)) == L.FIN_REPLICAS
+
+
 def test_workspace_queries():
     import scdhip.lib as L
     assert L.lib().scd_conv_wgrad_workspace(128, 9, 64, 4) == 4 * 128 * 9 * 64 * 4

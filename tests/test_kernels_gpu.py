@@ -38,6 +38,7 @@ CONV_CASES = [  # N, Cin, H, W, Cout, k, stride, pad
     (3, 64, 41, 37, 192, 3, 2, 1),      # ragged pixels / channels on the ring kernels
     (2, 192, 11, 13, 256, 3, 1, 1),     # 27 K stages (odd) over the intra-workgroup split-K kernel, ragged M
     (4, 512, 16, 16, 512, 3, 1, 1),     # layer4 conv2 shape at batch 4: split K, 72 stages
+    (4, 256, 128, 128, 64, 1, 1, 0),    # 1x1 into 64 channels over 256 tiles: the ring kernel, half-empty tiles
 ]
 
 
@@ -597,6 +598,7 @@ BNBWD_CASES = [
     (4, 128, 128, 384, 256, 3, 1, 1, True),      # heads / deconv shapes: one 3x3 phase
     (2, 40, 36, 384, 256, 3, 1, 1, False),       # too few tiles: GEMM + separate reduce
     (4, 128, 128, 64, 256, 1, 1, 0, True),       # Bottleneck conv1 1x1 (256 -> 64) dgrad
+    (4, 128, 128, 256, 64, 1, 1, 0, False),      # Bottleneck conv3 1x1 (64 -> 256) dgrad into 64 channels: ring
     (4, 128, 128, 256, 256, 3, 2, 1, True),      # Bottleneck stride-2 3x3: 4 sub-pixel phases, out_stride 2
     (4, 128, 128, 512, 256, 1, 2, 0, True),      # downsample 1x1 stride 2: one phase with taps, three empty
     (16, 66, 70, 128, 192, 3, 2, 1, True),       # ragged phases (odd/even extents), 192-wide tiles
