@@ -326,8 +326,6 @@ class ConvBNFn(torch.autograd.Function):
 
 
 _HEADS_WGRAD_LATE = os.environ.get("SCD_HEADS_WGRAD_LATE", "1") == "1"
-# the heads' weight gradient issued after the deconv BN backward apply that follows (SCD_HEADS_WGRAD_AFTER_BN=1)
-_HEADS_WGRAD_AFTER_BN = os.environ.get("SCD_HEADS_WGRAD_AFTER_BN", "0") == "1"
 
 
 class HeadsFn(torch.autograd.Function):
@@ -510,12 +508,6 @@ class HeadsFn(torch.autograd.Function):
         mods = [m for h in heads for m in h if isinstance(m, torch.nn.Module)]
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
-        if late and fuse and _HEADS_WGRAD_AFTER_BN and dev.type == "cuda":
-            # after the deconv BN's backward apply (the next thing the compute stream runs), so the side stream's
-            # one-workgroup-per-CU GEMM does not hold the CUs that HBM pass needs; the gradients are reported ready
-            # (FlatDDP buckets) only once their GEMMs are enqueued
-            ops.defer_until_next_bn_apply(lambda: (wgrads(), grads_ready(*mods)))
-            return dfeat, None, None
         if late:
             wgrads()             # side stream ordered after the input gradient: it overlaps the deconv backward
         grads_ready(*mods)

@@ -890,31 +890,9 @@ def _new_side_stream(idx):
 
 def join_side_streams():
     """Make every device's compute stream wait for its side stream (end of backward)."""
-    _run_deferred(join=False)
     for idx, s in _Side.streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
     _Side.joined_task.clear()
-
-
-_DEFERRED = []
-
-
-def defer_until_next_bn_apply(fn):
-    """Run fn (a side-stream launch) right after the next BN backward apply is enqueued on the compute stream, so
-    that the side stream's workgroups do not hold the CUs that apply pass needs (HeadsFn: the heatmap head's weight
-    gradient after the deconv3 BN backward apply).  If no apply follows in this backward pass, fn runs at its end,
-    before the side streams are joined."""
-    _DEFERRED.append(fn)
-    torch.autograd.Variable._execution_engine.queue_callback(lambda: _run_deferred(join=True))
-
-
-def _run_deferred(join):
-    ran = False
-    while _DEFERRED:
-        _DEFERRED.pop(0)()
-        ran = True
-    if ran and join:
-        join_side_streams()
 
 
 def side_stream_for_comm(dev):
@@ -1179,8 +1157,6 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None)
     dy = torch.empty_like(y)
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),
            ptr(dz_out), stream())
-    if _DEFERRED:
-        _run_deferred(join=False)
     return dy
 
 

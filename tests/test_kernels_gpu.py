@@ -246,8 +246,11 @@ def test_heads_serpentine_k_order(dtype, monkeypatch):
     rows = torch.cat([torch.arange(t * 192, t * 192 + 192) for t in fwd_tiles]).to(DEV)
     assert torch.equal(h1.view(-1, 384)[rows], h0.view(-1, 384)[rows])
     assert rel_err(h1, h0) < 1e-2 and not torch.equal(h1, h0)
+    # the 1x1 tails read the hidden activation rounded to the 16-bit type, so a summation-order change in the 3x3 GEMM
+    # moves a head output by up to one rounding of the hidden value (measured 8.3e-4 bf16, 1.4e-4 fp16, normwise)
+    tol = 2e-3 if dtype == torch.bfloat16 else 3e-4
     for a, b in zip(o1, o0):
-        assert rel_err(a, b) < 1e-4
+        assert rel_err(a, b) < tol
 
 
 @pytest.mark.parametrize("packed", [False, True])

@@ -20,6 +20,7 @@ def main():
     a = ap.parse_args()
     import trainer.model.centerOffsetRes10 as plugin
     from scdhip.flat import FlatAdam
+    from scdhip.loss import mean_backward
     from trainer.dataset.syntheticSCD import SCD
     dev = torch.device("cuda", 0)
     model = plugin.model(**plugin.modelParams).to(dev).set_compute_dtype(torch.bfloat16).train()
@@ -31,8 +32,7 @@ def main():
     def step():
         opt.zero_grad()
         loss, _ = plugin.loss(model(x, decode=False), ys)
-        loss = loss.mean()
-        loss.backward()
+        loss = mean_backward(loss)
         opt.step()
         return loss
 

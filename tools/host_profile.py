@@ -29,6 +29,7 @@ def main():
         torch.autograd.set_multithreading_enabled(False)
 
     from scdhip.flat import FlatAdam
+    from scdhip.loss import mean_backward
     from trainer.dataset.syntheticSCD import SCD
     plugin = importlib.import_module("trainer.model.centerOffsetRes10")
     dev = torch.device("cuda", 0)
@@ -44,7 +45,7 @@ def main():
         opt.zero_grad()
         lossfn.prepare(ys)
         loss, _ = lossfn(model(x, decode=False), ys)
-        loss.mean().backward()
+        mean_backward(loss)
         opt.step()
 
     for _ in range(3):
