@@ -210,7 +210,9 @@ int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk, const floa
  * (several channel-slice launches) runs scd_bn_fin_standalone after itself, so the result never depends on the path.
  * The statistics buffer is the producer's own stats argument ([SCD_STAT_REPLICAS][2][C]; a fusing launch uses the
  * first SCD_FIN_REPLICAS).  C must equal the producer's channel count; the fields are not checked on the host. */
+#ifndef SCD_FIN_REPLICAS
 #define SCD_FIN_REPLICAS 16
+#endif
 typedef struct scd_bn_fin {
     int* counter;              /* one int, zero between launches (device memory) */
     int backward;              /* 0: forward statistics, 1: backward sums */

@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply2_kernel(const T
 // the finalize of a scd_bn_fin descriptor (device memory) over all SCD_STAT_REPLICAS replicas, as its own launch: what a
 // _fin entry point runs when its producer path could not finalize in its last workgroup
 __global__ __launch_bounds__(1024) void bn_fin_standalone_kernel(const scd_bn_fin* fin, double* stats, int ld) {
-    bn_fin_compute(fin, stats, ld, blockDim.x, SCD_STAT_REPLICAS);
+    bn_fin_compute<SCD_STAT_REPLICAS>(fin, stats, ld, blockDim.x);
 }
 
 // elementwise BN kernels keep one channel chunk per thread: the grid stride (grid * 256 threads) must be a

@@ -191,6 +191,11 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) { unsafeAtomic
 // statistics buffer they add into, and read the descriptor only in the tail -- so it costs the kernel body one
 // pointer argument, not twenty (kernel arguments are loaded into SGPRs up front: the by-value form spilled SGPRs in
 // the ping-pong GEMM and VGPRs in the BN reduce).
+// SCD_FIN_ABL (timing-only ablation builds, `make variant`; never the product): 1 = the last workgroup skips the
+// finalize arithmetic, 2 = no vmcnt drain before the arrival count
+#ifndef SCD_FIN_ABL
+#define SCD_FIN_ABL 0
+#endif
 struct BnFinDev {
     const scd_bn_fin* f;      // device memory; NULL: the launch does not finalize
     double* stats;            // the producer's statistics, [rep][2][ld]
@@ -208,7 +213,9 @@ __device__ __forceinline__ int stat_rep(const BnFinDev& d, int bid) {
 // writes back the XCD's whole L2 every time and made the producers 1.2-10x slower.
 __device__ __forceinline__ bool bn_fin_arrive(int* counter) {
     __shared__ int fin_last;
+#if SCD_FIN_ABL != 2
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     __syncthreads();
     if (threadIdx.x == 0)
         fin_last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -219,27 +226,29 @@ __device__ __forceinline__ bool bn_fin_arrive(int* counter) {
 // The finalize of one layer by threads 0 .. nact-1 of the last workgroup: the replicas summed in a fixed order
 // (agent-scope loads: they were written by other XCDs' atomics) and re-zeroed, then bn_finalize_kernel's /
 // bn_bwd_finalize_kernel's arithmetic.
-__device__ __forceinline__ void bn_fin_compute(const scd_bn_fin* fp, double* stats, int ld, int nact,
-                                               int nrep = SCD_FIN_REPLICAS) {
+template <int NREP = SCD_FIN_REPLICAS>
+__device__ __forceinline__ void bn_fin_compute(const scd_bn_fin* fp, double* stats, int ld, int nact) {
     const int C = fp->C;
     const int bwd = fp->backward;
     const double count = fp->count;
+    // CH replicas (2 CH loads) in flight at a time: within the register budget of the BN kernels (BN_EW_WAVES)
+    constexpr int CH = NREP < 4 ? NREP : 4;
+    static_assert(NREP % CH == 0, "replica count");
     for (int c = threadIdx.x; c < C; c += nact) {
         double* p0 = stats + c;
         double s = 0.0, q = 0.0;
-        // 4 replicas (8 loads) in flight at a time: within the register budget of the BN kernels (BN_EW_WAVES)
-        for (int r0 = 0; r0 < nrep; r0 += 4) {
-            double vs[4], vq[4];
+        for (int r0 = 0; r0 < NREP; r0 += CH) {
+            double vs[CH], vq[CH];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < CH; ++r) {
                 vs[r] = __hip_atomic_load(p0 + (long)(2 * (r0 + r)) * ld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 vq[r] = __hip_atomic_load(p0 + (long)(2 * (r0 + r) + 1) * ld, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) { s += vs[r]; q += vq[r]; }
+            for (int r = 0; r < CH; ++r) { s += vs[r]; q += vq[r]; }
         }
-        for (int r = 0; r < nrep; ++r) {
+        for (int r = 0; r < NREP; ++r) {
             p0[(long)(2 * r) * ld] = 0.0;
             p0[(long)(2 * r + 1) * ld] = 0.0;
         }
@@ -282,8 +291,10 @@ __device__ __forceinline__ void bn_fin_tail2(const BnFinDev& d0, const BnFinDev*
     if (!d0.f) return;
     int* counter = d0.f->counter;
     if (!bn_fin_arrive(counter)) return;
+#if SCD_FIN_ABL != 1
     bn_fin_compute(d0.f, d0.stats, d0.ld, nact);
     if (d1 && d1->f) bn_fin_compute(d1->f, d1->stats, d1->ld, nact);
+#endif
     if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void bn_fin_tail(const BnFinDev& d, int nact) { bn_fin_tail2(d, nullptr, nact); }

@@ -183,7 +183,9 @@ def check(rc, name):
 
 
 def call(name, *args):
-    check(getattr(lib(), name)(*args), name)
+    rc = getattr(_LIB or lib(), name)(*args)
+    if rc:
+        check(rc, name)
 
 
 def ptr_array(ptrs):

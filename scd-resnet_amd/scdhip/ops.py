@@ -477,20 +477,49 @@ def pack_weight(w, dtype, mode, ldp=None, out=None, row_off=0, _cache=True):
 
 # ------------------------------------------------------------------ gather-GEMM convolution
 
+class _Phases:
+    """A GEMM's phase descriptors as the ctypes array the C-ABI takes (built once per geometry and reused: the
+    launches of a step would otherwise rebuild ~40 of them in Python)."""
+    __slots__ = ("arr", "n", "list")
+
+    def __init__(self, phases):
+        self.list = phases
+        self.n = len(phases)
+        self.arr = (L.GemmPhase * max(1, self.n))(*phases)
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        return iter(self.list)
+
+
+_PHASES = {}
+
+
 def _fwd_phase(kh, kw, pad, Ho, Wo):
-    ph = L.GemmPhase()
-    ph.Qh, ph.Qw, ph.rho_h, ph.rho_w = Ho, Wo, 0, 0
-    ph.ntaps = kh * kw
-    for r in range(kh):
-        for s in range(kw):
-            t = r * kw + s
-            ph.dh[t], ph.dw[t], ph.wt[t] = r - pad, s - pad, t
-    return [ph]
+    key = ("f", kh, kw, pad, Ho, Wo)
+    ps = _PHASES.get(key)
+    if ps is None:
+        ph = L.GemmPhase()
+        ph.Qh, ph.Qw, ph.rho_h, ph.rho_w = Ho, Wo, 0, 0
+        ph.ntaps = kh * kw
+        for r in range(kh):
+            for s in range(kw):
+                t = r * kw + s
+                ph.dh[t], ph.dw[t], ph.wt[t] = r - pad, s - pad, t
+        ps = _PHASES[key] = _Phases([ph])
+    return ps
 
 
-def _dgrad_phases(kh, kw, stride, pad, Hc, Wc):
+def _dgrad_phases(kh, kw, stride, pad, Hc, Wc, nonempty=False):
     """Sub-pixel decomposition of the input-gradient of Conv2d(kh,kw,stride,pad) whose input is
-    (Hc,Wc): output pixel st*q+rho gathers dy at q + (rho+pad-r)/st for taps r = rho+pad (mod st)."""
+    (Hc,Wc): output pixel st*q+rho gathers dy at q + (rho+pad-r)/st for taps r = rho+pad (mod st).
+    nonempty: without the phases that have no taps."""
+    key = ("d", kh, kw, stride, pad, Hc, Wc, nonempty)
+    ps = _PHASES.get(key)
+    if ps is not None:
+        return ps
     phases = []
     for rh in range(stride):
         for rw in range(stride):
@@ -507,8 +536,10 @@ def _dgrad_phases(kh, kw, stride, pad, Hc, Wc):
                 ph.dh[t] = (rh + pad - r) // stride
                 ph.dw[t] = (rw + pad - s) // stride
                 ph.wt[t] = r * kw + s
-            phases.append(ph)
-    return phases
+            if ph.ntaps > 0 or not nonempty:
+                phases.append(ph)
+    ps = _PHASES[key] = _Phases(phases)
+    return ps
 
 
 def _c(t):
@@ -535,23 +566,23 @@ def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, sta
         x = pad_channels(_c(x), Ci, Cp, N * Hi * Wi).view(N, Hi, Wi, Cp)
         wpack = pad_channels(wpack, Ci, Cp, wpack.shape[0] * T).view(wpack.shape[0], T * Cp)
         Ci = Cp
-    arr = (L.GemmPhase * len(phases))(*phases)
+    arr, nph = phases.arr, phases.n
     if bn_bwd is not None:
         # bn_bwd = (st, y_pre_bn, stats): the next BN+ReLU layer's backward sums from the GEMM epilogue
         st, ybn, bstats = bn_bwd
         assert bias is None and stats is None and not relu and not accumulate
         L.call("scd_conv_gemm_bnbwd", dt(x), ptr(x), ptr(wpack), ptr(y), N, Hi, Wi, Ci, Ho, Wo, Co, in_stride,
-               out_stride, wpack.shape[1], len(phases), arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
+               out_stride, wpack.shape[1], nph, arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
                ptr(st.shift), ptr(bstats), stream())
         return y
     if fin is not None:
         # fin: FinForward -- the GEMM's last workgroup finalizes the BN statistics it accumulated
         L.call("scd_conv_gemm_fin", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo,
-               Co, in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr,
+               Co, in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), nph, arr,
                fin.ptr(y.numel() // Co), stream())
         return y
     L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
-           in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), len(phases), arr, stream())
+           in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), nph, arr, stream())
     return y
 
 
@@ -573,12 +604,10 @@ def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumula
     N = dy.shape[0]
     if out is None:
         out = torch.empty(N, Hc, Wc, Cin, dtype=dy.dtype, device=dy.device)
-    phases = _dgrad_phases(kh, kw, stride, pad, Hc, Wc)
-    if accumulate:
-        # sub-pixel phases without taps (a 1x1 stride-2 conv reaches one pixel in four) would only add zeros
-        phases = [ph for ph in phases if ph.ntaps > 0]
-        if not phases:
-            return out
+    # accumulating: sub-pixel phases without taps (a 1x1 stride-2 conv reaches one pixel in four) would only add zeros
+    phases = _dgrad_phases(kh, kw, stride, pad, Hc, Wc, nonempty=accumulate)
+    if not phases.n:
+        return out
     return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, phases, stats=stats, accumulate=accumulate, bn_bwd=bn_bwd,
                  fin=fin)
 
@@ -929,13 +958,17 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
     N, Ho, Wo, Cg = g.shape
     _, Hi, Wi, Ci = x.shape
     T = kh * kw
-    dh = L.int_array([r - pad for r in range(kh) for s in range(kw)])
-    dw = L.int_array([s - pad for r in range(kh) for s in range(kw)])
-    M = N * Ho * Wo
-    ns = L.lib().scd_conv_wgrad_nsplit2(dt(g), M, Ho, Wo, Cg, T, Ci)
-    ws = torch.empty(L.lib().scd_conv_wgrad_workspace(Cg, T, Ci, ns) // 4, dtype=torch.float32, device=g.device)
-    L.call("scd_conv_wgrad", dt(g), ptr(g), ptr(x), ptr(ws), ns, N, Ho, Wo, Cg, Hi, Wi, Ci, stride, T, dh, dw,
-           stream())
+    d = dt(g)
+    key = (d, N, Ho, Wo, Cg, Ci, kh, kw, pad)
+    plan = _WGRAD_PLANS.get(key)
+    if plan is None:
+        dh = L.int_array([r - pad for r in range(kh) for s in range(kw)])
+        dw = L.int_array([s - pad for r in range(kh) for s in range(kw)])
+        ns = L.lib().scd_conv_wgrad_nsplit2(d, N * Ho * Wo, Ho, Wo, Cg, T, Ci)
+        plan = _WGRAD_PLANS[key] = (dh, dw, ns, L.lib().scd_conv_wgrad_workspace(Cg, T, Ci, ns) // 4)
+    dh, dw, ns, wsn = plan
+    ws = torch.empty(wsn, dtype=torch.float32, device=g.device)
+    L.call("scd_conv_wgrad", d, ptr(g), ptr(x), ptr(ws), ns, N, Ho, Wo, Cg, Hi, Wi, Ci, stride, T, dh, dw, stream())
     if rows is None:
         rows = [(0, Cg, dst, ld)]
     # red_taps: read the T*Ci workspace columns as red_taps taps of T*Ci/red_taps channels (a 1x1 GEMM over
@@ -944,10 +977,23 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
     cv = Cr if cvalid is None else cvalid
     for i in range(0, len(rows), 4):      # up to four row slices per reduce launch
         part = rows[i:i + 4]
-        L.call("scd_wgrad_reduce_rows", ptr(ws), ns, Cg, Tr, Cr, len(part), L.int_array([r[0] for r in part]),
-               L.int_array([r[1] for r in part]), L.long_array([r[3][0] for r in part]),
-               L.long_array([r[3][1] for r in part]), L.long_array([r[3][2] for r in part]),
-               L.ptr_array([ptr(r[2]) for r in part]), cv, int(accumulate), grad_alpha(g), stream())
+        rkey = tuple((r[0], r[1], ptr(r[2]), tuple(r[3])) for r in part)
+        arrs = _WGRAD_ROWS.get(rkey)
+        if arrs is None:
+            if len(_WGRAD_ROWS) > 4096:
+                _WGRAD_ROWS.clear()
+            arrs = _WGRAD_ROWS[rkey] = (
+                L.int_array([r[0] for r in part]), L.int_array([r[1] for r in part]),
+                L.long_array([r[3][0] for r in part]), L.long_array([r[3][1] for r in part]),
+                L.long_array([r[3][2] for r in part]), L.ptr_array([ptr(r[2]) for r in part]))
+        L.call("scd_wgrad_reduce_rows", ptr(ws), ns, Cg, Tr, Cr, len(part), *arrs, cv, int(accumulate), grad_alpha(g),
+               stream())
+
+
+# geometry -> (dh, dw, split count, workspace floats); (row slices) -> the reduce's argument arrays (keyed by the
+# destination pointers, which are views of the persistent flat gradient buffer)
+_WGRAD_PLANS = {}
+_WGRAD_ROWS = {}
 
 
 # ------------------------------------------------------------------ BatchNorm (training)
@@ -979,7 +1025,9 @@ class _FinSlot:
         n = ctypes.sizeof(L.BnFin)
         self.counter = torch.zeros(1, dtype=torch.int32, device=dev)
         self.dbuf = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.dptr = self.dbuf.data_ptr()
         self.last = None
+        self.key = None
         self.keep = []
 
     def write(self, desc):
@@ -991,7 +1039,7 @@ class _FinSlot:
             self.dbuf.copy_(host, non_blocking=True)
             self.keep = (self.keep + [host])[-4:]
             self.last = b
-        return self.dbuf.data_ptr()
+        return self.dptr
 
 
 def _fin_slot(bn, which):
@@ -1027,31 +1075,38 @@ class FinForward:
 
     def __init__(self, bn, C):
         self.bn, self.C = bn, C
-        buf = getattr(bn, "_scd_fin_st", None)
-        if buf is None or buf.numel() != 7 * C or buf.device != bn.weight.device:
+        views = getattr(bn, "_scd_fin_views", None)
+        if views is None or views[0].numel() != 7 * C or views[0].device != bn.weight.device:
             buf = torch.empty(7 * C, device=bn.weight.device)     # mean, invstd, scale, shift | backward coef
             bn._scd_fin_st = buf
+            views = bn._scd_fin_views = (buf, buf[:C], buf[C:2 * C], buf[2 * C:3 * C], buf[3 * C:4 * C])
         st = BNState()
-        st.mean, st.invstd, st.scale, st.shift = buf[:C], buf[C:2 * C], buf[2 * C:3 * C], buf[3 * C:4 * C]
+        st.mean, st.invstd, st.scale, st.shift = views[1:]
         st.fin = True
         gen = getattr(bn, "_scd_fin_gen", 0) + 1
         bn._scd_fin_gen = gen
         bn._scd_fin_busy = gen
         st.owner = (weakref.ref(bn), gen)
-        weakref.finalize(st, _fin_release, weakref.ref(bn), gen)
+        weakref.finalize(st, _fin_release, st.owner[0], gen)
         self.st = st
 
     def ptr(self, count):
         bn, st = self.bn, self.st
         st.count = count
-        d = L.BnFin()
         slot = _fin_slot(bn, "fwd")
+        # the descriptor changes only with the count or a re-allocated parameter / buffer
+        key = (count, bn.weight.data_ptr(), ptr(bn.bias), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+               bn.num_batches_tracked.data_ptr(), st.mean.data_ptr(), bn.momentum, bn.eps)
+        if key == slot.key:
+            return slot.dptr
+        d = L.BnFin()
         d.counter, d.backward, d.C, d.count = slot.counter.data_ptr(), 0, self.C, float(count)
         d.gamma, d.beta = ptr(bn.weight), ptr(bn.bias)
         d.running_mean, d.running_var = ptr(bn.running_mean), ptr(bn.running_var)
         d.num_batches = ptr(bn.num_batches_tracked)
         d.momentum, d.eps = float(bn.momentum), float(bn.eps)
         d.mean, d.invstd, d.scale, d.shift = ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift)
+        slot.key = key
         return slot.write(d)
 
 
@@ -1067,15 +1122,21 @@ def fin_backward(bn, st, C, alpha):
     only for BN quantities of a fused forward (persistent buffers; the coefficients go to the same buffer)."""
     if not (getattr(st, "fin", False) and _fin_ok(bn)):
         return None
-    coef = bn._scd_fin_st[4 * C:7 * C]
-    d = L.BnFin()
+    buf = bn._scd_fin_st
+    coef = bn._scd_fin_views[0][4 * C:7 * C]
     slot = _fin_slot(bn, "bwd")
+    dg, db = grad_of(bn.weight), grad_of(bn.bias)
+    key = (st.count, C, bn.weight.data_ptr(), buf.data_ptr(), ptr(dg), ptr(db), float(alpha))
+    if key == slot.key:
+        return slot.dptr, coef
+    d = L.BnFin()
     d.counter, d.backward, d.C, d.count = slot.counter.data_ptr(), 1, C, float(st.count)
     d.gamma = ptr(bn.weight)
     d.mean, d.invstd = ptr(st.mean), ptr(st.invstd)
-    d.dgamma, d.dbeta = ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias))
+    d.dgamma, d.dbeta = ptr(dg), ptr(db)
     d.gscale = float(alpha)
     d.coef = ptr(coef)
+    slot.key = key
     return slot.write(d), coef
 
 
