@@ -171,13 +171,21 @@ int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int H, int W, 
 
 /* Direct stem convolution (bf16): Conv2d(1,64,7,stride 2,pad 3,no bias) of residuals.py:211 with the
  * [pixel][tap] tile built in LDS from the input patch (no column tensor in HBM); wpk = the [64][64] packed
- * weight (pack_weight mode 0, ldp 64); y (N,Ho,Wo,64) NHWC; stats as scd_conv_gemm (may be NULL).
+ * weight (pack_weight mode 0, ldp 64); y (N,Ho,Wo,64) NHWC; stats as scd_conv_gemm (may be NULL).  y == NULL
+ * (stats required): the statistics only -- the first pass of the pooled forward below.
  * Requires Wo % 128 == 0 and Ho % 2 == 0. */
 int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H, int W,
                       int Ho, int Wo, void* stream);
 /* ... with the stem BN's forward finalize fused (scd_bn_fin; residuals.py:211-212) */
 int scd_stem_conv_fwd_fin(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H, int W,
                           int Ho, int Wo, const struct scd_bn_fin* fin, void* stream);
+/* The stem forward's second pass (residuals.py:211-213: conv, BN, ReLU, MaxPool2d(3, 2, 1)): the conv recomputed per
+ * tile in LDS, BN (scale / shift from the finalize of the first pass's statistics) + ReLU + max pool, so the
+ * full-resolution conv output never reaches HBM.  out (N,Ho/2,Wo/2,64), argmax (same shape, u8 window index 0..8,
+ * first maximum in row-major window order) as scd_stem_pool_fwd of the conv's y, and ymax (same shape) = y at each
+ * argmax (the pre-BN value the backward needs).  Requires Wo % 128 == 0 and Ho % 2 == 0 (Ho, Wo of the conv). */
+int scd_stem_conv_pool_fwd(int dtype, const float* x, const void* wpk, const float* scale, const float* shift,
+                           void* out, uint8_t* argmax, void* ymax, int N, int H, int W, void* stream);
 /* Its weight gradient: ws[z][co][k] (fp32, nsplit x 64 x 64) = sum over split z's pixels of
  * dy[pix][co] * col[pix][k]; reduce with scd_wgrad_reduce(ws, nsplit, 64, 1, 64, ..., cvalid = 49).
  * coef != NULL fuses the stem BN backward apply: dy is then the masked dz, ybn the BN input, and the
@@ -197,6 +205,10 @@ int scd_stem_bwd_nsplit(void);
 int scd_stem_bwd_fused(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
                        const float* shift, const float* mean, const float* invstd, const float* x, double* stats,
                        float* ws, int nsplit, float* tg, int N, int H, int W, int Ho, int Wo, void* stream);
+/* ... from ymax of scd_stem_conv_pool_fwd (pooled layout) instead of the full-resolution y: the same results */
+int scd_stem_bwd_fused_pooled(int dtype, const void* dout, const uint8_t* argmax, const void* ymax, const float* scale,
+                              const float* shift, const float* mean, const float* invstd, const float* x, double* stats,
+                              float* ws, int nsplit, float* tg, int N, int H, int W, int Ho, int Wo, void* stream);
 int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk, const float* coef, float* dst, int accumulate,
                          float alpha, void* stream);
 
@@ -213,8 +225,11 @@ int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk, const floa
 #ifndef SCD_FIN_REPLICAS
 #define SCD_FIN_REPLICAS 16
 #endif
+/* arrival counters: one per shard of workgroups (blockIdx % 64) plus the count of finished shards */
+#define SCD_FIN_SHARDS 64
+#define SCD_FIN_COUNTERS (SCD_FIN_SHARDS + 1)
 typedef struct scd_bn_fin {
-    int* counter;              /* one int, zero between launches (device memory) */
+    int* counter;              /* SCD_FIN_COUNTERS ints, zero between launches (device memory) */
     int backward;              /* 0: forward statistics, 1: backward sums */
     int C;
     double count;              /* elements per channel (rows) */

@@ -58,6 +58,8 @@
 #define scd_stem_bwd_nsplit scd_stem_bwd_nsplit__f16
 #define scd_conv_dgrad_s2 scd_conv_dgrad_s2__f16
 #define scd_stem_bwd_fused scd_stem_bwd_fused__f16
+#define scd_stem_bwd_fused_pooled scd_stem_bwd_fused_pooled__f16
+#define scd_stem_conv_pool_fwd scd_stem_conv_pool_fwd__f16
 #define scd_stem_bwd_combine scd_stem_bwd_combine__f16
 #define scd_pad_channels scd_pad_channels__f16
 #define __bf16 _Float16
@@ -113,6 +115,8 @@ SCD_F16_DECL(scd_heads_sparse_fixup)
 SCD_F16_DECL(scd_stem_conv_fwd)
 SCD_F16_DECL(scd_stem_conv_wgrad)
 SCD_F16_DECL(scd_stem_bwd_fused)
+SCD_F16_DECL(scd_stem_bwd_fused_pooled)
+SCD_F16_DECL(scd_stem_conv_pool_fwd)
 SCD_F16_DECL(scd_conv_dgrad_s2)
 SCD_F16_DECL(scd_stem_bwd_combine)
 SCD_F16_DECL(scd_pad_channels)
@@ -212,30 +216,59 @@ __device__ __forceinline__ int stat_rep(const BnFinDev& d, int bid) {
 // the one counter add that signals them.  An agent-scope release/acquire here (a `__threadfence()` per workgroup)
 // writes back the XCD's whole L2 every time and made the producers 1.2-10x slower.
 __device__ __forceinline__ bool bn_fin_arrive(int* counter) {
+    // two levels, so no counter word takes more than ~1/64 of the launch's arrivals (one word serialises its returning
+    // atomics at ~90 per us: a resident-grid launch of 2048 workgroups, all finishing together, waited ~20 us on one):
+    // workgroup b counts in on shard b % 64, the last of a shard counts the shard in on counter[SCD_FIN_SHARDS]
     __shared__ int fin_last;
 #if SCD_FIN_ABL != 2
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
     __syncthreads();
-    if (threadIdx.x == 0)
-        fin_last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   (int)(gridDim.x * gridDim.y * gridDim.z) - 1;
+    if (threadIdx.x == 0) {
+        const int nblk = (int)(gridDim.x * gridDim.y * gridDim.z);
+        const int bid = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+        const int sh = bid % SCD_FIN_SHARDS;
+        const int nsh = nblk < SCD_FIN_SHARDS ? nblk : SCD_FIN_SHARDS;
+        const int members = (nblk - sh + SCD_FIN_SHARDS - 1) / SCD_FIN_SHARDS;
+        int last = __hip_atomic_fetch_add(counter + sh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1;
+        if (last)
+            last = __hip_atomic_fetch_add(counter + SCD_FIN_SHARDS, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   nsh - 1;
+        fin_last = last;
+    }
     __syncthreads();
     return fin_last != 0;
 }
+// global-address-space view of a pointer read from a descriptor (plain `global_` accesses instead of `flat_`)
+template <typename T> __device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
 // The finalize of one layer by threads 0 .. nact-1 of the last workgroup: the replicas summed in a fixed order
 // (agent-scope loads: they were written by other XCDs' atomics) and re-zeroed, then bn_finalize_kernel's /
-// bn_bwd_finalize_kernel's arithmetic.
+// bn_bwd_finalize_kernel's arithmetic.  This runs after every other workgroup has left, so its latency is the
+// launch's: the descriptor is copied to registers once (its fields would otherwise be re-read after every store
+// through one of its pointers) and every per-channel operand is loaded before the first wait.
 template <int NREP = SCD_FIN_REPLICAS>
 __device__ __forceinline__ void bn_fin_compute(const scd_bn_fin* fp, double* stats, int ld, int nact) {
-    const int C = fp->C;
-    const int bwd = fp->backward;
-    const double count = fp->count;
+    const scd_bn_fin f = *fp;
+    const int C = f.C;
+    const double count = f.count;
     // CH replicas (2 CH loads) in flight at a time: within the register budget of the BN kernels (BN_EW_WAVES)
     constexpr int CH = NREP < 4 ? NREP : 4;
     static_assert(NREP % CH == 0, "replica count");
     for (int c = threadIdx.x; c < C; c += nact) {
-        double* p0 = stats + c;
+        float g = 1.f, b = 0.f, rm = 0.f, rv = 0.f, is = 0.f, mu = 0.f, dg = 0.f, db = 0.f;
+        if (f.gamma) g = gptr(f.gamma)[c];
+        if (!f.backward) {
+            if (f.beta) b = gptr(f.beta)[c];
+            if (f.running_mean) { rm = gptr(f.running_mean)[c]; rv = gptr(f.running_var)[c]; }
+        } else {
+            is = gptr(f.invstd)[c];
+            mu = gptr(f.mean)[c];
+            if (f.dgamma) dg = gptr(f.dgamma)[c];
+            if (f.dbeta) db = gptr(f.dbeta)[c];
+        }
+        __attribute__((address_space(1))) double* p0 = gptr(stats) + c;
         double s = 0.0, q = 0.0;
         for (int r0 = 0; r0 < NREP; r0 += CH) {
             double vs[CH], vq[CH];
@@ -248,42 +281,39 @@ __device__ __forceinline__ void bn_fin_compute(const scd_bn_fin* fp, double* sta
 #pragma unroll
             for (int r = 0; r < CH; ++r) { s += vs[r]; q += vq[r]; }
         }
+#pragma unroll
         for (int r = 0; r < NREP; ++r) {
             p0[(long)(2 * r) * ld] = 0.0;
             p0[(long)(2 * r + 1) * ld] = 0.0;
         }
-        if (!bwd) {
+        if (!f.backward) {
             const double mean = s / count;
             double var = q / count - mean * mean;
             if (var < 0.0) var = 0.0;
-            const float invstd = (float)(1.0 / sqrt(var + (double)fp->eps));
-            const float g = fp->gamma ? fp->gamma[c] : 1.f;
-            const float b = fp->beta ? fp->beta[c] : 0.f;
+            const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
             const float sc = g * invstd;
-            fp->mean[c] = (float)mean;
-            fp->invstd[c] = invstd;
-            fp->scale[c] = sc;
-            fp->shift[c] = b - (float)mean * sc;
-            if (fp->running_mean) {
-                const float m = fp->momentum;
+            gptr(f.mean)[c] = (float)mean;
+            gptr(f.invstd)[c] = invstd;
+            gptr(f.scale)[c] = sc;
+            gptr(f.shift)[c] = b - (float)mean * sc;
+            if (f.running_mean) {
+                const float m = f.momentum;
                 const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-                fp->running_mean[c] = (1.f - m) * fp->running_mean[c] + m * (float)mean;
-                fp->running_var[c] = (1.f - m) * fp->running_var[c] + m * (float)unbiased;
+                gptr(f.running_mean)[c] = (1.f - m) * rm + m * (float)mean;
+                gptr(f.running_var)[c] = (1.f - m) * rv + m * (float)unbiased;
             }
         } else {
-            if (fp->dgamma) fp->dgamma[c] += fp->gscale * (float)q;
-            if (fp->dbeta) fp->dbeta[c] += fp->gscale * (float)s;
-            const float g = fp->gamma ? fp->gamma[c] : 1.f;
-            const float is = fp->invstd[c];
+            if (f.dgamma) gptr(f.dgamma)[c] = dg + f.gscale * (float)q;
+            if (f.dbeta) gptr(f.dbeta)[c] = db + f.gscale * (float)s;
             const float sc = g * is;
             const float k1 = (float)(s / count);
             const float k2 = (float)(q / count);
-            fp->coef[c] = sc;
-            fp->coef[C + c] = -sc * is * k2;
-            fp->coef[2 * C + c] = -sc * k1 + sc * is * k2 * fp->mean[c];
+            gptr(f.coef)[c] = sc;
+            gptr(f.coef)[C + c] = -sc * is * k2;
+            gptr(f.coef)[2 * C + c] = -sc * k1 + sc * is * k2 * mu;
         }
     }
-    if (threadIdx.x == 0 && !bwd && fp->num_batches) *fp->num_batches += 1;
+    if (threadIdx.x == 0 && !f.backward && f.num_batches) *gptr(f.num_batches) += 1;
 }
 // the tail of a producer (one layer; d1 != NULL: a second layer whose statistics the launch produced too, counted on
 // d0's counter); every remaining thread calls it at the kernel's end
@@ -295,7 +325,8 @@ __device__ __forceinline__ void bn_fin_tail2(const BnFinDev& d0, const BnFinDev*
     bn_fin_compute(d0.f, d0.stats, d0.ld, nact);
     if (d1 && d1->f) bn_fin_compute(d1->f, d1->stats, d1->ld, nact);
 #endif
-    if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = threadIdx.x; i < SCD_FIN_COUNTERS; i += nact)
+        __hip_atomic_store(counter + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void bn_fin_tail(const BnFinDev& d, int nact) { bn_fin_tail2(d, nullptr, nact); }
 // host: the kernels' view of a `_fin` entry point's argument (off when fin == NULL)

@@ -27,6 +27,8 @@ def _c(t):
 
 # stem backward as one pass (ops.stem_backward_fused); SCD_STEM_FUSED_BWD=0: pool backward + fused-apply weight gradient
 _STEM_FUSED_BWD = os.environ.get("SCD_STEM_FUSED_BWD", "1") != "0"
+# stem forward in two passes without the full-resolution conv output (ops.stem_conv_pool_fwd); SCD_STEM_POOLED=0: off
+_STEM_POOLED = os.environ.get("SCD_STEM_POOLED", "1") != "0"
 
 
 def _conv_ld(w):
@@ -99,6 +101,20 @@ class StemFn(torch.autograd.Function):
         ref_geom = tuple(conv.weight.shape) == (64, 1, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3
         direct = ops.stem_direct_ok(x, dtype) and ref_geom
         fin = ops.fin_forward(bn, C) if training else None
+        pooled = direct and _STEM_FUSED_BWD and _STEM_POOLED and ops.stem_pool_ok(x, dtype)
+        if pooled:
+            # conv -> statistics only, finalize, then the conv again with BN + ReLU + MaxPool on the tile in LDS: the
+            # backward needs y only at the pool's argmax positions (ymax), so y is never written
+            x = _c(x)
+            wpk = ops.pack_weight(conv.weight, dtype, 0, ldp=64)
+            if training:
+                ops.stem_conv_fwd(x, wpk, stats=stats, fin=fin, store=False)
+            st = fin.st if fin is not None else ops.bn_finalize(bn, stats, C, ops.stem_out_count(x), training)
+            out, am, ym = ops.stem_conv_pool_fwd(x, wpk, st)
+            ctx.save_for_backward(x, ym, am)
+            ctx.st, ctx.conv, ctx.bn, ctx.direct, ctx.pooled = st, conv, bn, True, True
+            ctx.wpk = wpk
+            return out
         if direct:
             # direct 7x7/s2 conv: the tap tile is built in LDS from the input patch (no column tensor)
             x = _c(x)
@@ -113,7 +129,7 @@ class StemFn(torch.autograd.Function):
         st = fin.st if fin is not None else ops.bn_finalize(bn, stats, C, y.numel() // C, training)
         out, am = ops.stem_pool_fwd(y, st)
         ctx.save_for_backward(cols, y, am)
-        ctx.st, ctx.conv, ctx.bn, ctx.direct = st, conv, bn, direct
+        ctx.st, ctx.conv, ctx.bn, ctx.direct, ctx.pooled = st, conv, bn, direct, False
         ctx.wpk = wpk if direct else None
         return out
 
@@ -121,7 +137,10 @@ class StemFn(torch.autograd.Function):
     def backward(ctx, dout):
         conv, bn, st = ctx.conv, ctx.bn, ctx.st
         cols, y, am = ctx.saved_tensors
-        if ctx.direct and _STEM_FUSED_BWD:
+        if ctx.pooled:
+            # y here is ymax (pooled layout)
+            ops.stem_backward_fused(bn, _c(dout), am, y, st, cols, ctx.wpk, ops.grad_of(conv.weight), pooled=True)
+        elif ctx.direct and _STEM_FUSED_BWD:
             # pool / ReLU / BN / weight-gradient backward in one pass over the pooled gradient (dz stays on chip)
             ops.stem_backward_fused(bn, _c(dout), am, y, st, cols, ctx.wpk, ops.grad_of(conv.weight))
         elif ctx.direct:

@@ -23,6 +23,7 @@ MAX_TAPS = 16
 MAX_PHASES = 4
 STAT_REPLICAS = 64
 FIN_REPLICAS = 16
+FIN_COUNTERS = 65          # SCD_FIN_COUNTERS: 64 arrival shards + the shard count
 
 c_int, c_long, c_float, c_double, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
                                                         ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)
@@ -85,6 +86,8 @@ SIGNATURES = {
     "scd_stem_bwd_nsplit": (I, []),
     "scd_conv_dgrad_s2": (I, [I, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_bwd_fused": (I, [I, P, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P]),
+    "scd_stem_bwd_fused_pooled": (I, [I, P, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P]),
+    "scd_stem_conv_pool_fwd": (I, [I, P, P, P, P, P, P, P, I, I, I, P]),
     "scd_stem_bwd_combine": (I, [I, P, P, P, P, I, F, P]),
     "scd_stem_pool_bwd_bn": (I, [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stats_collapse": (I, [P, I, I, P]),

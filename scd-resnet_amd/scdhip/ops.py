@@ -1015,7 +1015,7 @@ class BNFinalize:
     BN quantities it points at are persistent per module: a forward takes them only while no earlier forward's
     quantities are still referenced by an autograd graph (else it falls back to fresh buffers and the separate
     finalize).  SCD_BN_FIN_FUSE=0: off."""
-    enabled = os.environ.get("SCD_BN_FIN_FUSE", "1") != "0"
+    enabled = os.environ.get("SCD_BN_FIN_FUSE", "0") == "1"
 
 
 class _FinSlot:
@@ -1023,7 +1023,7 @@ class _FinSlot:
 
     def __init__(self, dev):
         n = ctypes.sizeof(L.BnFin)
-        self.counter = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.counter = torch.zeros(L.FIN_COUNTERS, dtype=torch.int32, device=dev)
         self.dbuf = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.dptr = self.dbuf.data_ptr()
         self.last = None
@@ -1296,19 +1296,48 @@ def stem_direct_ok(x, dtype):
     return dtype in HALF and Wo % 128 == 0 and Ho % 2 == 0
 
 
-def stem_conv_fwd(x, wpk, stats=None, fin=None):
+def stem_conv_fwd(x, wpk, stats=None, fin=None, store=True):
     """Conv2d(1,64,7,s2,p3) of NCHW fp32 x -> (N,Ho,Wo,64) bf16 NHWC (+BN sums); wpk = pack_weight(w, bf16, 0, ldp=64).
-    fin: FinForward of the stem BN (its finalize by the conv's last workgroup)."""
+    fin: FinForward of the stem BN (its finalize by the conv's last workgroup).  store=False: the BN sums only (the
+    first pass of the pooled forward, stem_conv_pool_fwd); returns None."""
     _need_gpu(x)
     N, _, H, W = x.shape
     Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    y = torch.empty(N, Ho, Wo, 64, dtype=wpk.dtype, device=x.device)
+    y = torch.empty(N, Ho, Wo, 64, dtype=wpk.dtype, device=x.device) if store else None
     if fin is not None:
         L.call("scd_stem_conv_fwd_fin", dt(wpk), ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo,
                fin.ptr(N * Ho * Wo), stream())
         return y
     L.call("scd_stem_conv_fwd", dt(wpk), ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo, stream())
     return y
+
+
+def stem_conv_pool_fwd(x, wpk, st):
+    """The stem's conv recomputed + BN (st) + ReLU + MaxPool(3,2,1) (scd_stem_conv_pool_fwd): (out, argmax, ymax), all
+    (N, Ho/2, Wo/2, 64); the full-resolution conv output is never materialised."""
+    _need_gpu(x)
+    N, _, H, W = x.shape
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
+    out = torch.empty(N, Hp, Wp, 64, dtype=wpk.dtype, device=x.device)
+    am = torch.empty(N, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
+    ym = torch.empty(N, Hp, Wp, 64, dtype=wpk.dtype, device=x.device)
+    L.call("scd_stem_conv_pool_fwd", dt(wpk), ptr(x), ptr(wpk), ptr(st.scale), ptr(st.shift), ptr(out), ptr(am),
+           ptr(ym), N, H, W, stream())
+    return out, am, ym
+
+
+def stem_out_count(x):
+    """Pixels of the stem conv output per channel (the BN count)."""
+    H, W = x.shape[2], x.shape[3]
+    return x.shape[0] * ((H + 6 - 7) // 2 + 1) * ((W + 6 - 7) // 2 + 1)
+
+
+def stem_pool_ok(x, dtype):
+    """The pooled forward's shapes: 16-bit, conv output width a multiple of 128 and even height (scd_stem_conv_pool_fwd)."""
+    H, W = x.shape[2], x.shape[3]
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    return dtype in HALF and Wo % 128 == 0 and Ho % 2 == 0 and Ho >= 2
 
 
 def stem_conv_wgrad(dy, x, dst, accumulate=True, ybn=None, coef=None):
@@ -1346,17 +1375,21 @@ def stem_pool_bwd_bn(bn, dout, am, y, st):
     return dz, bn_backward_coef(bn, st, stats, C, grad_alpha(y))
 
 
-def stem_backward_fused(bn, dout, am, y, st, x, wpk, dst):
+def stem_backward_fused(bn, dout, am, y, st, x, wpk, dst, pooled=False):
     """The stem's MaxPool / ReLU / BN / conv weight-gradient backward in one pass (scd_stem_bwd_fused): the BN
     backward sums (dgamma / dbeta accumulated, SyncBN all-reduce as bn_backward_coef) and dst (64,1,7,7) += the weight
-    gradient a*T1 + b*W G + c*s; the full-resolution dz is never materialised."""
-    N, Ho, Wo, C = y.shape
+    gradient a*T1 + b*W G + c*s; the full-resolution dz is never materialised.  pooled: y is ymax of
+    stem_conv_pool_fwd (pooled layout, scd_stem_bwd_fused_pooled)."""
+    N, C = y.shape[0], y.shape[3]
+    H, W = x.shape[2], x.shape[3]
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
     ns = L.lib().scd_stem_bwd_nsplit()
     ws = torch.empty(ns * 2 * 64 * 64, dtype=torch.float32, device=y.device)
     tg = torch.empty(2 * 64 * 64, dtype=torch.float32, device=y.device)
     stats = bn_stats(bn, "bwd")
-    L.call("scd_stem_bwd_fused", dt(y), ptr(dout), ptr(am), ptr(y), ptr(st.scale), ptr(st.shift), ptr(st.mean),
-           ptr(st.invstd), ptr(x), ptr(stats), ptr(ws), ns, ptr(tg), N, x.shape[2], x.shape[3], Ho, Wo, stream())
+    L.call("scd_stem_bwd_fused_pooled" if pooled else "scd_stem_bwd_fused", dt(y), ptr(dout), ptr(am), ptr(y),
+           ptr(st.scale), ptr(st.shift), ptr(st.mean), ptr(st.invstd), ptr(x), ptr(stats), ptr(ws), ns, ptr(tg), N, H,
+           W, Ho, Wo, stream())
     alpha = grad_alpha(y)
     coef = bn_backward_coef(bn, st, stats, C, alpha)
     L.call("scd_stem_bwd_combine", dt(y), ptr(tg), ptr(wpk), ptr(coef), ptr(dst), 1, float(alpha), stream())

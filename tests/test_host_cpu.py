@@ -62,6 +62,8 @@ def test_bn_fin_struct_matches_header(tmp_path):
     assert vals[1:] == [getattr(L.BnFin, n).offset for n in names]
     m = re.search(r"#define SCD_FIN_REPLICAS (\d+)", open(HEADER).read())
     assert int(m.group(1)) == L.FIN_REPLICAS
+    m = re.search(r"#define SCD_FIN_SHARDS (\d+)", open(HEADER).read())
+    assert int(m.group(1)) + 1 == L.FIN_COUNTERS
 
 
 def test_workspace_queries():

@@ -432,6 +432,56 @@ def test_stem_one_pass_backward(shape, dtype):
     assert rel_err(dwa, ref) < 2e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(2, 512, 512), (3, 260, 256)])
+def test_stem_pooled_forward_matches_two_kernels(shape, dtype):
+    """The pooled stem forward (scd_stem_conv_fwd with y = NULL for the statistics, then scd_stem_conv_pool_fwd: the conv
+    recomputed with BN + ReLU + MaxPool on the tile) against conv -> y -> scd_stem_pool_fwd: the same statistics (fp64
+    atomics: up to their summation order), the same out and argmax bits, ymax = y at every argmax, and the backward
+    from ymax (scd_stem_bwd_fused_pooled) equal to the backward from y up to the fp64 summation order of its sums."""
+    from scdhip import ops
+    N, H, W = shape
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(N, 1, H, W, generator=g).to(DEV)
+    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).to(DEV)
+    assert ops.stem_pool_ok(x, dtype)
+    bns = [torch.nn.BatchNorm2d(64).to(DEV) for _ in range(2)]
+    with torch.no_grad():
+        bns[0].weight.uniform_(0.5, 1.5)
+        bns[0].bias.normal_()
+    bns[1].load_state_dict(bns[0].state_dict())
+    wpk = ops.pack_weight(w, dtype, 0, ldp=64)
+    stats = ops.new_stats(64, DEV)
+    y = ops.stem_conv_fwd(x, wpk, stats=stats)
+    stats2 = ops.new_stats(64, DEV)
+    assert ops.stem_conv_fwd(x, wpk, stats=stats2, store=False) is None
+    s1, s2 = stats.view(-1, 2, 64).sum(0), stats2.view(-1, 2, 64).sum(0)
+    assert ((s2 - s1).abs().max() / s1.abs().max()).item() < 1e-12
+    st = ops.bn_finalize(bns[0], stats, 64, y.numel() // 64)
+    out, am = ops.stem_pool_fwd(y, st)
+    out2, am2, ym = ops.stem_conv_pool_fwd(x, wpk, st)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out) and torch.equal(am2, am)
+    # ymax = y at the argmax (window index d: conv row 2 po - 1 + d // 3, column 2 pq - 1 + d % 3)
+    Hp, Wp = out.shape[1], out.shape[2]
+    d = am.long()
+    po = torch.arange(Hp, device=DEV).view(1, Hp, 1, 1)
+    pq = torch.arange(Wp, device=DEV).view(1, 1, Wp, 1)
+    r = (2 * po - 1 + d // 3).clamp(0, y.shape[1] - 1)
+    c = (2 * pq - 1 + d % 3).clamp(0, y.shape[2] - 1)
+    n = torch.arange(N, device=DEV).view(N, 1, 1, 1).expand_as(d)
+    ch = torch.arange(64, device=DEV).view(1, 1, 1, 64).expand_as(d)
+    assert torch.equal(ym, y[n, r, c, ch])
+    dout = torch.randn(out.shape, generator=g).to(DEV, dtype)
+    dwa = torch.full_like(w, 0.5)
+    dwb = torch.full_like(w, 0.5)
+    ops.stem_backward_fused(bns[0], dout, am, y, st, x, wpk, dwa)
+    ops.stem_backward_fused(bns[1], dout, am, ym, st, x, wpk, dwb, pooled=True)
+    torch.cuda.synchronize()
+    for a, b in ((bns[0].weight.grad, bns[1].weight.grad), (bns[0].bias.grad, bns[1].bias.grad), (dwa, dwb)):
+        assert rel_err(b, a) < 1e-6
+
+
 def test_cpool_fwd_bwd_fp32():
     from scdhip import ops
     g = torch.Generator().manual_seed(5)
