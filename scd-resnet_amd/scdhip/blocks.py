@@ -27,8 +27,10 @@ def _c(t):
 
 # stem backward as one pass (ops.stem_backward_fused); SCD_STEM_FUSED_BWD=0: pool backward + fused-apply weight gradient
 _STEM_FUSED_BWD = os.environ.get("SCD_STEM_FUSED_BWD", "1") != "0"
-# stem forward in two passes without the full-resolution conv output (ops.stem_conv_pool_fwd); SCD_STEM_POOLED=0: off
-_STEM_POOLED = os.environ.get("SCD_STEM_POOLED", "1") != "0"
+# stem forward in two passes without the full-resolution conv output (ops.stem_conv_pool_fwd), SCD_STEM_POOLED=1: measured
+# 2.8% slower per step than conv -> y -> pool (the stem conv is bound by its LDS / VALU tile build, 84 us of the 106 with
+# y stored, so a second conv pass costs more than the 268-MB write and two reads it saves), hence off by default
+_STEM_POOLED = os.environ.get("SCD_STEM_POOLED", "0") == "1"
 
 
 def _conv_ld(w):
