@@ -189,7 +189,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* y, T* out, int C
 // rows [r0, r1): thread = (row lane rsub, 16-B channel chunk ch); 4 rows per step are loaded before
 // any is used (4 x 3 independent 16-B loads in flight per thread); the block's partials are folded
 // over row lanes in LDS by all threads and added to one fp64 replica slot per channel.
-template <typename T>
+// FIN: the build that finalizes in its last workgroup (scd_bn_bwd_reduce_fin); the plain one carries no tail code (the
+// tail took the kernel from 71 VGPRs to its 80-VGPR bound plus spills)
+template <typename T, bool FIN = false>
 __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y,
                                                             const float* rsc, const float* rsh,
                                                             const float* mean, const float* invstd, int C, int ld,
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T
         red[nt * E + rsub * C + ch * E + e] = q[e];
     }
     __syncthreads();
-    const int rep = stat_rep(fin, blockIdx.x);
+    const int rep = FIN ? stat_rep(fin, blockIdx.x) : (int)(blockIdx.x % SCD_STAT_REPLICAS);
     for (int c = tid; c < C; c += nt) {
         double ss = 0.0, qq = 0.0;
         for (int k = 0; k < rpi; ++k) {
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T
         atomic_add_f64(stats + ((long)rep * 2 + 0) * ld + c, ss);
         atomic_add_f64(stats + ((long)rep * 2 + 1) * ld + c, qq);
     }
-    bn_fin_tail(fin, nt);
+    if constexpr (FIN) bn_fin_tail(fin, nt, red);
 }
 
 __global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply_kernel(const T*
 // 110-120, 158-165; CornerPool branchMergeBn + shortcutBn, cornerNetCPool.py:117-122): both take the same gradient
 // dout through the same ReLU mask, so one pass reads dout and the mask once for both.  Per element and per thread the
 // arithmetic is that of bn_bwd_reduce_kernel / bn_bwd_apply_kernel with a mask (no BN+ReLU recompute).
-template <typename T>
+template <typename T, bool FIN = false>
 __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
                                                              const float* mean_a, const float* invstd_a,
                                                              const float* mean_b, const float* invstd_b, int C, int ld,
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const 
         const unsigned i = r * (unsigned)ld + ch * E;
         acc_raw(*(const uint4*)(dout + i), *(const uint4*)(mask + i), *(const uint4*)(ya + i), *(const uint4*)(yb + i));
     }
-    const int rep = stat_rep(fin_a, blockIdx.x);
+    const int rep = FIN ? stat_rep(fin_a, blockIdx.x) : (int)(blockIdx.x % SCD_STAT_REPLICAS);
     // pass 1: sum dz (both layers) and layer a's sum dz*xhat; pass 2: layer b's
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -454,7 +456,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const 
         atomic_add_f64(stats_b + ((long)rep * 2 + 1) * ld + c, qq);
     }
     // both layers' finalizes by the last workgroup (fin_a's counter)
-    bn_fin_tail2(fin_a, &fin_b, nt);
+    if constexpr (FIN) bn_fin_tail2(fin_a, &fin_b, nt, red);
 }
 
 template <typename T>
@@ -637,10 +639,18 @@ extern "C" int scd_bn_bwd_reduce_fin(int dtype, const void* dout, const void* ma
         const char* yy = (const char*)y + (size_t)c0 * esz;
         const float* rs = relu_scale ? relu_scale + c0 : nullptr;
         const float* rh = relu_shift ? relu_shift + c0 : nullptr;
-        if (dtype == SCD_DT_BF16)
+        if (dtype == SCD_DT_BF16 && fuse)
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
+                               (const __bf16*)dz, (const __bf16*)mk, (const __bf16*)yy, rs, rh, mean + c0, invstd + c0,
+                               sC, C, (unsigned)rows, (unsigned)rpb, stats + c0, fd);
+        else if (dtype == SCD_DT_BF16)
             hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)dz,
                                (const __bf16*)mk, (const __bf16*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
                                (unsigned)rows, (unsigned)rpb, stats + c0, fd);
+        else if (dtype == SCD_DT_F32 && fuse)
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
+                               (const float*)dz, (const float*)mk, (const float*)yy, rs, rh, mean + c0, invstd + c0, sC,
+                               C, (unsigned)rows, (unsigned)rpb, stats + c0, fd);
         else if (dtype == SCD_DT_F32)
             hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const float*)dz,
                                (const float*)mk, (const float*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
@@ -690,11 +700,21 @@ extern "C" int scd_bn_bwd_reduce2_fin(int dtype, const void* dout, const void* m
         const size_t o = (size_t)c0 * esz;
         const char *d = (const char*)dout + o, *m = (const char*)mask + o, *a = (const char*)ya + o,
                    *b = (const char*)yb + o;
-        if (dtype == SCD_DT_BF16)
+        if (dtype == SCD_DT_BF16 && fuse)
+            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
+                               (const __bf16*)d, (const __bf16*)m, (const __bf16*)a, (const __bf16*)b, mean_a + c0,
+                               invstd_a + c0, mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb,
+                               stats_a + c0, stats_b + c0, fa, fb);
+        else if (dtype == SCD_DT_BF16)
             hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)d,
                                (const __bf16*)m, (const __bf16*)a, (const __bf16*)b, mean_a + c0, invstd_a + c0,
                                mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
                                stats_b + c0, fa, fb);
+        else if (dtype == SCD_DT_F32 && fuse)
+            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<float, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
+                               (const float*)d, (const float*)m, (const float*)a, (const float*)b, mean_a + c0,
+                               invstd_a + c0, mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb,
+                               stats_a + c0, stats_b + c0, fa, fb);
         else if (dtype == SCD_DT_F32)
             hipLaunchKernelGGL((bn_bwd_reduce2_kernel<float>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const float*)d,
                                (const float*)m, (const float*)a, (const float*)b, mean_a + c0, invstd_a + c0,

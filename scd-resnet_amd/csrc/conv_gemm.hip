@@ -506,7 +506,7 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void conv_gemm_kernel(GemmParams 
     }
 
     gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
-    bn_fin_tail(p.fin, 256);            // (KS 2: the second K group has returned; threads 0..255 remain)
+    bn_fin_tail(p.fin, 256, smem);            // (KS 2: the second K group has returned; threads 0..255 remain)
 }
 
 // -------------------------------------------------------------------------------------
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
         const int rep = stat_rep(p.fin, blockIdx.x);
         atomic_add_f64(p.stats + ((long)rep * 2 + (tid >> 6)) * p.Co + (tid & 63), (double)bnsum);
     }
-    bn_fin_tail(p.fin, 512);
+    bn_fin_tail(p.fin, 512, smem);
 }
 
 template <bool HEADS, bool BNB = false>
@@ -932,7 +932,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
-    bn_fin_tail(p.fin, 512);
+    bn_fin_tail(p.fin, 512, smem);
 }
 
 // -------------------------------------------------------------------------------------
@@ -1413,7 +1413,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             }
         }
     }
-    bn_fin_tail(p.fin, 512);
+    bn_fin_tail(p.fin, 512, smem);
 }
 
 // -------------------------------------------------------------------------------------

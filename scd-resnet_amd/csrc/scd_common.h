@@ -215,11 +215,13 @@ __device__ __forceinline__ int stat_rep(const BnFinDev& d, int bid) {
 // them with agent-scope (sc1) loads, so no fence is needed -- only every wave's own atomics drained (vmcnt) before
 // the one counter add that signals them.  An agent-scope release/acquire here (a `__threadfence()` per workgroup)
 // writes back the XCD's whole L2 every time and made the producers 1.2-10x slower.
-__device__ __forceinline__ bool bn_fin_arrive(int* counter) {
+// flag: one int of the kernel's own LDS (free once the workgroup's epilogue has passed the first barrier here): a
+// second `__shared__` object in an LDS-DMA kernel makes the compiler's wait counting drain every DMA prefetch
+// (s_waitcnt vmcnt(0) before the fragment reads: the ring kernel lost 20-35 % per call)
+__device__ __forceinline__ bool bn_fin_arrive(int* counter, int* flag) {
     // two levels, so no counter word takes more than ~1/64 of the launch's arrivals (one word serialises its returning
     // atomics at ~90 per us: a resident-grid launch of 2048 workgroups, all finishing together, waited ~20 us on one):
     // workgroup b counts in on shard b % 64, the last of a shard counts the shard in on counter[SCD_FIN_SHARDS]
-    __shared__ int fin_last;
 #if SCD_FIN_ABL != 2
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -234,10 +236,10 @@ __device__ __forceinline__ bool bn_fin_arrive(int* counter) {
         if (last)
             last = __hip_atomic_fetch_add(counter + SCD_FIN_SHARDS, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                    nsh - 1;
-        fin_last = last;
+        *flag = last;
     }
     __syncthreads();
-    return fin_last != 0;
+    return *flag != 0;
 }
 // global-address-space view of a pointer read from a descriptor (plain `global_` accesses instead of `flat_`)
 template <typename T> __device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
@@ -317,10 +319,10 @@ __device__ __forceinline__ void bn_fin_compute(const scd_bn_fin* fp, double* sta
 }
 // the tail of a producer (one layer; d1 != NULL: a second layer whose statistics the launch produced too, counted on
 // d0's counter); every remaining thread calls it at the kernel's end
-__device__ __forceinline__ void bn_fin_tail2(const BnFinDev& d0, const BnFinDev* d1, int nact) {
+__device__ __forceinline__ void bn_fin_tail2(const BnFinDev& d0, const BnFinDev* d1, int nact, void* lds) {
     if (!d0.f) return;
     int* counter = d0.f->counter;
-    if (!bn_fin_arrive(counter)) return;
+    if (!bn_fin_arrive(counter, (int*)lds)) return;
 #if SCD_FIN_ABL != 1
     bn_fin_compute(d0.f, d0.stats, d0.ld, nact);
     if (d1 && d1->f) bn_fin_compute(d1->f, d1->stats, d1->ld, nact);
@@ -328,7 +330,7 @@ __device__ __forceinline__ void bn_fin_tail2(const BnFinDev& d0, const BnFinDev*
     for (int i = threadIdx.x; i < SCD_FIN_COUNTERS; i += nact)
         __hip_atomic_store(counter + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void bn_fin_tail(const BnFinDev& d, int nact) { bn_fin_tail2(d, nullptr, nact); }
+__device__ __forceinline__ void bn_fin_tail(const BnFinDev& d, int nact, void* lds) { bn_fin_tail2(d, nullptr, nact, lds); }
 // host: the kernels' view of a `_fin` entry point's argument (off when fin == NULL)
 static inline BnFinDev bn_fin_dev(const scd_bn_fin* fin_dev, double* stats, int ld) {
     BnFinDev d;

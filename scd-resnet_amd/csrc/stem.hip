@@ -32,139 +32,131 @@ constexpr int FTW = 128, FTH = 2;
 constexpr int PROWS = SP * (FTH - 1) + KS;          // 9 input rows
 constexpr int PCOLS = SP * (FTW - 1) + KS + 1;      // 262 -> padded to an even count
 
-// The kernel can walk several tiles per workgroup (t = blockIdx.x, += gridDim.x; the next tile's input patch in flight
-// while the current one is built, multiplied and stored; weights in registers; BN sums added once per workgroup), but
-// is launched one tile per workgroup: the walk measured slower (scd_stem_conv_fwd).
-__global__ __launch_bounds__(256, 2) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
-                                                               __bf16* __restrict__ y, double* __restrict__ stats,
-                                                               int H, int W, int Ho, int Wo, int ntiles, BnFinDev fin) {
+__global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
+                                                            __bf16* __restrict__ y, double* __restrict__ stats,
+                                                            int H, int W, int Ho, int Wo, BnFinDev fin) {
     constexpr int AT = FTH * FTW * 128;             // A tile [256 px][64 taps] bf16, 128-B rows
+    constexpr int BT = CO * 128;                    // B tile [64 co][64 taps]
     constexpr int EROW = CO * 2 + 16;
-    constexpr int ST = 4 * 64 * EROW;               // output staging [4 waves][64 px][EROW] (over the A tile)
-    constexpr int SM = ST > AT ? ST : AT;
-    __shared__ __attribute__((aligned(16))) char smem[SM + PROWS * PCOLS * 4];
+    __shared__ __attribute__((aligned(16))) char smem[AT + BT + PROWS * PCOLS * 4];
     char* As = smem;
-    float* patch = (float*)(smem + SM);
+    char* Bs = smem + AT;
+    float* patch = (float*)(smem + AT + BT);
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int l16 = lane & 15, lg = lane >> 4, l7 = l16 & 7;
     const int tiles_w = Wo / FTW;
-    const int tiles_img = (Ho / FTH) * tiles_w;
+    const int bid = blockIdx.x;
+    const int n = bid / ((Ho / FTH) * tiles_w);
+    const int rem = bid - n * (Ho / FTH) * tiles_w;
+    const int oh0 = (rem / tiles_w) * FTH, ow0 = (rem - (rem / tiles_w) * tiles_w) * FTW;
+    const int ih0 = oh0 * SP - PD, iw0 = ow0 * SP - PD;
 
-    // B fragments of both K steps: rows b*16 + l16, 16-B chunk s*4 + lg of the [64 co][64 tap] packed weight
-    bf16x8 bfr[2][4];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) bfr[s][b] = *(const bf16x8*)(wpk + (b * 16 + l16) * 64 + (s * 4 + lg) * 8);
-
+    // weights: 64 rows x 8 chunks of 16 B
+    for (int i = tid; i < CO * 8; i += 256) {
+        const int r = i >> 3, c = i & 7;
+        *(uint4*)(Bs + swz128(r, c)) = *(const uint4*)(wpk + r * 64 + c * 8);
+    }
+    // input patch (zero outside the image): a fixed number of loads per thread from clamped addresses, all in flight
+    // at once (a bounds branch around each load made the compiler wait for every one before the next)
+    const float* xn = x + (size_t)n * H * W;
     constexpr int PN = (PROWS * PCOLS + 255) / 256;
     float pv[PN];
-    // input patch of tile t (zero outside the image): a fixed number of loads per thread from clamped addresses, all
-    // in flight at once (a bounds branch around each load made the compiler wait for every one before the next)
-    auto load_patch = [&](int t) {
-        const int n = t / tiles_img, rem = t - n * tiles_img;
-        const int oh0 = (rem / tiles_w) * FTH, ow0 = (rem - (rem / tiles_w) * tiles_w) * FTW;
-        const int ih0 = oh0 * SP - PD, iw0 = ow0 * SP - PD;
-        const float* xn = x + (size_t)n * H * W;
 #pragma unroll
-        for (int j = 0; j < PN; ++j) {
-            const int i = min(tid + 256 * j, PROWS * PCOLS - 1);
+    for (int j = 0; j < PN; ++j) {
+        const int i = min(tid + 256 * j, PROWS * PCOLS - 1);
+        const int r = i / PCOLS, c = i - (i / PCOLS) * PCOLS;
+        const int ih = min(max(ih0 + r, 0), H - 1), iw = min(max(iw0 + c, 0), W - 1);
+        pv[j] = xn[(size_t)ih * W + iw];
+    }
+#pragma unroll
+    for (int j = 0; j < PN; ++j) {
+        const int i = tid + 256 * j;
+        if (i < PROWS * PCOLS) {
             const int r = i / PCOLS, c = i - (i / PCOLS) * PCOLS;
             const int ih = ih0 + r, iw = iw0 + c;
-            const float v = xn[(size_t)min(max(ih, 0), H - 1) * W + min(max(iw, 0), W - 1)];
-            pv[j] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? v : 0.f;
+            patch[i] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? pv[j] : 0.f;
         }
-    };
+    }
+    __syncthreads();
+    // im2col tile: thread -> pixel p = tid, all 64 taps (8 chunks of 8)
+    {
+        const int pr = tid / FTW, pc = tid - (tid / FTW) * FTW;
+        const float* pp = patch + (SP * pr) * PCOLS + SP * pc;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            bf16x8 v;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = c * 8 + e;
+                v[e] = (__bf16)(k < KK ? pp[(k / KS) * PCOLS + (k % KS)] : 0.f);
+            }
+            *(bf16x8*)(As + swz128(tid, c)) = v;
+        }
+    }
+    __syncthreads();
+
+    // MFMA: wave w owns pixels 64w .. 64w+63 (4 blocks) x all 64 channels (4 blocks), K = 64 (2 steps)
+    const int lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, lg = lane >> 4, l7 = l16 & 7;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int co = ((s * 4 + lg) ^ l7) << 4;
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(As + (wave * 64 + a * 16 + l16) * 128 + co);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) bfr[b] = *(const bf16x8*)(Bs + (b * 16 + l16) * 128 + co);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();          // A tile no longer read: reuse it for the output staging
+
+    // epilogue: lane holds pixel a*16+l16 (of its wave) and channels b*16+4lg .. +3.  y == NULL: statistics only (the
+    // first pass of the pooled forward, stem_conv_pool_kernel)
     float csum[4][4], csq[4][4];
+    char* ep = smem + wave * 64 * EROW;
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
-
-    if (blockIdx.x < ntiles) load_patch(blockIdx.x);
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int n = t / tiles_img, rem = t - n * tiles_img;
-        const int oh0 = (rem / tiles_w) * FTH, ow0 = (rem - (rem / tiles_w) * tiles_w) * FTW;
 #pragma unroll
-        for (int j = 0; j < PN; ++j) {
-            const int i = tid + 256 * j;
-            if (i < PROWS * PCOLS) patch[i] = pv[j];
-        }
-        if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x);     // in flight during this tile
-        __syncthreads();
-        // im2col tile: thread -> pixel p = tid, all 64 taps (8 chunks of 8)
-        {
-            const int pr = tid / FTW, pc = tid - (tid / FTW) * FTW;
-            const float* pp = patch + (SP * pr) * PCOLS + SP * pc;
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                bf16x8 v;
+        for (int b = 0; b < 4; ++b) {
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            bf16x4 o;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int k = c * 8 + e;
-                    v[e] = (__bf16)(k < KK ? pp[(k / KS) * PCOLS + (k % KS)] : 0.f);
-                }
-                *(bf16x8*)(As + swz128(tid, c)) = v;
+            for (int r = 0; r < 4; ++r) {
+                const float v = acc[a][b][r];
+                o[r] = (__bf16)v;
+                csum[b][r] += v;
+                csq[b][r] += v * v;
             }
+            if (y) *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
         }
-        __syncthreads();
-        // MFMA: wave w owns pixels 64w .. 64w+63 (4 blocks) x all 64 channels (4 blocks), K = 64 (2 steps)
-        f32x4 acc[4][4];
+    __syncthreads();
+    // the 2 x 128 output pixels are two contiguous 16-KB runs of NHWC
+    if (y) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int co = ((s * 4 + lg) ^ l7) << 4;
-            bf16x8 af[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(As + (wave * 64 + a * 16 + l16) * 128 + co);
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][b], af[a], acc[a][b], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) {
+            const int idx = tid + 256 * j;            // 16-B chunk of the 256 x 128-B tile
+            const int p = idx >> 3, c = idx & 7;
+            const int w = p >> 6, pl = p & 63;
+            const uint4 v = *(const uint4*)(smem + w * 64 * EROW + pl * EROW + c * 16);
+            const int pr = p / FTW, pc = p - (p / FTW) * FTW;
+            *(uint4*)(y + (((size_t)n * Ho + oh0 + pr) * Wo + ow0 + pc) * CO + c * 8) = v;
         }
-        __syncthreads();          // A tile no longer read: the output staging goes over it
-        // epilogue: lane holds pixel a*16+l16 (of its wave) and channels b*16+4lg .. +3.  y == NULL: statistics only
-        // (the first pass of the pooled forward, stem_conv_pool_kernel)
-        char* ep = smem + wave * 64 * EROW;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                bf16x4 o;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float v = acc[a][b][r];
-                    o[r] = (__bf16)v;
-                    csum[b][r] += v;
-                    csq[b][r] += v * v;
-                }
-                if (y) *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
-            }
-        if (y) {
-            __syncthreads();
-            // the 2 x 128 output pixels are two contiguous 16-KB runs of NHWC
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int idx = tid + 256 * j;            // 16-B chunk of the 256 x 128-B tile
-                const int p = idx >> 3, c = idx & 7;
-                const int w = p >> 6, pl = p & 63;
-                const uint4 v = *(const uint4*)(smem + w * 64 * EROW + pl * EROW + c * 16);
-                const int pr = p / FTW, pc = p - (p / FTW) * FTW;
-                *(uint4*)(y + (((size_t)n * Ho + oh0 + pr) * Wo + ow0 + pc) * CO + c * 8) = v;
-            }
-        }
-        // the next tile's patch store and barrier order these staging reads before the next im2col writes
     }
     if (stats) {
-        __syncthreads();
-        float* red = patch;                                 // [4 waves][64 ch][2] over the patch (no longer read)
+        float* red = (float*)(smem + 4 * 64 * EROW);        // [4 waves][64 ch][2]
 #pragma unroll
         for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -181,12 +173,12 @@ __global__ __launch_bounds__(256, 2) void stem_conv_fwd_kernel(const float* __re
             double s = 0.0, q = 0.0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) { s += red[(w * CO + tid) * 2]; q += red[(w * CO + tid) * 2 + 1]; }
-            const int rep = stat_rep(fin, blockIdx.x);
+            const int rep = stat_rep(fin, bid);
             atomic_add_f64(stats + ((long)rep * 2 + 0) * CO + tid, s);
             atomic_add_f64(stats + ((long)rep * 2 + 1) * CO + tid, q);
         }
     }
-    bn_fin_tail(fin, 256);
+    bn_fin_tail(fin, 256, smem);
 }
 
 // ---- forward, second pass: the conv recomputed, then BN + ReLU + MaxPool(3, 2, 1) (residuals.py:209-216) on the
@@ -778,11 +770,12 @@ extern "C" int scd_stem_conv_fwd_fin(int dtype, const float* x, const void* wpk,
     if (dtype != SCD_DT_BF16 || N <= 0 || Ho != (H + 2 * PD - KS) / SP + 1 || Wo != (W + 2 * PD - KS) / SP + 1 ||
         Wo % FTW || Ho % FTH || (fin && !stats) || (!y && !stats))
         return SCD_ERR_ARG;
-    // one workgroup per tile: the resident-grid walk (next patch in flight) measured slower, 121 vs 106 us with y and
-    // 95 vs 84 us statistics-only at B = 32 -- the kernel is bound by its LDS / VALU tile build, not by load latency
-    const int ntiles = N * (Ho / FTH) * (Wo / FTW);
-    hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, x, (const __bf16*)wpk,
-                       (__bf16*)y, stats, H, W, Ho, Wo, ntiles, bn_fin_dev(fin, stats, CO));
+    // one workgroup per tile (a resident-grid walk with the next tile's patch in flight and the weights in registers
+    // measured slower, 121 vs 106 us with y and 95 vs 84 us statistics-only at B = 32: the kernel is bound by its LDS /
+    // VALU tile build, not by load latency)
+    const int blocks = N * (Ho / FTH) * (Wo / FTW);
+    hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (const __bf16*)wpk,
+                       (__bf16*)y, stats, H, W, Ho, Wo, bn_fin_dev(fin, stats, CO));
     SCD_RETURN_LAUNCH();
 }
 
