@@ -523,6 +523,10 @@ int scd_event_create(void** ev);
 int scd_event_destroy(void* ev);
 int scd_event_record(void* ev, void* stream);
 int scd_event_elapsed_ms(void* start, void* end, float* ms);
+/* A stream restricted to the CUs set in mask (nwords x 32 bits, bit i = CU i; hipExtStreamCreateWithCUMask): the
+ * optional CU-confined weight-gradient side stream (SCD_SIDE_CUS).  Destroy with scd_stream_destroy. */
+int scd_stream_create_cumask(const unsigned* mask, int nwords, void** stream);
+int scd_stream_destroy(void* stream);
 
 const char* scd_version(void);
 

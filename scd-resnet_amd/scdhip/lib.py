@@ -151,6 +151,8 @@ SIGNATURES = {
     "scd_event_destroy": (I, [P]),
     "scd_event_record": (I, [P, P]),
     "scd_event_elapsed_ms": (I, [P, P, ctypes.POINTER(c_float)]),
+    "scd_stream_create_cumask": (I, [ctypes.POINTER(ctypes.c_uint), I, PP]),
+    "scd_stream_destroy": (I, [P]),
     "scd_version": (ctypes.c_char_p, []),
 }
 

@@ -914,7 +914,21 @@ def side_stream(dev):
 
 
 def _new_side_stream(idx):
-    return torch.cuda.Stream(device=idx, priority=_Side.priority)
+    ncu = int(os.environ.get("SCD_SIDE_CUS", "0"))
+    if ncu <= 0:
+        return torch.cuda.Stream(device=idx, priority=_Side.priority)
+    # SCD_SIDE_CUS=n: the side stream confined to n CUs spread evenly over the device (scd_stream_create_cumask; a
+    # CU-masked stream takes the default priority, still below the step's high-priority compute stream)
+    total = torch.cuda.get_device_properties(idx).multi_processor_count
+    ncu = min(ncu, total)
+    words = (ctypes.c_uint * ((total + 31) // 32))()
+    for j in range(ncu):
+        i = (j * total) // ncu
+        words[i // 32] |= 1 << (i % 32)
+    h = ctypes.c_void_p()
+    with torch.cuda.device(idx):
+        L.call("scd_stream_create_cumask", words, len(words), ctypes.byref(h))
+    return torch.cuda.ExternalStream(h.value, device=idx)
 
 
 def join_side_streams():
