@@ -2651,6 +2651,11 @@ static int ring_mode() {
     return mode;
 }
 
+static int narrow_ring_mode() {
+    // SCD_GEMM_NARROW_RING=1: narrow 1x1 shapes on the ring kernel (read per call: A/B)
+    const char* e = getenv("SCD_GEMM_NARROW_RING");
+    return e ? atoi(e) : 0;
+}
 static int pp_mode() {
     static int mode = -2;
     if (mode == -2) {
@@ -2822,6 +2827,12 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
     if (dtype == SCD_DT_BF16 && !narrow) {
         const int rm = ring_mode();
         ring = rm >= 0 ? rm != 0 : cdiv(Mtot, 256) * cdiv(p.Co, 128) >= 256;   // >= one tile per CU
+    } else if (dtype == SCD_DT_BF16 && narrow_ring_mode() && nphase == 1 && phases[0].ntaps == 1 && p.Ci >= 128 &&
+               cdiv(Mtot, 256) >= 256) {
+        // 1x1 convs into <= 64 channels over many pixels (the Bottleneck conv1 forward and conv3 input gradient at
+        // Res50 1024^2, residuals.py:122-165): HBM-bound skinny GEMMs on the LDS-DMA ring kernel, half its 128-column
+        // tile empty, instead of the register-staged 256 x 64 kernel
+        ring = true;
     }
     const int BM = ring ? 256 : (narrow ? 256 : 128), BN = (narrow && !ring) ? 64 : 128;
     p.ntn = cdiv(p.Co, BN);
