@@ -2652,9 +2652,11 @@ static int ring_mode() {
 }
 
 static int narrow_ring_mode() {
-    // SCD_GEMM_NARROW_RING=1: narrow 1x1 shapes on the ring kernel (read per call: A/B)
+    // SCD_GEMM_NARROW_RING=0: narrow 1x1 shapes on the register-staged 256 x 64 kernel (read per call: A/B).  On the
+    // ring kernel: Res50 1024^2 fp16 +0.4 % (the 256 x 64 kernel's 88 launches of 268 us per 11 steps become ring
+    // launches), Res10 neutral (profiles/r4_ab.txt)
     const char* e = getenv("SCD_GEMM_NARROW_RING");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
 }
 static int pp_mode() {
     static int mode = -2;
