@@ -348,7 +348,7 @@ def test_block_bn_backward_sums_from_dgrad_match_separate_reduce(name):
                                         ("centerOffsetRes50", torch.float32)])
 def test_fused_bn_finalize_matches_separate(name, dtype):
     """BN finalize by the last workgroup of its statistics producer (ops.BNFinalize: the _fin entry points, a
-    device-memory scd_bn_fin descriptor, 16 statistics replicas) against the separate finalize kernels: three
+    device-memory scd_bn_fin descriptor; opt-in, SCD_BN_FIN_FUSE=1) against the separate finalize kernels: three
     training steps (descriptors written once, counters reset by the kernels) give the same losses, running
     statistics and gradients up to the replicas' fp64 summation order; plus a pass with two forwards before their
     backward (the second forward finds the module's buffers held and takes the separate finalize)."""
@@ -359,6 +359,7 @@ def test_fused_bn_finalize_matches_separate(name, dtype):
     x2 = T.batch_inputs(52, 2, S).to(DEV)
     ys = [y.to(DEV) for y in T.batch_targets(53, 2, S // 4)]
     res = {}
+    was = ops.BNFinalize.enabled
     for fuse in (False, True):
         ops.BNFinalize.enabled = fuse
         try:
@@ -381,7 +382,7 @@ def test_fused_bn_finalize_matches_separate(name, dtype):
                          {k: v.detach().double().cpu().clone() for k, v in m.state_dict().items()
                           if "running" in k})
         finally:
-            ops.BNFinalize.enabled = True
+            ops.BNFinalize.enabled = was
     tol = 1e-5 if dtype == torch.float32 else 5e-2
     np.testing.assert_allclose(res[True][0], res[False][0], rtol=tol)
     worst = max(((a - res[False][1][k]).norm() / max(res[False][1][k].norm(), 1e-12)).item()
@@ -390,3 +391,27 @@ def test_fused_bn_finalize_matches_separate(name, dtype):
     assert worst < (1e-4 if dtype == torch.float32 else 1e-1), worst
     for k, a in res[True][2].items():
         np.testing.assert_allclose(a.numpy(), res[False][2][k].numpy(), rtol=tol, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("defer", [1, 2])
+def test_heads_wgrad_deferral_same_gradients(defer, monkeypatch):
+    """The heads' weight gradient issued behind the next `defer` BN backward applies (SCD_HEADS_WGRAD_DEFER) gives the
+    gradients of the undeferred order (fp32 parity mode: up to the fp64 BN statistics' summation order), and nothing
+    deferred is lost when the backward ends first."""
+    from scdhip import blocks
+    from scdhip.flat import FlatAdam
+    x = T.batch_inputs(61, 2, 256).to(DEV)
+    ys = [y.to(DEV) for y in T.batch_targets(62, 2, 64)]
+    res = {}
+    for d in (0, defer):
+        monkeypatch.setattr(blocks, "_HEADS_WGRAD_DEFER", d)
+        m, plugin, _, _ = make_model(torch.float32, "centerOffsetRes10")
+        opt = FlatAdam(filter(lambda p: p.requires_grad, m.parameters()))
+        opt.zero_grad()
+        loss, _ = plugin.loss(m(x, decode=False), ys)
+        loss.mean().backward()
+        torch.cuda.synchronize()
+        res[d] = {k: p.grad.detach().double().cpu().clone() for k, p in m.named_parameters()}
+    for k, a in res[defer].items():
+        b = res[0][k]
+        assert (a - b).norm().item() <= 1e-5 * max(b.norm().item(), 1e-12), k
