@@ -69,6 +69,9 @@ class CenterNetLossFn(torch.autograd.Function):
         loss = out[0:1]
         stats = out[1:4]
         ctx.mark_non_differentiable(stats)
+        # the statistics never carry a gradient: without this autograd fills a zeros tensor for them (one ATen launch
+        # between the loss and the heads' backward)
+        ctx.set_materialize_grads(False)
         return loss, stats
 
     @staticmethod
@@ -108,6 +111,9 @@ class FocalOnlyLossFn(torch.autograd.Function):
         ctx.save_for_backward(factors, *grads)
         stats = out[1:]
         ctx.mark_non_differentiable(stats)
+        # the statistics never carry a gradient: without this autograd fills a zeros tensor for them (one ATen launch
+        # between the loss and the heads' backward)
+        ctx.set_materialize_grads(False)
         return out[0:1], stats
 
     @staticmethod

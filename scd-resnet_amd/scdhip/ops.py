@@ -1183,12 +1183,7 @@ def fin_backward(bn, st, C, alpha):
 
 def bn_finalize(bn, stats, C, count, training=True):
     """Finalize statistics of a torch.nn.BatchNorm2d-shaped module `bn` (weight/bias/running_*)."""
-    dev = bn.weight.device
-    st = BNState()
-    st.mean = torch.empty(C, device=dev)
-    st.invstd = torch.empty(C, device=dev)
-    st.scale = torch.empty(C, device=dev)
-    st.shift = torch.empty(C, device=dev)
+    st = _bn_state(C, bn.weight.device)
     if training:
         return _bn_finalize_launch(bn, st, stats, _allreduce_stats(stats, C), C, count)
     else:
@@ -1209,11 +1204,9 @@ def _bn_finalize_launch(bn, st, stats, nrep, C, count):
 
 
 def _bn_state(C, dev):
+    # one allocation for the four per-channel vectors (one caching-allocator call per BN layer instead of four)
     st = BNState()
-    st.mean = torch.empty(C, device=dev)
-    st.invstd = torch.empty(C, device=dev)
-    st.scale = torch.empty(C, device=dev)
-    st.shift = torch.empty(C, device=dev)
+    st.mean, st.invstd, st.scale, st.shift = torch.empty(4, C, device=dev).unbind(0)
     return st
 
 
