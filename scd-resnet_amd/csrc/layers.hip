@@ -215,8 +215,12 @@ __global__ void im2col_stem_kernel(const float* x, T* cols, int N, int H, int W,
 }
 
 // ---------------------------------------------------------------- stem BN+ReLU+MaxPool(3,2,1)
+// workgroups of 256 per CU the pool is compiled for (registers: its nine 16-B window loads in flight per thread)
+#ifndef STEM_POOL_OCC
+#define STEM_POOL_OCC 4
+#endif
 template <typename T>
-__global__ void stem_pool_fwd_kernel(const T* y, const float* scale, const float* shift, T* out, uint8_t* argmax,
+__global__ __launch_bounds__(256, STEM_POOL_OCC) void stem_pool_fwd_kernel(const T* y, const float* scale, const float* shift, T* out, uint8_t* argmax,
                                      int N, int H, int W, int C, int Ho, int Wo) {
     constexpr int E = Vec16<T>::N;
     const unsigned cpp = C / E;

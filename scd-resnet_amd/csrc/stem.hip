@@ -29,10 +29,14 @@ __device__ __forceinline__ float stem_row16_sum(float v) {
 
 // ---- forward: one workgroup = 2 output rows x 128 output columns (256 pixels) of one image
 constexpr int FTW = 128, FTH = 2;
+// workgroups per CU the forward conv is compiled for (registers); its LDS (49 KB) admits 3
+#ifndef STEM_FWD_OCC
+#define STEM_FWD_OCC 3
+#endif
 constexpr int PROWS = SP * (FTH - 1) + KS;          // 9 input rows
 constexpr int PCOLS = SP * (FTW - 1) + KS + 1;      // 262 -> padded to an even count
 
-__global__ __launch_bounds__(256) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
+__global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
                                                             __bf16* __restrict__ y, double* __restrict__ stats,
                                                             int H, int W, int Ho, int Wo, BnFinDev fin) {
     constexpr int AT = FTH * FTW * 128;             // A tile [256 px][64 taps] bf16, 128-B rows
