@@ -347,9 +347,6 @@ class ConvBNFn(torch.autograd.Function):
 
 
 _HEADS_WGRAD_LATE = os.environ.get("SCD_HEADS_WGRAD_LATE", "1") == "1"
-# SCD_HEADS_WGRAD_DEFER=k: the heads' weight gradient issued after the k-th BN backward apply that follows (0: right
-# after the heads' input gradient)
-_HEADS_WGRAD_DEFER = int(os.environ.get("SCD_HEADS_WGRAD_DEFER", "0"))
 
 
 class HeadsFn(torch.autograd.Function):
@@ -532,10 +529,6 @@ class HeadsFn(torch.autograd.Function):
         mods = [m for h in heads for m in h if isinstance(m, torch.nn.Module)]
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
-        if late and _HEADS_WGRAD_DEFER > 0 and dev.type == "cuda":
-            # the gradients are reported ready (FlatDDP buckets) only once their GEMMs are enqueued
-            ops.defer_side_launch(lambda: (wgrads(), grads_ready(*mods)), _HEADS_WGRAD_DEFER)
-            return dfeat, None, None
         if late:
             wgrads()             # side stream ordered after the input gradient: it overlaps the deconv backward
         grads_ready(*mods)

@@ -933,36 +933,9 @@ def _new_side_stream(idx):
 
 def join_side_streams():
     """Make every device's compute stream wait for its side stream (end of backward)."""
-    _run_deferred(everything=True)
     for idx, s in _Side.streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
     _Side.joined_task.clear()
-
-
-_DEFERRED = []          # [BN backward applies still to pass, fn]
-
-
-def defer_side_launch(fn, applies):
-    """Run fn (side-stream launches) right after the `applies`-th BN backward apply from now is enqueued on the compute
-    stream (HeadsFn, SCD_HEADS_WGRAD_DEFER: the heatmap head's weight gradient behind the deconv BN backward applies,
-    so its one-workgroup-per-CU GEMM does not hold the CUs those passes and the deconv input gradient need).  Whatever
-    is still deferred at the end of the backward runs before the side streams are joined."""
-    _DEFERRED.append([applies, fn])
-    torch.autograd.Variable._execution_engine.queue_callback(lambda: _run_deferred(everything=True))
-
-
-def _run_deferred(everything=False, applied=False):
-    if not _DEFERRED:
-        return
-    keep = []
-    due = []
-    for item in _DEFERRED:
-        if applied:
-            item[0] -= 1
-        (due if everything or item[0] <= 0 else keep).append(item)
-    _DEFERRED[:] = keep
-    for _, fn in due:
-        fn()
 
 
 def side_stream_for_comm(dev):
@@ -1252,8 +1225,6 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None)
     dy = torch.empty_like(y)
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),
            ptr(dz_out), stream())
-    if _DEFERRED:
-        _run_deferred(applied=True)
     return dy
 
 

@@ -391,27 +391,3 @@ def test_fused_bn_finalize_matches_separate(name, dtype):
     assert worst < (1e-4 if dtype == torch.float32 else 1e-1), worst
     for k, a in res[True][2].items():
         np.testing.assert_allclose(a.numpy(), res[False][2][k].numpy(), rtol=tol, atol=1e-6, err_msg=k)
-
-
-@pytest.mark.parametrize("defer", [1, 2])
-def test_heads_wgrad_deferral_same_gradients(defer, monkeypatch):
-    """The heads' weight gradient issued behind the next `defer` BN backward applies (SCD_HEADS_WGRAD_DEFER) gives the
-    gradients of the undeferred order (fp32 parity mode: up to the fp64 BN statistics' summation order), and nothing
-    deferred is lost when the backward ends first."""
-    from scdhip import blocks
-    from scdhip.flat import FlatAdam
-    x = T.batch_inputs(61, 2, 256).to(DEV)
-    ys = [y.to(DEV) for y in T.batch_targets(62, 2, 64)]
-    res = {}
-    for d in (0, defer):
-        monkeypatch.setattr(blocks, "_HEADS_WGRAD_DEFER", d)
-        m, plugin, _, _ = make_model(torch.float32, "centerOffsetRes10")
-        opt = FlatAdam(filter(lambda p: p.requires_grad, m.parameters()))
-        opt.zero_grad()
-        loss, _ = plugin.loss(m(x, decode=False), ys)
-        loss.mean().backward()
-        torch.cuda.synchronize()
-        res[d] = {k: p.grad.detach().double().cpu().clone() for k, p in m.named_parameters()}
-    for k, a in res[defer].items():
-        b = res[0][k]
-        assert (a - b).norm().item() <= 1e-5 * max(b.norm().item(), 1e-12), k
