@@ -35,6 +35,11 @@ constexpr int FTW = 128, FTH = 2;
 #endif
 constexpr int PROWS = SP * (FTH - 1) + KS;          // 9 input rows
 constexpr int PCOLS = SP * (FTW - 1) + KS + 1;      // 262 -> padded to an even count
+// the forward's input patch in LDS with each row split by column parity (as the backward's, bpatch_idx): the 64 lanes
+// of a wave (64 consecutive pixels) then read 64 consecutive floats per tap instead of every other one (2-way bank
+// conflicts on every tap read of the im2col build)
+constexpr int FPAR = 132;                            // >= 131 columns per parity
+constexpr int FROW = 2 * FPAR;
 
 __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
                                                             __bf16* __restrict__ y, double* __restrict__ stats,
@@ -42,7 +47,7 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
     constexpr int AT = FTH * FTW * 128;             // A tile [256 px][64 taps] bf16, 128-B rows
     constexpr int BT = CO * 128;                    // B tile [64 co][64 taps]
     constexpr int EROW = CO * 2 + 16;
-    __shared__ __attribute__((aligned(16))) char smem[AT + BT + PROWS * PCOLS * 4];
+    __shared__ __attribute__((aligned(16))) char smem[AT + BT + PROWS * FROW * 4];
     char* As = smem;
     char* Bs = smem + AT;
     float* patch = (float*)(smem + AT + BT);
@@ -78,21 +83,22 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
         if (i < PROWS * PCOLS) {
             const int r = i / PCOLS, c = i - (i / PCOLS) * PCOLS;
             const int ih = ih0 + r, iw = iw0 + c;
-            patch[i] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? pv[j] : 0.f;
+            patch[r * FROW + (c & 1) * FPAR + (c >> 1)] =
+                ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? pv[j] : 0.f;
         }
     }
     __syncthreads();
     // im2col tile: thread -> pixel p = tid, all 64 taps (8 chunks of 8)
     {
         const int pr = tid / FTW, pc = tid - (tid / FTW) * FTW;
-        const float* pp = patch + (SP * pr) * PCOLS + SP * pc;
+        const float* pp = patch + (SP * pr) * FROW + pc;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             bf16x8 v;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int k = c * 8 + e;
-                v[e] = (__bf16)(k < KK ? pp[(k / KS) * PCOLS + (k % KS)] : 0.f);
+                v[e] = (__bf16)(k < KK ? pp[(k / KS) * FROW + ((k % KS) & 1) * FPAR + ((k % KS) >> 1)] : 0.f);
             }
             *(bf16x8*)(As + swz128(tid, c)) = v;
         }
@@ -494,6 +500,14 @@ __global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __re
 // x 8 channel chunks = one item per thread).  W G uses the conv's bf16 weights in fp32 (the forward multiplied
 // the same operands), so dW matches the unfused path up to the bf16 rounding of y and dy that it no longer has.
 constexpr int BTW = 64;                              // conv columns per tile (two conv rows per tile)
+// The backward's input patch in LDS with each row split by column parity (even columns at 0.., odd at PPAR..) and rows
+// PROW floats apart: tap (kh, kw) of pixel px reads row kh at parity kw & 1, index px + kw / 2, so the 16 taps x 4
+// pixel groups of a wave's column-build read hit 64 distinct banks but for a few taps of a third kernel row (row
+// offsets 4 (mod 16) apart, parities 8 apart); the plain layout (column 2 px + kw, rows 134 apart) averaged ~4
+// bank-conflict cycles per LDS instruction in this kernel (profiles/r4_sq_stem.txt)
+constexpr int PPAR = 72;                             // >= 67 columns per parity, = 8 (mod 16)
+constexpr int PROW = 148;                            // >= PPAR + 67, = 4 (mod 16)
+__device__ __forceinline__ int bpatch_idx(int r, int c) { return r * PROW + (c & 1) * PPAR + (c >> 1); }
 constexpr int BPROWS = 9;                            // input rows of a tile: conv rows 2bo, 2bo+1 -> 4bo-3 .. 4bo+5
 constexpr int ONE_TAP = KK;                          // col tap 49 = 1
 
@@ -508,7 +522,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
     int H, int W, int Ho, int Wo, int ntiles, int chunk) {
     constexpr int DT = WPX * DROW;                   // one conv row of dz: [64 px][DROW]
     constexpr int CT = 64 * 128;                     // one conv row of columns: [64 taps][64 px] bf16
-    __shared__ __attribute__((aligned(16))) char smem[2 * DT + 2 * CT + BPROWS * WPCOLS * 4];
+    __shared__ __attribute__((aligned(16))) char smem[2 * DT + 2 * CT + BPROWS * PROW * 4];
     // the BN parameters in LDS ([scale | shift | mean | invstd][64]), read per 2x2 block: 32 VGPRs fewer than holding
     // each thread's 8 channels of all four in registers (the kernel sits at its 256-VGPR bound)
     __shared__ __attribute__((aligned(16))) float prm[4 * CO];
@@ -638,7 +652,10 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
 #pragma unroll
         for (int q = 0; q < (BPROWS * WPCOLS + 255) / 256; ++q) {
             const int i = tid + 256 * q;
-            if (i < BPROWS * WPCOLS) patch[i] = rp[q];
+            if (i < BPROWS * WPCOLS) {
+                const int r = i / WPCOLS, c = i - (i / WPCOLS) * WPCOLS;
+                patch[bpatch_idx(r, c)] = rp[q];
+            }
         }
         if (t + 1 < t1) load_tile(t + 1);                 // in flight during this tile's column build and MFMAs
         __syncthreads();
@@ -654,7 +671,8 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         const int px = pq * 16 + h * 8 + e;
-                        v[e] = (__bf16)(k < KK ? patch[(2 * a + kh) * WPCOLS + SP * px + kw] : (k == ONE_TAP ? 1.f : 0.f));
+                        v[e] = (__bf16)(k < KK ? patch[(2 * a + kh) * PROW + (kw & 1) * PPAR + px + (kw >> 1)]
+                                              : (k == ONE_TAP ? 1.f : 0.f));
                     }
                     *(bf16x8*)(Cs + a * CT + swz128(k, pq * 2 + h)) = v;
                 }
