@@ -19,8 +19,6 @@ CSRC = os.path.join(os.path.dirname(HERE), "scd-resnet_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 # kernel-name fragment -> most `s_waitcnt vmcnt(0)` allowed between its first and last MFMA (what the schedules write:
-# the NQ = 2 weight-gradient stage hand-off and the layer1 weight gradient's per-stage wait; the heads kernel's
-# range includes its epilogue's 1x1 tails)
 # the NQ = 2 weight-gradient stage hand-off, the layer1 weight gradient's per-stage wait, the row-ring kernel's
 # per-tile waits (its loop is the run of tiles: 5 plain, 3 with the BN-backward sums); the heads kernel's range
 # includes its epilogue's 1x1 tails).  Keys are regular expressions on the mangled kernel name.
