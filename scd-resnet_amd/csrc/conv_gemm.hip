@@ -2048,6 +2048,11 @@ __device__ __forceinline__ int wr_f(int r) { return (r & 3) | ((r >> 1) & 4); }
 // 3/4 of stage t, like the A rows of the forward kernel; X ([64 px][512 B], read whole in phase 1) is
 // fetched in phases 1/2.  Counted waits as conv_gemm_pp_kernel (NB2 = 2).  Requires Wo % 64 == 0 and
 // (Ho*Wo) % 64 == 0: a stage is part of one output row, addressed by a scalar cursor (see FASTX 1).
+// NQ 2 (48-KB stages, half the MFMAs per stage of NQ 4): three stage buffers, two stages of DMA in flight -- a stage
+// is ~1000 MFMA cycles, shorter than the operand fetch latency under load (SCD_PP2_NBUF=2: two buffers).
+#ifndef SCD_PP2_NBUF
+#define SCD_PP2_NBUF 3
+#endif
 template <int NQ>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     constexpr int KP = 64, EPC = 8;
@@ -2056,7 +2061,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     constexpr int WIN = 64 * NQ;                      // channels per window (256, 192 or 128)
     static_assert(NQ >= 2 && NQ <= 4, "NQ");
     constexpr int STAGE = GBYTES + KP * 512;          // + X image
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    constexpr int NBUF = NQ == 2 ? SCD_PP2_NBUF : 2;
+    static_assert(NBUF == 2 || NBUF == 3, "NBUF");
+    __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -2207,7 +2214,17 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) issue_g(pix0, smem, q);
         advance();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (NBUF == 3) {
+            // stage 1 into the second buffer; wait for stage 0 only (6 DMAs a stage per wave)
+            issue_x(pix0 + KP, smem + STAGE, 0);
+            issue_x(pix0 + KP, smem + STAGE, 1);
+            issue_g(pix0 + KP, smem + STAGE, 0);
+            issue_g(pix0 + KP, smem + STAGE, 1);
+            advance();
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         bar();
         if (grp == 1) bar();
         // schedule (stage t fetches stage t+1 into the other buffer): phase 1: X half 0, phase 2: X half 1,
@@ -2219,11 +2236,16 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         // must be retired before the barrier after which group 0 reads it: group 0's post-MFMA barrier of phase 2,
         // which for group 1 (one barrier behind) is the barrier BEFORE its phase-2 MFMAs -- group 0 waits vmcnt(0)
         // after its MFMAs, group 1 before that barrier (waiting after it, as group 0 does, let group 0 read group 1's
-        // half of the stage before it had landed: NaN weight gradients, layer2 downsample, cornerNetCPool B=32)
+        // half of the stage before it had landed: NaN weight gradients, layer2 downsample, cornerNetCPool B=32).
+        // Three buffers: stage t issues stage t+2 into the buffer stage t-1 used (the same overwrite rule), and the
+        // waits keep stage t+2's six DMAs in flight (vmcnt(6)) while retiring stage t+1's.
+        int bcur = 0;
         for (int t = 0; t < nk; ++t) {
-            char* cur = smem + (t & 1) * STAGE;
-            char* nxt = smem + ((t & 1) ^ 1) * STAGE;
-            const int k1 = pix0 + (t + 1) * KP;      // >= pix1 on the last stage: the DMAs read nothing
+            char* cur = smem + bcur * STAGE;
+            const int bnxt = NBUF == 3 ? (bcur == 0 ? 2 : bcur - 1) : (bcur ^ 1);
+            char* nxt = smem + bnxt * STAGE;
+            bcur = NBUF == 3 ? (bcur == 2 ? 0 : bcur + 1) : (bcur ^ 1);
+            const int k1 = pix0 + (t + NBUF - 1) * KP;      // >= pix1 near the end: the DMAs read nothing
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 bf16x8 (&gf)[2][2] = (q & 1) ? gfy : gfx;
@@ -2234,11 +2256,17 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
                     if (q == 1) {
                         advance();
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (grp == 1) {
+                            if constexpr (NBUF == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        }
                     }
                     bar();
                     mfma_q(q, gf);
-                    if (q == 1 && grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (q == 1 && grp == 0) {
+                        if constexpr (NBUF == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
                     bar();
                     continue;
                 }
