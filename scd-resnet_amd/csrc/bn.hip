@@ -12,6 +12,16 @@
 // kernel holds 2 x 216 of the 512 VGPRs per SIMD lane (one 8-wave workgroup per CU), so a wave that needs 88 could
 // not start on any CU until those workgroups retire (in the step the deconv2 BN backward apply then waited out the
 // whole deconv3 weight gradient)
+// vectors in flight per thread in bn_bwd_apply_kernel (80 VGPRs at 2, no spill): beside the weight-gradient stream's
+// one-workgroup-per-CU GEMM a CU holds one or two of its waves per SIMD, so the bytes each wave keeps in flight set
+// its bandwidth there (the fp16 build stays at 1: at 2 it spills 8 bytes)
+#ifndef BN_APPLY_U
+#ifdef SCD_F16_BUILD
+#define BN_APPLY_U 1
+#else
+#define BN_APPLY_U 2
+#endif
+#endif
 #ifndef BN_EW_WAVES
 #define BN_EW_WAVES 6
 #endif
@@ -303,10 +313,10 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply_kernel(const T*
                                                            const float* rsh, const float* coef, int C, unsigned nvec,
                                                            T* dy, T* dz_out) {
     constexpr int E = Vec16<T>::N;
-    // BN_BWD_U vectors in flight, kept packed (16 B each) until used: <= 88 VGPRs, so the kernel's waves fit beside
-    // a one-workgroup-per-CU GEMM of the weight-gradient stream (2 x 212 of the 512 VGPRs per lane) instead of
+    // BN_APPLY_U vectors in flight, kept packed (16 B each) until used: <= 80 VGPRs, so the kernel's waves fit beside
+    // a one-workgroup-per-CU GEMM of the weight-gradient stream (2 x 216 of the 512 VGPRs per lane) instead of
     // waiting for its workgroups to retire
-    constexpr int U = BN_BWD_U;
+    constexpr int U = BN_APPLY_U;
     // fixed channel chunk per thread (see bn_apply_kernel): coefficients in registers
     const unsigned cpr = (unsigned)C / E;
     const unsigned v0 = blockIdx.x * blockDim.x + threadIdx.x;
