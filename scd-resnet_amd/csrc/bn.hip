@@ -2,6 +2,7 @@
 // Statistics are accumulated in fp64 into SCD_STAT_REPLICAS replicas (spreads the atomics),
 // finalised per channel; apply / backward passes are 16-byte-vectorised elementwise kernels.
 #include <algorithm>
+#include <type_traits>
 
 #include "scd_common.h"
 
@@ -226,47 +227,51 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T
     float s[E], q[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) { s[e] = 0.f; q[e] = 0.f; }
-    auto acc = [&](const float* d, const float* yv, const float* mk) {
-        float mu[E], is[E], ka[E], kb[E];
-        lds_params<E>(sp, ch * E, mu);
-        lds_params<E>(sp, C + ch * E, is);
-        if (rsc) { lds_params<E>(sp, 2 * C + ch * E, ka); lds_params<E>(sp, 3 * C + ch * E, kb); }
+    // one loop per mask kind (0: none, 1: the stored activation, 2: BN+ReLU recomputed from y), as in
+    // bn_bwd_apply_kernel: no per-element branch regions
+    auto run = [&](auto kind) {
+        constexpr int MK = decltype(kind)::value;
+        auto acc_raw = [&](const uint4& rd, const uint4& ry, const uint4& rm) {
+            float d[E], yv[E], mk[E], mu[E], is[E], ka[E], kb[E];
+            Vec16<T>::load(&rd, d);
+            Vec16<T>::load(&ry, yv);
+            if constexpr (MK == 1) Vec16<T>::load(&rm, mk);
+            lds_params<E>(sp, ch * E, mu);
+            lds_params<E>(sp, C + ch * E, is);
+            if constexpr (MK == 2) { lds_params<E>(sp, 2 * C + ch * E, ka); lds_params<E>(sp, 3 * C + ch * E, kb); }
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            // relu mask: the stored activation (mask) or, for BN+ReLU, the forward's own y*scale+shift > 0
-            const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
-            const float dz = off ? 0.f : d[e];
-            s[e] += dz;
-            q[e] += dz * (yv[e] - mu[e]) * is[e];
+            for (int e = 0; e < E; ++e) {
+                bool off = false;
+                if constexpr (MK == 1) off = !(mk[e] > 0.f);
+                if constexpr (MK == 2) off = !(yv[e] * ka[e] + kb[e] > 0.f);
+                const float dz = off ? 0.f : d[e];
+                s[e] += dz;
+                q[e] += dz * (yv[e] - mu[e]) * is[e];
+            }
+        };
+        unsigned r = r0 + rsub;
+        for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+            uint4 rd[U], ry[U], rm[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const unsigned i = (r + u * rpi) * (unsigned)ld + ch * E;
+                rd[u] = *(const uint4*)(dout + i);
+                ry[u] = *(const uint4*)(y + i);
+                rm[u] = MK == 1 ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc_raw(rd[u], ry[u], rm[u]);
+        }
+        for (; r < r1; r += rpi) {
+            const unsigned i = r * (unsigned)ld + ch * E;
+            const uint4 rd = *(const uint4*)(dout + i), ry = *(const uint4*)(y + i);
+            const uint4 rm = MK == 1 ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
+            acc_raw(rd, ry, rm);
         }
     };
-    // raw 16-B vectors (kept packed until used: fewer VGPRs, see bn_bwd_apply_kernel)
-    auto acc_raw = [&](const uint4& rd, const uint4& ry, const uint4& rm) {
-        float d[E], yv[E], mk[E];
-        Vec16<T>::load(&rd, d);
-        Vec16<T>::load(&ry, yv);
-        if (mask) Vec16<T>::load(&rm, mk);
-        acc(d, yv, mk);
-    };
-    unsigned r = r0 + rsub;
-    for (; r + (U - 1) * rpi < r1; r += U * rpi) {
-        uint4 rd[U], ry[U], rm[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const unsigned i = (r + u * rpi) * (unsigned)ld + ch * E;
-            rd[u] = *(const uint4*)(dout + i);
-            ry[u] = *(const uint4*)(y + i);
-            rm[u] = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc_raw(rd[u], ry[u], rm[u]);
-    }
-    for (; r < r1; r += rpi) {
-        const unsigned i = r * (unsigned)ld + ch * E;
-        const uint4 rd = *(const uint4*)(dout + i), ry = *(const uint4*)(y + i);
-        const uint4 rm = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
-        acc_raw(rd, ry, rm);
-    }
+    if (mask) run(std::integral_constant<int, 1>{});
+    else if (rsc) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 0>{});
     // red[stat][rsub][channel]
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -330,45 +335,55 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply_kernel(const T*
         stage_params(sp, src, 5, cb, W);
     }
     const int cl = c0 - cb;
-    // raw 16-B vectors -> dz (masked gradient) and dy, stored
-    auto body = [&](size_t i, const uint4& rd, const uint4& ry, const uint4& rm) {
-        float d[E], yv[E], mk[E], ca[E], cq[E], cc[E], ka[E], kb[E];
-        Vec16<T>::load(&rd, d);
-        Vec16<T>::load(&ry, yv);
-        if (mask) Vec16<T>::load(&rm, mk);
-        lds_params<E>(sp, cl, ca);
-        lds_params<E>(sp, W + cl, cq);
-        lds_params<E>(sp, 2 * W + cl, cc);
-        if (rsc) { lds_params<E>(sp, 3 * W + cl, ka); lds_params<E>(sp, 4 * W + cl, kb); }
+    // raw 16-B vectors -> dz (masked gradient) and dy, stored.  One loop per mask kind (0: none, 1: the stored
+    // activation, 2: BN+ReLU recomputed from y): with the kind a runtime test inside the element loop the compiler
+    // built the loop from per-element branch regions (8 per vector)
+    auto run = [&](auto kind) {
+        constexpr int MK = decltype(kind)::value;
+        auto body = [&](size_t i, const uint4& rd, const uint4& ry, const uint4& rm) {
+            float d[E], yv[E], mk[E], ca[E], cq[E], cc[E], ka[E], kb[E];
+            Vec16<T>::load(&rd, d);
+            Vec16<T>::load(&ry, yv);
+            if constexpr (MK == 1) Vec16<T>::load(&rm, mk);
+            lds_params<E>(sp, cl, ca);
+            lds_params<E>(sp, W + cl, cq);
+            lds_params<E>(sp, 2 * W + cl, cc);
+            if constexpr (MK == 2) { lds_params<E>(sp, 3 * W + cl, ka); lds_params<E>(sp, 4 * W + cl, kb); }
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const bool off = mask ? !(mk[e] > 0.f) : (rsc ? !(yv[e] * ka[e] + kb[e] > 0.f) : false);
-            const float dz = off ? 0.f : d[e];
-            d[e] = dz;
-            yv[e] = ca[e] * dz + cq[e] * yv[e] + cc[e];
+            for (int e = 0; e < E; ++e) {
+                bool off = false;
+                if constexpr (MK == 1) off = !(mk[e] > 0.f);
+                if constexpr (MK == 2) off = !(yv[e] * ka[e] + kb[e] > 0.f);
+                const float dz = off ? 0.f : d[e];
+                d[e] = dz;
+                yv[e] = ca[e] * dz + cq[e] * yv[e] + cc[e];
+            }
+            Vec16<T>::store(dy + i, yv);
+            if (dz_out) Vec16<T>::store(dz_out + i, d);
+        };
+        unsigned v = v0;
+        for (; v + (U - 1) * stride < nvec; v += U * stride) {
+            uint4 rd[U], ry[U], rm[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t i = (size_t)(v + u * stride) * E;
+                rd[u] = *(const uint4*)(dout + i);
+                ry[u] = *(const uint4*)(y + i);
+                rm[u] = MK == 1 ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) body((size_t)(v + u * stride) * E, rd[u], ry[u], rm[u]);
         }
-        Vec16<T>::store(dy + i, yv);
-        if (dz_out) Vec16<T>::store(dz_out + i, d);
+        for (; v < nvec; v += stride) {
+            const size_t i = (size_t)v * E;
+            const uint4 rd = *(const uint4*)(dout + i), ry = *(const uint4*)(y + i);
+            const uint4 rm = MK == 1 ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
+            body(i, rd, ry, rm);
+        }
     };
-    unsigned v = v0;
-    for (; v + (U - 1) * stride < nvec; v += U * stride) {
-        uint4 rd[U], ry[U], rm[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const size_t i = (size_t)(v + u * stride) * E;
-            rd[u] = *(const uint4*)(dout + i);
-            ry[u] = *(const uint4*)(y + i);
-            rm[u] = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) body((size_t)(v + u * stride) * E, rd[u], ry[u], rm[u]);
-    }
-    for (; v < nvec; v += stride) {
-        const size_t i = (size_t)v * E;
-        const uint4 rd = *(const uint4*)(dout + i), ry = *(const uint4*)(y + i);
-        const uint4 rm = mask ? *(const uint4*)(mask + i) : make_uint4(0, 0, 0, 0);
-        body(i, rd, ry, rm);
-    }
+    if (mask) run(std::integral_constant<int, 1>{});
+    else if (rsc) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 0>{});
 }
 
 // ---- two BN layers behind one residual join (BasicBlock / Bottleneck bn2|bn3 + downsample BN, residuals.py:

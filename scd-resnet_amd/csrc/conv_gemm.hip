@@ -1211,9 +1211,16 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                 v[r] = acc[a][b][r] + bias[r];
                 if (p.relu) v[r] = fmaxf(v[r], 0.f);
             }
-            if (!p.bnbwd && m < M) {
+            if (!p.bnbwd) {
+                // a select per element, not a branch region per fragment (the sums never hold -0, so adding +0 for
+                // rows past M leaves them unchanged)
+                const bool mok = m < M;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+                for (int r = 0; r < 4; ++r) {
+                    const float t = mok ? v[r] : 0.f;
+                    csum[b][r] += t;
+                    csq[b][r] += t * t;
+                }
             }
             typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
             bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
@@ -1276,12 +1283,14 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             }
         }
     } else {
+        // (128 * CPR is a multiple of 64: the same trip count in every lane) rows past M / columns past Co compute on
+        // a valid address (pixel 0, channel 0) and skip only the store: no branch around the accumulate load
         for (int idx = lane; idx < 128 * CPR; idx += 64) {
             const int row = idx / CPR, ch = idx - (idx / CPR) * CPR;
             const int m = mt * BM + 128 * grp + row;
             const int col = nt * BN + wc * WCOLS + ch * EPC;
-            if (m >= M || col >= p.Co) continue;
-            T* dst = (T*)(p.y) + out_off(m, col);
+            const bool ok = m < M && col < p.Co;
+            T* dst = (T*)(p.y) + out_off(ok ? m : 0, ok ? col : 0);
             uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
             if (p.accumulate) {
                 float a[EPC], o[EPC];
@@ -1292,7 +1301,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                 Vec16<T>::store(&v, a);
             }
             if constexpr (dbg == 60) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));   // ablation 60: no stores
-            else *(uint4*)dst = v;
+            else if (ok) *(uint4*)dst = v;
         }
     }
     if (p.stats) {

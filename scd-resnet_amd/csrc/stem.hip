@@ -623,7 +623,9 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
                             const bool hit = ((aw[e >> 2] >> (8 * (e & 3))) & 0xffu) == sel;
-                            if (hit) g[e] += d[e];
+                            // a select, not a branch (as `if (hit) g += d` the compiler emitted 63 exec-masked
+                            // branch regions per tile); g is never -0, so adding +0 leaves it unchanged
+                            g[e] += hit ? d[e] : 0.f;
                             if constexpr (PY) {
                                 const unsigned m = 0xffffu << (16 * (e & 1));
                                 ybw[e >> 1] = hit ? (ybw[e >> 1] & ~m) | (ymw[e >> 1] & m) : ybw[e >> 1];
@@ -652,7 +654,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
 #pragma unroll
         for (int q = 0; q < (BPROWS * WPCOLS + 255) / 256; ++q) {
             const int i = tid + 256 * q;
-            if (i < BPROWS * WPCOLS) {
+            if ((q + 1) * 256 <= BPROWS * WPCOLS || i < BPROWS * WPCOLS) {   // (only the last q can be partial)
                 const int r = i / WPCOLS, c = i - (i / WPCOLS) * WPCOLS;
                 patch[bpatch_idx(r, c)] = rp[q];
             }
@@ -662,7 +664,11 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
         // ---- transposed column tiles of both conv rows: thread -> tap k = tid / 4, pixels 16 (tid % 4) .. +15
         {
             const int k = tid >> 2, pq = tid & 3;
-            const int kh = k / KS, kw = k - (k / KS) * KS;
+            // taps >= KK read tap KK-1's address and drop it: an LDS read under `k < KK` became an exec-masked
+            // branch per read (32 per tile)
+            const int kc = min(k, KK - 1);
+            const int kh = kc / KS, kw = kc - (kc / KS) * KS;
+            const float kfill = k == ONE_TAP ? 1.f : 0.f;
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -671,8 +677,8 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         const int px = pq * 16 + h * 8 + e;
-                        v[e] = (__bf16)(k < KK ? patch[(2 * a + kh) * PROW + (kw & 1) * PPAR + px + (kw >> 1)]
-                                              : (k == ONE_TAP ? 1.f : 0.f));
+                        const float pv = patch[(2 * a + kh) * PROW + (kw & 1) * PPAR + px + (kw >> 1)];
+                        v[e] = (__bf16)(k < KK ? pv : kfill);
                     }
                     *(bf16x8*)(Cs + a * CT + swz128(k, pq * 2 + h)) = v;
                 }
