@@ -89,3 +89,50 @@ def test_lds_dma_main_loops_keep_counted_waits(tmp_path):
                                                                                                   ceiling)
             seen[frag] += 1
     assert all(seen.values()), seen
+
+
+def _loop_span(lines):
+    """[start, end) of the longest loop (a label and the last backward branch to it)."""
+    labels = {}
+    for k, l in enumerate(lines):
+        m = re.match(r"^(\.LBB\d+_\d+):", l)
+        if m:
+            labels[m.group(1)] = k
+    best = (0, 0, 0)
+    for k, l in enumerate(lines):
+        m = re.search(r"s_c?branch\w*\s+(\.LBB\d+_\d+)\b", l)
+        if m and m.group(1) in labels and labels[m.group(1)] < k and k - labels[m.group(1)] > best[0]:
+            best = (k - labels[m.group(1)], labels[m.group(1)], k)
+    return best[1], best[2]
+
+
+# kernel-name regex -> most exec-masked branch regions (`s_and_saveexec`) allowed in its longest loop: the stem
+# backward's tile loop and the BN backward elementwise loops were built from per-read / per-element branch regions
+# until round 4 (63 per stem tile, 8 per BN vector) -- a runtime condition around an LDS read or a per-element pointer
+# test turns into them silently
+BRANCH_CEILING = {
+    ("stem.hip", r"stem_bwd_fused_kernelILb0E"): 4,
+    ("bn.hip", r"bn_bwd_apply_kernelIDF16bE"): 4,
+    ("bn.hip", r"bn_bwd_reduce_kernelIDF16bLb0E"): 4,
+}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
+def test_inner_loops_have_no_branch_regions(tmp_path):
+    asm = {}
+    for src in sorted({s for s, _ in BRANCH_CEILING}):
+        out = tmp_path / (src + ".s")
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "--cuda-device-only", "-O3", "-std=c++17", "-munsafe-fp-atomics",
+                        "-I", CSRC, "-I", os.path.join(os.path.dirname(os.path.dirname(CSRC)), "include"),
+                        "-S", os.path.join(CSRC, src), "-o", str(out)], check=True, capture_output=True, timeout=600)
+        asm[src] = _kernels(out.read_text())
+    for (src, frag), ceiling in BRANCH_CEILING.items():
+        names = [n for n in asm[src] if re.search(frag, n)]
+        assert names, frag
+        for name in names:
+            lines = asm[src][name]
+            lo, hi = _loop_span(lines)
+            assert hi > lo, name
+            regions = sum("s_and_saveexec" in l for l in lines[lo:hi])
+            assert regions <= ceiling, "%s: %d exec-masked branch regions in its main loop (at most %d)" % (
+                name, regions, ceiling)
