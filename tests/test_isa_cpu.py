@@ -5,7 +5,9 @@ The ring / ping-pong / row-ring / weight-gradient kernels keep two or three DMA 
 when it cannot prove the DMA'd LDS does not alias what is read -- e.g. when the kernel gains a second `__shared__`
 object (round 4: the fused-finalize arrival flag did that and the ring GEMM lost 20-35 % per call with bit-identical
 results, so only a timing A/B showed it).  This test compiles conv_gemm.hip to assembly and checks that the MFMA region
-of each such kernel has no more full drains than the schedule itself writes.
+of each such kernel has no more full drains than the schedule itself writes.  A second test counts exec-masked branch
+regions in the main loops of the stem backward and the BN backward kernels (their round-4 predecessors had 63, 16 and
+8; now at most 3).
 """
 import os
 import re
