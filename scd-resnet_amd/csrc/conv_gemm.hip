@@ -121,6 +121,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
     const int wave = tid >> 6;
     const int wm = wave / WN, wn = wave - (wave / WN) * WN;
     const int l16 = lane & 15, lg = lane >> 4;
+    // the LDS-DMA ring kernel (256 x 128) takes its loads from clamped addresses with the values selected after and its
+    // statistics by select (no branch regions); the register-staged kernels keep the branches (at their 256-VGPR bound
+    // the selects' live values spill)
+    constexpr bool SELF = BM == 256 && BN == 128;
     // ---- epilogue 1: bias / relu in registers, BN partial sums, stage the wave's 64x64 tile in LDS
     char* ep = smem + wave * 64 * EROW;
     float csum[4][4], csq[4][4];
@@ -150,19 +154,36 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
         float bmu[4], bis[4], bsc[4], bsh[4];
         uint2 yq[4];
         if constexpr (BNB) {
+            // every load from a valid address (channel 0 / pixel 0 when masked off) and the value selected after:
+            // a load under the test is a branch region the compiler waits on before the next load
             const bool okc = col0 < p.Co;
-            const float4 f0 = okc ? *(const float4*)(p.bn_mean + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 f1 = okc ? *(const float4*)(p.bn_invstd + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 f2 = okc ? *(const float4*)(p.bn_rsc + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 f3 = okc ? *(const float4*)(p.bn_rsh + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int cl = okc ? col0 : 0;
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 f0, f1, f2, f3;
+            if constexpr (SELF) {
+                const float4 l0 = *(const float4*)(p.bn_mean + cl), l1 = *(const float4*)(p.bn_invstd + cl);
+                const float4 l2 = *(const float4*)(p.bn_rsc + cl), l3 = *(const float4*)(p.bn_rsh + cl);
+                f0 = okc ? l0 : z4; f1 = okc ? l1 : z4; f2 = okc ? l2 : z4; f3 = okc ? l3 : z4;
+            } else {
+                f0 = okc ? *(const float4*)(p.bn_mean + col0) : z4;
+                f1 = okc ? *(const float4*)(p.bn_invstd + col0) : z4;
+                f2 = okc ? *(const float4*)(p.bn_rsc + col0) : z4;
+                f3 = okc ? *(const float4*)(p.bn_rsh + col0) : z4;
+            }
             bmu[0] = f0.x; bmu[1] = f0.y; bmu[2] = f0.z; bmu[3] = f0.w;
             bis[0] = f1.x; bis[1] = f1.y; bis[2] = f1.z; bis[3] = f1.w;
             bsc[0] = f2.x; bsc[1] = f2.y; bsc[2] = f2.z; bsc[3] = f2.w;
             bsh[0] = f3.x; bsh[1] = f3.y; bsh[2] = f3.z; bsh[3] = f3.w;
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
-                yq[a] = (pix[a] >= 0 && okc) ? *(const uint2*)(p.bny + ((long)pix[a] * p.Co + col0) * 2)
-                                             : make_uint2(0, 0);
+            for (int a = 0; a < 4; ++a) {
+                const bool ok = pix[a] >= 0 && okc;
+                if constexpr (SELF) {
+                    const uint2 raw = *(const uint2*)(p.bny + ((long)(ok ? pix[a] : 0) * p.Co + cl) * 2);
+                    yq[a] = ok ? raw : make_uint2(0, 0);
+                } else {
+                    yq[a] = ok ? *(const uint2*)(p.bny + ((long)pix[a] * p.Co + col0) * 2) : make_uint2(0, 0);
+                }
+            }
         }
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
@@ -173,7 +194,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
                 for (int r = 0; r < 4; ++r) {
                     v[r] = acc[a][b][r] + bias[r];
                     if (p.relu) v[r] = fmaxf(v[r], 0.f);
-                    if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+                    if constexpr (SELF) {
+                        // a select, not a branch region (the sums never hold -0: adding +0 past M leaves them unchanged)
+                        const float t = m < M ? v[r] : 0.f;
+                        csum[b][r] += t;
+                        csq[b][r] += t * t;
+                    } else {
+                        if (m < M) { csum[b][r] += v[r]; csq[b][r] += v[r] * v[r]; }
+                    }
                 }
             } else {
                 // the following BN+ReLU layer's backward sums over the gradient as stored (16-bit)
@@ -208,14 +236,20 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
 #pragma unroll
         for (int j = 0; j < 64 / RPI; ++j) {
             const int row = lane / CPR + RPI * j;
-            const int m = mt * BM + wm * 64 + row;
-            if (m >= M || col >= p.Co) continue;
+            const int mr = mt * BM + wm * 64 + row;
+            // ring kernel: rows past M / columns past Co address pixel 0 / channel 0 and skip only the store (no branch
+            // around the accumulate load)
+            const bool ok = mr < M && col < p.Co;
+            if constexpr (!SELF) {
+                if (!ok) continue;
+            }
+            const int m = SELF ? (ok ? mr : 0) : mr;
             const int n = m / QQ;
             const int rem = m - n * QQ;
             const int qh = rem / ph.Qw;
             const int qw = rem - qh * ph.Qw;
             const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
-            T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+            T* dst = (T*)(p.y) + ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + (SELF ? (ok ? col : 0) : col);
             uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
             if (p.accumulate) {
                 float a[EPC], o[EPC];
@@ -225,7 +259,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
                 for (int e = 0; e < EPC; ++e) a[e] += o[e];
                 Vec16<T>::store(&v, a);
             }
-            *(uint4*)dst = v;
+            if (!SELF || ok) *(uint4*)dst = v;
         }
     }
     if (p.stats) {
