@@ -15,13 +15,9 @@
 // whole deconv3 weight gradient)
 // vectors in flight per thread in bn_bwd_apply_kernel (80 VGPRs at 2, no spill): beside the weight-gradient stream's
 // one-workgroup-per-CU GEMM a CU holds one or two of its waves per SIMD, so the bytes each wave keeps in flight set
-// its bandwidth there (the fp16 build stays at 1: at 2 it spills 8 bytes)
+// its bandwidth there (75 VGPRs at 2 in both 16-bit builds since the loop is specialised per mask kind)
 #ifndef BN_APPLY_U
-#ifdef SCD_F16_BUILD
-#define BN_APPLY_U 1
-#else
 #define BN_APPLY_U 2
-#endif
 #endif
 #ifndef BN_EW_WAVES
 #define BN_EW_WAVES 6
