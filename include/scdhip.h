@@ -77,20 +77,6 @@ int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void* y, int N,
                         int Wo, int Co, int in_stride, int out_stride, int wrow, int nphase,
                         const scd_gemm_phase* phases, const void* bn_y, const float* mean, const float* invstd,
                         const float* relu_scale, const float* relu_shift, double* bn_stats, void* stream);
-/* scd_conv_gemm / scd_conv_gemm_bnbwd with the BN finalize of their statistics fused (struct scd_bn_fin below, a
- * device-memory descriptor; fin == NULL: the plain entry point).  Replace the GEMM + scd_bn_finalize / scd_bn_bwd_finalize launch pairs of
- * residuals.py:91-95, 259-263, 298-307 at world 1. */
-struct scd_bn_fin;
-int scd_conv_gemm_fin(int dtype, const void* x, const void* w, void* y, const float* bias, double* stats, int N,
-                      int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride, int wrow, int relu,
-                      int accumulate, int nphase, const scd_gemm_phase* phases, const struct scd_bn_fin* fin,
-                      void* stream);
-int scd_conv_gemm_bnbwd_fin(int dtype, const void* x, const void* w, void* y, int N, int Hi, int Wi, int Ci, int Ho,
-                            int Wo, int Co, int in_stride, int out_stride, int wrow, int nphase,
-                            const scd_gemm_phase* phases, const void* bn_y, const float* mean, const float* invstd,
-                            const float* relu_scale, const float* relu_shift, double* bn_stats,
-                            const struct scd_bn_fin* fin, void* stream);
-
 /* Head convolution with the CenterNet tails fused into the epilogue: hid = relu(conv3x3(x, w) + bias)
  * (N,H,W,nh*128) NHWC and, from the same tile, outs[h] (N,od[h],H,W) fp32 = w1[h] . hid_h + b1[h].
  * Replaces the three terminal Sequentials (centerNetOffset.py:106-110) in one launch; w is the
@@ -171,21 +157,10 @@ int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int H, int W, 
 
 /* Direct stem convolution (bf16): Conv2d(1,64,7,stride 2,pad 3,no bias) of residuals.py:211 with the
  * [pixel][tap] tile built in LDS from the input patch (no column tensor in HBM); wpk = the [64][64] packed
- * weight (pack_weight mode 0, ldp 64); y (N,Ho,Wo,64) NHWC; stats as scd_conv_gemm (may be NULL).  y == NULL
- * (stats required): the statistics only -- the first pass of the pooled forward below.
+ * weight (pack_weight mode 0, ldp 64); y (N,Ho,Wo,64) NHWC; stats as scd_conv_gemm (may be NULL).
  * Requires Wo % 128 == 0 and Ho % 2 == 0. */
 int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H, int W,
                       int Ho, int Wo, void* stream);
-/* ... with the stem BN's forward finalize fused (scd_bn_fin; residuals.py:211-212) */
-int scd_stem_conv_fwd_fin(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H, int W,
-                          int Ho, int Wo, const struct scd_bn_fin* fin, void* stream);
-/* The stem forward's second pass (residuals.py:211-213: conv, BN, ReLU, MaxPool2d(3, 2, 1)): the conv recomputed per
- * tile in LDS, BN (scale / shift from the finalize of the first pass's statistics) + ReLU + max pool, so the
- * full-resolution conv output never reaches HBM.  out (N,Ho/2,Wo/2,64), argmax (same shape, u8 window index 0..8,
- * first maximum in row-major window order) as scd_stem_pool_fwd of the conv's y, and ymax (same shape) = y at each
- * argmax (the pre-BN value the backward needs).  Requires Wo % 128 == 0 and Ho % 2 == 0 (Ho, Wo of the conv). */
-int scd_stem_conv_pool_fwd(int dtype, const float* x, const void* wpk, const float* scale, const float* shift,
-                           void* out, uint8_t* argmax, void* ymax, int N, int H, int W, void* stream);
 /* Its weight gradient: ws[z][co][k] (fp32, nsplit x 64 x 64) = sum over split z's pixels of
  * dy[pix][co] * col[pix][k]; reduce with scd_wgrad_reduce(ws, nsplit, 64, 1, 64, ..., cvalid = 49).
  * coef != NULL fuses the stem BN backward apply: dy is then the masked dz, ybn the BN input, and the
@@ -205,52 +180,8 @@ int scd_stem_bwd_nsplit(void);
 int scd_stem_bwd_fused(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
                        const float* shift, const float* mean, const float* invstd, const float* x, double* stats,
                        float* ws, int nsplit, float* tg, int N, int H, int W, int Ho, int Wo, void* stream);
-/* ... from ymax of scd_stem_conv_pool_fwd (pooled layout) instead of the full-resolution y: the same results */
-int scd_stem_bwd_fused_pooled(int dtype, const void* dout, const uint8_t* argmax, const void* ymax, const float* scale,
-                              const float* shift, const float* mean, const float* invstd, const float* x, double* stats,
-                              float* ws, int nsplit, float* tg, int N, int H, int W, int Ho, int Wo, void* stream);
 int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk, const float* coef, float* dst, int accumulate,
                          float alpha, void* stream);
-
-/* ---- BN finalize fused into the statistics producer (world 1: no SyncBN all-reduce between the two) ----
- * A `_fin` entry point takes a pointer to one of these IN DEVICE MEMORY (the caller writes it once and rewrites it
- * when a field changes; the kernels read it only in their tail, so it costs the kernel body one pointer argument):
- * the producer's workgroups count themselves in on `counter` when their statistics are added, and the last one reads
- * the SCD_FIN_REPLICAS replicas the launch used (in a fixed order), writes what scd_bn_finalize (backward == 0) or
- * scd_bn_bwd_finalize (backward == 1) would, re-zeroes the replicas and resets the counter -- one launch less per BN
- * layer and direction (the finalize kernels were ~5 us each, 30 per Res10 step).  A producer path that cannot do it
- * (several channel-slice launches) runs scd_bn_fin_standalone after itself, so the result never depends on the path.
- * The statistics buffer is the producer's own stats argument ([SCD_STAT_REPLICAS][2][C]; a fusing launch uses the
- * first SCD_FIN_REPLICAS).  C must equal the producer's channel count; the fields are not checked on the host. */
-#ifndef SCD_FIN_REPLICAS
-#define SCD_FIN_REPLICAS 16
-#endif
-/* arrival counters: one per shard of workgroups (blockIdx % 64) plus the count of finished shards */
-#define SCD_FIN_SHARDS 64
-#define SCD_FIN_COUNTERS (SCD_FIN_SHARDS + 1)
-typedef struct scd_bn_fin {
-    int* counter;              /* SCD_FIN_COUNTERS ints, zero between launches (device memory) */
-    int backward;              /* 0: forward statistics, 1: backward sums */
-    int C;
-    double count;              /* elements per channel (rows) */
-    const float* gamma;        /* weight (may be NULL: 1) */
-    const float* beta;         /* forward: bias (may be NULL: 0) */
-    float* running_mean;       /* forward: running statistics (may be NULL), num_batches_tracked += 1 */
-    float* running_var;
-    int64_t* num_batches;
-    float momentum, eps;
-    float* mean;               /* forward: written; backward: read (the forward's batch mean / invstd) */
-    float* invstd;
-    float* scale;              /* forward: written (gamma * invstd, beta - mean * scale) */
-    float* shift;
-    float* dgamma;             /* backward: dgamma (+)= gscale * sum dz*xhat, dbeta (+)= gscale * sum dz (may be NULL) */
-    float* dbeta;
-    float gscale;
-    float* coef;               /* backward: written, [3][C] as scd_bn_bwd_finalize */
-} scd_bn_fin;
-/* The finalize of descriptor `fin` (device memory) over all SCD_STAT_REPLICAS replicas of stats ([rep][2][ld]) as its
- * own launch (the unfused form of the `_fin` entry points). */
-int scd_bn_fin_standalone(const scd_bn_fin* fin, double* stats, int ld, void* stream);
 
 /* ---- training BatchNorm2d (residuals.py:92,95,212,262,306; momentum 0.1, eps 1e-5) ---- */
 /* sum replicas [nrep][2][C] -> [2][C] in place (replica 0); used before a SyncBN all-reduce */
@@ -274,10 +205,6 @@ int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const f
 int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
                       const float* relu_shift, const float* mean, const float* invstd, int C, long total,
                       double* stats, void* stream);
-/* ... with the backward finalize fused (scd_bn_fin, backward = 1) */
-int scd_bn_bwd_reduce_fin(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
-                          const float* relu_shift, const float* mean, const float* invstd, int C, long total,
-                          double* stats, const struct scd_bn_fin* fin, void* stream);
 /* dgamma (+)= gscale * sum dz*xhat, dbeta (+)= gscale * sum dz; coef[3][C] for dy = a*dz + b*y + c.
  * With SyncBN the sums are global; gscale = 1/world keeps the DDP-averaged dgamma/dbeta equal to the
  * reference's (torch SyncBatchNorm returns the LOCAL weight/bias gradients, DDP then averages them). */
@@ -296,11 +223,6 @@ int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* 
 int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
                        const float* mean_a, const float* invstd_a, const float* mean_b, const float* invstd_b, int C,
                        long total, double* stats_a, double* stats_b, void* stream);
-/* ... with both layers' backward finalizes fused (fin_a, fin_b: scd_bn_fin, backward = 1) */
-int scd_bn_bwd_reduce2_fin(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
-                           const float* mean_a, const float* invstd_a, const float* mean_b, const float* invstd_b,
-                           int C, long total, double* stats_a, double* stats_b, const struct scd_bn_fin* fin_a,
-                           const struct scd_bn_fin* fin_b, void* stream);
 int scd_bn_bwd_apply2(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
                       const float* coef_a, const float* coef_b, int C, long total, void* dya, void* dyb, void* stream);
 
@@ -523,10 +445,6 @@ int scd_event_create(void** ev);
 int scd_event_destroy(void* ev);
 int scd_event_record(void* ev, void* stream);
 int scd_event_elapsed_ms(void* start, void* end, float* ms);
-/* A stream restricted to the CUs set in mask (nwords x 32 bits, bit i = CU i; hipExtStreamCreateWithCUMask): the
- * optional CU-confined weight-gradient side stream (SCD_SIDE_CUS).  Destroy with scd_stream_destroy. */
-int scd_stream_create_cumask(const unsigned* mask, int nwords, void** stream);
-int scd_stream_destroy(void* stream);
 
 const char* scd_version(void);
 

@@ -92,7 +92,9 @@ __global__ void bn_finalize_kernel(double* stats, int nrep, int C, double count,
     invstd_o[c] = invstd;
     scale_o[c] = sc;
     shift_o[c] = b - (float)mean * sc;
-    if (stats && rmean) {
+    // (statistics that are NaN -- a failed peer-memory SyncBN all-reduce poisons its result, scdhip/peer.py -- leave the
+    // running statistics as they were, so a checkpoint written after the failure still carries the last good ones)
+    if (stats && rmean && mean == mean && var == var) {
         const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
         rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
         rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
@@ -196,14 +198,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* y, T* out, int C
 // rows [r0, r1): thread = (row lane rsub, 16-B channel chunk ch); 4 rows per step are loaded before
 // any is used (4 x 3 independent 16-B loads in flight per thread); the block's partials are folded
 // over row lanes in LDS by all threads and added to one fp64 replica slot per channel.
-// FIN: the build that finalizes in its last workgroup (scd_bn_bwd_reduce_fin); the plain one carries no tail code (the
-// tail took the kernel from 71 VGPRs to its 80-VGPR bound plus spills)
-template <typename T, bool FIN = false>
+template <typename T>
 __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T* dout, const T* mask, const T* y,
                                                             const float* rsc, const float* rsh,
                                                             const float* mean, const float* invstd, int C, int ld,
-                                                            unsigned rows, unsigned rows_per_block, double* stats,
-                                                            BnFinDev fin) {
+                                                            unsigned rows, unsigned rows_per_block, double* stats) {
     constexpr int E = Vec16<T>::N;
     constexpr int U = BN_BWD_U;
     constexpr int nt = 256;
@@ -275,7 +274,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T
         red[nt * E + rsub * C + ch * E + e] = q[e];
     }
     __syncthreads();
-    const int rep = FIN ? stat_rep(fin, blockIdx.x) : (int)(blockIdx.x % SCD_STAT_REPLICAS);
+    const int rep = (int)(blockIdx.x % SCD_STAT_REPLICAS);
     for (int c = tid; c < C; c += nt) {
         double ss = 0.0, qq = 0.0;
         for (int k = 0; k < rpi; ++k) {
@@ -285,7 +284,6 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T
         atomic_add_f64(stats + ((long)rep * 2 + 0) * ld + c, ss);
         atomic_add_f64(stats + ((long)rep * 2 + 1) * ld + c, qq);
     }
-    if constexpr (FIN) bn_fin_tail(fin, nt, red);
 }
 
 __global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
@@ -386,12 +384,12 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply_kernel(const T*
 // 110-120, 158-165; CornerPool branchMergeBn + shortcutBn, cornerNetCPool.py:117-122): both take the same gradient
 // dout through the same ReLU mask, so one pass reads dout and the mask once for both.  Per element and per thread the
 // arithmetic is that of bn_bwd_reduce_kernel / bn_bwd_apply_kernel with a mask (no BN+ReLU recompute).
-template <typename T, bool FIN = false>
+template <typename T>
 __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const T* dout, const T* mask, const T* ya, const T* yb,
                                                              const float* mean_a, const float* invstd_a,
                                                              const float* mean_b, const float* invstd_b, int C, int ld,
                                                              unsigned rows, unsigned rows_per_block, double* stats_a,
-                                                             double* stats_b, BnFinDev fin_a, BnFinDev fin_b) {
+                                                             double* stats_b) {
     constexpr int E = Vec16<T>::N;
     constexpr int U = BN_BWD_U;
     constexpr int nt = 256;
@@ -449,7 +447,7 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const 
         const unsigned i = r * (unsigned)ld + ch * E;
         acc_raw(*(const uint4*)(dout + i), *(const uint4*)(mask + i), *(const uint4*)(ya + i), *(const uint4*)(yb + i));
     }
-    const int rep = FIN ? stat_rep(fin_a, blockIdx.x) : (int)(blockIdx.x % SCD_STAT_REPLICAS);
+    const int rep = (int)(blockIdx.x % SCD_STAT_REPLICAS);
     // pass 1: sum dz (both layers) and layer a's sum dz*xhat; pass 2: layer b's
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -476,8 +474,6 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce2_kernel(const 
         for (int k = 0; k < rpi; ++k) qq += red[nt * E + k * C + c];
         atomic_add_f64(stats_b + ((long)rep * 2 + 1) * ld + c, qq);
     }
-    // both layers' finalizes by the last workgroup (fin_a's counter)
-    if constexpr (FIN) bn_fin_tail2(fin_a, &fin_b, nt, red);
 }
 
 template <typename T>
@@ -539,12 +535,6 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_apply2_kernel(const T
     }
 }
 
-// the finalize of a scd_bn_fin descriptor (device memory) over all SCD_STAT_REPLICAS replicas, as its own launch: what a
-// _fin entry point runs when its producer path could not finalize in its last workgroup
-__global__ __launch_bounds__(1024) void bn_fin_standalone_kernel(const scd_bn_fin* fin, double* stats, int ld) {
-    bn_fin_compute<SCD_STAT_REPLICAS>(fin, stats, ld, blockDim.x);
-}
-
 // elementwise BN kernels keep one channel chunk per thread: the grid stride (grid * 256 threads) must be a
 // multiple of the chunks per row cpr, i.e. cpr divides 256 or is a multiple of it (grid a multiple of cpr/256)
 inline bool ew_rows_ok(int cpr) { return cpr > 0 && (256 % cpr == 0 || cpr % 256 == 0); }
@@ -584,12 +574,6 @@ extern "C" int scd_stats_collapse_to(double* stats, int nrep, int C, double* out
     SCD_RETURN_LAUNCH();
 }
 
-extern "C" int scd_bn_fin_standalone(const scd_bn_fin* fin, double* stats, int ld, void* stream) {
-    if (!fin || !stats || ld <= 0) return SCD_ERR_ARG;
-    hipLaunchKernelGGL(bn_fin_standalone_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, fin, stats, ld);
-    SCD_RETURN_LAUNCH();
-}
-
 extern "C" int scd_bn_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                                const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
                                float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
@@ -626,15 +610,7 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
 extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
                                  const float* relu_shift, const float* mean,
                                  const float* invstd, int C, long total, double* stats, void* stream) {
-    return scd_bn_bwd_reduce_fin(dtype, dout, mask, y, relu_scale, relu_shift, mean, invstd, C, total, stats, nullptr,
-                                 stream);
-}
-
-extern "C" int scd_bn_bwd_reduce_fin(int dtype, const void* dout, const void* mask, const void* y,
-                                     const float* relu_scale, const float* relu_shift, const float* mean,
-                                     const float* invstd, int C, long total, double* stats, const scd_bn_fin* fin,
-                                     void* stream) {
-    SCD_F16_FWD(scd_bn_bwd_reduce_fin, dout, mask, y, relu_scale, relu_shift, mean, invstd, C, total, stats, fin, stream);
+    SCD_F16_FWD(scd_bn_bwd_reduce, dout, mask, y, relu_scale, relu_shift, mean, invstd, C, total, stats, stream);
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
@@ -651,37 +627,25 @@ extern "C" int scd_bn_bwd_reduce_fin(int dtype, const void* dout, const void* ma
     const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
     const int blocks = cdiv(rows, rpb);
     const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
-    // the finalize rides on the launch when one launch covers every channel; otherwise the separate kernel
-    const bool fuse = fin && sC == C && rows > 0;
-    const BnFinDev fd = bn_fin_dev(fuse ? fin : nullptr, stats, C);
     for (int c0 = 0; c0 < C; c0 += sC) {
         const char* dz = (const char*)dout + (size_t)c0 * esz;
         const char* mk = mask ? (const char*)mask + (size_t)c0 * esz : nullptr;
         const char* yy = (const char*)y + (size_t)c0 * esz;
         const float* rs = relu_scale ? relu_scale + c0 : nullptr;
         const float* rh = relu_shift ? relu_shift + c0 : nullptr;
-        if (dtype == SCD_DT_BF16 && fuse)
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
-                               (const __bf16*)dz, (const __bf16*)mk, (const __bf16*)yy, rs, rh, mean + c0, invstd + c0,
-                               sC, C, (unsigned)rows, (unsigned)rpb, stats + c0, fd);
-        else if (dtype == SCD_DT_BF16)
+        if (dtype == SCD_DT_BF16)
             hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)dz,
                                (const __bf16*)mk, (const __bf16*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
-                               (unsigned)rows, (unsigned)rpb, stats + c0, fd);
-        else if (dtype == SCD_DT_F32 && fuse)
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
-                               (const float*)dz, (const float*)mk, (const float*)yy, rs, rh, mean + c0, invstd + c0, sC,
-                               C, (unsigned)rows, (unsigned)rpb, stats + c0, fd);
+                               (unsigned)rows, (unsigned)rpb, stats + c0);
         else if (dtype == SCD_DT_F32)
             hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const float*)dz,
                                (const float*)mk, (const float*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
-                               (unsigned)rows, (unsigned)rpb, stats + c0, fd);
+                               (unsigned)rows, (unsigned)rpb, stats + c0);
         else
             return SCD_ERR_ARG;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
-    if (fin && !fuse) return scd_bn_fin_standalone(fin, stats, C, stream);
     return 0;
 }
 
@@ -689,19 +653,11 @@ extern "C" int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask,
                                   const float* mean_a, const float* invstd_a, const float* mean_b,
                                   const float* invstd_b, int C, long total, double* stats_a, double* stats_b,
                                   void* stream) {
-    return scd_bn_bwd_reduce2_fin(dtype, dout, mask, ya, yb, mean_a, invstd_a, mean_b, invstd_b, C, total, stats_a,
-                                  stats_b, nullptr, nullptr, stream);
-}
-
-extern "C" int scd_bn_bwd_reduce2_fin(int dtype, const void* dout, const void* mask, const void* ya, const void* yb,
-                                      const float* mean_a, const float* invstd_a, const float* mean_b,
-                                      const float* invstd_b, int C, long total, double* stats_a, double* stats_b,
-                                      const scd_bn_fin* fin_a, const scd_bn_fin* fin_b, void* stream) {
-    SCD_F16_FWD(scd_bn_bwd_reduce2_fin, dout, mask, ya, yb, mean_a, invstd_a, mean_b, invstd_b, C, total, stats_a, stats_b,
-                fin_a, fin_b, stream);
+    SCD_F16_FWD(scd_bn_bwd_reduce2, dout, mask, ya, yb, mean_a, invstd_a, mean_b, invstd_b, C, total, stats_a, stats_b,
+                stream);
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
-    if (!dout || !mask || !ya || !yb || C % E || (!fin_a != !fin_b)) return SCD_ERR_ARG;
+    if (!dout || !mask || !ya || !yb || C % E) return SCD_ERR_ARG;
     const long rows = total / C;
     const int cpr = C / E;
     if (!ew_rows_ok(cpr) || total >= (1L << 31)) return SCD_ERR_ARG;
@@ -714,41 +670,24 @@ extern "C" int scd_bn_bwd_reduce2_fin(int dtype, const void* dout, const void* m
     const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
     const int blocks = cdiv(rows, rpb);
     const int esz = dtype == SCD_DT_BF16 ? 2 : 4;
-    const bool fuse = fin_a && sC == C && rows > 0;
-    const BnFinDev fa = bn_fin_dev(fuse ? fin_a : nullptr, stats_a, C);
-    const BnFinDev fb = bn_fin_dev(fuse ? fin_b : nullptr, stats_b, C);
     for (int c0 = 0; c0 < C; c0 += sC) {
         const size_t o = (size_t)c0 * esz;
         const char *d = (const char*)dout + o, *m = (const char*)mask + o, *a = (const char*)ya + o,
                    *b = (const char*)yb + o;
-        if (dtype == SCD_DT_BF16 && fuse)
-            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
-                               (const __bf16*)d, (const __bf16*)m, (const __bf16*)a, (const __bf16*)b, mean_a + c0,
-                               invstd_a + c0, mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb,
-                               stats_a + c0, stats_b + c0, fa, fb);
-        else if (dtype == SCD_DT_BF16)
+        if (dtype == SCD_DT_BF16)
             hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)d,
                                (const __bf16*)m, (const __bf16*)a, (const __bf16*)b, mean_a + c0, invstd_a + c0,
                                mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
-                               stats_b + c0, fa, fb);
-        else if (dtype == SCD_DT_F32 && fuse)
-            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<float, true>), dim3(blocks), dim3(256), 4 * sC * 4, st,
-                               (const float*)d, (const float*)m, (const float*)a, (const float*)b, mean_a + c0,
-                               invstd_a + c0, mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb,
-                               stats_a + c0, stats_b + c0, fa, fb);
+                               stats_b + c0);
         else if (dtype == SCD_DT_F32)
             hipLaunchKernelGGL((bn_bwd_reduce2_kernel<float>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const float*)d,
                                (const float*)m, (const float*)a, (const float*)b, mean_a + c0, invstd_a + c0,
                                mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
-                               stats_b + c0, fa, fb);
+                               stats_b + c0);
         else
             return SCD_ERR_ARG;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
-    }
-    if (fin_a && !fuse) {
-        const int rc = scd_bn_fin_standalone(fin_a, stats_a, C, stream);
-        return rc ? rc : scd_bn_fin_standalone(fin_b, stats_b, C, stream);
     }
     return 0;
 }

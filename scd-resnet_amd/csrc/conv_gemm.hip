@@ -64,8 +64,6 @@ struct GemmParams {
     int shuf;
     // heads384: K-stage order reversed on every other round of 256 workgroups (kserp = 1; SCD_HEADS_SERP)
     int kserp;
-    // BN finalize of the statistics (p.stats) by the launch's last workgroup (scd_conv_gemm_fin / _bnbwd_fin)
-    BnFinDev fin;
 };
 
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
@@ -283,7 +281,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
                 double s = 0.0, q = 0.0;
 #pragma unroll
                 for (int w = 0; w < BM / 64; ++w) { s += red[(w * BN + tid) * 2]; q += red[(w * BN + tid) * 2 + 1]; }
-                const int rep = stat_rep(p.fin, bid);
+                const int rep = bid % SCD_STAT_REPLICAS;
                 atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
                 atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
             }
@@ -540,7 +538,6 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void conv_gemm_kernel(GemmParams 
     }
 
     gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
-    bn_fin_tail(p.fin, 256, smem);            // (KS 2: the second K group has returned; threads 0..255 remain)
 }
 
 // -------------------------------------------------------------------------------------
@@ -820,10 +817,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
 
     // ---- BN sums: once per workgroup into replica blockIdx % SCD_STAT_REPLICAS
     if ((BNB || p.stats) && tid < 128) {
-        const int rep = stat_rep(p.fin, blockIdx.x);
+        const int rep = blockIdx.x % SCD_STAT_REPLICAS;
         atomic_add_f64(p.stats + ((long)rep * 2 + (tid >> 6)) * p.Co + (tid & 63), (double)bnsum);
     }
-    bn_fin_tail(p.fin, 512, smem);
 }
 
 template <bool HEADS, bool BNB = false>
@@ -966,7 +962,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     gemm_epilogue<T, BM, BN, WN, HEADS, BNB>(p, acc, smem, tid, bid, mt, nt, M, QQ, ph);
-    bn_fin_tail(p.fin, 512, smem);
 }
 
 // -------------------------------------------------------------------------------------
@@ -1383,7 +1378,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             if (col < p.Co) {
                 const double s = (double)red[tid * 2] + (double)red[(BN + tid) * 2];
                 const double q = (double)red[tid * 2 + 1] + (double)red[(BN + tid) * 2 + 1];
-                const int rep = stat_rep(p.fin, bid);
+                const int rep = bid % SCD_STAT_REPLICAS;
                 atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
                 atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
             }
@@ -1456,7 +1451,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             }
         }
     }
-    bn_fin_tail(p.fin, 512, smem);
 }
 
 // -------------------------------------------------------------------------------------
@@ -2956,7 +2950,6 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.bnbwd = 0; p.bny = nullptr; p.bn_mean = p.bn_invstd = p.bn_rsc = p.bn_rsh = nullptr;
     p.hid_keep = nullptr; p.hid_cols = 1 << 30;
     p.shuf = 0;
-    memset(&p.fin, 0, sizeof(p.fin));
     {
         // read per call (tests switch them to compare the variants)
         const char* e = getenv("SCD_HEADS_SERP");
@@ -2974,24 +2967,11 @@ extern "C" int scd_conv_gemm(int dtype, const void* x, const void* w, void* y, c
                              int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride,
                              int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
                              void* stream) {
-    return scd_conv_gemm_fin(dtype, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu,
-                             accumulate, nphase, phases, nullptr, stream);
-}
-
-extern "C" int scd_conv_gemm_fin(int dtype, const void* x, const void* w, void* y, const float* bias, double* stats,
-                                 int N, int Hi, int Wi, int Ci, int Ho, int Wo, int Co, int in_stride, int out_stride,
-                                 int wrow, int relu, int accumulate, int nphase, const scd_gemm_phase* phases,
-                                 const scd_bn_fin* fin, void* stream) {
-    SCD_F16_FWD(scd_conv_gemm_fin, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu, accumulate, nphase, phases, fin, stream);
-    if (fin && !stats) return SCD_ERR_ARG;
+    SCD_F16_FWD(scd_conv_gemm, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu,
+                accumulate, nphase, phases, stream);
     GemmParams p;
     fill_params(p, x, w, y, bias, stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, relu, accumulate);
-    long M = 0;
-    for (int i = 0; i < nphase && i < SCD_MAX_PHASES; ++i) M += (long)N * phases[i].Qh * phases[i].Qw;
-    if (M > 0) p.fin = bn_fin_dev(fin, stats, Co);
-    const int rc = conv_gemm_launch(dtype, p, nphase, phases, stream);
-    if (rc || M > 0) return rc;
-    return fin ? scd_bn_fin_standalone(fin, stats, Co, stream) : 0;
+    return conv_gemm_launch(dtype, p, nphase, phases, stream);
 }
 
 extern "C" int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void* y, int N, int Hi, int Wi, int Ci,
@@ -2999,34 +2979,23 @@ extern "C" int scd_conv_gemm_bnbwd(int dtype, const void* x, const void* w, void
                                    const scd_gemm_phase* phases, const void* bn_y, const float* mean,
                                    const float* invstd, const float* relu_scale, const float* relu_shift,
                                    double* bn_stats, void* stream) {
-    return scd_conv_gemm_bnbwd_fin(dtype, x, w, y, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, nphase, phases,
-                                   bn_y, mean, invstd, relu_scale, relu_shift, bn_stats, nullptr, stream);
-}
-
-extern "C" int scd_conv_gemm_bnbwd_fin(int dtype, const void* x, const void* w, void* y, int N, int Hi, int Wi, int Ci,
-                                       int Ho, int Wo, int Co, int in_stride, int out_stride, int wrow, int nphase,
-                                       const scd_gemm_phase* phases, const void* bn_y, const float* mean,
-                                       const float* invstd, const float* relu_scale, const float* relu_shift,
-                                       double* bn_stats, const scd_bn_fin* fin, void* stream) {
-    SCD_F16_FWD(scd_conv_gemm_bnbwd_fin, x, w, y, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, nphase, phases, bn_y, mean, invstd, relu_scale, relu_shift, bn_stats, fin, stream);
+    SCD_F16_FWD(scd_conv_gemm_bnbwd, x, w, y, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, nphase, phases,
+                bn_y, mean, invstd, relu_scale, relu_shift, bn_stats, stream);
     if (!bn_y || !mean || !invstd || !relu_scale || !relu_shift || !bn_stats || Co % 4) return SCD_ERR_ARG;
     GemmParams p;
     fill_params(p, x, w, y, nullptr, bn_stats, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, 0, 0);
     p.bnbwd = 1;
     p.bny = (const char*)bn_y; p.bn_mean = mean; p.bn_invstd = invstd; p.bn_rsc = relu_scale; p.bn_rsh = relu_shift;
-    long M = 0;
-    for (int i = 0; i < nphase && i < SCD_MAX_PHASES; ++i) M += (long)N * phases[i].Qh * phases[i].Qw;
     if (dtype == SCD_DT_BF16) {
-        if (M > 0) p.fin = bn_fin_dev(fin, bn_stats, Co);
         const int rc = conv_gemm_launch(dtype, p, nphase, phases, stream);
-        if (rc != SCD_ERR_ARG) return (rc || M > 0 || !fin) ? rc : scd_bn_fin_standalone(fin, bn_stats, Co, stream);
+        if (rc != SCD_ERR_ARG) return rc;
     }
-    // shapes the fused-sum kernels do not take: plain GEMM, then the separate BN-backward reduction (+ finalize)
+    // shapes the fused-sum kernels do not take: plain GEMM, then the separate BN-backward reduction
     fill_params(p, x, w, y, nullptr, nullptr, N, Hi, Wi, Ci, Ho, Wo, Co, in_stride, out_stride, wrow, 0, 0);
     const int rc = conv_gemm_launch(dtype, p, nphase, phases, stream);
     if (rc) return rc;
-    return scd_bn_bwd_reduce_fin(dtype, y, nullptr, bn_y, relu_scale, relu_shift, mean, invstd, Co, (long)N * Ho * Wo * Co,
-                                 bn_stats, fin, stream);
+    return scd_bn_bwd_reduce(dtype, y, nullptr, bn_y, relu_scale, relu_shift, mean, invstd, Co, (long)N * Ho * Wo * Co,
+                             bn_stats, stream);
 }
 
 extern "C" int scd_conv_dgrad_s2(int dtype, const void* dy, const void* w3, void* dx, int N, int Hq, int Wq, int Cg,

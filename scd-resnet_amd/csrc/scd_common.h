@@ -12,12 +12,6 @@
 #ifdef SCD_F16_BUILD
 #define scd_conv_gemm scd_conv_gemm__f16
 #define scd_conv_gemm_bnbwd scd_conv_gemm_bnbwd__f16
-#define scd_conv_gemm_fin scd_conv_gemm_fin__f16
-#define scd_conv_gemm_bnbwd_fin scd_conv_gemm_bnbwd_fin__f16
-#define scd_stem_conv_fwd_fin scd_stem_conv_fwd_fin__f16
-#define scd_bn_bwd_reduce_fin scd_bn_bwd_reduce_fin__f16
-#define scd_bn_bwd_reduce2_fin scd_bn_bwd_reduce2_fin__f16
-#define scd_bn_fin_standalone scd_bn_fin_standalone__f16
 #define scd_conv_gemm_heads scd_conv_gemm_heads__f16
 #define scd_conv_gemm_heads_keep scd_conv_gemm_heads_keep__f16
 #define scd_conv_wgrad_workspace scd_conv_wgrad_workspace__f16
@@ -58,8 +52,6 @@
 #define scd_stem_bwd_nsplit scd_stem_bwd_nsplit__f16
 #define scd_conv_dgrad_s2 scd_conv_dgrad_s2__f16
 #define scd_stem_bwd_fused scd_stem_bwd_fused__f16
-#define scd_stem_bwd_fused_pooled scd_stem_bwd_fused_pooled__f16
-#define scd_stem_conv_pool_fwd scd_stem_conv_pool_fwd__f16
 #define scd_stem_bwd_combine scd_stem_bwd_combine__f16
 #define scd_pad_channels scd_pad_channels__f16
 #define __bf16 _Float16
@@ -85,11 +77,6 @@
 #define SCD_F16_DECL(fn) extern "C" decltype(fn) fn##__f16;
 SCD_F16_DECL(scd_conv_gemm)
 SCD_F16_DECL(scd_conv_gemm_bnbwd)
-SCD_F16_DECL(scd_conv_gemm_fin)
-SCD_F16_DECL(scd_conv_gemm_bnbwd_fin)
-SCD_F16_DECL(scd_stem_conv_fwd_fin)
-SCD_F16_DECL(scd_bn_bwd_reduce_fin)
-SCD_F16_DECL(scd_bn_bwd_reduce2_fin)
 SCD_F16_DECL(scd_conv_gemm_heads)
 SCD_F16_DECL(scd_conv_gemm_heads_keep)
 SCD_F16_DECL(scd_conv_wgrad_nsplit2)
@@ -115,8 +102,6 @@ SCD_F16_DECL(scd_heads_sparse_fixup)
 SCD_F16_DECL(scd_stem_conv_fwd)
 SCD_F16_DECL(scd_stem_conv_wgrad)
 SCD_F16_DECL(scd_stem_bwd_fused)
-SCD_F16_DECL(scd_stem_bwd_fused_pooled)
-SCD_F16_DECL(scd_stem_conv_pool_fwd)
 SCD_F16_DECL(scd_conv_dgrad_s2)
 SCD_F16_DECL(scd_stem_bwd_combine)
 SCD_F16_DECL(scd_pad_channels)
@@ -189,156 +174,6 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // fp64 atomic add (global_atomic_add_f64 on gfx950)
 __device__ __forceinline__ void atomic_add_f64(double* p, double v) { unsafeAtomicAdd(p, v); }
 __device__ __forceinline__ void atomic_add_f32(float* p, float v) { unsafeAtomicAdd(p, v); }
-
-// ---- BN finalize fused into the statistics producer (scd_bn_fin, include/scdhip.h) ----
-// The descriptor lives in device memory (written once by the caller); the kernels take its pointer plus the
-// statistics buffer they add into, and read the descriptor only in the tail -- so it costs the kernel body one
-// pointer argument, not twenty (kernel arguments are loaded into SGPRs up front: the by-value form spilled SGPRs in
-// the ping-pong GEMM and VGPRs in the BN reduce).
-// SCD_FIN_ABL (timing-only ablation builds, `make variant`; never the product): 1 = the last workgroup skips the
-// finalize arithmetic, 2 = no vmcnt drain before the arrival count
-#ifndef SCD_FIN_ABL
-#define SCD_FIN_ABL 0
-#endif
-struct BnFinDev {
-    const scd_bn_fin* f;      // device memory; NULL: the launch does not finalize
-    double* stats;            // the producer's statistics, [rep][2][ld]
-    int ld;
-};
-// replica a workgroup adds its statistics into: the first SCD_FIN_REPLICAS when the launch finalizes them itself
-__device__ __forceinline__ int stat_rep(const BnFinDev& d, int bid) {
-    return d.f ? bid % SCD_FIN_REPLICAS : bid % SCD_STAT_REPLICAS;
-}
-// Called by every remaining thread of every workgroup at its end: true in the last workgroup to arrive, once every
-// other workgroup's statistics atomics are visible.  The hand-off is "8-byte agent atomics on both sides": the
-// statistics are fp64 atomic adds (performed at the memory side, never dirty in an L2) and the last workgroup reads
-// them with agent-scope (sc1) loads, so no fence is needed -- only every wave's own atomics drained (vmcnt) before
-// the one counter add that signals them.  An agent-scope release/acquire here (a `__threadfence()` per workgroup)
-// writes back the XCD's whole L2 every time and made the producers 1.2-10x slower.
-// flag: one int of the kernel's own LDS (free once the workgroup's epilogue has passed the first barrier here): a
-// second `__shared__` object in an LDS-DMA kernel makes the compiler's wait counting drain every DMA prefetch
-// (s_waitcnt vmcnt(0) before the fragment reads: the ring kernel lost 20-35 % per call)
-__device__ __forceinline__ bool bn_fin_arrive(int* counter, int* flag) {
-    // two levels, so no counter word takes more than ~1/64 of the launch's arrivals (one word serialises its returning
-    // atomics at ~90 per us: a resident-grid launch of 2048 workgroups, all finishing together, waited ~20 us on one):
-    // workgroup b counts in on shard b % 64, the last of a shard counts the shard in on counter[SCD_FIN_SHARDS]
-#if SCD_FIN_ABL != 2
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int nblk = (int)(gridDim.x * gridDim.y * gridDim.z);
-        const int bid = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-        const int sh = bid % SCD_FIN_SHARDS;
-        const int nsh = nblk < SCD_FIN_SHARDS ? nblk : SCD_FIN_SHARDS;
-        const int members = (nblk - sh + SCD_FIN_SHARDS - 1) / SCD_FIN_SHARDS;
-        int last = __hip_atomic_fetch_add(counter + sh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == members - 1;
-        if (last)
-            last = __hip_atomic_fetch_add(counter + SCD_FIN_SHARDS, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   nsh - 1;
-        *flag = last;
-    }
-    __syncthreads();
-    return *flag != 0;
-}
-// global-address-space view of a pointer read from a descriptor (plain `global_` accesses instead of `flat_`)
-template <typename T> __device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
-    return (__attribute__((address_space(1))) T*)p;
-}
-// The finalize of one layer by threads 0 .. nact-1 of the last workgroup: the replicas summed in a fixed order
-// (agent-scope loads: they were written by other XCDs' atomics) and re-zeroed, then bn_finalize_kernel's /
-// bn_bwd_finalize_kernel's arithmetic.  This runs after every other workgroup has left, so its latency is the
-// launch's: the descriptor is copied to registers once (its fields would otherwise be re-read after every store
-// through one of its pointers) and every per-channel operand is loaded before the first wait.
-template <int NREP = SCD_FIN_REPLICAS>
-__device__ __forceinline__ void bn_fin_compute(const scd_bn_fin* fp, double* stats, int ld, int nact) {
-    const scd_bn_fin f = *fp;
-    const int C = f.C;
-    const double count = f.count;
-    // CH replicas (2 CH loads) in flight at a time: within the register budget of the BN kernels (BN_EW_WAVES)
-    constexpr int CH = NREP < 4 ? NREP : 4;
-    static_assert(NREP % CH == 0, "replica count");
-    for (int c = threadIdx.x; c < C; c += nact) {
-        float g = 1.f, b = 0.f, rm = 0.f, rv = 0.f, is = 0.f, mu = 0.f, dg = 0.f, db = 0.f;
-        if (f.gamma) g = gptr(f.gamma)[c];
-        if (!f.backward) {
-            if (f.beta) b = gptr(f.beta)[c];
-            if (f.running_mean) { rm = gptr(f.running_mean)[c]; rv = gptr(f.running_var)[c]; }
-        } else {
-            is = gptr(f.invstd)[c];
-            mu = gptr(f.mean)[c];
-            if (f.dgamma) dg = gptr(f.dgamma)[c];
-            if (f.dbeta) db = gptr(f.dbeta)[c];
-        }
-        __attribute__((address_space(1))) double* p0 = gptr(stats) + c;
-        double s = 0.0, q = 0.0;
-        for (int r0 = 0; r0 < NREP; r0 += CH) {
-            double vs[CH], vq[CH];
-#pragma unroll
-            for (int r = 0; r < CH; ++r) {
-                vs[r] = __hip_atomic_load(p0 + (long)(2 * (r0 + r)) * ld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                vq[r] = __hip_atomic_load(p0 + (long)(2 * (r0 + r) + 1) * ld, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int r = 0; r < CH; ++r) { s += vs[r]; q += vq[r]; }
-        }
-#pragma unroll
-        for (int r = 0; r < NREP; ++r) {
-            p0[(long)(2 * r) * ld] = 0.0;
-            p0[(long)(2 * r + 1) * ld] = 0.0;
-        }
-        if (!f.backward) {
-            const double mean = s / count;
-            double var = q / count - mean * mean;
-            if (var < 0.0) var = 0.0;
-            const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-            const float sc = g * invstd;
-            gptr(f.mean)[c] = (float)mean;
-            gptr(f.invstd)[c] = invstd;
-            gptr(f.scale)[c] = sc;
-            gptr(f.shift)[c] = b - (float)mean * sc;
-            if (f.running_mean) {
-                const float m = f.momentum;
-                const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
-                gptr(f.running_mean)[c] = (1.f - m) * rm + m * (float)mean;
-                gptr(f.running_var)[c] = (1.f - m) * rv + m * (float)unbiased;
-            }
-        } else {
-            if (f.dgamma) gptr(f.dgamma)[c] = dg + f.gscale * (float)q;
-            if (f.dbeta) gptr(f.dbeta)[c] = db + f.gscale * (float)s;
-            const float sc = g * is;
-            const float k1 = (float)(s / count);
-            const float k2 = (float)(q / count);
-            gptr(f.coef)[c] = sc;
-            gptr(f.coef)[C + c] = -sc * is * k2;
-            gptr(f.coef)[2 * C + c] = -sc * k1 + sc * is * k2 * mu;
-        }
-    }
-    if (threadIdx.x == 0 && !f.backward && f.num_batches) *gptr(f.num_batches) += 1;
-}
-// the tail of a producer (one layer; d1 != NULL: a second layer whose statistics the launch produced too, counted on
-// d0's counter); every remaining thread calls it at the kernel's end
-__device__ __forceinline__ void bn_fin_tail2(const BnFinDev& d0, const BnFinDev* d1, int nact, void* lds) {
-    if (!d0.f) return;
-    int* counter = d0.f->counter;
-    if (!bn_fin_arrive(counter, (int*)lds)) return;
-#if SCD_FIN_ABL != 1
-    bn_fin_compute(d0.f, d0.stats, d0.ld, nact);
-    if (d1 && d1->f) bn_fin_compute(d1->f, d1->stats, d1->ld, nact);
-#endif
-    for (int i = threadIdx.x; i < SCD_FIN_COUNTERS; i += nact)
-        __hip_atomic_store(counter + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void bn_fin_tail(const BnFinDev& d, int nact, void* lds) { bn_fin_tail2(d, nullptr, nact, lds); }
-// host: the kernels' view of a `_fin` entry point's argument (off when fin == NULL)
-static inline BnFinDev bn_fin_dev(const scd_bn_fin* fin_dev, double* stats, int ld) {
-    BnFinDev d;
-    d.f = (fin_dev && stats) ? fin_dev : nullptr;
-    d.stats = stats;
-    d.ld = ld;
-    return d;
-}
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 

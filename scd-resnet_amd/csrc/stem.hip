@@ -43,7 +43,7 @@ constexpr int FROW = 2 * FPAR;
 
 __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
                                                             __bf16* __restrict__ y, double* __restrict__ stats,
-                                                            int H, int W, int Ho, int Wo, BnFinDev fin) {
+                                                            int H, int W, int Ho, int Wo) {
     constexpr int AT = FTH * FTW * 128;             // A tile [256 px][64 taps] bf16, 128-B rows
     constexpr int BT = CO * 128;                    // B tile [64 co][64 taps]
     constexpr int EROW = CO * 2 + 16;
@@ -129,8 +129,7 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
     }
     __syncthreads();          // A tile no longer read: reuse it for the output staging
 
-    // epilogue: lane holds pixel a*16+l16 (of its wave) and channels b*16+4lg .. +3.  y == NULL: statistics only (the
-    // first pass of the pooled forward, stem_conv_pool_kernel)
+    // epilogue: lane holds pixel a*16+l16 (of its wave) and channels b*16+4lg .. +3
     float csum[4][4], csq[4][4];
     char* ep = smem + wave * 64 * EROW;
 #pragma unroll
@@ -150,20 +149,18 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
                 csum[b][r] += v;
                 csq[b][r] += v * v;
             }
-            if (y) *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
+            *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
         }
     __syncthreads();
     // the 2 x 128 output pixels are two contiguous 16-KB runs of NHWC
-    if (y) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int idx = tid + 256 * j;            // 16-B chunk of the 256 x 128-B tile
-            const int p = idx >> 3, c = idx & 7;
-            const int w = p >> 6, pl = p & 63;
-            const uint4 v = *(const uint4*)(smem + w * 64 * EROW + pl * EROW + c * 16);
-            const int pr = p / FTW, pc = p - (p / FTW) * FTW;
-            *(uint4*)(y + (((size_t)n * Ho + oh0 + pr) * Wo + ow0 + pc) * CO + c * 8) = v;
-        }
+    for (int j = 0; j < 8; ++j) {
+        const int idx = tid + 256 * j;            // 16-B chunk of the 256 x 128-B tile
+        const int p = idx >> 3, c = idx & 7;
+        const int w = p >> 6, pl = p & 63;
+        const uint4 v = *(const uint4*)(smem + w * 64 * EROW + pl * EROW + c * 16);
+        const int pr = p / FTW, pc = p - (p / FTW) * FTW;
+        *(uint4*)(y + (((size_t)n * Ho + oh0 + pr) * Wo + ow0 + pc) * CO + c * 8) = v;
     }
     if (stats) {
         float* red = (float*)(smem + 4 * 64 * EROW);        // [4 waves][64 ch][2]
@@ -183,190 +180,10 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
             double s = 0.0, q = 0.0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) { s += red[(w * CO + tid) * 2]; q += red[(w * CO + tid) * 2 + 1]; }
-            const int rep = stat_rep(fin, bid);
+            const int rep = bid % SCD_STAT_REPLICAS;
             atomic_add_f64(stats + ((long)rep * 2 + 0) * CO + tid, s);
             atomic_add_f64(stats + ((long)rep * 2 + 1) * CO + tid, q);
         }
-    }
-    bn_fin_tail(fin, 256, smem);
-}
-
-// ---- forward, second pass: the conv recomputed, then BN + ReLU + MaxPool(3, 2, 1) (residuals.py:209-216) on the
-// tile in LDS.  The 268-MB conv output of the one-pass forward (B = 32) is never written: the first pass
-// (stem_conv_fwd_kernel with y = NULL) only accumulates the BN statistics, this one reads the input image again
-// (17 MB) and writes the pooled output, its argmax bytes and ymax = the pre-BN conv value at each argmax (what the
-// backward needs of y: dz is nonzero only there).  One workgroup = one pooled row x 64 pooled columns = conv rows
-// 2po-1 .. 2po+1 x conv columns 2pq0-1 .. 2pq0+127 (387 conv pixels, 25 MFMA blocks of 16; the conv row shared with
-// the previous pooled row and the halo column are computed twice: 1.5x the conv's 13 GFLOP; persistent with the next
-// tile's patch in flight, as stem_conv_fwd_kernel).  The conv pixels are
-// the forward kernel's (same bf16 taps, same two-step MFMA order, rounded to bf16 before the BN), and the window is
-// scanned as stem_pool_fwd_kernel scans it, so out / argmax are bit-identical to conv -> y -> scd_stem_pool_fwd.
-constexpr int PQ = 64;                               // pooled columns per workgroup
-constexpr int PCC = 2 * PQ + 1;                      // conv columns of the tile (129)
-constexpr int PCR = 3;                               // conv rows of the tile
-constexpr int PSLOTS = 400;                          // PCR * PCC = 387 conv pixels, padded to 25 blocks of 16
-constexpr int PPROWS = SP * (PCR - 1) + KS;          // 11 input rows
-constexpr int PPCOLS = SP * (PCC - 1) + KS + 1;      // 264 input columns (even)
-constexpr int PEROW = CO * 2 + 16;                   // conv tile row stride in LDS (144 B: conflict-free row writes)
-
-__global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
-                                                                const float* __restrict__ scale, const float* __restrict__ shift,
-                                                                __bf16* __restrict__ out, uint8_t* __restrict__ argmax,
-                                                                __bf16* __restrict__ ymax, int H, int W, int Ho, int Wo,
-                                                                int ntiles) {
-    constexpr int AT = PSLOTS * 128;                 // A tile [slot][64 taps] bf16, 128-B rows
-    constexpr int CT = PSLOTS * PEROW;               // conv tile [slot][64 ch] bf16 (over the A tile)
-    constexpr int SM = CT > AT ? CT : AT;
-    constexpr int BT = CO * 128;                     // B tile [64 co][64 taps], loaded once, beside the tiles
-    __shared__ __attribute__((aligned(16))) char smem[SM + BT + PPROWS * PPCOLS * 4];
-    char* As = smem;
-    char* Bs = smem + SM;
-    float* patch = (float*)(smem + SM + BT);
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int l16 = lane & 15, lg = lane >> 4, l7 = l16 & 7;
-    const int Hp = Ho / 2, Wp = Wo / 2;
-    const int tiles_w = Wp / PQ;
-    const int tiles_img = Hp * tiles_w;
-
-    for (int i = tid; i < CO * 8; i += 256) {       // (in LDS, not registers: the 7 x 4 accumulators need them)
-        const int r = i >> 3, c = i & 7;
-        *(uint4*)(Bs + swz128(r, c)) = *(const uint4*)(wpk + r * 64 + c * 8);
-    }
-    const int ch = tid & 7;                          // this thread's 8-channel chunk in the pooling (256 % 8 == 0)
-    __shared__ __attribute__((aligned(16))) float prm[2 * CO];     // scale | shift, read per pooled item
-    if (tid < CO) { prm[tid] = scale[tid]; prm[CO + tid] = shift[tid]; }
-
-    constexpr int PN = (PPROWS * PPCOLS + 255) / 256;
-    float pv[PN];
-    auto load_patch = [&](int t) {
-        const int n = t / tiles_img, rem = t - n * tiles_img;
-        const int po = rem / tiles_w, pq0 = (rem - (rem / tiles_w) * tiles_w) * PQ;
-        const int ih0 = (2 * po - 1) * SP - PD, iw0 = (2 * pq0 - 1) * SP - PD;
-        const float* xn = x + (size_t)n * H * W;
-#pragma unroll
-        for (int j = 0; j < PN; ++j) {
-            const int i = min(tid + 256 * j, PPROWS * PPCOLS - 1);
-            const int r = i / PPCOLS, c = i - (i / PPCOLS) * PPCOLS;
-            const int ih = ih0 + r, iw = iw0 + c;
-            const float v = xn[(size_t)min(max(ih, 0), H - 1) * W + min(max(iw, 0), W - 1)];
-            pv[j] = ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? v : 0.f;
-        }
-    };
-    if (blockIdx.x < ntiles) load_patch(blockIdx.x);
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int n = t / tiles_img, rem = t - n * tiles_img;
-        const int po = rem / tiles_w, pq0 = (rem - (rem / tiles_w) * tiles_w) * PQ;
-        const int cr0 = 2 * po - 1, cc0 = 2 * pq0 - 1;   // first conv row / column of the tile (may be -1)
-#pragma unroll
-        for (int j = 0; j < PN; ++j) {
-            const int i = tid + 256 * j;
-            if (i < PPROWS * PPCOLS) patch[i] = pv[j];
-        }
-        if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x);     // in flight during this tile
-        __syncthreads();
-        // im2col tile: slot s = conv pixel (s / PCC, s % PCC) of the tile, all 64 taps; slots >= 387 are zero
-        for (int sl = tid; sl < PSLOTS; sl += 256) {
-            const int pr = sl / PCC, pc = sl - (sl / PCC) * PCC;
-            const bool live = sl < PCR * PCC;
-            const float* pp = patch + (SP * (live ? pr : 0)) * PPCOLS + SP * (live ? pc : 0);
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                bf16x8 v;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int k = c * 8 + e;
-                    v[e] = (__bf16)(live && k < KK ? pp[(k / KS) * PPCOLS + (k % KS)] : 0.f);
-                }
-                *(bf16x8*)(As + swz128(sl, c)) = v;
-            }
-        }
-        __syncthreads();
-        // MFMA: wave w owns pixel blocks w, w + 4, ... (7 or 6 of the 25) x all 64 channels, K = 64 (2 steps)
-        constexpr int NB = (PSLOTS / 16 + 3) / 4;    // 7
-        f32x4 acc[NB][4];
-#pragma unroll
-        for (int a = 0; a < NB; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int co = ((s * 4 + lg) ^ l7) << 4;
-            bf16x8 bfr[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) bfr[b] = *(const bf16x8*)(Bs + (b * 16 + l16) * 128 + co);
-#pragma unroll
-            for (int a = 0; a < NB; ++a) {
-                const int blk = wave + 4 * a;
-                if (blk < PSLOTS / 16) {
-                    const bf16x8 af = *(const bf16x8*)(As + (blk * 16 + l16) * 128 + co);
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af, acc[a][b], 0, 0, 0);
-                }
-            }
-        }
-        __syncthreads();          // A tile no longer read: the conv tile [slot][64 ch] bf16 goes over it
-#pragma unroll
-        for (int a = 0; a < NB; ++a) {
-            const int blk = wave + 4 * a;
-            if (blk < PSLOTS / 16) {
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                    bf16x4 o;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[a][b][r];
-                    *(bf16x4*)(smem + (blk * 16 + l16) * PEROW + (b * 16 + lg * 4) * 2) = o;
-                }
-            }
-        }
-        __syncthreads();
-        // pooling: item = (pooled column, 8-channel chunk), two per thread
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int pq = (tid + 256 * j) >> 3;
-            float sc[8], sh[8];
-            *(float4*)sc = *(const float4*)(prm + ch * 8); *(float4*)(sc + 4) = *(const float4*)(prm + ch * 8 + 4);
-            *(float4*)sh = *(const float4*)(prm + CO + ch * 8);
-            *(float4*)(sh + 4) = *(const float4*)(prm + CO + ch * 8 + 4);
-            float best[8];
-            int arg[8];
-            unsigned short ybest[8];                  // raw bf16 bits of y at the running argmax
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; ybest[e] = 0; }
-#pragma unroll
-            for (int d = 0; d < 9; ++d) {
-                const int r = d / 3, c = 2 * pq + d % 3;
-                const bool in = (unsigned)(cr0 + r) < (unsigned)Ho && (unsigned)(cc0 + c) < (unsigned)Wo;
-                const uint4 raw = *(const uint4*)(smem + (r * PCC + c) * PEROW + ch * 16);
-                float v[8];
-                Vec16<__bf16>::load(&raw, v);
-                const unsigned rw[4] = {raw.x, raw.y, raw.z, raw.w};
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float z = in ? fmaxf(v[e] * sc[e] + sh[e], 0.f) : -INFINITY;
-                    if (z > best[e]) {
-                        best[e] = z; arg[e] = d;
-                        ybest[e] = (unsigned short)((rw[e >> 1] >> (16 * (e & 1))) & 0xffffu);
-                    }
-                }
-            }
-            const size_t o = (((size_t)n * Hp + po) * Wp + pq0 + pq) * CO + ch * 8;
-            Vec16<__bf16>::store(out + o, best);
-            unsigned lo = 0, hi = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) lo |= (unsigned)arg[e] << (8 * e);
-#pragma unroll
-            for (int e = 4; e < 8; ++e) hi |= (unsigned)arg[e] << (8 * (e - 4));
-            *(uint2*)(argmax + o) = make_uint2(lo, hi);
-            uint4 yo;
-            yo.x = ybest[0] | ((unsigned)ybest[1] << 16); yo.y = ybest[2] | ((unsigned)ybest[3] << 16);
-            yo.z = ybest[4] | ((unsigned)ybest[5] << 16); yo.w = ybest[6] | ((unsigned)ybest[7] << 16);
-            *(uint4*)(ymax + o) = yo;
-        }
-        // the next tile's patch store and barrier order these conv-tile reads before the next im2col writes
     }
 }
 
@@ -511,10 +328,6 @@ __device__ __forceinline__ int bpatch_idx(int r, int c) { return r * PROW + (c &
 constexpr int BPROWS = 9;                            // input rows of a tile: conv rows 2bo, 2bo+1 -> 4bo-3 .. 4bo+5
 constexpr int ONE_TAP = KK;                          // col tap 49 = 1
 
-// PY: y is ymax of stem_conv_pool_kernel (pooled layout: the pre-BN conv value at each pooled output's argmax), read
-// beside dout at the pooled positions instead of y at the 2x2 conv block; dz is nonzero only at a pooled output's
-// argmax, where the two agree, so the results are the same bits.
-template <bool PY>
 __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
     const __bf16* __restrict__ dout, const uint8_t* __restrict__ argmax, const __bf16* __restrict__ y,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
@@ -573,15 +386,12 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                 rd[oi][oj] = *(const uint4*)(dout + o);
                 const uint2 av = *(const uint2*)(argmax + o);        // o is in range either way: no branch
                 ra[oi][oj] = ok ? av : make_uint2(0xffffffffu, 0xffffffffu);
-                if constexpr (PY) ry[oi][oj] = *(const uint4*)(y + o);
             }
-        if constexpr (!PY) {
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    ry[a][b] = *(const uint4*)(y + (((long)n * Ho + 2 * bo + a) * Wo + 2 * bc + b) * CO + ch * 8);
-        }
+            for (int b = 0; b < 2; ++b)
+                ry[a][b] = *(const uint4*)(y + (((long)n * Ho + 2 * bo + a) * Wo + 2 * bc + b) * CO + ch * 8);
         const float* xn = x + (size_t)n * H * W;
         const int ih0 = 4 * bo - PD, iw0 = 2 * w0 - PD;
 #pragma unroll
@@ -606,9 +416,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                 float g[8], v[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) g[e] = 0.f;
-                // PY: the y bits of this position, picked from the ymax of a pooled output whose argmax it is (every
-                // such output holds the same value; where none does, dz is zero and y does not matter)
-                uint4 yb = PY ? make_uint4(0u, 0u, 0u, 0u) : ry[a][b];
+                const uint4 yb = ry[a][b];
 #pragma unroll
                 for (int oi = 0; oi < 2; ++oi)
 #pragma unroll
@@ -618,18 +426,12 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                         float d[8];
                         Vec16<__bf16>::load(&rd[oi][oj], d);
                         const unsigned aw[2] = {ra[oi][oj].x, ra[oi][oj].y};
-                        unsigned* ybw = (unsigned*)&yb;
-                        const unsigned* ymw = (const unsigned*)&ry[oi][oj];
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
                             const bool hit = ((aw[e >> 2] >> (8 * (e & 3))) & 0xffu) == sel;
                             // a select, not a branch (as `if (hit) g += d` the compiler emitted 63 exec-masked
                             // branch regions per tile); g is never -0, so adding +0 leaves it unchanged
                             g[e] += hit ? d[e] : 0.f;
-                            if constexpr (PY) {
-                                const unsigned m = 0xffffu << (16 * (e & 1));
-                                ybw[e >> 1] = hit ? (ybw[e >> 1] & ~m) | (ymw[e >> 1] & m) : ybw[e >> 1];
-                            }
                         }
                     }
                 Vec16<__bf16>::load(&yb, v);
@@ -789,34 +591,15 @@ SCD_KERNEL_NS_END
 
 extern "C" int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H,
                                  int W, int Ho, int Wo, void* stream) {
-    return scd_stem_conv_fwd_fin(dtype, x, wpk, y, stats, N, H, W, Ho, Wo, nullptr, stream);
-}
-
-extern "C" int scd_stem_conv_fwd_fin(int dtype, const float* x, const void* wpk, void* y, double* stats, int N, int H,
-                                     int W, int Ho, int Wo, const scd_bn_fin* fin, void* stream) {
-    SCD_F16_FWD(scd_stem_conv_fwd_fin, x, wpk, y, stats, N, H, W, Ho, Wo, fin, stream);
+    SCD_F16_FWD(scd_stem_conv_fwd, x, wpk, y, stats, N, H, W, Ho, Wo, stream);
     if (dtype != SCD_DT_BF16 || N <= 0 || Ho != (H + 2 * PD - KS) / SP + 1 || Wo != (W + 2 * PD - KS) / SP + 1 ||
-        Wo % FTW || Ho % FTH || (fin && !stats) || (!y && !stats))
+        Wo % FTW || Ho % FTH || !y)
         return SCD_ERR_ARG;
     // one workgroup per tile (a resident-grid walk with the next tile's patch in flight and the weights in registers
-    // measured slower, 121 vs 106 us with y and 95 vs 84 us statistics-only at B = 32: the kernel is bound by its LDS /
-    // VALU tile build, not by load latency)
+    // measured slower, 121 vs 106 us: the kernel is bound by its LDS / VALU tile build, not by load latency)
     const int blocks = N * (Ho / FTH) * (Wo / FTW);
     hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (const __bf16*)wpk,
-                       (__bf16*)y, stats, H, W, Ho, Wo, bn_fin_dev(fin, stats, CO));
-    SCD_RETURN_LAUNCH();
-}
-
-extern "C" int scd_stem_conv_pool_fwd(int dtype, const float* x, const void* wpk, const float* scale,
-                                      const float* shift, void* out, uint8_t* argmax, void* ymax, int N, int H, int W,
-                                      void* stream) {
-    SCD_F16_FWD(scd_stem_conv_pool_fwd, x, wpk, scale, shift, out, argmax, ymax, N, H, W, stream);
-    const int Ho = (H + 2 * PD - KS) / SP + 1, Wo = (W + 2 * PD - KS) / SP + 1;
-    if (dtype != SCD_DT_BF16 || N <= 0 || Ho < 2 || Ho % 2 || Wo % (2 * PQ) || !out || !argmax || !ymax)
-        return SCD_ERR_ARG;
-    const int ntiles = N * (Ho / 2) * (Wo / (2 * PQ));
-    hipLaunchKernelGGL(stem_conv_pool_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, x, (const __bf16*)wpk,
-                       scale, shift, (__bf16*)out, argmax, (__bf16*)ymax, H, W, Ho, Wo, ntiles);
+                       (__bf16*)y, stats, H, W, Ho, Wo);
     SCD_RETURN_LAUNCH();
 }
 
@@ -849,53 +632,25 @@ extern "C" int scd_stem_bwd_nsplit(void) {
     return 2 * cus;
 }
 
-static int stem_bwd_fused_launch(bool pooled_y, const void* dout, const uint8_t* argmax, const void* y,
-                                 const float* scale, const float* shift, const float* mean, const float* invstd,
-                                 const float* x, double* stats, float* ws, int nsplit, float* tg, int N, int H, int W,
-                                 int Ho, int Wo, void* stream);
-
 extern "C" int scd_stem_bwd_fused(int dtype, const void* dout, const uint8_t* argmax, const void* y, const float* scale,
                                   const float* shift, const float* mean, const float* invstd, const float* x,
                                   double* stats, float* ws, int nsplit, float* tg, int N, int H, int W, int Ho, int Wo,
                                   void* stream) {
     SCD_F16_FWD(scd_stem_bwd_fused, dout, argmax, y, scale, shift, mean, invstd, x, stats, ws, nsplit, tg, N, H, W, Ho,
                 Wo, stream);
-    if (dtype != SCD_DT_BF16) return SCD_ERR_ARG;
-    return stem_bwd_fused_launch(false, dout, argmax, y, scale, shift, mean, invstd, x, stats, ws, nsplit, tg, N, H, W,
-                                 Ho, Wo, stream);
-}
-
-extern "C" int scd_stem_bwd_fused_pooled(int dtype, const void* dout, const uint8_t* argmax, const void* ymax,
-                                         const float* scale, const float* shift, const float* mean, const float* invstd,
-                                         const float* x, double* stats, float* ws, int nsplit, float* tg, int N, int H,
-                                         int W, int Ho, int Wo, void* stream) {
-    SCD_F16_FWD(scd_stem_bwd_fused_pooled, dout, argmax, ymax, scale, shift, mean, invstd, x, stats, ws, nsplit, tg, N,
-                H, W, Ho, Wo, stream);
-    if (dtype != SCD_DT_BF16) return SCD_ERR_ARG;
-    return stem_bwd_fused_launch(true, dout, argmax, ymax, scale, shift, mean, invstd, x, stats, ws, nsplit, tg, N, H,
-                                 W, Ho, Wo, stream);
-}
-
-static int stem_bwd_fused_launch(bool pooled_y, const void* dout, const uint8_t* argmax, const void* y,
-                                 const float* scale, const float* shift, const float* mean, const float* invstd,
-                                 const float* x, double* stats, float* ws, int nsplit, float* tg, int N, int H, int W,
-                                 int Ho, int Wo, void* stream) {
-    if (nsplit < 1 || Wo % BTW || Ho % 2 || Ho != (H + 2 * PD - KS) / SP + 1 || Wo != (W + 2 * PD - KS) / SP + 1 ||
-        (long)N * Ho * Wo * CO >= (1L << 31))
+    if (dtype != SCD_DT_BF16 || nsplit < 1 || Wo % BTW || Ho % 2 || Ho != (H + 2 * PD - KS) / SP + 1 ||
+        Wo != (W + 2 * PD - KS) / SP + 1 || (long)N * Ho * Wo * CO >= (1L << 31))
         return SCD_ERR_ARG;
     const int ntiles = N * (Ho / 2) * (Wo / BTW);
     const int chunk = (ntiles + nsplit - 1) / nsplit;
     const int grid = (ntiles + chunk - 1) / chunk;
     hipStream_t st = (hipStream_t)stream;
-    if (pooled_y)
-        hipLaunchKernelGGL(stem_bwd_fused_kernel<true>, dim3(grid), dim3(256), 0, st, (const __bf16*)dout, argmax,
-                           (const __bf16*)y, scale, shift, mean, invstd, x, stats, ws, H, W, Ho, Wo, ntiles, chunk);
-    else
-        hipLaunchKernelGGL(stem_bwd_fused_kernel<false>, dim3(grid), dim3(256), 0, st, (const __bf16*)dout, argmax,
-                           (const __bf16*)y, scale, shift, mean, invstd, x, stats, ws, H, W, Ho, Wo, ntiles, chunk);
+    hipLaunchKernelGGL(stem_bwd_fused_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)dout, argmax,
+                       (const __bf16*)y, scale, shift, mean, invstd, x, stats, ws, H, W, Ho, Wo, ntiles, chunk);
     hipLaunchKernelGGL(stem_bwd_reduce_kernel, dim3(2 * CO * 64 / 32), dim3(256), 0, st, (const float*)ws, grid, tg);
     SCD_RETURN_LAUNCH();
 }
+
 
 extern "C" int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk, const float* coef, float* dst,
                                     int accumulate, float alpha, void* stream) {

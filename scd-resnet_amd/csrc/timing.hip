@@ -39,14 +39,3 @@ extern "C" int scd_event_elapsed_ms(void* start, void* end, float* ms) {
     if (e != hipSuccess) return (int)e;
     return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end);
 }
-
-
-// A stream whose kernels may only use the CUs set in `mask` (nwords x 32 bits, bit i = CU i): the weight-gradient
-// side stream confined to part of the chip (SCD_SIDE_CUS), so its long-running workgroups cannot take every CU the
-// compute stream's critical chain needs.
-extern "C" int scd_stream_create_cumask(const unsigned* mask, int nwords, void** stream) {
-    if (!mask || nwords <= 0 || !stream) return SCD_ERR_ARG;
-    return (int)hipExtStreamCreateWithCUMask((hipStream_t*)stream, (uint32_t)nwords, mask);
-}
-
-extern "C" int scd_stream_destroy(void* stream) { return stream ? (int)hipStreamDestroy((hipStream_t)stream) : 0; }

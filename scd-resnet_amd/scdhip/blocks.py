@@ -27,10 +27,6 @@ def _c(t):
 
 # stem backward as one pass (ops.stem_backward_fused); SCD_STEM_FUSED_BWD=0: pool backward + fused-apply weight gradient
 _STEM_FUSED_BWD = os.environ.get("SCD_STEM_FUSED_BWD", "1") != "0"
-# stem forward in two passes without the full-resolution conv output (ops.stem_conv_pool_fwd), SCD_STEM_POOLED=1: measured
-# 2.8% slower per step than conv -> y -> pool (the stem conv is bound by its LDS / VALU tile build, 84 us of the 106 with
-# y stored, so a second conv pass costs more than the 268-MB write and two reads it saves), hence off by default
-_STEM_POOLED = os.environ.get("SCD_STEM_POOLED", "0") == "1"
 
 
 def _conv_ld(w):
@@ -39,15 +35,14 @@ def _conv_ld(w):
     return (w.shape[1] * T, T, 1)
 
 
-def _conv_stats(x, conv, bn, stride, pad, training, timer=None, fin=None):
-    """conv (no bias) -> raw y, with the BN statistics accumulated in the GEMM epilogue (training; fin: and
-    finalized by the GEMM's last workgroup, ops.FinForward)."""
+def _conv_stats(x, conv, bn, stride, pad, training, timer=None):
+    """conv (no bias) -> raw y, with the BN statistics accumulated in the GEMM epilogue (training)."""
     C = conv.weight.shape[0]
     kh, kw = conv.weight.shape[2], conv.weight.shape[3]
     wp = ops.pack_weight(conv.weight, x.dtype, 0)
     stats = ops.bn_stats(bn, "fwd") if training else None
     t0 = ops.LaunchTimer.record(timer) if timer else None
-    y = ops.conv_fwd(x, wp, C, kh, kw, stride, pad, stats=stats, fin=fin)
+    y = ops.conv_fwd(x, wp, C, kh, kw, stride, pad, stats=stats)
     if timer:
         ops.LaunchTimer.close(timer, t0)
     return y, stats
@@ -56,25 +51,15 @@ def _conv_stats(x, conv, bn, stride, pad, training, timer=None, fin=None):
 def _train_bn_conv(x, conv, bn, stride, pad, training, timer=None):
     """conv (no bias) -> raw y + BN statistics -> BNState.  timer: LaunchTimer name for the GEMM (bench.py)."""
     C = conv.weight.shape[0]
-    fin = ops.fin_forward(bn, C) if training else None
-    y, stats = _conv_stats(x, conv, bn, stride, pad, training, timer, fin=fin)
-    if fin is not None:
-        return y, fin.st
+    y, stats = _conv_stats(x, conv, bn, stride, pad, training, timer)
     return y, ops.bn_finalize(bn, stats, C, y.numel() // C, training)
 
 
 def _conv1_and_downsample(x, blk, conv1, bn1, s1, pad1, sd):
     """A block's first conv and its downsample conv (both read only the block input; residuals.py:99-120,
-    145-165), then both BN finalizes together: with SyncBN one all-reduce for the two layers (at world 1 each GEMM
-    finalizes its own layer, ops.FinForward)."""
+    145-165), then both BN finalizes together: with SyncBN one all-reduce for the two layers."""
     bnd = blk.downsample[1]
     C1, Cd = conv1.weight.shape[0], blk.downsample[0].weight.shape[0]
-    f1 = ops.fin_forward(bn1, C1)
-    fd = ops.fin_forward(bnd, Cd) if f1 is not None else None
-    if f1 is not None and fd is not None:
-        y1, _ = _conv_stats(x, conv1, bn1, s1, pad1, True, fin=f1)
-        yd, _ = _conv_stats(x, blk.downsample[0], bnd, sd, 0, True, fin=fd)
-        return y1, f1.st, yd, fd.st
     y1, s1st = _conv_stats(x, conv1, bn1, s1, pad1, True)
     yd, sdst = _conv_stats(x, blk.downsample[0], bnd, sd, 0, True)
     st1, std = ops.bn_finalize_pair(bn1, s1st, C1, y1.numel() // C1, bnd, sdst, Cd, yd.numel() // Cd)
@@ -102,36 +87,21 @@ class StemFn(torch.autograd.Function):
         stats = ops.bn_stats(bn, "fwd") if training else None
         ref_geom = tuple(conv.weight.shape) == (64, 1, 7, 7) and conv.stride[0] == 2 and conv.padding[0] == 3
         direct = ops.stem_direct_ok(x, dtype) and ref_geom
-        fin = ops.fin_forward(bn, C) if training else None
-        pooled = direct and _STEM_FUSED_BWD and _STEM_POOLED and ops.stem_pool_ok(x, dtype)
-        if pooled:
-            # conv -> statistics only, finalize, then the conv again with BN + ReLU + MaxPool on the tile in LDS: the
-            # backward needs y only at the pool's argmax positions (ymax), so y is never written
-            x = _c(x)
-            wpk = ops.pack_weight(conv.weight, dtype, 0, ldp=64)
-            if training:
-                ops.stem_conv_fwd(x, wpk, stats=stats, fin=fin, store=False)
-            st = fin.st if fin is not None else ops.bn_finalize(bn, stats, C, ops.stem_out_count(x), training)
-            out, am, ym = ops.stem_conv_pool_fwd(x, wpk, st)
-            ctx.save_for_backward(x, ym, am)
-            ctx.st, ctx.conv, ctx.bn, ctx.direct, ctx.pooled = st, conv, bn, True, True
-            ctx.wpk = wpk
-            return out
         if direct:
             # direct 7x7/s2 conv: the tap tile is built in LDS from the input patch (no column tensor)
             x = _c(x)
             wpk = ops.pack_weight(conv.weight, dtype, 0, ldp=64)
-            y = ops.stem_conv_fwd(x, wpk, stats=stats, fin=fin)
+            y = ops.stem_conv_fwd(x, wpk, stats=stats)
             cols = x
         else:
             cols = ops.im2col_stem(x, dtype, kh=conv.weight.shape[2], kw=conv.weight.shape[3],
                                    stride=conv.stride[0], pad=conv.padding[0])
             wp = ops.pack_weight(conv.weight, dtype, 0, ldp=cols.shape[-1])
-            y = ops.conv_fwd(cols, wp, C, 1, 1, 1, 0, stats=stats, fin=fin)
-        st = fin.st if fin is not None else ops.bn_finalize(bn, stats, C, y.numel() // C, training)
+            y = ops.conv_fwd(cols, wp, C, 1, 1, 1, 0, stats=stats)
+        st = ops.bn_finalize(bn, stats, C, y.numel() // C, training)
         out, am = ops.stem_pool_fwd(y, st)
         ctx.save_for_backward(cols, y, am)
-        ctx.st, ctx.conv, ctx.bn, ctx.direct, ctx.pooled = st, conv, bn, direct, False
+        ctx.st, ctx.conv, ctx.bn, ctx.direct = st, conv, bn, direct
         ctx.wpk = wpk if direct else None
         return out
 
@@ -139,10 +109,7 @@ class StemFn(torch.autograd.Function):
     def backward(ctx, dout):
         conv, bn, st = ctx.conv, ctx.bn, ctx.st
         cols, y, am = ctx.saved_tensors
-        if ctx.pooled:
-            # y here is ymax (pooled layout)
-            ops.stem_backward_fused(bn, _c(dout), am, y, st, cols, ctx.wpk, ops.grad_of(conv.weight), pooled=True)
-        elif ctx.direct and _STEM_FUSED_BWD:
+        if ctx.direct and _STEM_FUSED_BWD:
             # pool / ReLU / BN / weight-gradient backward in one pass over the pooled gradient (dz stays on chip)
             ops.stem_backward_fused(bn, _c(dout), am, y, st, cols, ctx.wpk, ops.grad_of(conv.weight))
         elif ctx.direct:
@@ -154,7 +121,6 @@ class StemFn(torch.autograd.Function):
             dy = ops.bn_backward(bn, st, dz, y)
             T = conv.weight.shape[2] * conv.weight.shape[3]
             ops.conv_wgrad(dy, cols, 1, 1, 1, 0, ops.grad_of(conv.weight), (T, 1, 0), cvalid=T)
-        ops.fin_release(st)
         grads_ready(conv, bn)
         return None, None, None, None, None
 
@@ -210,7 +176,6 @@ class BasicBlockFn(torch.autograd.Function):
             # the downsample's input gradient last: += over the pixels its 1x1 taps reach only (one in four at stride 2)
             ops.conv_dgrad(dyd, ops.pack_weight(blk.downsample[0].weight, x.dtype, 1), Cin, H, W, 1, 1, s, 0, out=dx,
                            accumulate=True)
-        ops.fin_release(st1, st2, std)
         grads_ready(blk)
         return dx, None, None
 
@@ -272,7 +237,6 @@ class BottleneckFn(torch.autograd.Function):
         if dyd is not None:
             ops.conv_dgrad(dyd, ops.pack_weight(blk.downsample[0].weight, x.dtype, 1), Cin, H, W, 1, 1, s, 0, out=dx,
                            accumulate=True)
-        ops.fin_release(st1, st2, st3, std)
         grads_ready(blk)
         return dx, None, None
 
@@ -287,9 +251,8 @@ class DeconvBNFn(torch.autograd.Function):
         s, p = deconv.stride[0], deconv.padding[0]
         Cout = w.shape[1]
         stats = ops.bn_stats(bn, "fwd") if bn.training else None
-        fin = ops.fin_forward(bn, Cout) if bn.training else None
-        y = ops.deconv_fwd(x, ops.pack_weight(w, x.dtype, 1), Cout, k, s, p, stats=stats, fin=fin)
-        st = fin.st if fin is not None else ops.bn_finalize(bn, stats, Cout, y.numel() // Cout, bn.training)
+        y = ops.deconv_fwd(x, ops.pack_weight(w, x.dtype, 1), Cout, k, s, p, stats=stats)
+        st = ops.bn_finalize(bn, stats, Cout, y.numel() // Cout, bn.training)
         out = ops.bn_apply(y, st, True)
         ctx.save_for_backward(x, y, out)
         ctx.st, ctx.deconv, ctx.bn = st, deconv, bn
@@ -314,7 +277,6 @@ class DeconvBNFn(torch.autograd.Function):
                               bn_bwd=ops.fused_bn_bwd_args(ctx.prod) if fuse else None)
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dx)
-        ops.fin_release(st)
         grads_ready(deconv, bn)
         return dx, None, None, None
 
@@ -341,12 +303,8 @@ class ConvBNFn(torch.autograd.Function):
         dy = ops.bn_backward(bn, st, _c(dout), y, relu=ctx.relu)
         ops.conv_wgrad(dy, x, kh, kw, s, p, ops.grad_of(w), _conv_ld(w))
         dx = ops.conv_dgrad(dy, ops.pack_weight(w, x.dtype, 1), x.shape[3], x.shape[1], x.shape[2], kh, kw, s, p)
-        ops.fin_release(st)
         grads_ready(conv, bn)
         return dx, None, None, None, None
-
-
-_HEADS_WGRAD_LATE = os.environ.get("SCD_HEADS_WGRAD_LATE", "1") == "1"
 
 
 class HeadsFn(torch.autograd.Function):
@@ -509,9 +467,6 @@ class HeadsFn(torch.autograd.Function):
             ops.conv_wgrad(dhid_s.view(1, 1, Sl, Cs), xcol.view(1, 1, Sl, 9 * Cin), 1, 1, 1, 0, None, None,
                            rows=[((i - nd) * Hd, (i - nd + 1) * Hd, ops.grad_of(heads[i][0].weight), ld)
                                  for i in range(nd, nh)], red_taps=9)
-        late = _HEADS_WGRAD_LATE
-        if not late:
-            wgrads()
         # input gradient: dense heads' GEMM (+ the deconv BN's backward sums), then the sparse heads' part
         fuse = ctx.prod is not None and dt in ops.HALF
         bn_args = ops.fused_bn_bwd_args(ctx.prod) if fuse else None
@@ -529,8 +484,7 @@ class HeadsFn(torch.autograd.Function):
         mods = [m for h in heads for m in h if isinstance(m, torch.nn.Module)]
         if fuse:
             ops.mark_bn_bwd_fused(ctx.prod[0], dfeat)
-        if late:
-            wgrads()             # side stream ordered after the input gradient: it overlaps the deconv backward
+        wgrads()                 # side stream ordered after the input gradient: it overlaps the deconv backward
         grads_ready(*mods)
         return dfeat, None, None
 
@@ -604,7 +558,6 @@ class CornerPoolFn(torch.autograd.Function):
             ops.conv_wgrad(dy, x, 3, 3, 1, 1, ops.grad_of(br.conv.weight), _conv_ld(br.conv.weight))
             ops.conv_dgrad(dy, ops.pack_weight(br.conv.weight, x.dtype, 1), C, H, W, 3, 3, 1, 1, out=dx,
                            accumulate=True)
-        ops.fin_release(st1, st2, stm, sts, stl)
         grads_ready(mod)
         if slot is not None:
             return ops.shared_grad_out(x, slot, dx if prev is None else None), None, None, None

@@ -221,8 +221,11 @@ class FlatSGD(_FlatOptimizer):
         return None
 
     def state_dict(self):
+        # torch emits a momentum_buffer only once a step has created it: the flat buffer exists from flat() on, so the
+        # device flag hyper[2] (set by the first step or a loaded buffer) says whether it is one yet
+        init = self._buf is not None and self._hyper is not None and float(self._hyper[2].item()) != 0.0
         return {"step": self._step, "param_groups": self._groups_sd(),
-                "momentum_buffer": None if self._buf is None else self._buf.cpu()}
+                "momentum_buffer": self._buf.cpu() if init else None}
 
     def load_state_dict(self, sd):
         buf = sd.get("momentum_buffer")

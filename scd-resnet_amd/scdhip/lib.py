@@ -22,8 +22,6 @@ DT_F16 = 2
 MAX_TAPS = 16
 MAX_PHASES = 4
 STAT_REPLICAS = 64
-FIN_REPLICAS = 16
-FIN_COUNTERS = 65          # SCD_FIN_COUNTERS: 64 arrival shards + the shard count
 
 c_int, c_long, c_float, c_double, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
                                                         ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p)
@@ -32,16 +30,6 @@ c_int, c_long, c_float, c_double, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_l
 class GemmPhase(ctypes.Structure):
     _fields_ = [("Qh", c_int), ("Qw", c_int), ("rho_h", c_int), ("rho_w", c_int), ("ntaps", c_int),
                 ("dh", c_int * MAX_TAPS), ("dw", c_int * MAX_TAPS), ("wt", c_int * MAX_TAPS)]
-
-
-class BnFin(ctypes.Structure):
-    """struct scd_bn_fin (include/scdhip.h): a BN finalize fused into its statistics producer; the kernels read a
-    device-memory copy of it (ops.BNFinalize writes it)."""
-    _fields_ = [("counter", c_void_p), ("backward", c_int), ("C", c_int), ("count", c_double), ("gamma", c_void_p),
-                ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
-                ("num_batches", c_void_p), ("momentum", c_float), ("eps", c_float), ("mean", c_void_p),
-                ("invstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p), ("dgamma", c_void_p),
-                ("dbeta", c_void_p), ("gscale", c_float), ("coef", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -61,10 +49,6 @@ LP = ctypes.POINTER(c_long)
 # name -> (restype, argtypes); mirrors include/scdhip.h one to one
 SIGNATURES = {
     "scd_conv_gemm": (I, [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P]),
-    "scd_conv_gemm_fin": (I, [I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P,
-                              P]),
-    "scd_conv_gemm_bnbwd_fin": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P, P, P,
-                                    P, P, P, P, P]),
     "scd_conv_gemm_heads": (I, [I, P, P, P, P, I, I, I, I, I, IP, PP, PP, PP, P]),
     "scd_conv_gemm_heads_keep": (I, [I, P, P, P, P, I, I, I, I, I, IP, PP, PP, PP, P, I, P]),
     "scd_conv_gemm_bnbwd": (I, [I, P, P, P, I, I, I, I, I, I, I, I, I, I, I, ctypes.POINTER(GemmPhase), P, P, P, P,
@@ -80,14 +64,11 @@ SIGNATURES = {
     "scd_pad_channels": (I, [I, P, L, I, I, P, P]),
     "scd_im2col_stem": (I, [I, P, P, I, I, I, I, I, I, I, I, I, I, P]),
     "scd_stem_conv_fwd": (I, [I, P, P, P, P, I, I, I, I, I, P]),
-    "scd_stem_conv_fwd_fin": (I, [I, P, P, P, P, I, I, I, I, I, P, P]),
     "scd_stem_conv_wgrad_nsplit": (I, [L]),
     "scd_stem_conv_wgrad": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_bwd_nsplit": (I, []),
     "scd_conv_dgrad_s2": (I, [I, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_bwd_fused": (I, [I, P, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P]),
-    "scd_stem_bwd_fused_pooled": (I, [I, P, P, P, P, P, P, P, P, P, P, I, P, I, I, I, I, I, P]),
-    "scd_stem_conv_pool_fwd": (I, [I, P, P, P, P, P, P, P, I, I, I, P]),
     "scd_stem_bwd_combine": (I, [I, P, P, P, P, I, F, P]),
     "scd_stem_pool_bwd_bn": (I, [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stats_collapse": (I, [P, I, I, P]),
@@ -95,12 +76,9 @@ SIGNATURES = {
     "scd_bn_finalize": (I, [P, I, I, D, P, P, P, P, P, F, F, P, P, P, P, P]),
     "scd_bn_apply": (I, [I, P, P, I, L, P, P, P, P, P, I, P]),
     "scd_bn_bwd_reduce": (I, [I, P, P, P, P, P, P, P, I, L, P, P]),
-    "scd_bn_bwd_reduce_fin": (I, [I, P, P, P, P, P, P, P, I, L, P, P, P]),
-    "scd_bn_fin_standalone": (I, [P, P, I, P]),
     "scd_bn_bwd_finalize": (I, [P, I, I, D, P, P, P, P, P, F, P, P]),
     "scd_bn_bwd_apply": (I, [I, P, P, P, P, P, P, I, L, P, P, P]),
     "scd_bn_bwd_reduce2": (I, [I, P, P, P, P, P, P, P, P, I, L, P, P, P]),
-    "scd_bn_bwd_reduce2_fin": (I, [I, P, P, P, P, P, P, P, P, I, L, P, P, P, P, P]),
     "scd_bn_bwd_apply2": (I, [I, P, P, P, P, P, P, I, L, P, P, P]),
     "scd_stem_pool_fwd": (I, [I, P, P, P, P, P, I, I, I, I, I, I, P]),
     "scd_stem_pool_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
@@ -151,8 +129,6 @@ SIGNATURES = {
     "scd_event_destroy": (I, [P]),
     "scd_event_record": (I, [P, P]),
     "scd_event_elapsed_ms": (I, [P, P, ctypes.POINTER(c_float)]),
-    "scd_stream_create_cumask": (I, [ctypes.POINTER(ctypes.c_uint), I, PP]),
-    "scd_stream_destroy": (I, [P]),
     "scd_version": (ctypes.c_char_p, []),
 }
 

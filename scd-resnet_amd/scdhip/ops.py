@@ -8,7 +8,6 @@ import contextlib
 import ctypes
 import math
 import os
-import weakref
 
 import torch
 import torch.distributed as dist
@@ -554,7 +553,7 @@ def pad_channels(t, C, Cp, rows):
 
 
 def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, stats=None, relu=False,
-          accumulate=False, bn_bwd=None, fin=None):
+          accumulate=False, bn_bwd=None):
     N, Hi, Wi, Ci = x.shape
     bk = 64 if x.dtype in HALF else 32
     if Ci % bk:
@@ -575,32 +574,25 @@ def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, sta
                out_stride, wpack.shape[1], nph, arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
                ptr(st.shift), ptr(bstats), stream())
         return y
-    if fin is not None:
-        # fin: FinForward -- the GEMM's last workgroup finalizes the BN statistics it accumulated
-        L.call("scd_conv_gemm_fin", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo,
-               Co, in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), nph, arr,
-               fin.ptr(y.numel() // Co), stream())
-        return y
     L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
            in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), nph, arr, stream())
     return y
 
 
-def conv_fwd(x, wpack, Co, kh, kw, stride, pad, bias=None, stats=None, relu=False, out=None, fin=None):
-    """Conv2d forward (NHWC); wpack = pack_weight(w, mode=0).  fin: FinForward of the BN the stats belong to."""
+def conv_fwd(x, wpack, Co, kh, kw, stride, pad, bias=None, stats=None, relu=False, out=None):
+    """Conv2d forward (NHWC); wpack = pack_weight(w, mode=0)."""
     _need_gpu(x)
     N, H, W, _ = x.shape
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
     if out is None:
         out = torch.empty(N, Ho, Wo, Co, dtype=x.dtype, device=x.device)
-    return _gemm(x, wpack, out, Co, Ho, Wo, stride, 1, _fwd_phase(kh, kw, pad, Ho, Wo), bias, stats, relu, fin=fin)
+    return _gemm(x, wpack, out, Co, Ho, Wo, stride, 1, _fwd_phase(kh, kw, pad, Ho, Wo), bias, stats, relu)
 
 
-def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumulate=False, stats=None, bn_bwd=None,
-               fin=None):
+def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumulate=False, stats=None, bn_bwd=None):
     """Input-gradient of Conv2d (NHWC) as a phase-decomposed gather-GEMM; wpack_t = pack_weight(w, mode=1).
-    Also ConvTranspose2d forward (with the transposed conv's geometry).  bn_bwd: see _gemm; fin: FinForward."""
+    Also ConvTranspose2d forward (with the transposed conv's geometry).  bn_bwd: see _gemm."""
     N = dy.shape[0]
     if out is None:
         out = torch.empty(N, Hc, Wc, Cin, dtype=dy.dtype, device=dy.device)
@@ -608,8 +600,7 @@ def conv_dgrad(dy, wpack_t, Cin, Hc, Wc, kh, kw, stride, pad, out=None, accumula
     phases = _dgrad_phases(kh, kw, stride, pad, Hc, Wc, nonempty=accumulate)
     if not phases.n:
         return out
-    return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, phases, stats=stats, accumulate=accumulate, bn_bwd=bn_bwd,
-                 fin=fin)
+    return _gemm(dy, wpack_t, out, Cin, Hc, Wc, 1, stride, phases, stats=stats, accumulate=accumulate, bn_bwd=bn_bwd)
 
 
 class DgradS2:
@@ -636,13 +627,13 @@ def conv_dgrad_w(dy, w, Hc, Wc, stride, pad, out=None, accumulate=False):
                       accumulate=accumulate)
 
 
-def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None, fin=None):
+def deconv_fwd(x, wpack_t, Cout, k=4, stride=2, pad=1, stats=None):
     """ConvTranspose2d(k, stride, pad, output_padding=0) forward; wpack_t = pack_weight(W_t, mode=1)."""
     _need_gpu(x)
     N, H, W, _ = x.shape
     Ho = (H - 1) * stride - 2 * pad + k
     Wo = (W - 1) * stride - 2 * pad + k
-    return conv_dgrad(x, wpack_t, Cout, Ho, Wo, k, k, stride, pad, stats=stats, fin=fin)
+    return conv_dgrad(x, wpack_t, Cout, Ho, Wo, k, k, stride, pad, stats=stats)
 
 
 def deconv_dgrad(dy, wpack, Cin, k=4, stride=2, pad=1, out=None, accumulate=False, bn_bwd=None):
@@ -914,21 +905,7 @@ def side_stream(dev):
 
 
 def _new_side_stream(idx):
-    ncu = int(os.environ.get("SCD_SIDE_CUS", "0"))
-    if ncu <= 0:
-        return torch.cuda.Stream(device=idx, priority=_Side.priority)
-    # SCD_SIDE_CUS=n: the side stream confined to n CUs spread evenly over the device (scd_stream_create_cumask; a
-    # CU-masked stream takes the default priority, still below the step's high-priority compute stream)
-    total = torch.cuda.get_device_properties(idx).multi_processor_count
-    ncu = min(ncu, total)
-    words = (ctypes.c_uint * ((total + 31) // 32))()
-    for j in range(ncu):
-        i = (j * total) // ncu
-        words[i // 32] |= 1 << (i % 32)
-    h = ctypes.c_void_p()
-    with torch.cuda.device(idx):
-        L.call("scd_stream_create_cumask", words, len(words), ctypes.byref(h))
-    return torch.cuda.ExternalStream(h.value, device=idx)
+    return torch.cuda.Stream(device=idx, priority=_Side.priority)
 
 
 def join_side_streams():
@@ -1013,145 +990,8 @@ _WGRAD_ROWS = {}
 # ------------------------------------------------------------------ BatchNorm (training)
 
 class BNState:
-    """Per-call BN quantities kept for backward (fin: they live in the module's persistent finalize buffers)."""
-    __slots__ = ("mean", "invstd", "scale", "shift", "count", "fin", "owner", "__weakref__")
-
-    def __init__(self):
-        self.fin = False
-        self.owner = None
-
-
-# ---- BN finalize fused into its statistics producer (scd_bn_fin, include/scdhip.h)
-class BNFinalize:
-    """Training at world 1 (no SyncBN all-reduce between the statistics and their finalize): the producing kernel's
-    last workgroup finalizes (the _fin entry points) instead of a separate ~5-us launch per BN layer and direction.
-    The descriptor the kernels read lives in device memory, written when its fields change (the first step), so the
-    BN quantities it points at are persistent per module: a forward takes them only while no earlier forward's
-    quantities are still referenced by an autograd graph (else it falls back to fresh buffers and the separate
-    finalize).  SCD_BN_FIN_FUSE=0: off."""
-    enabled = os.environ.get("SCD_BN_FIN_FUSE", "0") == "1"
-
-
-class _FinSlot:
-    """One BN module and direction: the arrival counter, the device copy of the descriptor and its last bytes."""
-
-    def __init__(self, dev):
-        n = ctypes.sizeof(L.BnFin)
-        self.counter = torch.zeros(L.FIN_COUNTERS, dtype=torch.int32, device=dev)
-        self.dbuf = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.dptr = self.dbuf.data_ptr()
-        self.last = None
-        self.key = None
-        self.keep = []
-
-    def write(self, desc):
-        b = bytes(desc)
-        if b != self.last:
-            # rare (first step, a new batch size, a re-created .grad): a stream-ordered copy from pinned memory, kept
-            # alive until it has certainly run
-            host = torch.frombuffer(bytearray(b), dtype=torch.uint8).pin_memory()
-            self.dbuf.copy_(host, non_blocking=True)
-            self.keep = (self.keep + [host])[-4:]
-            self.last = b
-        return self.dptr
-
-
-def _fin_slot(bn, which):
-    slot = getattr(bn, "_scd_fin_" + which, None)
-    if slot is None or slot.dbuf.device != bn.weight.device:
-        slot = _FinSlot(bn.weight.device)
-        setattr(bn, "_scd_fin_" + which, slot)
-    return slot
-
-
-def _fin_ok(bn):
-    return (BNFinalize.enabled and bn.training and _BNSync.group is None and bn.weight is not None and
-            bn.weight.is_cuda and bn.momentum is not None)
-
-
-def _fin_release(ref, gen):
-    bn = ref()
-    if bn is not None and getattr(bn, "_scd_fin_busy", 0) == gen:
-        bn._scd_fin_busy = 0
-
-
-def fin_release(*sts):
-    """A Function's backward is done with its BN quantities: the module's persistent finalize buffers may serve the
-    next forward (also released when the BNState is garbage-collected, e.g. after a forward without backward)."""
-    for st in sts:
-        if st is not None and st.fin and st.owner is not None:
-            _fin_release(*st.owner)
-
-
-class FinForward:
-    """The forward finalize of `bn` fused into its statistics producer: ``ptr(count)`` is the scd_bn_fin argument of
-    the producing launch, ``st`` the BN quantities it writes."""
-
-    def __init__(self, bn, C):
-        self.bn, self.C = bn, C
-        views = getattr(bn, "_scd_fin_views", None)
-        if views is None or views[0].numel() != 7 * C or views[0].device != bn.weight.device:
-            buf = torch.empty(7 * C, device=bn.weight.device)     # mean, invstd, scale, shift | backward coef
-            bn._scd_fin_st = buf
-            views = bn._scd_fin_views = (buf, buf[:C], buf[C:2 * C], buf[2 * C:3 * C], buf[3 * C:4 * C])
-        st = BNState()
-        st.mean, st.invstd, st.scale, st.shift = views[1:]
-        st.fin = True
-        gen = getattr(bn, "_scd_fin_gen", 0) + 1
-        bn._scd_fin_gen = gen
-        bn._scd_fin_busy = gen
-        st.owner = (weakref.ref(bn), gen)
-        weakref.finalize(st, _fin_release, st.owner[0], gen)
-        self.st = st
-
-    def ptr(self, count):
-        bn, st = self.bn, self.st
-        st.count = count
-        slot = _fin_slot(bn, "fwd")
-        # the descriptor changes only with the count or a re-allocated parameter / buffer
-        key = (count, bn.weight.data_ptr(), ptr(bn.bias), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
-               bn.num_batches_tracked.data_ptr(), st.mean.data_ptr(), bn.momentum, bn.eps)
-        if key == slot.key:
-            return slot.dptr
-        d = L.BnFin()
-        d.counter, d.backward, d.C, d.count = slot.counter.data_ptr(), 0, self.C, float(count)
-        d.gamma, d.beta = ptr(bn.weight), ptr(bn.bias)
-        d.running_mean, d.running_var = ptr(bn.running_mean), ptr(bn.running_var)
-        d.num_batches = ptr(bn.num_batches_tracked)
-        d.momentum, d.eps = float(bn.momentum), float(bn.eps)
-        d.mean, d.invstd, d.scale, d.shift = ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift)
-        slot.key = key
-        return slot.write(d)
-
-
-def fin_forward(bn, C):
-    """A FinForward for a training BN whose statistics producer can finalize them (world 1), else None."""
-    if not _fin_ok(bn) or getattr(bn, "_scd_fin_busy", 0):
-        return None
-    return FinForward(bn, C)
-
-
-def fin_backward(bn, st, C, alpha):
-    """(descriptor pointer, coef) for the backward finalize of `bn` fused into its backward-sum producer, or None:
-    only for BN quantities of a fused forward (persistent buffers; the coefficients go to the same buffer)."""
-    if not (getattr(st, "fin", False) and _fin_ok(bn)):
-        return None
-    buf = bn._scd_fin_st
-    coef = bn._scd_fin_views[0][4 * C:7 * C]
-    slot = _fin_slot(bn, "bwd")
-    dg, db = grad_of(bn.weight), grad_of(bn.bias)
-    key = (st.count, C, bn.weight.data_ptr(), buf.data_ptr(), ptr(dg), ptr(db), float(alpha))
-    if key == slot.key:
-        return slot.dptr, coef
-    d = L.BnFin()
-    d.counter, d.backward, d.C, d.count = slot.counter.data_ptr(), 1, C, float(st.count)
-    d.gamma = ptr(bn.weight)
-    d.mean, d.invstd = ptr(st.mean), ptr(st.invstd)
-    d.dgamma, d.dbeta = ptr(dg), ptr(db)
-    d.gscale = float(alpha)
-    d.coef = ptr(coef)
-    slot.key = key
-    return slot.write(d), coef
+    """Per-call BN quantities kept for backward."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "count")
 
 
 def bn_finalize(bn, stats, C, count, training=True):
@@ -1208,20 +1048,11 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None)
     stats: the backward sums already accumulated by the producing GEMM (take_bn_bwd_fused)."""
     C = y.shape[-1]
     rsc, rsh = (ptr(st.scale), ptr(st.shift)) if (relu and mask is None) else (0, 0)
-    coef = None
     if stats is None:
         stats = bn_stats(bn, "bwd")
-        fin = fin_backward(bn, st, C, grad_alpha(y))
-        if fin is not None:
-            # the reduce's last workgroup finalizes (scd_bn_bwd_reduce_fin): dgamma / dbeta and the coefficients
-            L.call("scd_bn_bwd_reduce_fin", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean),
-                   ptr(st.invstd), C, y.numel(), ptr(stats), fin[0], stream())
-            coef = fin[1]
-        else:
-            L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd),
-                   C, y.numel(), ptr(stats), stream())
-    if coef is None:
-        coef = bn_backward_coef(bn, st, stats, C, grad_alpha(y))
+        L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd),
+               C, y.numel(), ptr(stats), stream())
+    coef = bn_backward_coef(bn, st, stats, C, grad_alpha(y))
     dy = torch.empty_like(y)
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),
            ptr(dz_out), stream())
@@ -1242,20 +1073,11 @@ def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
     C = y_a.shape[-1]
     sa, sb = bn_stats(bn_a, "bwd"), bn_stats(bn_b, "bwd")
     alpha = grad_alpha(y_a)
-    fa = fin_backward(bn_a, st_a, C, alpha)
-    fb = fin_backward(bn_b, st_b, C, alpha) if fa is not None else None
-    if fa is not None and fb is not None:
-        # both finalizes by the reduce's last workgroup (scd_bn_bwd_reduce2_fin)
-        L.call("scd_bn_bwd_reduce2_fin", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean),
-               ptr(st_a.invstd), ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), fa[0], fb[0],
-               stream())
-        ca, cb = fa[1], fb[1]
-    else:
-        L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean),
-               ptr(st_a.invstd), ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
-        sa, sb, nrep = _allreduce_stats_pair(sa, C, sb, C)
-        ca = _bn_bwd_finalize_launch(bn_a, st_a, sa, nrep, C, alpha)
-        cb = _bn_bwd_finalize_launch(bn_b, st_b, sb, nrep, C, alpha)
+    L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean),
+           ptr(st_a.invstd), ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
+    sa, sb, nrep = _allreduce_stats_pair(sa, C, sb, C)
+    ca = _bn_bwd_finalize_launch(bn_a, st_a, sa, nrep, C, alpha)
+    cb = _bn_bwd_finalize_launch(bn_b, st_b, sb, nrep, C, alpha)
     dya, dyb = torch.empty_like(y_a), torch.empty_like(y_b)
     L.call("scd_bn_bwd_apply2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(ca), ptr(cb), C, y_a.numel(),
            ptr(dya), ptr(dyb), stream())
@@ -1303,48 +1125,20 @@ def stem_direct_ok(x, dtype):
     return dtype in HALF and Wo % 128 == 0 and Ho % 2 == 0
 
 
-def stem_conv_fwd(x, wpk, stats=None, fin=None, store=True):
-    """Conv2d(1,64,7,s2,p3) of NCHW fp32 x -> (N,Ho,Wo,64) bf16 NHWC (+BN sums); wpk = pack_weight(w, bf16, 0, ldp=64).
-    fin: FinForward of the stem BN (its finalize by the conv's last workgroup).  store=False: the BN sums only (the
-    first pass of the pooled forward, stem_conv_pool_fwd); returns None."""
+def stem_conv_fwd(x, wpk, stats=None):
+    """Conv2d(1,64,7,s2,p3) of NCHW fp32 x -> (N,Ho,Wo,64) bf16 NHWC (+BN sums); wpk = pack_weight(w, bf16, 0, ldp=64)."""
     _need_gpu(x)
     N, _, H, W = x.shape
     Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    y = torch.empty(N, Ho, Wo, 64, dtype=wpk.dtype, device=x.device) if store else None
-    if fin is not None:
-        L.call("scd_stem_conv_fwd_fin", dt(wpk), ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo,
-               fin.ptr(N * Ho * Wo), stream())
-        return y
+    y = torch.empty(N, Ho, Wo, 64, dtype=wpk.dtype, device=x.device)
     L.call("scd_stem_conv_fwd", dt(wpk), ptr(x), ptr(wpk), ptr(y), ptr(stats), N, H, W, Ho, Wo, stream())
     return y
-
-
-def stem_conv_pool_fwd(x, wpk, st):
-    """The stem's conv recomputed + BN (st) + ReLU + MaxPool(3,2,1) (scd_stem_conv_pool_fwd): (out, argmax, ymax), all
-    (N, Ho/2, Wo/2, 64); the full-resolution conv output is never materialised."""
-    _need_gpu(x)
-    N, _, H, W = x.shape
-    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    Hp, Wp = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
-    out = torch.empty(N, Hp, Wp, 64, dtype=wpk.dtype, device=x.device)
-    am = torch.empty(N, Hp, Wp, 64, dtype=torch.uint8, device=x.device)
-    ym = torch.empty(N, Hp, Wp, 64, dtype=wpk.dtype, device=x.device)
-    L.call("scd_stem_conv_pool_fwd", dt(wpk), ptr(x), ptr(wpk), ptr(st.scale), ptr(st.shift), ptr(out), ptr(am),
-           ptr(ym), N, H, W, stream())
-    return out, am, ym
 
 
 def stem_out_count(x):
     """Pixels of the stem conv output per channel (the BN count)."""
     H, W = x.shape[2], x.shape[3]
     return x.shape[0] * ((H + 6 - 7) // 2 + 1) * ((W + 6 - 7) // 2 + 1)
-
-
-def stem_pool_ok(x, dtype):
-    """The pooled forward's shapes: 16-bit, conv output width a multiple of 128 and even height (scd_stem_conv_pool_fwd)."""
-    H, W = x.shape[2], x.shape[3]
-    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    return dtype in HALF and Wo % 128 == 0 and Ho % 2 == 0 and Ho >= 2
 
 
 def stem_conv_wgrad(dy, x, dst, accumulate=True, ybn=None, coef=None):
@@ -1382,11 +1176,10 @@ def stem_pool_bwd_bn(bn, dout, am, y, st):
     return dz, bn_backward_coef(bn, st, stats, C, grad_alpha(y))
 
 
-def stem_backward_fused(bn, dout, am, y, st, x, wpk, dst, pooled=False):
+def stem_backward_fused(bn, dout, am, y, st, x, wpk, dst):
     """The stem's MaxPool / ReLU / BN / conv weight-gradient backward in one pass (scd_stem_bwd_fused): the BN
     backward sums (dgamma / dbeta accumulated, SyncBN all-reduce as bn_backward_coef) and dst (64,1,7,7) += the weight
-    gradient a*T1 + b*W G + c*s; the full-resolution dz is never materialised.  pooled: y is ymax of
-    stem_conv_pool_fwd (pooled layout, scd_stem_bwd_fused_pooled)."""
+    gradient a*T1 + b*W G + c*s; the full-resolution dz is never materialised."""
     N, C = y.shape[0], y.shape[3]
     H, W = x.shape[2], x.shape[3]
     Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
@@ -1394,7 +1187,7 @@ def stem_backward_fused(bn, dout, am, y, st, x, wpk, dst, pooled=False):
     ws = torch.empty(ns * 2 * 64 * 64, dtype=torch.float32, device=y.device)
     tg = torch.empty(2 * 64 * 64, dtype=torch.float32, device=y.device)
     stats = bn_stats(bn, "bwd")
-    L.call("scd_stem_bwd_fused_pooled" if pooled else "scd_stem_bwd_fused", dt(y), ptr(dout), ptr(am), ptr(y),
+    L.call("scd_stem_bwd_fused", dt(y), ptr(dout), ptr(am), ptr(y),
            ptr(st.scale), ptr(st.shift), ptr(st.mean), ptr(st.invstd), ptr(x), ptr(stats), ptr(ws), ns, ptr(tg), N, H,
            W, Ho, Wo, stream())
     alpha = grad_alpha(y)
@@ -1439,7 +1232,11 @@ def adam_step_dev(p, g, m, v, hyper, beta1, beta2, eps, gscale=1.0):
 
 
 def sgd_step_dev(p, g, buf, hyper, momentum, dampening, weight_decay, nesterov, gscale=1.0):
-    """torch.optim.SGD step over the flat buffer (networkFactory.py:84-89); hyper = {lr, step} fp64 on the device."""
+    """torch.optim.SGD step over the flat buffer (networkFactory.py:84-89); hyper = {lr, step, initialised, snapshot}
+    fp64 on the device (scd_sgd_step_dev reads and writes all four)."""
+    if hyper.dtype != torch.float64 or hyper.numel() < 4 or not hyper.is_contiguous():
+        raise RuntimeError("sgd_step_dev: hyper must be a contiguous fp64 tensor of at least 4 elements "
+                           "{lr, step, initialised, snapshot}")
     _need_gpu(p)
     L.call("scd_sgd_step_dev", ptr(p), ptr(g), ptr(buf) if buf is not None else None, p.numel(), ptr(hyper),
            float(momentum), float(dampening), float(weight_decay), int(bool(nesterov)), float(gscale), stream())

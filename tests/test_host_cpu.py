@@ -43,29 +43,6 @@ def test_gemm_phase_struct_matches_header():
     assert ctypes.sizeof(L.GemmPhase) == 4 * (5 + 3 * L.MAX_TAPS)
 
 
-def test_bn_fin_struct_matches_header(tmp_path):
-    """ctypes scd_bn_fin (scdhip.lib.BnFin) has the C layout of include/scdhip.h: field offsets and size from a C
-    program compiled against the header with gcc."""
-    import ctypes
-    import subprocess
-
-    import scdhip.lib as L
-    names = [f[0] for f in L.BnFin._fields_]
-    src = tmp_path / "fin.c"
-    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "scdhip.h"\nint main(void){printf("%zu",'
-                   ' sizeof(scd_bn_fin));' + "".join('printf(" %%zu", offsetof(scd_bn_fin, %s));' % n for n in names)
-                   + "return 0;}\n")
-    exe = tmp_path / "fin"
-    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
-    vals = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
-    assert vals[0] == ctypes.sizeof(L.BnFin)
-    assert vals[1:] == [getattr(L.BnFin, n).offset for n in names]
-    m = re.search(r"#define SCD_FIN_REPLICAS (\d+)", open(HEADER).read())
-    assert int(m.group(1)) == L.FIN_REPLICAS
-    m = re.search(r"#define SCD_FIN_SHARDS (\d+)", open(HEADER).read())
-    assert int(m.group(1)) + 1 == L.FIN_COUNTERS
-
-
 def test_workspace_queries():
     import scdhip.lib as L
     assert L.lib().scd_conv_wgrad_workspace(128, 9, 64, 4) == 4 * 128 * 9 * 64 * 4
@@ -289,3 +266,14 @@ def test_mean_backward_matches_mean_then_backward():
         m2.backward()
         assert m1.shape == m2.shape == ()
         assert torch.equal(m1.detach(), m2.detach()) and torch.equal(w1.grad, w2.grad)
+
+
+def test_sgd_step_dev_checks_hyper():
+    """scd_sgd_step_dev reads and writes hyper[0..3]: a shorter or non-fp64 hyper is refused on the host before any
+    launch (ADVICE r4 ops.py:1441)."""
+    import torch
+    from scdhip import ops
+    p = torch.zeros(8)
+    for hyper in (torch.zeros(2, dtype=torch.float64), torch.zeros(4, dtype=torch.float32)):
+        with pytest.raises(RuntimeError, match="hyper"):
+            ops.sgd_step_dev(p, p, p, hyper, 0.9, 0.0, 0.0, False)

@@ -113,9 +113,9 @@ def _loop_span(lines):
 # until round 4 (63 per stem tile, 8 per BN vector) -- a runtime condition around an LDS read or a per-element pointer
 # test turns into them silently
 BRANCH_CEILING = {
-    ("stem.hip", r"stem_bwd_fused_kernelILb0E"): 4,
+    ("stem.hip", r"stem_bwd_fused_kernel"): 4,
     ("bn.hip", r"bn_bwd_apply_kernelIDF16bE"): 4,
-    ("bn.hip", r"bn_bwd_reduce_kernelIDF16bLb0E"): 4,
+    ("bn.hip", r"bn_bwd_reduce_kernelIDF16bE"): 4,
 }
 
 

@@ -432,56 +432,6 @@ def test_stem_one_pass_backward(shape, dtype):
     assert rel_err(dwa, ref) < 2e-2
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("shape", [(2, 512, 512), (3, 260, 256)])
-def test_stem_pooled_forward_matches_two_kernels(shape, dtype):
-    """The pooled stem forward (scd_stem_conv_fwd with y = NULL for the statistics, then scd_stem_conv_pool_fwd: the conv
-    recomputed with BN + ReLU + MaxPool on the tile) against conv -> y -> scd_stem_pool_fwd: the same statistics (fp64
-    atomics: up to their summation order), the same out and argmax bits, ymax = y at every argmax, and the backward
-    from ymax (scd_stem_bwd_fused_pooled) equal to the backward from y up to the fp64 summation order of its sums."""
-    from scdhip import ops
-    N, H, W = shape
-    g = torch.Generator().manual_seed(23)
-    x = torch.randn(N, 1, H, W, generator=g).to(DEV)
-    w = (torch.randn(64, 1, 7, 7, generator=g) / 7.0).to(DEV)
-    assert ops.stem_pool_ok(x, dtype)
-    bns = [torch.nn.BatchNorm2d(64).to(DEV) for _ in range(2)]
-    with torch.no_grad():
-        bns[0].weight.uniform_(0.5, 1.5)
-        bns[0].bias.normal_()
-    bns[1].load_state_dict(bns[0].state_dict())
-    wpk = ops.pack_weight(w, dtype, 0, ldp=64)
-    stats = ops.new_stats(64, DEV)
-    y = ops.stem_conv_fwd(x, wpk, stats=stats)
-    stats2 = ops.new_stats(64, DEV)
-    assert ops.stem_conv_fwd(x, wpk, stats=stats2, store=False) is None
-    s1, s2 = stats.view(-1, 2, 64).sum(0), stats2.view(-1, 2, 64).sum(0)
-    assert ((s2 - s1).abs().max() / s1.abs().max()).item() < 1e-12
-    st = ops.bn_finalize(bns[0], stats, 64, y.numel() // 64)
-    out, am = ops.stem_pool_fwd(y, st)
-    out2, am2, ym = ops.stem_conv_pool_fwd(x, wpk, st)
-    torch.cuda.synchronize()
-    assert torch.equal(out2, out) and torch.equal(am2, am)
-    # ymax = y at the argmax (window index d: conv row 2 po - 1 + d // 3, column 2 pq - 1 + d % 3)
-    Hp, Wp = out.shape[1], out.shape[2]
-    d = am.long()
-    po = torch.arange(Hp, device=DEV).view(1, Hp, 1, 1)
-    pq = torch.arange(Wp, device=DEV).view(1, 1, Wp, 1)
-    r = (2 * po - 1 + d // 3).clamp(0, y.shape[1] - 1)
-    c = (2 * pq - 1 + d % 3).clamp(0, y.shape[2] - 1)
-    n = torch.arange(N, device=DEV).view(N, 1, 1, 1).expand_as(d)
-    ch = torch.arange(64, device=DEV).view(1, 1, 1, 64).expand_as(d)
-    assert torch.equal(ym, y[n, r, c, ch])
-    dout = torch.randn(out.shape, generator=g).to(DEV, dtype)
-    dwa = torch.full_like(w, 0.5)
-    dwb = torch.full_like(w, 0.5)
-    ops.stem_backward_fused(bns[0], dout, am, y, st, x, wpk, dwa)
-    ops.stem_backward_fused(bns[1], dout, am, ym, st, x, wpk, dwb, pooled=True)
-    torch.cuda.synchronize()
-    for a, b in ((bns[0].weight.grad, bns[1].weight.grad), (bns[0].bias.grad, bns[1].bias.grad), (dwa, dwb)):
-        assert rel_err(b, a) < 1e-6
-
-
 def test_cpool_fwd_bwd_fp32():
     from scdhip import ops
     g = torch.Generator().manual_seed(5)
@@ -601,6 +551,36 @@ def test_flat_sgd_buffer_reset_matches_torch():
     with pytest.raises(ValueError):
         FlatSGD(pd, lr=1e-3).load_state_dict({"step": 1, "param_groups": [{"lr": 1e-3}],
                                               "momentum_buffer": torch.zeros(64 * 27 + 1000)})
+
+
+def test_flat_sgd_state_before_first_step_matches_torch():
+    """A FlatSGD state saved before any step (the flat buffer and its zero momentum buffer exist from zero_grad on)
+    carries no momentum_buffer, as torch's does, so a run resumed from it clones d on its first update also with
+    dampening != 0 (ADVICE r4 flat.py:227)."""
+    from scdhip.flat import FlatSGD
+    g = torch.Generator().manual_seed(17)
+    p0 = [torch.randn(64, 3, 3, 3, generator=g), torch.randn(1000, generator=g)]
+    pt = [x.clone().requires_grad_(True) for x in p0]
+    kw = dict(lr=2.5e-4, momentum=0.9, weight_decay=1e-4, dampening=0.25)
+    opt_t = torch.optim.SGD(pt, **kw)
+    pd = [torch.nn.Parameter(x.clone().to(DEV)) for x in p0]
+    opt = FlatSGD(pd, **kw)
+    opt.zero_grad()
+    sd = opt.state_dict()
+    assert sd["momentum_buffer"] is None and "momentum_buffer" not in opt_t.state_dict()["state"].get(0, {})
+    opt = FlatSGD(pd, **kw)
+    opt.load_state_dict(sd)
+    for _ in range(3):
+        opt.zero_grad()
+        for a, b in zip(pt, pd):
+            gr = torch.randn(a.shape, generator=g)
+            a.grad = gr.clone()
+            b.grad.copy_(gr.to(DEV))
+        opt_t.step()
+        opt.step()
+    assert opt.state_dict()["momentum_buffer"] is not None
+    for a, b in zip(pt, pd):
+        np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().numpy(), rtol=1e-6, atol=1e-7)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -342,52 +342,3 @@ def test_block_bn_backward_sums_from_dgrad_match_separate_reduce(name):
         a, b = grads[0][k], grads[1][k]
         tol = 1e-2 if k.startswith(("heatmap", "offset", "regr", "deconvolutionLayers")) else deep
         assert (a - b).abs().max().item() <= tol * max(1e-6, b.abs().max().item()), k
-
-
-@pytest.mark.parametrize("name,dtype", [("centerOffsetRes10", torch.float32), ("centerOffsetRes10", torch.bfloat16),
-                                        ("centerOffsetRes50", torch.float32)])
-def test_fused_bn_finalize_matches_separate(name, dtype):
-    """BN finalize by the last workgroup of its statistics producer (ops.BNFinalize: the _fin entry points, a
-    device-memory scd_bn_fin descriptor; opt-in, SCD_BN_FIN_FUSE=1) against the separate finalize kernels: three
-    training steps (descriptors written once, counters reset by the kernels) give the same losses, running
-    statistics and gradients up to the replicas' fp64 summation order; plus a pass with two forwards before their
-    backward (the second forward finds the module's buffers held and takes the separate finalize)."""
-    from scdhip import ops
-    from scdhip.flat import FlatAdam
-    S = 128 if name.endswith("50") else 256
-    x = T.batch_inputs(51, 2, S).to(DEV)
-    x2 = T.batch_inputs(52, 2, S).to(DEV)
-    ys = [y.to(DEV) for y in T.batch_targets(53, 2, S // 4)]
-    res = {}
-    was = ops.BNFinalize.enabled
-    for fuse in (False, True):
-        ops.BNFinalize.enabled = fuse
-        try:
-            m, plugin, _, _ = make_model(dtype, name)
-            opt = FlatAdam(filter(lambda p: p.requires_grad, m.parameters()))
-            losses = []
-            for _ in range(3):
-                opt.zero_grad()
-                loss, _ = plugin.loss(m(x, decode=False), ys)
-                loss.mean().backward()
-                opt.step()
-                losses.append(loss.item())
-            opt.zero_grad()
-            la, _ = plugin.loss(m(x, decode=False), ys)
-            lb, _ = plugin.loss(m(x2, decode=False), ys)
-            (la.mean() + lb.mean()).backward()
-            torch.cuda.synchronize()
-            res[fuse] = (losses + [la.item(), lb.item()],
-                         {k: p.grad.detach().double().cpu().clone() for k, p in m.named_parameters()},
-                         {k: v.detach().double().cpu().clone() for k, v in m.state_dict().items()
-                          if "running" in k})
-        finally:
-            ops.BNFinalize.enabled = was
-    tol = 1e-5 if dtype == torch.float32 else 5e-2
-    np.testing.assert_allclose(res[True][0], res[False][0], rtol=tol)
-    worst = max(((a - res[False][1][k]).norm() / max(res[False][1][k].norm(), 1e-12)).item()
-                for k, a in res[True][1].items())
-    print(name, dtype, "worst normwise gradient difference fused vs separate finalize %.2e" % worst)
-    assert worst < (1e-4 if dtype == torch.float32 else 1e-1), worst
-    for k, a in res[True][2].items():
-        np.testing.assert_allclose(a.numpy(), res[False][2][k].numpy(), rtol=tol, atol=1e-6, err_msg=k)

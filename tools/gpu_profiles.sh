@@ -1,11 +1,11 @@
-# Usage: bash tools/gpu_r3_profiles.sh [tag] -- the round's measurement set, written to gpurun_out/<tag>_*:
+# Usage: bash tools/gpu_profiles.sh [tag] -- the round's measurement set, written to gpurun_out/<tag>_*:
 #  PMC HBM bytes (FETCH_SIZE / WRITE_SIZE passes) of the configs[3]/[4] dominant kernels (tools/pmc_kernels.py) and of
 #  the Res10 bench command; then the bench lines (Res10 with the CPU baseline, Res50 1024^2 fp16, cornerNetCPool),
 #  which read those PMC summaries, and rocprofv3 kernel traces of each bench command.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T=${1:-r3}
+T=${1:-r5}
 O=gpurun_out
 mkdir -p $O
 pmc() {   # pmc <name> <counter> <cmd...>

@@ -1,10 +1,10 @@
-# Usage: bash tools/gpu_r4_final.sh [tag] -- the round's GPU suite, then the Res10 bench line and its rocprofv3 trace
-# (kernel summary, step timeline, rocprofv3 --stats), into gpurun_out/<tag>_*; PMC passes and the other configs:
-# tools/gpu_r3_profiles.sh <tag> (pmc + configs) run separately
+# Usage: bash tools/gpu_suite.sh [tag] -- the GPU suite, then the Res10 bench line and its rocprofv3 trace (kernel
+# summary, step timeline, rocprofv3 --stats) and the host issue cost, into gpurun_out/<tag>_*; PMC passes and the
+# other configs: tools/gpu_profiles.sh <tag>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T=${1:-r4}
+T=${1:-r5}
 O=gpurun_out
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -q --timeout 150 --timeout-method thread -m gpu -rf tests > $O/${T}_tests.log 2>&1
