@@ -300,7 +300,9 @@ def main():
     opt = FlatAdam(filter(lambda p: p.requires_grad, model.parameters()))
     if world > 1:
         if torch.cuda.device_count() > 1 or share:
-            ops.set_bn_sync(ops.syncbn_group())   # SyncBN rule of networkFactory.py:128 (WORLD unless opted out)
+            # SyncBN rule of networkFactory.py:128: peer-memory statistics when every rank maps its peers (buckets
+            # then overlap the backward), else RCCL (ops.setup_syncbn)
+            ops.setup_syncbn(log=(lambda m: print("bench: " + m, file=sys.stderr, flush=True)) if rank == 0 else None)
         model = FlatDDP(model)
     lossfn = plugin.loss
 
@@ -457,10 +459,10 @@ def main():
             shared = ops.bn_sync_shares_group(model.group)
             line["exchange"] = {"ddp_ms_per_step": line["ms_per_step"], "local_ms_per_step": round(local_ms, 3),
                                 "local_over_ddp": round(local_ms / line["ms_per_step"], 4),
-                                "syncbn": "peer memory" if ops.bn_sync_peer() is not None else
-                                ("WORLD (shared with the buckets)" if shared else "own communicator")
-                                if ops.bn_sync_group() is not None else "off",
-                                "buckets_overlap_backward": bool(model.overlap_buckets())}
+                                "syncbn": ops.bn_sync_mode(), "syncbn_shares_bucket_group": bool(shared),
+                                "peer_fallback_reason": ops._BNSync.why,
+                                "buckets_overlap_backward": bool(model.overlap_buckets()),
+                                "early_bucket_launches": int(model.early_launches)}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_baseline_steps)
         print(json.dumps(line), flush=True)

@@ -396,7 +396,8 @@ int scd_sgd_step_dev(float* p, const float* g, float* buf, long n, double* hyper
 /* ---- corner pooling (cornerPooling/source/{top,bottom,left,right}Pool.cpp) ----
  * dir: 0 top (max over k>=h), 1 bottom (k<=h), 2 left (k>=w), 3 right (k<=w); NHWC dtype.
  * Backward routes grad to the running argmax, ties keep the first-scanned index
- * (strict '>' update, topPool.cpp:61-65). */
+ * (strict '>' update, topPool.cpp:61-65), each run summed in scan order as the reference's scatter_add loop
+ * (topPool.cpp:56-70): fp32 results are bit-identical to the reference backward's. */
 int scd_cpool_fwd(int dtype, int dir, const void* x, const void* addend, void* y, int N, int H, int W, int C,
                   void* stream);                     /* y = pool(x) (+ addend, nullable: the CornerPool branch sum) */
 int scd_cpool_bwd(int dtype, int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C,

@@ -3,9 +3,9 @@
 // backward per pool; here one launch per direction: each thread owns a (n, line, channel-chunk)
 // and scans the line in registers (coalesced across channels, 8 positions of loads in flight).
 // Backward routes each dy to the running argmax of the same scan; ties keep the first-scanned
-// position (strict '>' update, topPool.cpp:61-65); every position is written exactly once, as a
-// 16-byte vector (no memset, deterministic).  HBM-bound: fwd reads x (+ the addend) and writes y,
-// bwd reads x and dy and writes dx.
+// position (strict '>' update, topPool.cpp:61-65); runs are summed in the reference's scan order
+// (no memset, deterministic, fp32 bit-identical to the reference).  HBM-bound: fwd reads x (+ the
+// addend) and writes y, bwd reads x and dy and writes dx.
 #include "scd_common.h"
 
 namespace {
@@ -116,90 +116,73 @@ __global__ __launch_bounds__(256) void cpool_fwd_kernel(int dir, const T* __rest
     }
 }
 
-// Backward in two register scans per line, every dx position written once as a 16-B vector:
-//  1. forward over x: position k is a record of element e iff k == 0 or x[k][e] > the running max (strict:
-//     ties keep the first-scanned position, topPool.cpp:61-65); one byte of record bits per position goes to
-//     this thread's column of an LDS table [L/8][256 threads] of 8-byte words;
-//  2. reverse over dy: acc += dy[k]; a record takes dx[k] = acc and restarts acc, any other position gets 0.
-//     A record's dx is then the sum of dy over its run up to the next record -- the positions whose running
-//     argmax it is (the reference's scatter_add, summed in the reverse order).
+// Backward in ONE forward register scan per line (x and dy read once, dx written once): position k is a record of
+// element e iff k == 0 or x[k][e] > the running max (strict: ties keep the first-scanned position,
+// topPool.cpp:61-65), and dy[k] joins the run of element e's current record.  The run is summed in scan order,
+// acc = dy[r], then acc += dy[r+1], ... -- the order of the reference's scatter_add loop (topPool.cpp:56-70:
+// output[argmax] += grad[k] for k along the scan), so dx is bit-identical to the reference's in fp32.  Every position
+// is written once as a 16-B vector of zeros when it is scanned; a closed run's sum goes to its record position as one
+// element store when the element's next record is reached (and for every element at the end of the line): records
+// are few (~ln L per element on random data), and the element store follows the zero vector at that position in
+// this thread's program order.
 template <typename T, int U>
 __global__ __launch_bounds__(256) void cpool_bwd_kernel(int dir, const T* __restrict__ x, const T* __restrict__ dy,
                                                         T* __restrict__ dx, int N, int H, int W, int C, long lines) {
-    static_assert(U == 8, "one 8-byte flag word per 8 positions");
     constexpr int E = Vec16<T>::N;
-    extern __shared__ uint2 flags[];
     const long i = blockIdx.x * 256L + threadIdx.x;
     if (i >= lines) return;
     const Line ln = line_of(dir, i, N, H, W, C, E);
     const int L = ln.L;
-    uint4 cx[U];
+    uint4 cx[U], cg[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) cx[u] = *(const uint4*)(x + ln.start + (long)min(u, L - 1) * ln.sstep);
-    float mv[E];
+    for (int u = 0; u < U; ++u) {
+        const long off = ln.start + (long)min(u, L - 1) * ln.sstep;
+        cx[u] = *(const uint4*)(x + off);
+        cg[u] = *(const uint4*)(dy + off);
+    }
+    float mv[E], acc[E], zero[E];
+    int rk[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { mv[e] = 0.f; acc[e] = 0.f; rk[e] = 0; zero[e] = 0.f; }
     for (int k0 = 0; k0 < L; k0 += U) {
-        uint4 nx[U];
+        uint4 nx[U], ng[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) nx[u] = *(const uint4*)(x + ln.start + (long)min(k0 + U + u, L - 1) * ln.sstep);
-        unsigned fb[U];
+        for (int u = 0; u < U; ++u) {          // prefetch the next U positions (clamped: always a valid address)
+            const long off = ln.start + (long)min(k0 + U + u, L - 1) * ln.sstep;
+            nx[u] = *(const uint4*)(x + off);
+            ng[u] = *(const uint4*)(dy + off);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int k = k0 + u;
-            float v[E];
+            if (k >= L) break;
+            float v[E], g[E];
             Vec16<T>::load(&cx[u], v);
-            unsigned b = 0;
+            Vec16<T>::load(&cg[u], g);
+            Vec16<T>::store(dx + ln.start + (long)k * ln.sstep, zero);
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 const bool rec = (k == 0) || (v[e] > mv[e]);
-                if (rec) mv[e] = v[e];
-                b |= (rec ? 1u : 0u) << e;
+                if (rec) {
+                    if (k > 0) dx[ln.start + (long)rk[e] * ln.sstep + e] = from_f<T>(acc[e]);
+                    mv[e] = v[e];
+                    acc[e] = g[e];
+                    rk[e] = k;
+                } else {
+                    acc[e] += g[e];
+                }
             }
-            fb[u] = k < L ? b : 0u;
-        }
-        flags[(k0 / U) * 256 + threadIdx.x] =
-            make_uint2(fb[0] | fb[1] << 8 | fb[2] << 16 | fb[3] << 24, fb[4] | fb[5] << 8 | fb[6] << 16 | fb[7] << 24);
-#pragma unroll
-        for (int u = 0; u < U; ++u) cx[u] = nx[u];
-    }
-    // pass 2: chunks in reverse scan order, positions inside a chunk from the last down
-    const int nch = (L + U - 1) / U;
-    uint4 cg[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) cg[u] = *(const uint4*)(dy + ln.start + (long)min((nch - 1) * U + u, L - 1) * ln.sstep);
-    float acc[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) acc[e] = 0.f;
-    for (int c = nch - 1; c >= 0; --c) {
-        uint4 ng[U];
-        const int cn = c > 0 ? c - 1 : 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) ng[u] = *(const uint4*)(dy + ln.start + (long)min(cn * U + u, L - 1) * ln.sstep);
-        const uint2 fw = flags[c * 256 + threadIdx.x];
-#pragma unroll
-        for (int u = U - 1; u >= 0; --u) {
-            const int k = c * U + u;
-            if (k >= L) continue;
-            const unsigned b = ((u < 4 ? fw.x : fw.y) >> (8 * (u & 3))) & 0xffu;
-            float g[E], o[E];
-            Vec16<T>::load(&cg[u], g);
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                acc[e] += g[e];
-                const bool rec = (b >> e) & 1u;
-                o[e] = rec ? acc[e] : 0.f;
-                if (rec) acc[e] = 0.f;
-            }
-            Vec16<T>::store(dx + ln.start + (long)k * ln.sstep, o);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) cg[u] = ng[u];
+        for (int u = 0; u < U; ++u) { cx[u] = nx[u]; cg[u] = ng[u]; }
     }
+#pragma unroll
+    for (int e = 0; e < E; ++e) dx[ln.start + (long)rk[e] * ln.sstep + e] = from_f<T>(acc[e]);
 }
 
 #ifndef CPOOL_FWD_VB
 #define CPOOL_FWD_VB 16
 #endif
-constexpr int CPOOL_MAX_L = 640;      // LDS record table: L/8 words of 8 B per thread, 256 threads (<= 160 KiB)
 
 template <typename T>
 int launch_fwd(int dir, const void* x, const void* addend, void* y, int N, int H, int W, int C, hipStream_t st) {
@@ -220,11 +203,8 @@ template <typename T>
 int launch_bwd(int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C, hipStream_t st) {
     const long lines = (long)N * (dir < 2 ? W : H) * (C / Vec16<T>::N);
     if (lines == 0) return 0;
-    const int L = dir < 2 ? H : W;
-    if (L > CPOOL_MAX_L) return SCD_ERR_ARG;
     const int grid = (int)((lines + 255) / 256);
-    const size_t lds = (size_t)((L + 7) / 8) * 256 * 8;
-    hipLaunchKernelGGL((cpool_bwd_kernel<T, 8>), dim3(grid), dim3(256), lds, st, dir, (const T*)x, (const T*)dy,
+    hipLaunchKernelGGL((cpool_bwd_kernel<T, 8>), dim3(grid), dim3(256), 0, st, dir, (const T*)x, (const T*)dy,
                        (T*)dx, N, H, W, C, lines);
     SCD_RETURN_LAUNCH();
 }

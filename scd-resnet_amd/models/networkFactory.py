@@ -160,9 +160,9 @@ class NetworkFactory(object):
         torch.cuda.set_stream(torch.cuda.Stream(device=self.device, priority=-10))
         self.cuda()
         if distributed and self.GPUCOUNT > 1 and dist.get_world_size() > 1:
-            # SyncBatchNorm semantics (networkFactory.py:128-133) on WORLD beside FlatDDP (ops.syncbn_group;
-            # SCD_SYNCBN_OWN_GROUP=1 gives them a communicator of their own)
-            ops.set_bn_sync(ops.syncbn_group())
+            # SyncBatchNorm semantics (networkFactory.py:128-133): over peer memory when every rank maps its peers, so
+            # FlatDDP's buckets overlap the backward; else through RCCL (ops.setup_syncbn logs which and why)
+            ops.setup_syncbn(log=Logger.info if dist.get_rank() == 0 else None)
         self.model = FlatDDP(self.model)
         if defaultConfig.stepGraph and not (distributed and dist.get_world_size() > 1):
             self.stepGraph = StepGraph(self._trainStep, optimizer=self.optimizer, warmup=2)

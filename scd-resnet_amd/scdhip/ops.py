@@ -181,6 +181,7 @@ class _BNSync:
     group = None          # torch.distributed group for SyncBatchNorm semantics (None = local BN)
     world = 1
     peer = None           # scdhip.peer.PeerAllReduce when the peer-memory path is on
+    why = None            # setup_syncbn: why the peer-memory path is not in use (None when it is, or not tried)
 
 
 def new_bn_group():
@@ -232,6 +233,61 @@ def set_bn_sync(group, peer=None):
     if group is not None and peer and _BNSync.world > 1:
         from .peer import PeerAllReduce
         _BNSync.peer = PeerAllReduce(group)
+
+
+def setup_syncbn(log=None):
+    """SyncBatchNorm for a data-parallel run at world > 1 (networkFactory.py:128-133), with the transport chosen so
+    that FlatDDP's gradient buckets overlap the backward (networkFactory.py:126-136; BASELINE north_star: the
+    all-reduce "overlapped with backward"):
+
+    * default: the statistics over peer memory when every rank can map every peer's mailbox -- checked collectively,
+      with a probe all-reduce (scdhip.peer.PeerAllReduce.try_create) -- so SyncBN issues no collective at all and
+      FlatDDP launches each bucket on WORLD from inside the backward as soon as its gradients are written;
+    * else (a rank cannot map its peers, no GPU, or SCD_SYNCBN_PEER=0): through torch.distributed on
+      ops.syncbn_group() -- WORLD, where RCCL serialises them with the buckets on one communicator, so every bucket
+      goes at the end of the backward (FlatDDP.overlap_buckets) -- or a communicator of their own with
+      SCD_SYNCBN_OWN_GROUP=1.  SCD_SYNCBN_PEER=1 requires the peer path (raises if it cannot be set up).
+
+    Collective: every rank calls it once, before FlatDDP is built.  Returns bn_sync_mode(); `log` (a callable) gets
+    one line saying which transport runs and, for a fallback, why."""
+    want = os.environ.get("SCD_SYNCBN_PEER", "auto").lower()
+    if _BNSync.peer is not None:
+        _BNSync.peer.close()
+        _BNSync.peer = None
+    _BNSync.why = None
+    if want not in ("0", "off") and torch.cuda.is_available() and dist.get_world_size() > 1:
+        from .peer import PeerAllReduce
+        peer, why = PeerAllReduce.try_create(dist.group.WORLD)
+        if peer is None and want == "1":
+            raise RuntimeError("SCD_SYNCBN_PEER=1: the peer-memory SyncBN path could not be set up: %s" % why)
+        if peer is not None:
+            _BNSync.group, _BNSync.world, _BNSync.peer = dist.group.WORLD, dist.get_world_size(), peer
+        else:
+            _BNSync.why = why
+    elif want in ("0", "off"):
+        _BNSync.why = "SCD_SYNCBN_PEER=0"
+    else:
+        _BNSync.why = "no GPU" if not torch.cuda.is_available() else "world 1"
+    if _BNSync.peer is None:
+        set_bn_sync(syncbn_group(), peer=False)
+        _BNSync.why = _BNSync.why or "fallback"
+    mode = bn_sync_mode()
+    if log is not None:
+        log("SyncBN statistics: %s%s; gradient buckets %s" % (
+            mode, "" if _BNSync.peer is not None else " (peer memory not used: %s)" % _BNSync.why,
+            "all-reduced on WORLD from inside the backward" if mode != "rccl-world" else
+            "all-reduced at the end of the backward (SyncBN shares their RCCL communicator)"))
+    return mode
+
+
+def bn_sync_mode():
+    """'peer' (peer-memory kernels), 'rccl-world' (torch.distributed on WORLD, beside the gradient buckets),
+    'rccl-own' (a communicator of their own) or 'off' (local BN)."""
+    if _BNSync.group is None:
+        return "off"
+    if _BNSync.peer is not None:
+        return "peer"
+    return "rccl-world" if _BNSync.group is dist.group.WORLD else "rccl-own"
 
 
 def bn_sync_peer():

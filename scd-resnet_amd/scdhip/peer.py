@@ -3,8 +3,10 @@
 Every BN layer of a multi-GPU step all-reduces 2C fp64 sums twice (forward statistics, backward sums), each a small
 message on the critical path.  PeerAllReduce maps every rank's fine-grained mailbox into every process (hipIpc
 handles exchanged once through torch.distributed) and reduces with one kernel per call: write into every mailbox,
-flag, wait, sum in rank order.  Opt-in (ops.set_bn_sync(group, peer=True) or SCD_SYNCBN_PEER=1); RCCL stays the
-default until an 8-GPU run has compared them.  Single node, <= 8 ranks, eager steps (the epoch is a host counter).
+flag, wait, sum in rank order.  The default SyncBN transport at world > 1 when every rank can map every peer's mailbox
+(``try_create``: checked collectively at set-up, with a probe all-reduce; ops.setup_syncbn), because it takes the SyncBN
+statistics off the RCCL communicator, so FlatDDP can all-reduce its gradient buckets on WORLD from inside the backward;
+SCD_SYNCBN_PEER=0 forces RCCL.  Single node, <= 8 ranks, eager steps (the epoch is a host counter).
 
 Late ranks: a rank whose host is seconds behind (a checkpoint write, validation, first-step allocation, a GC pause) is
 waited for on the device, up to SCD_PEER_TIMEOUT_S (120 s).  Only a peer that never arrives is an error: the kernel then
@@ -23,8 +25,63 @@ import torch.distributed as dist
 from . import lib as L
 
 
+def _gather(obj, group):
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
 class PeerAllReduce:
+    @classmethod
+    def try_create(cls, group=None, cap=4096, timeout_s=None, probe_timeout_s=10.0):
+        """Collective and failure-tolerant: every rank returns a working PeerAllReduce, or every rank returns None, with
+        the reason (the first failing rank's).  The mailbox allocation, the IPC mapping of every peer's mailbox and one
+        probe all-reduce (rank-ordered sum checked against its closed form, within probe_timeout_s) must succeed on
+        every rank; the ranks agree on that through the group (all_gather_object) after each phase, so no rank is left
+        waiting in a collective another rank has abandoned."""
+        self = cls.__new__(cls)
+        self._setup(group, cap, timeout_s)
+        err = None
+        try:
+            self._alloc()
+        except RuntimeError as e:
+            err = "rank %d: mailbox allocation / IPC handle failed (%s)" % (self.rank, e)
+        got = _gather((None, err) if err else (bytes(self._handle), None), group)
+        if any(h is None for h, _ in got):
+            self.close()
+            return None, next(e for _, e in got if e)
+        handles = [h for h, _ in got]
+        try:
+            self._map(handles)
+        except RuntimeError as e:
+            err = "rank %d: mapping a peer's mailbox failed (%s)" % (self.rank, e)
+        errs = _gather(err, group)
+        if any(errs):
+            self.close()
+            return None, next(e for e in errs if e)
+        dist.barrier(group=group)           # every mailbox mapped before the first flag is written
+        dev = torch.device("cuda", torch.cuda.current_device())
+        v = torch.arange(16, dtype=torch.float64, device=dev) * (self.rank + 1) + 0.5
+        self.epoch += 1
+        L.call("scd_peer_allreduce_f64", v.data_ptr(), v.numel(), self.rank, self.R, self.boxes, self.cap, self.epoch,
+               self.err.data_ptr(), max(1, int(probe_timeout_s * 1000)), torch.cuda.current_stream().cuda_stream)
+        want = torch.arange(16, dtype=torch.float64) * (self.R * (self.R + 1) // 2) + 0.5 * self.R
+        ok = int(self.err.item()) == 0 and torch.equal(v.cpu(), want)
+        errs = _gather(None if ok else "rank %d: the probe all-reduce over peer memory failed (%s)" % (
+            self.rank, "timed out" if int(self.err.item()) else "wrong sum"), group)
+        if any(errs):
+            self.close()
+            return None, next(e for e in errs if e)
+        return self, None
+
     def __init__(self, group=None, cap=4096, timeout_s=None):
+        self._setup(group, cap, timeout_s)
+        self._alloc()
+        handles = _gather(bytes(self._handle), group)
+        self._map(handles)
+        dist.barrier(group=group)           # every mailbox mapped before the first flag is written
+
+    def _setup(self, group, cap, timeout_s):
         self.group = group
         if timeout_s is None:
             timeout_s = float(os.environ.get("SCD_PEER_TIMEOUT_S", "120"))
@@ -34,16 +91,25 @@ class PeerAllReduce:
         if self.R > 8:
             raise RuntimeError("PeerAllReduce: at most 8 ranks (one node)")
         self.cap = cap
+        self.own = None
+        self.mapped = []
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.err = torch.zeros(1, dtype=torch.int64, device=dev)     # sticky: epoch of the first failed call
+        self._err_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+        self._err_event = None
+        self.epoch = 0
+
+    def _alloc(self):
         lib = L.lib()
-        nbytes = lib.scd_peer_mailbox_bytes(self.R, cap)
+        nbytes = lib.scd_peer_mailbox_bytes(self.R, self.cap)
         own = ctypes.c_void_p()
         L.call("scd_peer_alloc", nbytes, ctypes.byref(own))
         self.own = own.value
         h = (ctypes.c_char * 64)()
         L.call("scd_peer_ipc_handle", self.own, h)
-        handles = [None] * self.R
-        dist.all_gather_object(handles, bytes(h), group=group)
-        self.mapped = []
+        self._handle = h
+
+    def _map(self, handles):
         boxes = []
         for r, hb in enumerate(handles):
             if r == self.rank:
@@ -54,13 +120,6 @@ class PeerAllReduce:
             self.mapped.append(p.value)
             boxes.append(p.value)
         self.boxes = (ctypes.c_void_p * self.R)(*boxes)
-        dev = torch.device("cuda", torch.cuda.current_device())
-        self.err = torch.zeros(1, dtype=torch.int64, device=dev)     # sticky: epoch of the first failed call
-        self._err_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
-        self._err_event = None
-        self.epoch = 0
-        dist.barrier(group=group)           # every mailbox mapped before the first flag is written
-
     def all_reduce(self, t):
         """In-place sum of the contiguous fp64 CUDA tensor t over the group (enqueued on the current stream)."""
         if t.dtype != torch.float64 or not t.is_contiguous() or t.numel() > self.cap:

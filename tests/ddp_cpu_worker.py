@@ -163,6 +163,20 @@ def check_bn_group(rank, world):
     finally:
         os.environ.pop("SCD_SYNCBN_OWN_GROUP", None)
         ops.set_bn_sync(None)
+    # setup_syncbn (networkFactory / bench): without a GPU the peer-memory path is not tried, SyncBN falls back to
+    # WORLD (every rank agrees, the reason is logged) and the buckets wait for the end of the backward
+    if not torch.cuda.is_available():
+        logs = []
+        try:
+            assert ops.setup_syncbn(log=logs.append) == "rccl-world"
+            assert ops.bn_sync_mode() == "rccl-world" and ops._BNSync.why == "no GPU", ops._BNSync.why
+            assert len(logs) == 1 and "no GPU" in logs[0] and "end of the backward" in logs[0], logs
+            os.environ["SCD_SYNCBN_OWN_GROUP"] = "1"
+            assert ops.setup_syncbn() == "rccl-own"
+        finally:
+            os.environ.pop("SCD_SYNCBN_OWN_GROUP", None)
+            ops.set_bn_sync(None)
+        assert ops.bn_sync_mode() == "off"
 
 
 def main():

@@ -1,7 +1,10 @@
 """One rank of the GPU data-parallel parity test (F7 at W=2, F7b at W=4): the ranks share cuda:0 over gloo (RCCL cannot
 put two ranks on one device; the 8-GPU RCCL path is the same code with backend "nccl").
-Checks SyncBN statistics + FlatDDP gradient averaging against the reference's golden vectors, with the SyncBN group
-policy of ops.syncbn_group (WORLD shared with the buckets unless SCD_SYNCBN_OWN_GROUP=1) or the peer-memory path."""
+Checks SyncBN statistics + FlatDDP gradient averaging against the reference's golden vectors with the SyncBN transport
+ops.setup_syncbn picks: by default the peer-memory path (the ranks map each other's mailboxes), so the gradient buckets
+are all-reduced from inside the backward; with SCD_SYNCBN_PEER=0 torch.distributed on WORLD beside the buckets (they
+then wait for the end of the backward) or, with SCD_SYNCBN_OWN_GROUP=1, on a group of its own.  EXPECT_SYNCBN names
+the mode the test requires."""
 import os
 import sys
 
@@ -28,9 +31,12 @@ def main():
     m = plugin.model(**plugin.modelParams)
     m.load_state_dict(O.hash_weights(entries))
     m = m.cuda().train().set_compute_dtype(torch.float32)
-    ops.set_bn_sync(ops.syncbn_group())        # SCD_SYNCBN_PEER=1: statistics over peer memory (scdhip/peer.py)
+    logs = []
+    mode = ops.setup_syncbn(log=logs.append)
+    print("rank %d: %s" % (rank, logs[0]), flush=True)
+    assert mode == os.environ["EXPECT_SYNCBN"], (mode, ops._BNSync.why)
     peer = ops.bn_sync_peer()
-    assert (peer is not None) == (os.environ.get("SCD_SYNCBN_PEER") == "1")
+    assert (peer is not None) == (mode == "peer")
     if peer is not None:
         # the primitive first (fails fast if the peers cannot see each other): rank-ordered sums, identical bits
         # on both ranks, and its latency
@@ -76,11 +82,14 @@ def main():
     for k, p in m.named_parameters():
         np.testing.assert_allclose(p.grad.double().norm().item(), first[k], rtol=1e-5, atol=1e-9, err_msg=k)
     # the head/deconv bucket is all-reduced from inside the backward pass, not from the end-of-backward callback --
-    # unless SyncBN shares FlatDDP's group (the default), where every bucket waits for the end of the backward
+    # unless SyncBN shares FlatDDP's group (SCD_SYNCBN_PEER=0 on WORLD), where every bucket waits for the end of it
+    assert ddp.overlap_buckets() == (mode != "rccl-world")
     if ddp.overlap_buckets():
         assert ddp.early_launches >= 1, (ddp.early_launches, len(ddp._buckets))
     else:
         assert ddp.early_launches == 0 and ops.bn_sync_shares_group(ddp.group), ddp.early_launches
+    print("rank %d: syncbn %s, %d of %d buckets launched inside the backward" % (rank, mode, ddp.early_launches,
+                                                                                  len(ddp._buckets)), flush=True)
     for k in g.files:
         if k.startswith("rs|"):
             np.testing.assert_allclose(sd[k[3:]].cpu().numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)

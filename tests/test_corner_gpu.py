@@ -71,6 +71,50 @@ def test_cpool_backward_matches_oracle_tie_rule(ties):
             np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
 
 
+def _reference_pool_ops():
+    """The reference's own corner-pool extensions (cornerPooling/source/*.cpp), compiled from their sources into
+    oracle/_ref by oracle/build_ref_cpool.py in the build container (test infrastructure; nothing in scd-resnet_amd
+    loads them).  Their backward allocates torch::CUDA tensors (topPool.cpp:44-45), so it runs only here, on the GPU."""
+    import importlib.machinery
+    import importlib.util
+    import os
+    mods = []
+    for name in ("topPool", "bottomPool", "leftPool", "rightPool"):       # = dir 0..3 of scd_cpool_*
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", name,
+                            name + ".so")
+        if not os.path.exists(path):
+            pytest.skip("oracle/_ref not built (needs /root/reference in the build container)")
+        loader = importlib.machinery.ExtensionFileLoader(name, path)
+        spec = importlib.util.spec_from_file_location(name, path, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        mods.append(mod)
+    return mods
+
+
+@pytest.mark.parametrize("ties", [False, True])
+def test_cpool_backward_matches_reference_cpp(ties):
+    """scd_cpool_bwd against the reference's own backward (topPool.cpp:33-74 and its siblings, run on cuda tensors as
+    the reference trains), fp32, bit for bit: random inputs and tie-heavy ones (values in {0, 1, 2}: the strict '>'
+    rule keeps the first-scanned argmax), at a ragged shape and the configs[3] pool shape's spatial size."""
+    from scdhip import ops
+    ref = _reference_pool_ops()
+    g = torch.Generator().manual_seed(5 + ties)
+    for (N, C, H, W) in [(2, 64, 9, 7), (1, 128, 128, 128)]:
+        x = (torch.randint(0, 3, (N, C, H, W), generator=g).float() if ties else
+             torch.randn(N, C, H, W, generator=g)).to(DEV)
+        dy = torch.randn(N, C, H, W, generator=g).to(DEV)
+        xh, dyh = _nhwc(x), _nhwc(dy)
+        for d, mod in enumerate(ref):
+            want = mod.backward(x, dy)[0]
+            torch.cuda.synchronize()
+            got = ops.cpool_bwd(xh, dyh, d).permute(0, 3, 1, 2)
+            np.testing.assert_array_equal(got.cpu().numpy(), want.cpu().numpy(), err_msg="dir %d" % d)
+            # and the forward, against the reference's forward on the same cuda tensors
+            np.testing.assert_array_equal(ops.cpool_fwd(xh, d).permute(0, 3, 1, 2).cpu().numpy(),
+                                          mod.forward(x)[0].cpu().numpy(), err_msg="fwd dir %d" % d)
+
+
 def _model(dtype=torch.float32):
     import trainer.model.cornerNetCPool as plugin
     entries, topo = OC.model_spec(10)

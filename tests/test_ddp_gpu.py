@@ -38,16 +38,19 @@ def _run(worker, world, **extra):
     return outs
 
 
-@pytest.mark.parametrize("world,sync", [(2, "world"), (2, "own"), (2, "peer"), (4, "world"), (4, "peer")])
+@pytest.mark.parametrize("world,sync", [(2, "default"), (2, "world"), (2, "own"), (4, "default"), (4, "world")])
 def test_syncbn_ddp_matches_reference(world, sync):
-    """F7 (W=2) and F7b (W=4, tests/golden/make_golden_ddp4.py) with the SyncBN statistics through torch.distributed
-    on WORLD beside the buckets (the default), on a group of their own, or through the peer-memory one-shot all-reduce
-    (scdhip/peer.py: IPC-mapped mailboxes, flag-synchronised kernel) -- the reference's golden vectors."""
-    outs = _run("ddp_gpu_worker.py", world, SCD_SYNCBN_PEER="1" if sync == "peer" else "0",
-                SCD_SYNCBN_OWN_GROUP="1" if sync == "own" else "0")
+    """F7 (W=2) and F7b (W=4, tests/golden/make_golden_ddp4.py) against the reference's golden vectors, with the SyncBN
+    transport of the default set-up (ops.setup_syncbn: peer-memory statistics, scdhip/peer.py, so the gradient buckets
+    are all-reduced from inside the backward -- asserted) and the RCCL fallbacks: torch.distributed on WORLD beside
+    the buckets (all at the end of the backward) or on a group of their own (SCD_SYNCBN_PEER=0)."""
+    env = {"default": dict(EXPECT_SYNCBN="peer"),
+           "world": dict(SCD_SYNCBN_PEER="0", EXPECT_SYNCBN="rccl-world"),
+           "own": dict(SCD_SYNCBN_PEER="0", SCD_SYNCBN_OWN_GROUP="1", EXPECT_SYNCBN="rccl-own")}[sync]
+    outs = _run("ddp_gpu_worker.py", world, **env)
     for o in outs:
         assert "OK rank" in o, o
-    print([line for o in outs for line in o.splitlines() if "per call" in line or "worst" in line])
+    print([line for o in outs for line in o.splitlines() if "per call" in line or "worst" in line or "buckets" in line])
 
 
 def test_rccl_world1_flatddp_syncbn():
