@@ -125,41 +125,43 @@ __global__ __launch_bounds__(256) void cpool_fwd_kernel(int dir, const T* __rest
 // element store when the element's next record is reached (and for every element at the end of the line): records
 // are few (~ln L per element on random data), and the element store follows the zero vector at that position in
 // this thread's program order.
-template <typename T, int U>
+template <typename T, int U, int VB>
 __global__ __launch_bounds__(256) void cpool_bwd_kernel(int dir, const T* __restrict__ x, const T* __restrict__ dy,
                                                         T* __restrict__ dx, int N, int H, int W, int C, long lines) {
-    constexpr int E = Vec16<T>::N;
+    typedef Vec<T, VB> V;
+    typedef typename V::raw R;
+    constexpr int E = V::N;
     const long i = blockIdx.x * 256L + threadIdx.x;
     if (i >= lines) return;
     const Line ln = line_of(dir, i, N, H, W, C, E);
     const int L = ln.L;
-    uint4 cx[U], cg[U];
+    R cx[U], cg[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const long off = ln.start + (long)min(u, L - 1) * ln.sstep;
-        cx[u] = *(const uint4*)(x + off);
-        cg[u] = *(const uint4*)(dy + off);
+        cx[u] = *(const R*)(x + off);
+        cg[u] = *(const R*)(dy + off);
     }
     float mv[E], acc[E], zero[E];
     int rk[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) { mv[e] = 0.f; acc[e] = 0.f; rk[e] = 0; zero[e] = 0.f; }
     for (int k0 = 0; k0 < L; k0 += U) {
-        uint4 nx[U], ng[U];
+        R nx[U], ng[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {          // prefetch the next U positions (clamped: always a valid address)
             const long off = ln.start + (long)min(k0 + U + u, L - 1) * ln.sstep;
-            nx[u] = *(const uint4*)(x + off);
-            ng[u] = *(const uint4*)(dy + off);
+            nx[u] = *(const R*)(x + off);
+            ng[u] = *(const R*)(dy + off);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int k = k0 + u;
             if (k >= L) break;
             float v[E], g[E];
-            Vec16<T>::load(&cx[u], v);
-            Vec16<T>::load(&cg[u], g);
-            Vec16<T>::store(dx + ln.start + (long)k * ln.sstep, zero);
+            V::load(&cx[u], v);
+            V::load(&cg[u], g);
+            V::store(dx + ln.start + (long)k * ln.sstep, zero);
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 const bool rec = (k == 0) || (v[e] > mv[e]);
@@ -199,14 +201,26 @@ int launch_fwd(int dir, const void* x, const void* addend, void* y, int N, int H
     SCD_RETURN_LAUNCH();
 }
 
-template <typename T>
-int launch_bwd(int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C, hipStream_t st) {
-    const long lines = (long)N * (dir < 2 ? W : H) * (C / Vec16<T>::N);
+template <typename T, int U, int VB>
+int launch_bwd_v(int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C, hipStream_t st) {
+    const long lines = (long)N * (dir < 2 ? W : H) * (C / Vec<T, VB>::N);
     if (lines == 0) return 0;
     const int grid = (int)((lines + 255) / 256);
-    hipLaunchKernelGGL((cpool_bwd_kernel<T, 8>), dim3(grid), dim3(256), 0, st, dir, (const T*)x, (const T*)dy,
+    hipLaunchKernelGGL((cpool_bwd_kernel<T, U, VB>), dim3(grid), dim3(256), 0, st, dir, (const T*)x, (const T*)dy,
                        (T*)dx, N, H, W, C, lines);
     SCD_RETURN_LAUNCH();
+}
+
+// SCD_CPOOL_BWD (A/B of the vector width and prefetch depth; read per call): 0 = 16-B vectors, 8 positions ahead,
+// 1 = 8-B vectors, 8 ahead, 2 = 16-B, 4 ahead, 3 = 8-B, 4 ahead
+template <typename T>
+int launch_bwd(int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C, hipStream_t st) {
+    const char* e = getenv("SCD_CPOOL_BWD");
+    const int v = e ? atoi(e) : 0;
+    if (v == 1) return launch_bwd_v<T, 8, 8>(dir, x, dy, dx, N, H, W, C, st);
+    if (v == 2) return launch_bwd_v<T, 4, 16>(dir, x, dy, dx, N, H, W, C, st);
+    if (v == 3) return launch_bwd_v<T, 4, 8>(dir, x, dy, dx, N, H, W, C, st);
+    return launch_bwd_v<T, 8, 16>(dir, x, dy, dx, N, H, W, C, st);
 }
 
 }  // namespace

@@ -215,56 +215,74 @@ __global__ void im2col_stem_kernel(const float* x, T* cols, int N, int H, int W,
 }
 
 // ---------------------------------------------------------------- stem BN+ReLU+MaxPool(3,2,1)
-// workgroups of 256 per CU the pool is compiled for (registers: its nine 16-B window loads in flight per thread)
+// One thread = one 16-B channel chunk of SPR consecutive pooled rows at one pooled column: it loads the 2 SPR + 1 conv
+// rows x 3 conv columns of those windows once (all in flight: clamped addresses, taps outside the image never win) --
+// conv row 2 oh + 1 is the bottom of window oh and the top of window oh + 1, which a thread per pooled output fetched
+// twice, from two workgroups usually on different XCDs (PMC: 1.5x the 268-MB read at B = 32; 9/8 here).
+// workgroups of 256 per CU the pool is compiled for (registers: its 27 window loads in flight per thread)
 #ifndef STEM_POOL_OCC
-#define STEM_POOL_OCC 4
+#define STEM_POOL_OCC 2
 #endif
+constexpr int SPR = 4;                              // pooled rows per thread
 template <typename T>
 __global__ __launch_bounds__(256, STEM_POOL_OCC) void stem_pool_fwd_kernel(const T* y, const float* scale, const float* shift, T* out, uint8_t* argmax,
                                      int N, int H, int W, int C, int Ho, int Wo) {
     constexpr int E = Vec16<T>::N;
+    constexpr int NR = 2 * SPR + 1;
     const unsigned cpp = C / E;
-    const unsigned total = (unsigned)N * Ho * Wo * cpp;
-    const unsigned HoWo = (unsigned)Ho * Wo;
+    const unsigned G = (unsigned)(Ho + SPR - 1) / SPR;
+    const unsigned GW = G * (unsigned)Wo;
+    const unsigned total = (unsigned)N * GW * cpp;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        const size_t pix = i / cpp;
-        const int ch = (int)(i - (unsigned)pix * cpp);
-        const int n = (int)((unsigned)pix / HoWo);
-        const int rem = (int)((unsigned)pix - (unsigned)n * HoWo);
-        const int oh = rem / Wo, ow = rem - (rem / Wo) * Wo;
-        float best[E], sc[E], sh[E];
-        int arg[E];
+        const unsigned item = i / cpp;
+        const int ch = (int)(i - item * cpp);
+        const int n = (int)(item / GW);
+        const unsigned rem = item - (unsigned)n * GW;
+        const int g = (int)(rem / (unsigned)Wo), ow = (int)(rem - (unsigned)g * Wo);
+        const int oh0 = g * SPR;
+        float sc[E], sh[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            best[e] = -INFINITY; arg[e] = 0;
-            sc[e] = scale[ch * E + e]; sh[e] = shift[ch * E + e];
-        }
-        // the 9 window loads from clamped addresses (all in flight at once; taps outside the image never win),
-        // compared in window order as before
-        float v[9][E];
+        for (int e = 0; e < E; ++e) { sc[e] = scale[ch * E + e]; sh[e] = shift[ch * E + e]; }
+        uint4 raw[NR][3];
 #pragma unroll
-        for (int d = 0; d < 9; ++d) {
-            const int h = min(max(2 * oh - 1 + d / 3, 0), H - 1), w = min(max(2 * ow - 1 + d % 3, 0), W - 1);
-            Vec16<T>::load(y + (((long)n * H + h) * W + w) * C + ch * E, v[d]);
-        }
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int d = 0; d < 9; ++d) {
-            const bool in = (unsigned)(2 * oh - 1 + d / 3) < (unsigned)H && (unsigned)(2 * ow - 1 + d % 3) < (unsigned)W;
+            for (int c = 0; c < 3; ++c) {
+                const int h = min(max(2 * oh0 - 1 + r, 0), H - 1), w = min(max(2 * ow - 1 + c, 0), W - 1);
+                raw[r][c] = *(const uint4*)(y + (((long)n * H + h) * W + w) * C + ch * E);
+            }
 #pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const float z = in ? fmaxf(v[d][e] * sc[e] + sh[e], 0.f) : -INFINITY;
-                if (z > best[e]) { best[e] = z; arg[e] = d; }
+        for (int j = 0; j < SPR; ++j) {
+            const int oh = oh0 + j;
+            float best[E];
+            int arg[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+            // the window in window order (first maximum wins, as before)
+#pragma unroll
+            for (int d = 0; d < 9; ++d) {
+                const bool in = (unsigned)(2 * oh - 1 + d / 3) < (unsigned)H && (unsigned)(2 * ow - 1 + d % 3) < (unsigned)W;
+                float v[E];
+                Vec16<T>::load(&raw[2 * j + d / 3][d % 3], v);
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const float z = in ? fmaxf(v[e] * sc[e] + sh[e], 0.f) : -INFINITY;
+                    if (z > best[e]) { best[e] = z; arg[e] = d; }
+                }
+            }
+            if (oh < Ho) {
+                const size_t pix = ((size_t)n * Ho + oh) * Wo + ow;
+                Vec16<T>::store(out + pix * C + ch * E, best);
+                // the E argmax bytes of this chunk in one store
+                unsigned lo = 0, hi = 0;
+#pragma unroll
+                for (int e = 0; e < E && e < 4; ++e) lo |= (unsigned)arg[e] << (8 * e);
+#pragma unroll
+                for (int e = 4; e < E; ++e) hi |= (unsigned)arg[e] << (8 * (e - 4));
+                if constexpr (E == 8) *(uint2*)(argmax + pix * C + ch * E) = make_uint2(lo, hi);
+                else *(unsigned*)(argmax + pix * C + ch * E) = lo;
             }
         }
-        Vec16<T>::store(out + pix * C + ch * E, best);
-        // the E argmax bytes of this chunk in one store
-        unsigned lo = 0, hi = 0;
-#pragma unroll
-        for (int e = 0; e < E && e < 4; ++e) lo |= (unsigned)arg[e] << (8 * e);
-#pragma unroll
-        for (int e = 4; e < E; ++e) hi |= (unsigned)arg[e] << (8 * (e - 4));
-        if constexpr (E == 8) *(uint2*)(argmax + pix * C + ch * E) = make_uint2(lo, hi);
-        else *(unsigned*)(argmax + pix * C + ch * E) = lo;
     }
 }
 
@@ -835,7 +853,8 @@ extern "C" int scd_stem_pool_fwd(int dtype, const void* y, const float* scale, c
     hipStream_t st = (hipStream_t)stream;
     const int E = dtype == SCD_DT_BF16 ? 8 : 4;
     if (C % E) return SCD_ERR_ARG;
-    const long total = (long)N * Ho * Wo * (C / E);
+    const long total = (long)N * ((Ho + SPR - 1) / SPR) * Wo * (C / E);
+    if (total >= (1L << 32)) return SCD_ERR_ARG;
     if (dtype == SCD_DT_BF16)
         hipLaunchKernelGGL((stem_pool_fwd_kernel<__bf16>), dim3(ew_blocks(total)), dim3(256), 0, st, (const __bf16*)y,
                            scale, shift, (__bf16*)out, argmax, N, H, W, C, Ho, Wo);

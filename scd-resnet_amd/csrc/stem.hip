@@ -368,19 +368,27 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
         for (int b = 0; b < 2; ++b) { acc1[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f}; acc2[a][b] = acc1[a][b]; }
 
     const int t0 = blockIdx.x * chunk, t1 = min(ntiles, t0 + chunk);
-    // raw operands of one tile, loaded one tile ahead (issued as soon as the previous tile's are consumed)
+    // raw operands of one tile, loaded one tile ahead (issued as soon as the previous tile's are consumed).  Tiles run
+    // down a column group (t = (n, column group jc, pooled row bo), bo fastest), so the pooled row bo + 1 of a tile is
+    // row bo of the next one: carried in registers instead of fetched again (each pooled row was read by two tiles:
+    // PMC 1.34x the algorithmic bytes of this kernel; ~1.1x with the carry)
     uint4 rd[2][2], ry[2][2];
     uint2 ra[2][2];
     float rp[(BPROWS * WPCOLS + 255) / 256];
-    auto load_tile = [&](int t) {
+    auto load_tile = [&](int t, bool carry) {
         const int n = t / tpi, rem = t - (t / tpi) * tpi;
-        const int bo = rem / gpr, jc = rem - (rem / gpr) * gpr;
+        const int jc = rem / Hp, bo = rem - (rem / Hp) * Hp;
         const int w0 = jc * BTW, bc = jc * (BTW / 2) + bl;
         const bool okh = bo + 1 < Hp, okw = bc + 1 < Wp;
+        if (carry) {                                      // workgroup-uniform
+#pragma unroll
+            for (int oj = 0; oj < 2; ++oj) { rd[0][oj] = rd[1][oj]; ra[0][oj] = ra[1][oj]; }
+        }
 #pragma unroll
         for (int oi = 0; oi < 2; ++oi)
 #pragma unroll
             for (int oj = 0; oj < 2; ++oj) {
+                if (oi == 0 && carry) continue;
                 const bool ok = (oi == 0 || okh) && (oj == 0 || okw);
                 const long o = (((long)n * Hp + bo + (ok ? oi : 0)) * Wp + bc + (ok ? oj : 0)) * CO + ch * 8;
                 rd[oi][oj] = *(const uint4*)(dout + o);
@@ -406,7 +414,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
             rp[q] = (i < BPROWS * WPCOLS && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ? v : 0.f;
         }
     };
-    if (t0 < t1) load_tile(t0);
+    if (t0 < t1) load_tile(t0, false);
     for (int t = t0; t < t1; ++t) {
         // ---- dz of the 2x2 conv block (2bo + a, 2bc + b), channels 8ch .. 8ch+7
 #pragma unroll
@@ -461,7 +469,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                 patch[bpatch_idx(r, c)] = rp[q];
             }
         }
-        if (t + 1 < t1) load_tile(t + 1);                 // in flight during this tile's column build and MFMAs
+        if (t + 1 < t1) load_tile(t + 1, (t + 1) % Hp != 0);      // in flight during this tile's column build and MFMAs
         __syncthreads();
         // ---- transposed column tiles of both conv rows: thread -> tap k = tid / 4, pixels 16 (tid % 4) .. +15
         {

@@ -381,6 +381,39 @@ def test_stem_fused_backward_matches_unfused():
     assert rel_err(dwb, dwa) < 2e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("shape", [(2, 128, 128), (3, 130, 96), (1, 7, 9)])
+def test_stem_pool_forward_matches_torch(shape, dtype):
+    """scd_stem_pool_fwd (BN apply + ReLU + MaxPool(3, 2, 1), residuals.py:212-214; four pooled rows per thread) against
+    float64 torch on the same 16-bit / fp32 conv output: the pooled value within one rounding of the output dtype, the
+    argmax byte the window index of the first maximum wherever the window's top two differ clearly; pooled heights
+    33 / 65 / 4 (ragged against the four rows per thread)."""
+    from scdhip import ops
+    N, H, W = shape
+    C = 64
+    g = torch.Generator().manual_seed(29)
+    y = torch.randn(N, H, W, C, generator=g).to(dtype).to(DEV)
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    st = ops.BNState()
+    st.scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    st.shift = torch.randn(C, generator=g).to(DEV)
+    out, am = ops.stem_pool_fwd(y, st)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    assert out.shape == (N, Ho, Wo, C) and am.shape == (N, Ho, Wo, C)
+    z = torch.relu(y.double() * st.scale.double() + st.shift.double()).permute(0, 3, 1, 2)
+    zp = torch.nn.functional.pad(z, (1, 1, 1, 1), value=float("-inf"))
+    win = zp.unfold(2, 3, 2).unfold(3, 3, 2).reshape(N, C, Ho, Wo, 9)
+    ref, arg = win.max(-1)
+    got = out.double().permute(0, 3, 1, 2)
+    ulp = {torch.bfloat16: 2.0 ** -7, torch.float16: 2.0 ** -10, torch.float32: 2.0 ** -23}[dtype]
+    assert ((got - ref).abs() <= ulp * ref.abs() + 1e-30).all()
+    top2 = win.topk(2, -1).values
+    clear = (top2[..., 0] - top2[..., 1]) > 1e-3 * top2[..., 0].abs()
+    ga = am.long().permute(0, 3, 1, 2)
+    assert clear.float().mean() > 0.9
+    assert torch.equal(ga[clear], arg[clear])
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(2, 512, 512), (3, 260, 256)])
 def test_stem_one_pass_backward(shape, dtype):

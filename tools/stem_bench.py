@@ -58,6 +58,9 @@ def main():
     dz, coef = ops.stem_pool_bwd_bn(bn, dout, am, y, st)
     rep("stem_conv_wgrad (+BN apply)", timed(lambda: ops.stem_conv_wgrad(dz, x, dw, ybn=y, coef=coef), a.reps))
     print("chain %.1f us" % sum(us for _, us in rows))
+    # the one-pass backward the model runs (scd_stem_bwd_fused + reduce + BN finalize + combine)
+    rep("stem_backward_fused (one pass)", timed(lambda: ops.stem_backward_fused(bn, dout, am, y, st, x, wpk, dw),
+                                                a.reps))
 
 if __name__ == "__main__":
     main()
