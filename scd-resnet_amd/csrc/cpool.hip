@@ -211,16 +211,13 @@ int launch_bwd_v(int dir, const void* x, const void* dy, void* dx, int N, int H,
     SCD_RETURN_LAUNCH();
 }
 
-// SCD_CPOOL_BWD (A/B of the vector width and prefetch depth; read per call): 0 = 16-B vectors, 8 positions ahead,
-// 1 = 8-B vectors, 8 ahead, 2 = 16-B, 4 ahead, 3 = 8-B, 4 ahead
+// 8-B vectors (4 bf16 / 2 fp32 elements per thread: twice the lines of 16-B vectors, 94 VGPRs) with 8 positions in
+// flight: 96-110 us for the (32, 128, 128, 128) bf16 pool against 127-139 us with 16-B vectors (tools/hbm_bench.py,
+// round 5); the two-pass reverse-order kernel it replaces took 84 us but summed each run in reverse, not bit-identical
+// to the reference
 template <typename T>
 int launch_bwd(int dir, const void* x, const void* dy, void* dx, int N, int H, int W, int C, hipStream_t st) {
-    const char* e = getenv("SCD_CPOOL_BWD");
-    const int v = e ? atoi(e) : 0;
-    if (v == 1) return launch_bwd_v<T, 8, 8>(dir, x, dy, dx, N, H, W, C, st);
-    if (v == 2) return launch_bwd_v<T, 4, 16>(dir, x, dy, dx, N, H, W, C, st);
-    if (v == 3) return launch_bwd_v<T, 4, 8>(dir, x, dy, dx, N, H, W, C, st);
-    return launch_bwd_v<T, 8, 16>(dir, x, dy, dx, N, H, W, C, st);
+    return launch_bwd_v<T, 8, 8>(dir, x, dy, dx, N, H, W, C, st);
 }
 
 }  // namespace

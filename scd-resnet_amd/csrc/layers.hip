@@ -216,14 +216,19 @@ __global__ void im2col_stem_kernel(const float* x, T* cols, int N, int H, int W,
 
 // ---------------------------------------------------------------- stem BN+ReLU+MaxPool(3,2,1)
 // One thread = one 16-B channel chunk of SPR consecutive pooled rows at one pooled column: it loads the 2 SPR + 1 conv
-// rows x 3 conv columns of those windows once (all in flight: clamped addresses, taps outside the image never win) --
-// conv row 2 oh + 1 is the bottom of window oh and the top of window oh + 1, which a thread per pooled output fetched
-// twice, from two workgroups usually on different XCDs (PMC: 1.5x the 268-MB read at B = 32; 9/8 here).
-// workgroups of 256 per CU the pool is compiled for (registers: its 27 window loads in flight per thread)
+// rows x 3 conv columns of those windows at once (clamped addresses; taps outside the image never win).  Conv row
+// 2 oh + 1 is the bottom of window oh and the top of window oh + 1, so one row per thread fetches 1.5x the conv output
+// (PMC, round 4) and four rows per thread 9/8 -- but in the step the conv output was just written and is read back
+// from the Infinity Cache, and the four-row build (203 VGPRs, 2 waves per SIMD) measured 99 us against 82 us for one
+// row per thread (round 5, tools/gpu_abn.sh): one row per thread stays.
+// workgroups of 256 per CU the pool is compiled for (registers: the window loads in flight per thread)
 #ifndef STEM_POOL_OCC
-#define STEM_POOL_OCC 2
+#define STEM_POOL_OCC 4
 #endif
-constexpr int SPR = 4;                              // pooled rows per thread
+#ifndef STEM_SPR
+#define STEM_SPR 1
+#endif
+constexpr int SPR = STEM_SPR;                       // pooled rows per thread
 template <typename T>
 __global__ __launch_bounds__(256, STEM_POOL_OCC) void stem_pool_fwd_kernel(const T* y, const float* scale, const float* shift, T* out, uint8_t* argmax,
                                      int N, int H, int W, int C, int Ho, int Wo) {
