@@ -195,6 +195,25 @@ int scd_bn_finalize(double* stats, int nrep, int C, double count, const float* g
                     const float* beta, float* running_mean, float* running_var, int64_t* num_batches,
                     float momentum, float eps, float* mean, float* invstd, float* scale, float* shift,
                     void* stream);
+/* Several layers' finalizes in ONE launch (a block's bn1 and downsample BN, whose statistics are complete together;
+ * residuals.py:99-120): layers[0 .. n) as scd_bn_finalize's arguments, n <= SCD_BN_FIN_MAX (host array). */
+#define SCD_BN_FIN_MAX 4
+typedef struct scd_bn_fin_args {
+    double* stats;             /* [nrep][2][C] fp64 sums, zeroed after reading (NULL: eval mode) */
+    int nrep, C;
+    double count;
+    const float* gamma;
+    const float* beta;
+    float* running_mean;
+    float* running_var;
+    int64_t* num_batches;
+    float momentum, eps;
+    float* mean;
+    float* invstd;
+    float* scale;
+    float* shift;
+} scd_bn_fin_args;
+int scd_bn_finalize_n(const scd_bn_fin_args* layers, int n, void* stream);
 /* out = act(y*scale + shift + R), R = 0 | res | res*rscale + rshift */
 int scd_bn_apply(int dtype, const void* y, void* out, int C, long total, const float* scale,
                  const float* shift, const void* res, const float* rscale, const float* rshift,
@@ -211,6 +230,21 @@ int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, const void*
 int scd_bn_bwd_finalize(double* stats, int nrep, int C, double count, const float* gamma,
                         const float* mean, const float* invstd, float* dgamma, float* dbeta,
                         float gscale, float* coef, void* stream);
+/* ... several layers in ONE launch (the two BN layers behind a residual join, whose sums scd_bn_bwd_reduce2 makes
+ * together): layers[0 .. n) as scd_bn_bwd_finalize's arguments, n <= SCD_BN_FIN_MAX (host array) */
+typedef struct scd_bn_bwd_fin_args {
+    double* stats;
+    int nrep, C;
+    double count;
+    const float* gamma;
+    const float* mean;
+    const float* invstd;
+    float* dgamma;
+    float* dbeta;
+    float gscale;
+    float* coef;
+} scd_bn_bwd_fin_args;
+int scd_bn_bwd_finalize_n(const scd_bn_bwd_fin_args* layers, int n, void* stream);
 /* dy = a*dz + b*y + c (dtype), dz masked as in scd_bn_bwd_reduce; optionally also writes dz */
 int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, const void* y, const float* relu_scale,
                      const float* relu_shift, const float* coef, int C, long total, void* dy, void* dz,

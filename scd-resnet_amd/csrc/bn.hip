@@ -66,12 +66,10 @@ __device__ __forceinline__ void wave_collect(double* stats, int nrep, int C, int
     q = wave_sum_d(b);
 }
 
-__global__ void bn_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
-                                   const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
-                                   float eps, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
-    const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt && stats) *nbt += 1;
-    if (c >= C) return;
+__device__ __forceinline__ void bn_finalize_channel(int c, double* stats, int nrep, int C, double count,
+                                                    const float* gamma, const float* beta, float* rmean, float* rvar,
+                                                    float momentum, float eps, float* mean_o, float* invstd_o,
+                                                    float* scale_o, float* shift_o) {
     double mean, var;
     if (stats) {
         double s, q;
@@ -99,6 +97,36 @@ __global__ void bn_finalize_kernel(double* stats, int nrep, int C, double count,
         rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
         rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
     }
+}
+
+__global__ void bn_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
+                                   float eps, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+    const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt && stats) *nbt += 1;
+    if (c >= C) return;
+    bn_finalize_channel(c, stats, nrep, C, count, gamma, beta, rmean, rvar, momentum, eps, mean_o, invstd_o, scale_o,
+                        shift_o);
+}
+
+// up to SCD_BN_FIN_MAX layers in one launch (scd_bn_finalize_n): layer i owns blocks [b0[i], b0[i + 1])
+struct FinN {
+    scd_bn_fin_args l[SCD_BN_FIN_MAX];
+    int b0[SCD_BN_FIN_MAX + 1];
+    int n;
+};
+__global__ void bn_finalize_n_kernel(FinN f) {
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < SCD_BN_FIN_MAX; ++k)
+        if (k < f.n && (int)blockIdx.x >= f.b0[k]) i = k;
+    const scd_bn_fin_args& a = f.l[i];
+    const int blk = blockIdx.x - f.b0[i];
+    const int c = blk * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (blk == 0 && threadIdx.x == 0 && a.num_batches && a.stats) *a.num_batches += 1;
+    if (c >= a.C) return;
+    bn_finalize_channel(c, a.stats, a.nrep, a.C, a.count, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum,
+                        a.eps, a.mean, a.invstd, a.scale, a.shift);
 }
 
 // E consecutive per-channel floats (E = 4 or 8, 16-B aligned) as float4 loads
@@ -286,11 +314,9 @@ __global__ __launch_bounds__(256, BN_EW_WAVES) void bn_bwd_reduce_kernel(const T
     }
 }
 
-__global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
-                                       const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                                       float gscale, float* coef) {
-    const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (c >= C) return;
+__device__ __forceinline__ void bn_bwd_finalize_channel(int c, double* stats, int nrep, int C, double count,
+                                                        const float* gamma, const float* mean, const float* invstd,
+                                                        float* dgamma, float* dbeta, float gscale, float* coef) {
     double s, q;
     wave_collect(stats, nrep, C, c, s, q);
     if ((threadIdx.x & 63) != 0) return;
@@ -305,6 +331,31 @@ __global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double co
     coef[c] = sc;
     coef[C + c] = -sc * is * k2;
     coef[2 * C + c] = -sc * k1 + sc * is * k2 * mean[c];
+}
+
+__global__ void bn_bwd_finalize_kernel(double* stats, int nrep, int C, double count, const float* gamma,
+                                       const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                       float gscale, float* coef) {
+    const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (c >= C) return;
+    bn_bwd_finalize_channel(c, stats, nrep, C, count, gamma, mean, invstd, dgamma, dbeta, gscale, coef);
+}
+
+struct BwdFinN {
+    scd_bn_bwd_fin_args l[SCD_BN_FIN_MAX];
+    int b0[SCD_BN_FIN_MAX + 1];
+    int n;
+};
+__global__ void bn_bwd_finalize_n_kernel(BwdFinN f) {
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < SCD_BN_FIN_MAX; ++k)
+        if (k < f.n && (int)blockIdx.x >= f.b0[k]) i = k;
+    const scd_bn_bwd_fin_args& a = f.l[i];
+    const int c = (blockIdx.x - f.b0[i]) * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (c >= a.C) return;
+    bn_bwd_finalize_channel(c, a.stats, a.nrep, a.C, a.count, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.gscale,
+                            a.coef);
 }
 
 template <typename T>
@@ -581,6 +632,41 @@ extern "C" int scd_bn_finalize(double* stats, int nrep, int C, double count, con
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(fin_blocks(C)), dim3(256), 0, (hipStream_t)stream, stats, nrep, C,
                        count, gamma, beta, running_mean, running_var, num_batches, momentum, eps, mean, invstd, scale,
                        shift);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_bn_finalize_n(const scd_bn_fin_args* layers, int n, void* stream) {
+    if (!layers || n < 1 || n > SCD_BN_FIN_MAX) return SCD_ERR_ARG;
+    FinN f;
+    memset(&f, 0, sizeof(f));
+    f.n = n;
+    int blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        if (layers[i].C <= 0) return SCD_ERR_ARG;
+        f.l[i] = layers[i];
+        f.b0[i] = blocks;
+        blocks += fin_blocks(layers[i].C);
+    }
+    f.b0[n] = blocks;
+    hipLaunchKernelGGL(bn_finalize_n_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, f);
+    SCD_RETURN_LAUNCH();
+}
+
+extern "C" int scd_bn_bwd_finalize_n(const scd_bn_bwd_fin_args* layers, int n, void* stream) {
+    if (!layers || n < 1 || n > SCD_BN_FIN_MAX) return SCD_ERR_ARG;
+    BwdFinN f;
+    memset(&f, 0, sizeof(f));
+    f.n = n;
+    int blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        if (layers[i].C <= 0 || !layers[i].stats || !layers[i].invstd || !layers[i].mean || !layers[i].coef)
+            return SCD_ERR_ARG;
+        f.l[i] = layers[i];
+        f.b0[i] = blocks;
+        blocks += fin_blocks(layers[i].C);
+    }
+    f.b0[n] = blocks;
+    hipLaunchKernelGGL(bn_bwd_finalize_n_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, f);
     SCD_RETURN_LAUNCH();
 }
 

@@ -23,6 +23,8 @@
 #define scd_stats_collapse scd_stats_collapse__f16
 #define scd_stats_collapse_to scd_stats_collapse_to__f16
 #define scd_bn_finalize scd_bn_finalize__f16
+#define scd_bn_finalize_n scd_bn_finalize_n__f16
+#define scd_bn_bwd_finalize_n scd_bn_bwd_finalize_n__f16
 #define scd_bn_apply scd_bn_apply__f16
 #define scd_bn_bwd_reduce scd_bn_bwd_reduce__f16
 #define scd_bn_bwd_finalize scd_bn_bwd_finalize__f16

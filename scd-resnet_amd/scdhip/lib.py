@@ -32,6 +32,21 @@ class GemmPhase(ctypes.Structure):
                 ("dh", c_int * MAX_TAPS), ("dw", c_int * MAX_TAPS), ("wt", c_int * MAX_TAPS)]
 
 
+class BnFinArgs(ctypes.Structure):
+    """struct scd_bn_fin_args (include/scdhip.h): one layer of scd_bn_finalize_n."""
+    _fields_ = [("stats", c_void_p), ("nrep", c_int), ("C", c_int), ("count", c_double), ("gamma", c_void_p),
+                ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p), ("num_batches", c_void_p),
+                ("momentum", c_float), ("eps", c_float), ("mean", c_void_p), ("invstd", c_void_p), ("scale", c_void_p),
+                ("shift", c_void_p)]
+
+
+class BnBwdFinArgs(ctypes.Structure):
+    """struct scd_bn_bwd_fin_args (include/scdhip.h): one layer of scd_bn_bwd_finalize_n."""
+    _fields_ = [("stats", c_void_p), ("nrep", c_int), ("C", c_int), ("count", c_double), ("gamma", c_void_p),
+                ("mean", c_void_p), ("invstd", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p),
+                ("gscale", c_float), ("coef", c_void_p)]
+
+
 class PackDesc(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("out", c_void_p), ("start", c_long), ("A", c_int), ("B", c_int), ("T", c_int),
                 ("mode", c_int), ("ldp", c_int), ("row_off", c_int), ("a_off", c_int), ("a_tot", c_int)]
@@ -77,6 +92,8 @@ SIGNATURES = {
     "scd_bn_apply": (I, [I, P, P, I, L, P, P, P, P, P, I, P]),
     "scd_bn_bwd_reduce": (I, [I, P, P, P, P, P, P, P, I, L, P, P]),
     "scd_bn_bwd_finalize": (I, [P, I, I, D, P, P, P, P, P, F, P, P]),
+    "scd_bn_finalize_n": (I, [ctypes.POINTER(BnFinArgs), I, P]),
+    "scd_bn_bwd_finalize_n": (I, [ctypes.POINTER(BnBwdFinArgs), I, P]),
     "scd_bn_bwd_apply": (I, [I, P, P, P, P, P, P, I, L, P, P, P]),
     "scd_bn_bwd_reduce2": (I, [I, P, P, P, P, P, P, P, P, I, L, P, P, P]),
     "scd_bn_bwd_apply2": (I, [I, P, P, P, P, P, P, I, L, P, P, P]),

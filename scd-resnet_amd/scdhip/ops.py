@@ -1081,11 +1081,19 @@ def _bn_state(C, dev):
 
 def bn_finalize_pair(bn_a, stats_a, Ca, count_a, bn_b, stats_b, Cb, count_b):
     """Training-mode bn_finalize of two layers whose statistics are complete together (a block's bn1 and its
-    downsample BN): with SyncBN one all-reduce for both (_allreduce_stats_pair)."""
+    downsample BN): with SyncBN one all-reduce for both (_allreduce_stats_pair), and both finalizes in one launch
+    (scd_bn_finalize_n)."""
     sa, sb, nrep = _allreduce_stats_pair(stats_a, Ca, stats_b, Cb)
-    st_a = _bn_finalize_launch(bn_a, _bn_state(Ca, bn_a.weight.device), sa, nrep, Ca, count_a)
-    st_b = _bn_finalize_launch(bn_b, _bn_state(Cb, bn_b.weight.device), sb, nrep, Cb, count_b)
-    return st_a, st_b
+    sts, args = [], (L.BnFinArgs * 2)()
+    for i, (bn, stats, C, count) in enumerate(((bn_a, sa, Ca, count_a), (bn_b, sb, Cb, count_b))):
+        st = _bn_state(C, bn.weight.device)
+        st.count = count * bn_sync_world()
+        args[i] = L.BnFinArgs(ptr(stats), nrep, C, float(st.count), ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+                              ptr(bn.running_var), ptr(bn.num_batches_tracked), float(bn.momentum), float(bn.eps),
+                              ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift))
+        sts.append(st)
+    L.call("scd_bn_finalize_n", args, 2, stream())
+    return sts[0], sts[1]
 
 
 def bn_apply(y, st, relu, res=None, rst=None, out=None):
@@ -1132,8 +1140,13 @@ def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
     L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean),
            ptr(st_a.invstd), ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
     sa, sb, nrep = _allreduce_stats_pair(sa, C, sb, C)
-    ca = _bn_bwd_finalize_launch(bn_a, st_a, sa, nrep, C, alpha)
-    cb = _bn_bwd_finalize_launch(bn_b, st_b, sb, nrep, C, alpha)
+    # both backward finalizes in one launch (scd_bn_bwd_finalize_n)
+    ca, cb = torch.empty(2, 3 * C, device=sa.device).unbind(0)
+    args = (L.BnBwdFinArgs * 2)()
+    for i, (bn, st, stats, coef) in enumerate(((bn_a, st_a, sa, ca), (bn_b, st_b, sb, cb))):
+        args[i] = L.BnBwdFinArgs(ptr(stats), nrep, C, float(st.count), ptr(bn.weight), ptr(st.mean), ptr(st.invstd),
+                                 ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), alpha / bn_sync_world(), ptr(coef))
+    L.call("scd_bn_bwd_finalize_n", args, 2, stream())
     dya, dyb = torch.empty_like(y_a), torch.empty_like(y_b)
     L.call("scd_bn_bwd_apply2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(ca), ptr(cb), C, y_a.numel(),
            ptr(dya), ptr(dyb), stream())

@@ -43,6 +43,28 @@ def test_gemm_phase_struct_matches_header():
     assert ctypes.sizeof(L.GemmPhase) == 4 * (5 + 3 * L.MAX_TAPS)
 
 
+@pytest.mark.parametrize("struct,cname", [("BnFinArgs", "scd_bn_fin_args"), ("BnBwdFinArgs", "scd_bn_bwd_fin_args")])
+def test_bn_finalize_n_structs_match_header(tmp_path, struct, cname):
+    """The ctypes mirrors of the scd_bn_finalize_n / scd_bn_bwd_finalize_n layer descriptors have the C layout of
+    include/scdhip.h: size and every field offset from a C program compiled against the header with gcc."""
+    import ctypes
+
+    import scdhip.lib as L
+    S = getattr(L, struct)
+    names = [f[0] for f in S._fields_]
+    src = tmp_path / "s.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "scdhip.h"\nint main(void){printf("%zu",'
+                   ' sizeof(' + cname + '));' + "".join('printf(" %%zu", offsetof(%s, %s));' % (cname, n) for n in names)
+                   + "return 0;}\n")
+    exe = tmp_path / "s"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(S)
+    assert vals[1:] == [getattr(S, n).offset for n in names]
+    m = re.search(r"#define SCD_BN_FIN_MAX (\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) >= 2
+
+
 def test_workspace_queries():
     import scdhip.lib as L
     assert L.lib().scd_conv_wgrad_workspace(128, 9, 64, 4) == 4 * 128 * 9 * 64 * 4
