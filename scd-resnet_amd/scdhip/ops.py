@@ -930,12 +930,6 @@ class _Side:
     enabled = os.environ.get("SCD_WGRAD_STREAM", "1") != "0"
     priority = 10         # mapped to the lowest valid stream priority
     streams = {}          # device index -> side stream
-    # the split reductions of the weight gradients on a stream of their own (SCD_REDUCE_STREAM=0: behind their GEMMs
-    # on the side stream): a reduce only feeds the optimizer / the DDP buckets, so the next layer's weight-gradient GEMM
-    # need not queue behind it -- at the end of the backward the layer1 GEMMs otherwise waited for layer2's reduces
-    # while the compute stream had finished (profiles/r5_step_timeline.txt)
-    split_reduce = os.environ.get("SCD_REDUCE_STREAM", "1") != "0"
-    rstreams = {}         # device index -> reduce stream
     joined_task = {}      # device index -> graph task whose end-of-backward join is queued
 
 
@@ -970,23 +964,10 @@ def _new_side_stream(idx):
     return torch.cuda.Stream(device=idx, priority=_Side.priority)
 
 
-def reduce_stream(idx):
-    """The device's split-reduce stream (a second low-priority stream), or None when the reduces stay on the side
-    stream."""
-    if not _Side.split_reduce:
-        return None
-    r = _Side.rstreams.get(idx)
-    if r is None:
-        r = _Side.rstreams[idx] = _new_side_stream(idx)
-    return r
-
-
 def join_side_streams():
-    """Make every device's compute stream wait for its side and reduce streams (end of backward)."""
+    """Make every device's compute stream wait for its side stream (end of backward)."""
     for idx, s in _Side.streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
-    for idx, r in _Side.rstreams.items():
-        torch.cuda.current_stream(idx).wait_stream(r)
     _Side.joined_task.clear()
 
 
@@ -997,12 +978,6 @@ def side_stream_for_comm(dev):
     s = _Side.streams.get(idx)
     if s is None or _graph_task() == -1:
         return None
-    r = _Side.rstreams.get(idx)
-    if r is not None:
-        # the reduces write the gradients last: issue from their stream, ordered after the other two
-        r.wait_stream(torch.cuda.current_stream(idx))
-        r.wait_stream(s)
-        return r
     s.wait_stream(torch.cuda.current_stream(idx))
     return s
 
@@ -1015,20 +990,17 @@ def _conv_wgrad_side(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate
     side = side_stream(g.device) if g.is_cuda else None
     if side is None:
         return _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows, red_taps)
-    red = reduce_stream(g.device.index if g.device.index is not None else torch.cuda.current_device())
     with torch.cuda.stream(side):
-        _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows, red_taps, red_stream=red)
+        _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid, accumulate, rows, red_taps)
     g.record_stream(side)
     x.record_stream(side)
 
 
-def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None, red_taps=1,
-                red_stream=None):
+def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True, rows=None, red_taps=1):
     """Weight gradient of the gather-GEMM: dst[(r-r0)*ld_n + ci*ld_c + t*ld_t] (+)= sum_pix g[pix,r] x[gather,ci].
 
     g: (N,Ho,Wo,Cg) NHWC output-gradient; x: (N,Hi,Wi,Ci) NHWC input; taps gather
     x at (stride*oh + r - pad, stride*ow + s - pad).  `rows` = list of (r0, r1, dst, ld) slices.
-    red_stream: run the split reduce there, ordered after the GEMM (the workspace is recorded on it).
     """
     N, Ho, Wo, Cg = g.shape
     _, Hi, Wi, Ci = x.shape
@@ -1044,15 +1016,6 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
     dh, dw, ns, wsn = plan
     ws = torch.empty(wsn, dtype=torch.float32, device=g.device)
     L.call("scd_conv_wgrad", d, ptr(g), ptr(x), ptr(ws), ns, N, Ho, Wo, Cg, Hi, Wi, Ci, stride, T, dh, dw, stream())
-    if red_stream is not None:
-        red_stream.wait_stream(torch.cuda.current_stream())
-        ws.record_stream(red_stream)
-        with torch.cuda.stream(red_stream):
-            return _wgrad_reduce(g, ws, ns, Cg, T, Ci, dst, ld, cvalid, accumulate, rows, red_taps)
-    return _wgrad_reduce(g, ws, ns, Cg, T, Ci, dst, ld, cvalid, accumulate, rows, red_taps)
-
-
-def _wgrad_reduce(g, ws, ns, Cg, T, Ci, dst, ld, cvalid, accumulate, rows, red_taps):
     if rows is None:
         rows = [(0, Cg, dst, ld)]
     # red_taps: read the T*Ci workspace columns as red_taps taps of T*Ci/red_taps channels (a 1x1 GEMM over
