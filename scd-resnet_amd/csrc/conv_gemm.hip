@@ -2375,44 +2375,23 @@ constexpr int L1W_NBUF = SCD_ABLATE == 45 ? 3 : SCD_ABLATE == 47 ? 4 : 2;
 __device__ __forceinline__ int l1w_f(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 1); }
 __device__ __forceinline__ int l1w_addr(int r, int unit, int pp) { return r * 128 + ((unit ^ l1w_f(r)) << 5) + 8 * pp; }
 
-// HALF (round 5): two workgroups of 4 waves per CU, workgroup h owning the input slices u = 2h, 2h + 1 of one pixel
-// range (the two are blocks b and b + 8: the same XCD, so the halo and output-gradient stages they both fetch come
-// from one L2).  The full-CU form's 8 waves meet at one barrier per stage, so on every SIMD both waves read their
-// fragments, then both run their MFMAs, then both wait for the next stage's DMA; with two independent workgroups per
-// CU one workgroup's MFMAs run while the other reads or waits (the same per-wave fragment reads per MFMA, twice the
-// stage DMA per CU).
-template <bool HALF>
-__global__ __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1) void conv_wgrad_l1_kernel(WgradParams p) {
-    constexpr int NW = HALF ? 4 : 8;                // waves per workgroup
-    constexpr int JH = (L1W_NHDMA + NW - 1) / NW;   // halo DMA instructions per wave (at most)
-    static_assert(!HALF || L1W_NBUF == 2, "the half-CU form keeps two stage buffers");
+__global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
     __shared__ __attribute__((aligned(16))) char smem[L1W_NBUF * L1W_STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int z, u, ks;                                   // split, input slice, k-step of each stage
-    if constexpr (HALF) {
-        const int b = blockIdx.x;
-        const bool grouped = (p.nsplit & 7) == 0;
-        z = grouped ? (b >> 4) * 8 + (b & 7) : b >> 1;
-        const int h = grouped ? (b >> 3) & 1 : b & 1;
-        u = 2 * h + (wave & 1);
-        ks = wave >> 1;
-    } else {
-        z = blockIdx.x;
-        u = wave & 3;
-        ks = wave >> 2;
-    }
+    const int u = wave & 3, ks = wave >> 2;         // input slice, k-step of each stage
+    const int z = blockIdx.x;
     const int M = p.N * p.Ho * p.Wo;
     const int pix0 = min(M, z * p.chunk), pix1 = min(M, pix0 + p.chunk);
     const int H = p.Ho, W = p.Wo;
 
-    // halo DMA: instruction i = wave + NW j (i < 27) fills region i / 9, rows 8 (i % 9) .. +7; lane: row + lane / 8,
+    // halo DMA: instruction i = wave + 8 j (i < 27) fills region i / 9, rows 8 (i % 9) .. +7; lane: row + lane / 8,
     // 16-B slot lane % 8 (source chunk swizzled)
-    int h_dy[JH], h_dx[JH], h_c8[JH];
-    bool h_ok[JH];
+    int h_dy[4], h_dx[4], h_c8[4];
+    bool h_ok[4];
 #pragma unroll
-    for (int j = 0; j < JH; ++j) {
-        const int i = wave + NW * j;
+    for (int j = 0; j < 4; ++j) {
+        const int i = wave + 8 * j;
         const int reg = i / 9, col = 8 * (i - reg * 9) + (lane >> 3);
         const int c = (lane & 7) ^ (l1w_f(col) << 1);
         h_ok[j] = col < L1W_HC;
@@ -2420,14 +2399,8 @@ __global__ __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1) void conv_wgrad_l1_
         h_dx[j] = col - 1;
         h_c8[j] = c * 8;
     }
-    // output-gradient DMA: 64 pixel rows of 128 B, 8 rows per instruction, 8 / NW instructions per wave
-    constexpr int NG = 8 / NW;
-    int g_R[NG], g_c8[NG];
-#pragma unroll
-    for (int j = 0; j < NG; ++j) {
-        g_R[j] = 8 * (wave + NW * j) + (lane >> 3);
-        g_c8[j] = ((lane & 7) ^ (l1w_f(g_R[j]) << 1)) * 8;
-    }
+    const int g_R = 8 * wave + (lane >> 3);
+    const int g_c8 = ((lane & 7) ^ (l1w_f(g_R) << 1)) * 8;
 
     int sn, soh, sow;
     {
@@ -2454,8 +2427,8 @@ __global__ __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1) void conv_wgrad_l1_
     auto issue = [&](int k0, char* buf) {
         const int S = __builtin_amdgcn_readfirstlane(((sn * H + soh) * W + sow) * 64);
 #pragma unroll
-        for (int j = 0; j < JH; ++j) {
-            const int i = wave + NW * j;
+        for (int j = 0; j < 4; ++j) {
+            const int i = wave + 8 * j;
             if (i < L1W_NHDMA) {
                 const int reg = i / 9;
                 const bool ok = h_ok[j] & (k0 < pix1) & ((unsigned)(soh + h_dy[j]) < (unsigned)H) &
@@ -2464,10 +2437,7 @@ __global__ __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1) void conv_wgrad_l1_
                           sel_off(ok, (S + (h_dy[j] * W + h_dx[j]) * 64 + h_c8[j]) * 2));
             }
         }
-#pragma unroll
-        for (int j = 0; j < NG; ++j)
-            dma16_asm(grs, buf + L1W_HBYTES + (wave + NW * j) * 1024,
-                      sel_off(k0 + g_R[j] < pix1, ((k0 + g_R[j]) * 64 + g_c8[j]) * 2));
+        dma16_asm(grs, buf + L1W_HBYTES + wave * 1024, sel_off(k0 + g_R < pix1, ((k0 + g_R) * 64 + g_c8) * 2));
     };
 
     const int l16 = lane & 15, lg = lane >> 4;
@@ -2581,10 +2551,9 @@ __global__ __launch_bounds__(HALF ? 256 : 512, HALF ? 2 : 1) void conv_wgrad_l1_
     __syncthreads();
     static_assert(2 * 36 * 64 * 16 <= L1W_NBUF * L1W_STAGE, "reduction buffer");
     f32x4* xch = (f32x4*)smem;
-    // (HALF: the workgroup's two slices in one round)
 #pragma unroll
-    for (int round = 0; round < (HALF ? 1 : 2); ++round) {
-        const bool mine = HALF || (u >> 1) == round;
+    for (int round = 0; round < 2; ++round) {
+        const bool mine = (u >> 1) == round;
         f32x4* slot = xch + (u & 1) * 36 * 64;
         if (mine && ks == 1) {
 #pragma unroll
@@ -3108,12 +3077,6 @@ static bool wgrad_use_l1(int dtype, long M, int Ho, int Wo, int Cg, int T, int C
            (long)Ho * Wo * 64 <= (1L << 30) && M >= 64;
 }
 
-// the half-CU form of the layer1 weight gradient (two workgroups per CU, conv_wgrad_l1_kernel<true>); read per call
-static bool wgrad_l1_half() {
-    const char* e = getenv("SCD_WGRAD_L1_HALF");
-    return e ? atoi(e) != 0 : true;
-}
-
 // >= 16 stages per workgroup, at most 128 workgroups (SCD_WGRAD_L1_NSPLIT): in the step this kernel shares the chip
 // with the compute stream's last layer1 / stem kernels, and half the splits halve its 64 x 576 fp32 slab reduce
 // (measured +1% per step against 256)
@@ -3241,10 +3204,7 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
         for (int t = 0; t < 9; ++t) std_taps &= dh[t] == t / 3 - 1 && dw[t] == t % 3 - 1;
         if (std_taps) {
             p.nsplit = nsplit;
-            if (wgrad_l1_half())
-                hipLaunchKernelGGL(conv_wgrad_l1_kernel<true>, dim3(2 * nsplit), dim3(256), 0, (hipStream_t)stream, p);
-            else
-                hipLaunchKernelGGL(conv_wgrad_l1_kernel<false>, dim3(nsplit), dim3(512), 0, (hipStream_t)stream, p);
+            hipLaunchKernelGGL(conv_wgrad_l1_kernel, dim3(nsplit), dim3(512), 0, (hipStream_t)stream, p);
             SCD_RETURN_LAUNCH();
         }
     }

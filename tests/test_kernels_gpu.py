@@ -757,32 +757,6 @@ def test_conv_wgrad_layer1(case, dtype):
     test_conv_fwd_dgrad_wgrad(case, dtype)
 
 
-@pytest.mark.parametrize("nsplit", [8, 13, 128])
-@pytest.mark.parametrize("N,H,W", [(32, 128, 128), (3, 64, 64), (2, 32, 192)])
-def test_conv_wgrad_layer1_half_matches_full(N, H, W, nsplit, monkeypatch):
-    """The layer1 weight gradient's two-workgroups-per-CU form (conv_wgrad_l1_kernel<true>: each workgroup two of the
-    four input slices) writes the same slab bits as the one-workgroup form, for split counts in whole XCD groups
-    (the pair on one XCD) and not (13: the linear pairing)."""
-    from scdhip import ops
-    L = ops.L
-    g = torch.Generator().manual_seed(81)
-    C = 64
-    dy = nhwc(torch.randn(N, C, H, W, generator=g), torch.bfloat16)
-    x = nhwc(torch.randn(N, C, H, W, generator=g), torch.bfloat16)
-    dh = L.int_array([t // 3 - 1 for t in range(9)])
-    dw = L.int_array([t % 3 - 1 for t in range(9)])
-    out = {}
-    for half in ("1", "0"):
-        monkeypatch.setenv("SCD_WGRAD_L1_HALF", half)
-        ws = torch.full((nsplit * C * 9 * C,), float("nan"), device=DEV)
-        L.call("scd_conv_wgrad", L.DT_BF16, ops.ptr(dy), ops.ptr(x), ops.ptr(ws), nsplit, N, H, W, C, H, W, C, 1, 9, dh,
-               dw, ops.stream())
-        torch.cuda.synchronize()
-        out[half] = ws
-    assert not torch.isnan(out["1"]).any()
-    assert torch.equal(out["1"], out["0"])
-
-
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 # (tiles of 256 px >= 2 x CUs give runs of 2..16 tiles per workgroup: the row ring is reused; fewer: one tile each)
 @pytest.mark.parametrize("N,H,W", [(4, 128, 128), (3, 64, 64), (2, 32, 128), (16, 128, 128), (64, 64, 64),
