@@ -1213,17 +1213,31 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
     constexpr int CPR = WCOLS * 2 / 16;                      // 16-B chunks per staged row (8 or 6)
     // output element offset of tile row `row` (< 128 of this group), channel `col` (M-range checked by the caller)
-    auto out_off = [&](int m, int col) -> long {
-        const int n = m / QQ;
-        const int rem = m - n * QQ;
-        const int qh = rem / ph.Qw;
-        const int qw = rem - qh * ph.Qw;
-        const int oh = p.os * qh + ph.rho_h, ow = p.os * qw + ph.rho_w;
+    // the store loops walk a lane's pixels m, m + RPI, m + 2 RPI, ... of the tile: (n, qh, qw) advanced by
+    // additions instead of two integer divisions per 16-B store (~50 VALU each, 16 stores per lane and tile)
+    struct PixPos { int n, qh, qw; };
+    auto pix_of = [&](int m) -> PixPos {
+        PixPos q;
+        q.n = m / QQ;
+        const int rem = m - q.n * QQ;
+        q.qh = rem / ph.Qw;
+        q.qw = rem - q.qh * ph.Qw;
+        return q;
+    };
+    auto pix_advance = [&](PixPos& q, int step) {
+        q.qw += step;
+        while (q.qw >= ph.Qw) {
+            q.qw -= ph.Qw;
+            if (++q.qh == ph.Qh) { q.qh = 0; ++q.n; }
+        }
+    };
+    auto out_off = [&](const PixPos& q, int col) -> long {
+        const int oh = p.os * q.qh + ph.rho_h, ow = p.os * q.qw + ph.rho_w;
         if (p.shuf) {
             const int c4 = p.Co >> 2, sp = col / c4;
-            return ((long)(n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 + (col - sp * c4);
+            return ((long)(q.n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 + (col - sp * c4);
         }
-        return ((long)(n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+        return ((long)(q.n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
     };
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -1280,13 +1294,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
 #pragma unroll
         for (int e = 0; e < EPC; ++e) { bs8[e] = 0.f; bq8[e] = 0.f; }
         constexpr int NIT = (128 + RPI - 1) / RPI;
+        PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
 #pragma unroll 4
         for (int it = 0; it < NIT; ++it) {
             const int row = it * RPI + rsub;
             const int m = mt * BM + 128 * grp + row;
             const bool ok = cok && row < 128 && m < M;
             // every load from a valid address (row 0 / pixel 0 when masked off): no branch around the loads
-            const long off = out_off(ok ? m : 0, cl);
+            const long off = ok ? out_off(pq, cl) : 0;
+            pix_advance(pq, RPI);
             uint4 v = *(const uint4*)(ep + (ok ? row : 0) * EROW + chx * 16);
             T* dst = (T*)(p.y) + off;
             if (p.accumulate) {
@@ -1312,15 +1328,20 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             }
         }
     } else {
-        // (128 * CPR is a multiple of 64: the same trip count in every lane) rows past M / columns past Co compute on
-        // a valid address (pixel 0, channel 0) and skip only the store: no branch around the accumulate load
-        for (int idx = lane; idx < 128 * CPR; idx += 64) {
-            const int row = idx / CPR, ch = idx - (idx / CPR) * CPR;
+        // lane: 16-B channel chunk chx of rows rsub, rsub + RPI, ... (RPI = 64 / CPR rows per pass; 4 lanes idle when
+        // CPR = 6).  Rows past M / columns past Co compute on a valid address (pixel 0, channel 0) and skip only the
+        // store: no branch around the accumulate load
+        constexpr int NIT = (128 + RPI - 1) / RPI;
+        const int col = nt * BN + wc * WCOLS + chx * EPC;
+        PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
+#pragma unroll 4
+        for (int it = 0; it < NIT; ++it) {
+            const int row = it * RPI + rsub;
             const int m = mt * BM + 128 * grp + row;
-            const int col = nt * BN + wc * WCOLS + ch * EPC;
-            const bool ok = m < M && col < p.Co;
-            T* dst = (T*)(p.y) + out_off(ok ? m : 0, ok ? col : 0);
-            uint4 v = *(const uint4*)(ep + row * EROW + ch * 16);
+            const bool ok = rsub < RPI && row < 128 && m < M && col < p.Co;
+            T* dst = (T*)(p.y) + (ok ? out_off(pq, col) : 0);
+            pix_advance(pq, RPI);
+            uint4 v = *(const uint4*)(ep + (ok ? row : 0) * EROW + chx * 16);
             if (p.accumulate) {
                 float a[EPC], o[EPC];
                 Vec16<T>::load(&v, a);

@@ -162,17 +162,25 @@ __global__ __launch_bounds__(256) void cpool_bwd_kernel(int dir, const T* __rest
             V::load(&cx[u], v);
             V::load(&cg[u], g);
             V::store(dx + ln.start + (long)k * ln.sstep, zero);
+            // the record test and the run state as selects; the closed runs' element stores in ONE branch region
+            // per position, entered only when some element has a record here (rare after the first positions)
+            bool rec[E];
+            bool any = false;
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const bool rec = (k == 0) || (v[e] > mv[e]);
-                if (rec) {
-                    if (k > 0) dx[ln.start + (long)rk[e] * ln.sstep + e] = from_f<T>(acc[e]);
-                    mv[e] = v[e];
-                    acc[e] = g[e];
-                    rk[e] = k;
-                } else {
-                    acc[e] += g[e];
-                }
+                rec[e] = (k == 0) || (v[e] > mv[e]);
+                any |= rec[e] && k > 0;
+            }
+            if (any) {
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (rec[e]) dx[ln.start + (long)rk[e] * ln.sstep + e] = from_f<T>(acc[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                mv[e] = rec[e] ? v[e] : mv[e];
+                acc[e] = rec[e] ? g[e] : acc[e] + g[e];
+                rk[e] = rec[e] ? k : rk[e];
             }
         }
 #pragma unroll
