@@ -22,6 +22,9 @@
 #ifndef SCD_ABLATE
 #define SCD_ABLATE 0
 #endif
+#ifndef S1X1_UA2
+#define S1X1_UA2 1    // conv1x1_stream_kernel: 32-pixel units where K = 64 (A/B build option)
+#endif
 #ifndef WGRAD_OCC
 #define WGRAD_OCC 2   // register-staged weight-gradient kernel: workgroups per CU the registers are budgeted for
 #endif
@@ -2712,8 +2715,266 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st, int ks = 1) {
     SCD_RETURN_LAUNCH();
 }
 
+// -------------------------------------------------------------------------------------
+// Streaming 1x1 GEMM for the HBM-bound 1x1 convolutions: stride 1, K = Ci in {64, 128, 256} channels in, N = Co in
+// {64, 128, 256} out, M pixels with M % 128 == 0 -- the Res50 Bottleneck layer1 convs and the conv3 / conv1 /
+// downsample input gradients at 1024^2 (residuals.py:122-165).  y[m][n] = sum_k x[m][k] w[n][k] moves 2(K + N) bytes
+// per pixel for 2KN flops (64 flops per byte at K = 256, N = 64), so HBM bounds it; the tiled GEMMs (one 256-pixel
+// tile per workgroup, one workgroup per CU, load -> compute -> store in sequence) ran these shapes at 2-3 TB/s.
+// Here the packed weights [N][K] stay in LDS for the workgroup's whole run (cpw chunks of 128 pixels, taken by the
+// waves as units of 16 or 32 pixels in turn), the operand goes from HBM straight into the MFMA fragments (16-B loads, K/32
+// per lane and unit) one unit ahead of its MFMAs, and 2-4 workgroups per CU keep 8-16 waves' loads outstanding.
+// Operands of the epilogue (the old output when accumulating, the pre-BN activation for the BN-backward sums) are
+// loaded before the next unit's operand, so no wait on them drains the prefetch.  SPL = 2: the waves work in pairs
+// on the same pixels, each on half of the N channels (the pair's second operand read hits L2), SPL = 4 all four on a
+// quarter each, so a wave's sums cover 64 channels at N = 128 / 256 as well.
+// Per output the MFMA chain is that of the ping-pong / ring / register-staged kernels (k in steps of 32, ascending;
+// weights as the A operand), so the outputs are the same bits.  Epilogue: channel blocks paired with
+// v_permlane16_swap (a lane then holds 8 consecutive channels of one pixel: 16-B stores); MODE 0 stores (+ forward BN
+// sums of the fp32 values when p.stats), 1 accumulates as the staged epilogues do (round(round(acc) + old)), 2 adds
+// the following BN+ReLU layer's backward sums (scd_conv_gemm_bnbwd: dz = stored gradient where y*rsc + rsh > 0).
+// The sums (64 channels per wave): per-lane partials over the run, 16-lane DPP sums, the waves' partials in a fixed
+// order, one fp64 replica add per channel and workgroup.
+template <int K, int N, int MODE, int SPL, int UA>
+__global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(GemmParams p, int cpw) {
+    typedef __bf16 T;
+    typedef __attribute__((ext_vector_type(4))) __bf16 hv4;
+    typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+    constexpr int KS = K / 32;                              // MFMA k-steps
+    constexpr int NH = N / SPL;                             // channels per wave
+    constexpr int NB = NH / 16;                             // 16-channel blocks per wave
+    constexpr int PXW = 4 / SPL;                            // waves on different pixels
+    constexpr int UP = 16 * UA;                             // pixels per unit (UA 16-pixel blocks)
+    constexpr int XM = (K / 8 >= 16 ? 16 : K / 8) - 1;      // LDS swizzle: chunk c of row r at c ^ (r & XM)
+    constexpr bool SUMS = NH == 64 && MODE != 1;
+    constexpr int NS = SUMS ? 4 * NB : 1;                   // per-lane channel slots of the sums
+    constexpr int WBYTES = N * K * 2;
+    constexpr int PBYTES = MODE == 2 ? 4 * N * 4 : 0;       // BN parameters (mean, invstd, relu scale / shift)
+    static_assert(NB % 2 == 0 && K % 64 == 0 && (SPL == 1 || SPL == 2 || SPL == 4), "shape");
+    static_assert(WBYTES >= PXW * N * 8, "sum exchange fits the weight buffer");
+    __shared__ __attribute__((aligned(16))) char smem[WBYTES + PBYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int pw = wave / SPL;                              // pixel wave
+    const int c0w = (wave % SPL) * NH;                      // the wave's first channel
+    for (int i = tid; i < N * K / 8; i += 256) {
+        const int r = i / (K / 8), c = i - r * (K / 8);
+        const uint4 v = *(const uint4*)(p.w + ((long)r * p.wrow + c * 8) * 2);
+        *(uint4*)(smem + r * K * 2 + ((c ^ (r & XM)) << 4)) = v;
+    }
+    float* bnp = (float*)(smem + WBYTES);
+    if constexpr (MODE == 2) {
+        for (int i = tid; i < N; i += 256) {
+            bnp[i] = p.bn_mean[i];
+            bnp[N + i] = p.bn_invstd[i];
+            bnp[2 * N + i] = p.bn_rsc[i];
+            bnp[3 * N + i] = p.bn_rsh[i];
+        }
+    }
+    __syncthreads();
+
+    const long chunk0 = (long)blockIdx.x * cpw;
+    const bool stats_on = SUMS && p.stats != nullptr;
+    float ssum[NS], ssq[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
+    // lane's store column of channel-block pair (b, b + 1): even lg block b, odd lg block b + 1 (permlane16_swap)
+    const int cst = c0w + 4 * lg + 12 * (lg & 1);
+
+    auto pix0 = [&](int u) -> long { return chunk0 * 128 + (u * PXW + pw) * UP; };
+    auto load_unit = [&](int u, bf16x8 (&xf)[UA][KS]) {
+#pragma unroll
+        for (int a = 0; a < UA; ++a) {
+            const char* row = p.x + ((pix0(u) + 16 * a + l16) * K + 8 * lg) * 2;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) xf[a][s] = *(const bf16x8*)(row + s * 64);
+        }
+    };
+    auto load_epi = [&](int u, uint4 (&ev)[UA][NB / 2]) {
+        if constexpr (MODE != 0) {
+            const char* src = MODE == 1 ? (const char*)p.y : p.bny;
+#pragma unroll
+            for (int a = 0; a < UA; ++a)
+#pragma unroll
+                for (int pb = 0; pb < NB / 2; ++pb)
+                    ev[a][pb] = *(const uint4*)(src + ((pix0(u) + 16 * a + l16) * N + 32 * pb + cst) * 2);
+        }
+    };
+    auto unit = [&](int u, const bf16x8 (&xf)[UA][KS], const uint4 (&ev)[UA][NB / 2]) {
+        f32x4 acc[UA][NB];
+#pragma unroll
+        for (int a = 0; a < UA; ++a)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        // the weight fragments are re-read from LDS per unit (an opaque base keeps the compiler from hoisting all
+        // KS x NB of them into registers for the whole run)
+        int wo = (c0w + l16) * K * 2;
+        asm volatile("" : "+v"(wo));
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int r = c0w + 16 * b + l16;
+                const bf16x8 wf = *(const bf16x8*)(smem + wo + 16 * b * K * 2 + (((4 * s + lg) ^ (r & XM)) << 4));
+#pragma unroll
+                for (int a = 0; a < UA; ++a)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[a][s], acc[a][b], 0, 0, 0);
+            }
+        if constexpr (MODE == 0 && SUMS) {
+            if (stats_on) {
+#pragma unroll
+                for (int a = 0; a < UA; ++a)
+#pragma unroll
+                    for (int b = 0; b < NB; ++b)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const float v = acc[a][b][i];
+                            ssum[4 * b + i] += v;
+                            ssq[4 * b + i] += v * v;
+                        }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < UA; ++a)
+#pragma unroll
+        for (int pb = 0; pb < NB / 2; ++pb) {
+            const long m = pix0(u) + 16 * a + l16;
+            hv4 h0, h1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { h0[i] = (T)acc[a][2 * pb][i]; h1[i] = (T)acc[a][2 * pb + 1][i]; }
+            const u32x2 x = __builtin_bit_cast(u32x2, h0), y = __builtin_bit_cast(u32x2, h1);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(x[0], y[0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(x[1], y[1], false, false);
+            uint4 st;
+            st.x = s0[0]; st.y = s1[0]; st.z = s0[1]; st.w = s1[1];
+            if constexpr (MODE == 1) {
+                float a8[8], o8[8];
+                Vec16<T>::load(&st, a8);
+                Vec16<T>::load(&ev[a][pb], o8);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a8[e] += o8[e];
+                Vec16<T>::store(&st, a8);
+            }
+            if constexpr (MODE == 2) {
+                float d8[8], y8[8], mu[8], is[8], sc[8], sh[8];
+                Vec16<T>::load(&st, d8);
+                Vec16<T>::load(&ev[a][pb], y8);
+                const int c0 = 32 * pb + cst;
+#pragma unroll
+                for (int e = 0; e < 8; e += 4) {
+                    const float4 f0 = *(const float4*)(bnp + c0 + e), f1 = *(const float4*)(bnp + N + c0 + e);
+                    const float4 f2 = *(const float4*)(bnp + 2 * N + c0 + e), f3 = *(const float4*)(bnp + 3 * N + c0 + e);
+                    mu[e] = f0.x; mu[e + 1] = f0.y; mu[e + 2] = f0.z; mu[e + 3] = f0.w;
+                    is[e] = f1.x; is[e + 1] = f1.y; is[e + 2] = f1.z; is[e + 3] = f1.w;
+                    sc[e] = f2.x; sc[e + 1] = f2.y; sc[e + 2] = f2.z; sc[e + 3] = f2.w;
+                    sh[e] = f3.x; sh[e + 1] = f3.y; sh[e + 2] = f3.z; sh[e + 3] = f3.w;
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float dz = y8[e] * sc[e] + sh[e] > 0.f ? d8[e] : 0.f;
+                    ssum[8 * pb + e] += dz;
+                    ssq[8 * pb + e] += dz * (y8[e] - mu[e]) * is[e];
+                }
+            }
+            *(uint4*)((T*)p.y + m * N + 32 * pb + cst) = st;
+        }
+    };
+
+    bf16x8 xa[UA][KS], xb[UA][KS];
+    uint4 ea[UA][NB / 2], eb[UA][NB / 2];
+    load_unit(0, xa);
+    // an even number of units per wave; the prefetch past the run re-reads its last unit (clamped: every load from a
+    // valid address)
+    const int nu = cpw * (128 / (UP * PXW));
+    for (int u = 0; u < nu; u += 2) {
+        load_epi(u, ea);
+        load_unit(u + 1, xb);
+        unit(u, xa, ea);
+        load_epi(u + 1, eb);
+        load_unit(min(u + 2, nu - 1), xa);
+        unit(u + 1, xb, eb);
+    }
+    if constexpr (SUMS) {
+        if (MODE == 2 || stats_on) {
+            __syncthreads();                                 // every wave is done with the weights: LDS reused
+            float* red = (float*)smem;                       // [pixel wave][N][2]
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const float s = row16_sum(ssum[j]), q = row16_sum(ssq[j]);
+                if (l16 == 0) {
+                    const int c = MODE == 2 ? 32 * (j >> 3) + cst + (j & 7) : c0w + 16 * (j >> 2) + 4 * lg + (j & 3);
+                    red[(pw * N + c) * 2] = s;
+                    red[(pw * N + c) * 2 + 1] = q;
+                }
+            }
+            __syncthreads();
+            if (tid < N) {
+                double s = 0.0, q = 0.0;
+#pragma unroll
+                for (int w = 0; w < PXW; ++w) { s += red[(w * N + tid) * 2]; q += red[(w * N + tid) * 2 + 1]; }
+                const int rep = (int)(blockIdx.x % SCD_STAT_REPLICAS);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + tid, s);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + tid, q);
+            }
+        }
+    }
+}
+
 SCD_KERNEL_NS_END
 }  // namespace
+
+// conv1x1_stream_kernel: -1 when the shape is not one it takes, else the launch status.  SCD_GEMM_STREAM1X1 (read
+// per call: tests compare the kernels bit for bit): 0 keeps these shapes on the tiled kernels, 2 (tests) makes every
+// GEMM the stream kernel does not take fail with SCD_ERR_ARG
+static int stream1x1_mode() {
+    const char* e = getenv("SCD_GEMM_STREAM1X1");
+    return e ? atoi(e) : 1;
+}
+static int num_cus();
+static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm_phase* phases, long Mtot,
+                            hipStream_t st) {
+    if (dtype != SCD_DT_BF16 || stream1x1_mode() == 0) return -1;
+    if (nphase != 1 || p.is != 1 || p.os != 1 || p.head_on || p.bias || p.relu || p.shuf) return -1;
+    const scd_gemm_phase& ph = phases[0];
+    if (ph.ntaps != 1 || ph.dh[0] || ph.dw[0] || ph.wt[0] || ph.rho_h || ph.rho_w || ph.Qh != p.Ho || ph.Qw != p.Wo ||
+        p.Hi != p.Ho || p.Wi != p.Wo || p.wrow != p.Ci)
+        return -1;
+    const int K = p.Ci, N = p.Co;
+    if (Mtot % 128 || Mtot < 131072 || Mtot * (long)(K > N ? K : N) >= (1L << 30)) return -1;
+    const bool sums = p.stats != nullptr;                    // forward statistics or BN-backward sums
+    if (p.accumulate && sums) return -1;
+    const long nchunks = Mtot / 128;
+    const long cus = num_cus();
+    long cpw = 2;
+    while (nchunks % (2 * cpw) == 0 && nchunks / (2 * cpw) >= 2 * cus) cpw *= 2;
+    if (nchunks % cpw) return -1;
+    const int grid = (int)(nchunks / cpw);
+    const int mode = p.bnbwd ? 2 : (p.accumulate ? 1 : 0);
+    // (two 16-pixel blocks per unit at K = 64 and <= 64 channels per wave: 4-KB operand loads per wave in flight; not
+    // with the BN-backward sums, whose registers it would spill)
+#define SCD_S1X1(KK, NN, MM, SS)                                                                                     \
+    if (K == KK && N == NN && mode == MM) {                                                                          \
+        constexpr int UA_ = (S1X1_UA2 && KK == 64 && NN / SS <= 64 && MM != 2) ? 2 : 1;                              \
+        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UA_>), dim3(grid), dim3(256), 0, st, p, (int)cpw); \
+        SCD_RETURN_LAUNCH();                                                                                         \
+    }
+    // N = 64: one wave per pixel unit; N = 128 / 256: 2 / 4 waves split the channels when there are sums to take (the
+    // per-lane partials of 64 channels), whole-width waves otherwise
+    SCD_S1X1(64, 64, 0, 1) SCD_S1X1(64, 64, 1, 1) SCD_S1X1(64, 64, 2, 1)
+    SCD_S1X1(128, 64, 0, 1) SCD_S1X1(128, 64, 1, 1) SCD_S1X1(128, 64, 2, 1)
+    SCD_S1X1(256, 64, 0, 1) SCD_S1X1(256, 64, 1, 1) SCD_S1X1(256, 64, 2, 1)
+    if (sums) {
+        SCD_S1X1(64, 128, 0, 2) SCD_S1X1(128, 128, 0, 2) SCD_S1X1(256, 128, 0, 2)
+        SCD_S1X1(64, 128, 2, 2) SCD_S1X1(128, 128, 2, 2) SCD_S1X1(256, 128, 2, 2)
+        SCD_S1X1(64, 256, 0, 4) SCD_S1X1(128, 256, 0, 4)
+    } else {
+        SCD_S1X1(64, 256, 0, 1) SCD_S1X1(64, 256, 1, 1) SCD_S1X1(128, 256, 0, 1)
+        SCD_S1X1(64, 128, 0, 1) SCD_S1X1(64, 128, 1, 1) SCD_S1X1(128, 128, 0, 1) SCD_S1X1(128, 128, 1, 1)
+        SCD_S1X1(256, 128, 0, 1) SCD_S1X1(256, 128, 1, 1)
+    }
+#undef SCD_S1X1
+    return -1;
+}
 
 // Kernel choice: the LDS-DMA ring kernel (256x128, bf16) for large outputs, the register-staged
 // 128x128 kernel otherwise, 256x64 for narrow outputs (Co <= 64).  SCD_GEMM_RING=0/1 forces it off/on.
@@ -2823,6 +3084,11 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         for (int t = 0; t < phases[i].ntaps; ++t)
             if (phases[i].wt[t] < 0 || (long)(phases[i].wt[t] + 1) * p.Ci > p.wrow) return SCD_ERR_ARG;
         Mtot += (long)p.N * phases[i].Qh * phases[i].Qw;
+    }
+    {
+        const int rc = launch_stream1x1(dtype, p, nphase, phases, Mtot, (hipStream_t)stream);
+        if (rc >= 0) return rc;
+        if (stream1x1_mode() == 2) return SCD_ERR_ARG;
     }
     if (p.head_on && dtype == SCD_DT_BF16 && heads384_mode() && nphase == 1 && p.Co == 384 && p.head_out[0] &&
         p.head_out[1] && p.head_out[2] && !p.head_out[3] && p.is == 1 && p.os == 1 && p.Ho == phases[0].Qh &&

@@ -806,6 +806,73 @@ def test_conv_l1p_matches_register_staged(N, H, W, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K,C", [(64, 64), (128, 64), (256, 64), (64, 128), (256, 128), (64, 256), (128, 256)])
+def test_conv1x1_stream_matches_tiled(K, C, dtype, monkeypatch):
+    """conv1x1_stream_kernel (HBM-bound stride-1 1x1 GEMMs: weights resident in LDS, operands streamed into the MFMA
+    fragments; the Res50 layer1 1x1 convs, residuals.py:122-165) against the tiled kernels on the same shapes: the
+    forward K -> C with its BN statistics, the input gradient C -> K, its += form and the BN-backward-sum form, each
+    where the stream kernel is built for the GEMM shape (K_gemm, N_gemm).  Outputs are bit-identical (same MFMA chain
+    per output); statistics and BN sums agree to fp32 summation-order noise.  SCD_GEMM_STREAM1X1=2 fails any GEMM the
+    stream kernel does not take, so the "2" results are its own."""
+    from scdhip import ops
+    sums = {(64, 64), (128, 64), (256, 64), (64, 128), (128, 128), (256, 128), (64, 256), (128, 256)}
+    plain = sums
+    accum = {(64, 64), (128, 64), (256, 64), (64, 128), (128, 128), (256, 128), (64, 256)}
+    bnbwd = {(64, 64), (128, 64), (256, 64), (64, 128), (128, 128), (256, 128)}
+    g = torch.Generator().manual_seed(113)
+    N, H, W = 2, 256, 256                                    # M = 131,072 pixels (the kernel's lower bound)
+    x = nhwc(torch.randn(N, K, H, W, generator=g), dtype)
+    w = (torch.randn(C, K, 1, 1, generator=g) / K ** 0.5).to(DEV)
+    dy = nhwc(torch.randn(N, C, H, W, generator=g), dtype)
+    base = nhwc(torch.randn(N, K, H, W, generator=g), dtype)
+    ybn = nhwc(torch.randn(N, K, H, W, generator=g), dtype)
+
+    class St:
+        pass
+    st = St()
+    st.mean = (torch.randn(K, generator=g) * 0.1).to(DEV)
+    st.invstd = (torch.rand(K, generator=g) + 0.5).to(DEV)
+    st.scale = (torch.rand(K, generator=g) + 0.5).to(DEV)
+    st.shift = (torch.randn(K, generator=g) * 0.2).to(DEV)
+    outs = {}
+    for mode in ("2", "0"):                  # the stream kernel only, the tiled kernels
+        monkeypatch.setenv("SCD_GEMM_STREAM1X1", mode)
+        wp, wt = ops.pack_weight(w, dtype, 0), ops.pack_weight(w, dtype, 1)
+        r = {}
+        if (K, C) in sums:
+            stats = torch.zeros(64 * 2 * C, dtype=torch.float64, device=DEV)
+            r["y"] = ops.conv_fwd(x, wp, C, 1, 1, 1, 0, stats=stats)
+            r["stats"] = stats.view(64, 2, C).sum(0)
+        if (C, K) in plain:
+            r["dx"] = ops.conv_dgrad(dy, wt, K, H, W, 1, 1, 1, 0)
+        if (C, K) in accum:
+            r["dx+"] = base.clone()
+            ops.conv_dgrad(dy, wt, K, H, W, 1, 1, 1, 0, out=r["dx+"], accumulate=True)
+        if (C, K) in bnbwd:
+            bst = torch.zeros(64 * 2 * K, dtype=torch.float64, device=DEV)
+            r["dxb"] = ops.conv_dgrad(dy, wt, K, H, W, 1, 1, 1, 0, bn_bwd=(st, ybn, bst))
+            r["bsums"] = bst.view(64, 2, K).sum(0)
+        torch.cuda.synchronize()
+        outs[mode] = r
+    assert outs["0"], "no GEMM of this case is built into the stream kernel"
+    for k, v in outs["0"].items():
+        if k in ("stats", "bsums"):
+            d = (outs["2"][k] - v).abs().max().item()
+            assert d <= 1e-5 * v.abs().max().item(), (k, d)
+        else:
+            assert torch.equal(outs["2"][k], v), k
+    if "y" in outs["2"]:
+        ref = F.conv2d(nchw(x).float(), w.cpu().to(dtype).float())
+        assert rel_err(nchw(outs["2"]["y"]), ref) < TOL[dtype]
+        yf = outs["2"]["y"].float().view(-1, C)
+        ref_s = torch.stack([yf.sum(0), (yf * yf).sum(0)]).double()
+        assert (outs["2"]["stats"] - ref_s).abs().max().item() <= 2e-2 * ref_s.abs().max().item()
+    if "dx" in outs["2"]:
+        dref = F.conv_transpose2d(nchw(dy).float(), w.cpu().to(dtype).float())
+        assert rel_err(nchw(outs["2"]["dx"]), dref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,Hq,Cg,Cin,taken", [(32, 64, 128, 64, True), (32, 32, 256, 128, True),
                                                (4, 16, 512, 256, False), (3, 17, 128, 64, False)])
 def test_conv_dgrad_s2_phase_gemm(N, Hq, Cg, Cin, taken, dtype):
