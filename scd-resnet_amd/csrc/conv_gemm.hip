@@ -2735,36 +2735,37 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st, int ks = 1) {
 // the following BN+ReLU layer's backward sums (scd_conv_gemm_bnbwd: dz = stored gradient where y*rsc + rsh > 0).
 // The sums (64 channels per wave): per-lane partials over the run, 16-lane DPP sums, the waves' partials in a fixed
 // order, one fp64 replica add per channel and workgroup.
-template <int K, int N, int MODE, int SPL, int UA>
-__global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(GemmParams p, int cpw) {
+template <int K, int N, int MODE, int SPL, int UA, int WV>
+__global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmParams p, int cpw) {
     typedef __bf16 T;
     typedef __attribute__((ext_vector_type(4))) __bf16 hv4;
     typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
     constexpr int KS = K / 32;                              // MFMA k-steps
     constexpr int NH = N / SPL;                             // channels per wave
     constexpr int NB = NH / 16;                             // 16-channel blocks per wave
-    constexpr int PXW = 4 / SPL;                            // waves on different pixels
+    constexpr int NT = 64 * WV;                             // threads (WV waves: 8 where the weights fill the LDS)
+    constexpr int PXW = WV / SPL;                           // waves on different pixels
     constexpr int UP = 16 * UA;                             // pixels per unit (UA 16-pixel blocks)
     constexpr int XM = (K / 8 >= 16 ? 16 : K / 8) - 1;      // LDS swizzle: chunk c of row r at c ^ (r & XM)
     constexpr bool SUMS = NH == 64 && MODE != 1;
     constexpr int NS = SUMS ? 4 * NB : 1;                   // per-lane channel slots of the sums
     constexpr int WBYTES = N * K * 2;
     constexpr int PBYTES = MODE == 2 ? 4 * N * 4 : 0;       // BN parameters (mean, invstd, relu scale / shift)
-    static_assert(NB % 2 == 0 && K % 64 == 0 && (SPL == 1 || SPL == 2 || SPL == 4), "shape");
+    static_assert(NB % 2 == 0 && K % 64 == 0 && WV % SPL == 0 && 128 % (16 * UA * PXW) == 0, "shape");
     static_assert(WBYTES >= PXW * N * 8, "sum exchange fits the weight buffer");
     __shared__ __attribute__((aligned(16))) char smem[WBYTES + PBYTES];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, lg = lane >> 4;
     const int pw = wave / SPL;                              // pixel wave
     const int c0w = (wave % SPL) * NH;                      // the wave's first channel
-    for (int i = tid; i < N * K / 8; i += 256) {
+    for (int i = tid; i < N * K / 8; i += NT) {
         const int r = i / (K / 8), c = i - r * (K / 8);
         const uint4 v = *(const uint4*)(p.w + ((long)r * p.wrow + c * 8) * 2);
         *(uint4*)(smem + r * K * 2 + ((c ^ (r & XM)) << 4)) = v;
     }
     float* bnp = (float*)(smem + WBYTES);
     if constexpr (MODE == 2) {
-        for (int i = tid; i < N; i += 256) {
+        for (int i = tid; i < N; i += NT) {
             bnp[i] = p.bn_mean[i];
             bnp[N + i] = p.bn_invstd[i];
             bnp[2 * N + i] = p.bn_rsc[i];
@@ -2908,13 +2909,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(GemmParams p, in
                 }
             }
             __syncthreads();
-            if (tid < N) {
+            for (int c = tid; c < N; c += NT) {
                 double s = 0.0, q = 0.0;
 #pragma unroll
-                for (int w = 0; w < PXW; ++w) { s += red[(w * N + tid) * 2]; q += red[(w * N + tid) * 2 + 1]; }
+                for (int w = 0; w < PXW; ++w) { s += red[(w * N + c) * 2]; q += red[(w * N + c) * 2 + 1]; }
                 const int rep = (int)(blockIdx.x % SCD_STAT_REPLICAS);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + tid, s);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + tid, q);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + c, s);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + c, q);
             }
         }
     }
@@ -2945,8 +2946,10 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
     if (p.accumulate && sums) return -1;
     const long nchunks = Mtot / 128;
     const long cus = num_cus();
+    // about one round of resident workgroups: 2 per CU, 1 for the 128-KB weight buffers
+    const long want = (long)K * N >= 65536 ? cus : 2 * cus;
     long cpw = 2;
-    while (nchunks % (2 * cpw) == 0 && nchunks / (2 * cpw) >= 2 * cus) cpw *= 2;
+    while (nchunks % (2 * cpw) == 0 && nchunks / (2 * cpw) >= want) cpw *= 2;
     if (nchunks % cpw) return -1;
     const int grid = (int)(nchunks / cpw);
     const int mode = p.bnbwd ? 2 : (p.accumulate ? 1 : 0);
@@ -2955,7 +2958,7 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
 #define SCD_S1X1(KK, NN, MM, SS)                                                                                     \
     if (K == KK && N == NN && mode == MM) {                                                                          \
         constexpr int UA_ = (S1X1_UA2 && KK == 64 && NN / SS <= 64 && MM != 2) ? 2 : 1;                              \
-        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UA_>), dim3(grid), dim3(256), 0, st, p, (int)cpw); \
+        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UA_, 4>), dim3(grid), dim3(256), 0, st, p, (int)cpw); \
         SCD_RETURN_LAUNCH();                                                                                         \
     }
     // N = 64: one wave per pixel unit; N = 128 / 256: 2 / 4 waves split the channels when there are sums to take (the
@@ -2963,6 +2966,19 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
     SCD_S1X1(64, 64, 0, 1) SCD_S1X1(64, 64, 1, 1) SCD_S1X1(64, 64, 2, 1)
     SCD_S1X1(128, 64, 0, 1) SCD_S1X1(128, 64, 1, 1) SCD_S1X1(128, 64, 2, 1)
     SCD_S1X1(256, 64, 0, 1) SCD_S1X1(256, 64, 1, 1) SCD_S1X1(256, 64, 2, 1)
+    // K x N = 64 K elements (128-KB weight buffer): one workgroup of 8 waves per CU
+#define SCD_S1X1W(KK, NN, MM, SS, UU)                                                                                \
+    if (K == KK && N == NN && mode == MM) {                                                                          \
+        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UU, 8>), dim3(grid), dim3(512), 0, st, p, (int)cpw); \
+        SCD_RETURN_LAUNCH();                                                                                         \
+    }
+    if (sums) {
+        SCD_S1X1W(512, 128, 0, 2, 1) SCD_S1X1W(512, 128, 2, 2, 1) SCD_S1X1W(128, 512, 0, 8, 2)
+    } else {
+        SCD_S1X1W(512, 128, 0, 1, 1) SCD_S1X1W(512, 128, 1, 1, 1) SCD_S1X1W(128, 512, 0, 2, 1)
+        SCD_S1X1W(128, 512, 1, 2, 1)
+    }
+#undef SCD_S1X1W
     if (sums) {
         SCD_S1X1(64, 128, 0, 2) SCD_S1X1(128, 128, 0, 2) SCD_S1X1(256, 128, 0, 2)
         SCD_S1X1(64, 128, 2, 2) SCD_S1X1(128, 128, 2, 2) SCD_S1X1(256, 128, 2, 2)
