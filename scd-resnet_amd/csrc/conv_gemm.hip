@@ -2757,19 +2757,21 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int l16 = lane & 15, lg = lane >> 4;
     const int pw = wave / SPL;                              // pixel wave
-    const int c0w = (wave % SPL) * NH;                      // the wave's first channel
+    const int c0w = (wave % SPL) * NH;                      // the wave's first channel (of the workgroup's slice)
+    const int cb = blockIdx.y * N;                          // the slice's first output channel (p.Co = N * gridDim.y)
+    const int ldy = p.Co;                                   // output (and epilogue operand) row stride
     for (int i = tid; i < N * K / 8; i += NT) {
         const int r = i / (K / 8), c = i - r * (K / 8);
-        const uint4 v = *(const uint4*)(p.w + ((long)r * p.wrow + c * 8) * 2);
+        const uint4 v = *(const uint4*)(p.w + ((long)(cb + r) * p.wrow + c * 8) * 2);
         *(uint4*)(smem + r * K * 2 + ((c ^ (r & XM)) << 4)) = v;
     }
     float* bnp = (float*)(smem + WBYTES);
     if constexpr (MODE == 2) {
         for (int i = tid; i < N; i += NT) {
-            bnp[i] = p.bn_mean[i];
-            bnp[N + i] = p.bn_invstd[i];
-            bnp[2 * N + i] = p.bn_rsc[i];
-            bnp[3 * N + i] = p.bn_rsh[i];
+            bnp[i] = p.bn_mean[cb + i];
+            bnp[N + i] = p.bn_invstd[cb + i];
+            bnp[2 * N + i] = p.bn_rsc[cb + i];
+            bnp[3 * N + i] = p.bn_rsh[cb + i];
         }
     }
     __syncthreads();
@@ -2798,7 +2800,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
             for (int a = 0; a < UA; ++a)
 #pragma unroll
                 for (int pb = 0; pb < NB / 2; ++pb)
-                    ev[a][pb] = *(const uint4*)(src + ((pix0(u) + 16 * a + l16) * N + 32 * pb + cst) * 2);
+                    ev[a][pb] = *(const uint4*)(src + ((pix0(u) + 16 * a + l16) * ldy + cb + 32 * pb + cst) * 2);
         }
     };
     auto unit = [&](int u, const bf16x8 (&xf)[UA][KS], const uint4 (&ev)[UA][NB / 2]) {
@@ -2877,7 +2879,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
                     ssq[8 * pb + e] += dz * (y8[e] - mu[e]) * is[e];
                 }
             }
-            *(uint4*)((T*)p.y + m * N + 32 * pb + cst) = st;
+            *(uint4*)((T*)p.y + m * ldy + cb + 32 * pb + cst) = st;
         }
     };
 
@@ -2914,8 +2916,8 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
 #pragma unroll
                 for (int w = 0; w < PXW; ++w) { s += red[(w * N + c) * 2]; q += red[(w * N + c) * 2 + 1]; }
                 const int rep = (int)(blockIdx.x % SCD_STAT_REPLICAS);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + c, s);
-                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + c, q);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + cb + c, s);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + cb + c, q);
             }
         }
     }
@@ -2941,24 +2943,30 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
         p.Hi != p.Ho || p.Wi != p.Wo || p.wrow != p.Ci)
         return -1;
     const int K = p.Ci, N = p.Co;
-    if (Mtot % 128 || Mtot < 131072 || Mtot * (long)(K > N ? K : N) >= (1L << 30)) return -1;
+    if (Mtot % 128 || Mtot < 65536 || Mtot * (long)(K > N ? K : N) >= (1L << 30)) return -1;
     const bool sums = p.stats != nullptr;                    // forward statistics or BN-backward sums
     if (p.accumulate && sums) return -1;
     const long nchunks = Mtot / 128;
     const long cus = num_cus();
+    const int mode = p.bnbwd ? 2 : (p.accumulate ? 1 : 0);
+    // the whole N in one workgroup where an instance holds it, else slices of 256 output channels (grid.y; every
+    // slice re-reads the operand, from L2 when the slices of a chunk run together)
+    for (int attempt = 0; attempt < 2; ++attempt) {
+    const int Nd = attempt == 0 ? N : 256;
+    if (attempt == 1 && (N <= 256 || N % 256)) break;
+    const int nsl = N / Nd;
     // about one round of resident workgroups: 2 per CU, 1 for the 128-KB weight buffers
-    const long want = (long)K * N >= 65536 ? cus : 2 * cus;
+    const long want = std::max(1L, ((long)K * Nd >= 65536 ? cus : 2 * cus) / nsl);
     long cpw = 2;
     while (nchunks % (2 * cpw) == 0 && nchunks / (2 * cpw) >= want) cpw *= 2;
     if (nchunks % cpw) return -1;
     const int grid = (int)(nchunks / cpw);
-    const int mode = p.bnbwd ? 2 : (p.accumulate ? 1 : 0);
     // (two 16-pixel blocks per unit at K = 64 and <= 64 channels per wave: 4-KB operand loads per wave in flight; not
     // with the BN-backward sums, whose registers it would spill)
 #define SCD_S1X1(KK, NN, MM, SS)                                                                                     \
-    if (K == KK && N == NN && mode == MM) {                                                                          \
+    if (K == KK && Nd == NN && mode == MM) {                                                                         \
         constexpr int UA_ = (S1X1_UA2 && KK == 64 && NN / SS <= 64 && MM != 2) ? 2 : 1;                              \
-        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UA_, 4>), dim3(grid), dim3(256), 0, st, p, (int)cpw); \
+        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UA_, 4>), dim3(grid, nsl), dim3(256), 0, st, p, (int)cpw); \
         SCD_RETURN_LAUNCH();                                                                                         \
     }
     // N = 64: one wave per pixel unit; N = 128 / 256: 2 / 4 waves split the channels when there are sums to take (the
@@ -2968,15 +2976,16 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
     SCD_S1X1(256, 64, 0, 1) SCD_S1X1(256, 64, 1, 1) SCD_S1X1(256, 64, 2, 1)
     // K x N = 64 K elements (128-KB weight buffer): one workgroup of 8 waves per CU
 #define SCD_S1X1W(KK, NN, MM, SS, UU)                                                                                \
-    if (K == KK && N == NN && mode == MM) {                                                                          \
-        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UU, 8>), dim3(grid), dim3(512), 0, st, p, (int)cpw); \
+    if (K == KK && Nd == NN && mode == MM) {                                                                         \
+        hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UU, 8>), dim3(grid, nsl), dim3(512), 0, st, p, (int)cpw); \
         SCD_RETURN_LAUNCH();                                                                                         \
     }
     if (sums) {
         SCD_S1X1W(512, 128, 0, 2, 1) SCD_S1X1W(512, 128, 2, 2, 1) SCD_S1X1W(128, 512, 0, 8, 2)
+        SCD_S1X1W(256, 256, 0, 4, 1) SCD_S1X1W(256, 256, 2, 4, 1)
     } else {
         SCD_S1X1W(512, 128, 0, 1, 1) SCD_S1X1W(512, 128, 1, 1, 1) SCD_S1X1W(128, 512, 0, 2, 1)
-        SCD_S1X1W(128, 512, 1, 2, 1)
+        SCD_S1X1W(128, 512, 1, 2, 1) SCD_S1X1W(256, 256, 0, 1, 1) SCD_S1X1W(256, 256, 1, 1, 1)
     }
 #undef SCD_S1X1W
     if (sums) {
@@ -2989,6 +2998,7 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
         SCD_S1X1(256, 128, 0, 1) SCD_S1X1(256, 128, 1, 1)
     }
 #undef SCD_S1X1
+    }
     return -1;
 }
 
