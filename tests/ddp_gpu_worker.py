@@ -25,7 +25,7 @@ def main():
     from scdhip import ops
     from scdhip.flat import FlatDDP
 
-    fixture, seeds = {2: ("ddp", (8, 9)), 4: ("ddp4", (31, 32))}[world]
+    fixture, seeds = {2: ("ddp", (8, 9)), 4: ("ddp4", (31, 32)), 8: ("ddp8", (51, 52))}[world]
     g = np.load(os.path.join(REPO, "tests", "golden", fixture + ".npz"))
     entries, _ = O.model_spec(10)
     m = plugin.model(**plugin.modelParams)

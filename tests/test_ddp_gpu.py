@@ -38,9 +38,11 @@ def _run(worker, world, **extra):
     return outs
 
 
-@pytest.mark.parametrize("world,sync", [(2, "default"), (2, "world"), (2, "own"), (4, "default"), (4, "world")])
+@pytest.mark.parametrize("world,sync", [(2, "default"), (2, "world"), (2, "own"), (4, "default"), (4, "world"),
+                                        (8, "default")])
 def test_syncbn_ddp_matches_reference(world, sync):
-    """F7 (W=2) and F7b (W=4, tests/golden/make_golden_ddp4.py) against the reference's golden vectors, with the SyncBN
+    """F7 (W=2), F7b (W=4) and F7c (W=8: the driver's scaling world size; tests/golden/make_golden_ddp4.py) against
+    the reference's golden vectors, with the SyncBN
     transport of the default set-up (ops.setup_syncbn: peer-memory statistics, scdhip/peer.py, so the gradient buckets
     are all-reduced from inside the backward -- asserted) and the RCCL fallbacks: torch.distributed on WORLD beside
     the buckets (all at the end of the backward) or on a group of their own (SCD_SYNCBN_PEER=0)."""
