@@ -3390,12 +3390,13 @@ static bool wgrad_use_l1(int dtype, long M, int Ho, int Wo, int Cg, int T, int C
            (long)Ho * Wo * 64 <= (1L << 30) && M >= 64;
 }
 
-// >= 16 stages per workgroup, at most 128 workgroups (SCD_WGRAD_L1_NSPLIT): in the step this kernel shares the chip
-// with the compute stream's last layer1 / stem kernels, and half the splits halve its 64 x 576 fp32 slab reduce
-// (measured +1% per step against 256)
+// >= 16 stages per workgroup, at most 192 workgroups (SCD_WGRAD_L1_NSPLIT): in the step this kernel shares the chip
+// with the compute stream's last layer1 / stem kernels, and fewer splits shrink its 64 x 576 fp32 slab reduce
+// (round 4: 128 measured +1% per step against 256; round 5: 192 +0.3% against 128 in 8 of 8 A/B pairs on two boxes,
+// profiles/r5_ab.txt)
 static int wgrad_l1_nsplit(long M) {
     static long cap = -2;
-    if (cap == -2) { const char* e = getenv("SCD_WGRAD_L1_NSPLIT"); cap = e ? atol(e) : 128; }
+    if (cap == -2) { const char* e = getenv("SCD_WGRAD_L1_NSPLIT"); cap = e ? atol(e) : 192; }
     return (int)std::max(1L, std::min(cap, M / 64 / 16));
 }
 
