@@ -22,6 +22,9 @@
 #ifndef SCD_ABLATE
 #define SCD_ABLATE 0
 #endif
+#ifndef S1X1_STG
+#define S1X1_STG 1    // conv1x1_stream_kernel: waves that share pixels take the operand from one LDS-DMA copy (A/B option)
+#endif
 #ifndef S1X1_UA2
 #define S1X1_UA2 1    // conv1x1_stream_kernel: 32-pixel units where K = 64 (A/B build option)
 #endif
@@ -2735,8 +2738,23 @@ int launch_gemm(GemmParams& p, int Mtot_tiles, hipStream_t st, int ks = 1) {
 // the following BN+ReLU layer's backward sums (scd_conv_gemm_bnbwd: dz = stored gradient where y*rsc + rsh > 0).
 // The sums (64 channels per wave): per-lane partials over the run, 16-lane DPP sums, the waves' partials in a fixed
 // order, one fp64 replica add per channel and workgroup.
+// The LDS plan of an instance.  SPL > 1 (STG): the SPL waves on the same pixels would each load the unit's operand as
+// fragment-shaped 16-B pieces (16 rows x 64 B per instruction, SPL times over); instead each loads 1 / SPL of it by
+// LDS-DMA in whole 128-B lines into a double-buffered LDS unit (the weights' swizzle), and all read their fragments
+// from there -- where the LDS holds it without cutting the workgroups per CU below two (or one where it held one).
+template <int K, int N, int MODE, int SPL, int UA, int WV>
+struct S1x1Plan {
+    static constexpr int WBYTES = N * K * 2;
+    static constexpr int PBYTES = MODE == 2 ? 4 * N * 4 : 0;       // BN parameters (mean, invstd, relu scale / shift)
+    static constexpr int XU = 16 * UA * K * 2;                     // bytes of one pixel wave's unit
+    static constexpr int XALL = 2 * (WV / SPL) * XU;               // two buffers per pixel wave
+    static constexpr int OCC0 = 163840 / (WBYTES + PBYTES), OCC1 = 163840 / (WBYTES + PBYTES + XALL);
+    static constexpr bool STG = S1X1_STG && SPL > 1 && OCC1 >= 1 && (OCC1 >= 2 || OCC0 < 2);
+    static constexpr int XBYTES = STG ? XALL : 0;
+};
 template <int K, int N, int MODE, int SPL, int UA, int WV>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmParams p, int cpw) {
+    typedef S1x1Plan<K, N, MODE, SPL, UA, WV> Plan;
     typedef __bf16 T;
     typedef __attribute__((ext_vector_type(4))) __bf16 hv4;
     typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
@@ -2749,12 +2767,13 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
     constexpr int XM = (K / 8 >= 16 ? 16 : K / 8) - 1;      // LDS swizzle: chunk c of row r at c ^ (r & XM)
     constexpr bool SUMS = NH == 64 && MODE != 1;
     constexpr int NS = SUMS ? 4 * NB : 1;                   // per-lane channel slots of the sums
-    constexpr int WBYTES = N * K * 2;
-    constexpr int PBYTES = MODE == 2 ? 4 * N * 4 : 0;       // BN parameters (mean, invstd, relu scale / shift)
+    constexpr int WBYTES = Plan::WBYTES, PBYTES = Plan::PBYTES, XU = Plan::XU, XBYTES = Plan::XBYTES;
+    constexpr bool STG = Plan::STG;
     static_assert(NB % 2 == 0 && K % 64 == 0 && WV % SPL == 0 && 128 % (16 * UA * PXW) == 0, "shape");
     static_assert(WBYTES >= PXW * N * 8, "sum exchange fits the weight buffer");
-    __shared__ __attribute__((aligned(16))) char smem[WBYTES + PBYTES];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    static_assert(!STG || (UP * K / 8) % (64 * SPL) == 0, "whole LDS-DMA instructions per wave");
+    __shared__ __attribute__((aligned(16))) char smem[WBYTES + PBYTES + XBYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, lg = lane >> 4;
     const int pw = wave / SPL;                              // pixel wave
     const int c0w = (wave % SPL) * NH;                      // the wave's first channel (of the workgroup's slice)
@@ -2885,17 +2904,71 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
 
     bf16x8 xa[UA][KS], xb[UA][KS];
     uint4 ea[UA][NB / 2], eb[UA][NB / 2];
-    load_unit(0, xa);
     // an even number of units per wave; the prefetch past the run re-reads its last unit (clamped: every load from a
     // valid address)
     const int nu = cpw * (128 / (UP * PXW));
-    for (int u = 0; u < nu; u += 2) {
-        load_epi(u, ea);
-        load_unit(u + 1, xb);
-        unit(u, xa, ea);
-        load_epi(u + 1, eb);
-        load_unit(min(u + 2, nu - 1), xa);
-        unit(u + 1, xb, eb);
+    if constexpr (STG) {
+        char* xs = smem + WBYTES + PBYTES;                  // [2 buffers][PXW][UP rows][K] (chunk c of row r at c ^ (r & XM))
+        constexpr int ND = UP * K / 8 / (64 * SPL);         // LDS-DMA instructions per wave and unit
+        constexpr int EW = MODE != 0 ? UA * NB / 2 : 0;     // epilogue operand loads per wave and unit
+        constexpr int SW = UA * NB / 2;                     // output stores per wave and unit
+        const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+        const int ws = wave % SPL;
+        auto dma_unit = [&](int u, int b) {
+            char* dst = xs + (b * PXW + pw) * XU;
+            const int px = (int)pix0(u);
+#pragma unroll
+            for (int i = 0; i < ND; ++i) {
+                const int q0 = (i * SPL + ws) * 64, q = q0 + lane;
+                const int r = q / (K / 8), c = (q % (K / 8)) ^ (r & XM);
+                dma16(xrs, dst + q0 * 16, ((px + r) * K + c * 8) * 2);
+            }
+        };
+        auto read_unit = [&](int b, bf16x8 (&xf)[UA][KS]) {
+            const char* src = xs + (b * PXW + pw) * XU;
+#pragma unroll
+            for (int a = 0; a < UA; ++a) {
+                const int r = 16 * a + l16;
+#pragma unroll
+                for (int s = 0; s < KS; ++s) xf[a][s] = *(const bf16x8*)(src + r * K * 2 + (((4 * s + lg) ^ (r & XM)) << 4));
+            }
+        };
+        // unit u sits in buffer u & 1; before a wave reads it, every wave's DMAs of it have landed (counted vmcnt: the
+        // epilogue operand loads of the unit and the stores of the one before were issued after them) and every wave
+        // is done with the unit before (the barrier), whose buffer the next DMA overwrites
+        dma_unit(0, 0);
+        load_epi(0, ea);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EW) : "memory");
+        __builtin_amdgcn_s_barrier();
+        for (int u = 0; u < nu; u += 2) {
+            if (u > 0) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EW + SW) : "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+            read_unit(0, xa);
+            asm volatile("" ::: "memory");
+            dma_unit(u + 1, 1);
+            load_epi(u + 1, eb);
+            unit(u, xa, ea);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EW + SW) : "memory");
+            __builtin_amdgcn_s_barrier();
+            read_unit(1, xb);
+            asm volatile("" ::: "memory");
+            dma_unit(min(u + 2, nu - 1), 0);
+            load_epi(min(u + 2, nu - 1), ea);
+            unit(u + 1, xb, eb);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped last DMA has landed before the LDS is reused
+    } else {
+        load_unit(0, xa);
+        for (int u = 0; u < nu; u += 2) {
+            load_epi(u, ea);
+            load_unit(u + 1, xb);
+            unit(u, xa, ea);
+            load_epi(u + 1, eb);
+            load_unit(min(u + 2, nu - 1), xa);
+            unit(u + 1, xb, eb);
+        }
     }
     if constexpr (SUMS) {
         if (MODE == 2 || stats_on) {
@@ -2933,6 +3006,11 @@ static int stream1x1_mode() {
     const char* e = getenv("SCD_GEMM_STREAM1X1");
     return e ? atoi(e) : 1;
 }
+// SCD_S1X1_OCC (read per call): at most this many stream workgroups per CU (0 / unset: as many as fit)
+static int s1x1_occ_cap() {
+    const char* e = getenv("SCD_S1X1_OCC");
+    return e ? atoi(e) : 0;
+}
 static int num_cus();
 static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm_phase* phases, long Mtot,
                             hipStream_t st) {
@@ -2944,6 +3022,7 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
         return -1;
     const int K = p.Ci, N = p.Co;
     if (Mtot % 128 || Mtot < 65536 || Mtot * (long)(K > N ? K : N) >= (1L << 30)) return -1;
+    p.xbytes = (int)(Mtot * K * 2);                          // the operand's buffer range (LDS-DMA path)
     const bool sums = p.stats != nullptr;                    // forward statistics or BN-backward sums
     if (p.accumulate && sums) return -1;
     const long nchunks = Mtot / 128;
@@ -2955,17 +3034,32 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
     const int Nd = attempt == 0 ? N : 256;
     if (attempt == 1 && (N <= 256 || N % 256)) break;
     const int nsl = N / Nd;
-    // about one round of resident workgroups: 2 per CU, 1 for the 128-KB weight buffers
-    const long want = std::max(1L, ((long)K * Nd >= 65536 ? cus : 2 * cus) / nsl);
-    long cpw = 2;
-    while (nchunks % (2 * cpw) == 0 && nchunks / (2 * cpw) >= want) cpw *= 2;
-    if (nchunks % cpw) return -1;
-    const int grid = (int)(nchunks / cpw);
+    // about one round of resident workgroups: as many per CU as the instance's registers and LDS allow (capped by
+    // SCD_S1X1_OCC when set), so every workgroup of the grid runs in the first round
+    auto plan = [&](const void* kern, int threads, int& per_cache, long& cpw, int& grid) -> bool {
+        if (per_cache < 0) {
+            int per = 1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, 0) != hipSuccess || per < 1) per = 1;
+            per_cache = per;
+        }
+        const int cap = s1x1_occ_cap();
+        const long per = cap > 0 ? std::min(cap, per_cache) : per_cache;
+        const long want = std::max(1L, per * cus / nsl);
+        cpw = 2;                                             // (even: the waves take units in pairs)
+        while (nchunks / cpw > want && nchunks % (2 * cpw) == 0) cpw *= 2;
+        if (nchunks % cpw) return false;
+        grid = (int)(nchunks / cpw);
+        return true;
+    };
+    long cpw = 0;
+    int grid = 0;
     // (two 16-pixel blocks per unit at K = 64 and <= 64 channels per wave: 4-KB operand loads per wave in flight; not
     // with the BN-backward sums, whose registers it would spill)
 #define SCD_S1X1(KK, NN, MM, SS)                                                                                     \
     if (K == KK && Nd == NN && mode == MM) {                                                                         \
         constexpr int UA_ = (S1X1_UA2 && KK == 64 && NN / SS <= 64 && MM != 2) ? 2 : 1;                              \
+        static int per_ = -1;                                                                                        \
+        if (!plan((const void*)conv1x1_stream_kernel<KK, NN, MM, SS, UA_, 4>, 256, per_, cpw, grid)) return -1;      \
         hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UA_, 4>), dim3(grid, nsl), dim3(256), 0, st, p, (int)cpw); \
         SCD_RETURN_LAUNCH();                                                                                         \
     }
@@ -2977,6 +3071,8 @@ static int launch_stream1x1(int dtype, GemmParams& p, int nphase, const scd_gemm
     // K x N = 64 K elements (128-KB weight buffer): one workgroup of 8 waves per CU
 #define SCD_S1X1W(KK, NN, MM, SS, UU)                                                                                \
     if (K == KK && Nd == NN && mode == MM) {                                                                         \
+        static int per_ = -1;                                                                                        \
+        if (!plan((const void*)conv1x1_stream_kernel<KK, NN, MM, SS, UU, 8>, 512, per_, cpw, grid)) return -1;       \
         hipLaunchKernelGGL((conv1x1_stream_kernel<KK, NN, MM, SS, UU, 8>), dim3(grid, nsl), dim3(512), 0, st, p, (int)cpw); \
         SCD_RETURN_LAUNCH();                                                                                         \
     }
