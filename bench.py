@@ -127,8 +127,10 @@ def pmc_traffic(kernel, batch, dtype, model="centerOffsetRes10", S=512):
     on the same shape -- for the other BASELINE configs), or None when none matches."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_*.json")),
-                   key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
+    # (round-numbered summaries only: r<N>_pmc_*.json, newest round first; any other name is skipped)
+    files = [f for f in glob.glob(os.path.join(REPO, "profiles", "r*_pmc_*.json"))
+             if re.match(r"r\d+_pmc_", os.path.basename(f))]
+    files.sort(key=lambda f: int(re.match(r"r(\d+)_", os.path.basename(f)).group(1)))
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
