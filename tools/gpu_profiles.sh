@@ -19,6 +19,7 @@ summ() {  # summ <name> <batch> <dtype> <command> <model> <S>
   w=$(find $O/${T}_pmc_$1_WRITE_SIZE -name "*counter_collection.csv" | head -1)
   python tools/pmc_summary.py $f $w $O/${T}_pmc_$1.json $2 $3 "$4" $5 $6 > $O/${T}_pmc_$1.txt && cp $O/${T}_pmc_$1.json profiles/
 }
+if [ -z "$SKIP_PMC" ]; then   # SKIP_PMC=1: the bench lines and traces only (the committed PMC summaries stay)
 for c in FETCH_SIZE WRITE_SIZE; do
   pmc cornernet $c python3 tools/pmc_kernels.py --case lastconv,cpool_add || exit 1
   pmc res50_1024 $c python3 tools/pmc_kernels.py --case heads_res50 || exit 1
@@ -28,6 +29,7 @@ summ cornernet 32 bf16 "python3 tools/pmc_kernels.py --case lastconv,cpool_add" 
 summ res50_1024 16 fp16 "python3 tools/pmc_kernels.py --case heads_res50" centerOffsetRes50 1024 || exit 1
 summ traffic 32 bf16 "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline" centerOffsetRes10 512 || exit 1
 echo pmc done
+fi
 timeout -k 10 400 python bench.py > $O/${T}_bench.json 2> $O/${T}_bench.err || exit 1
 cut -c1-200 $O/${T}_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/${T}_profbench.json 2> $O/${T}_prof.err || exit 1
