@@ -22,6 +22,9 @@
 #ifndef SCD_ABLATE
 #define SCD_ABLATE 0
 #endif
+#ifndef S1X1_FULLROW
+#define S1X1_FULLROW 1  // conv1x1_stream_kernel: stores of whole 128-B row pieces (A/B option)
+#endif
 #ifndef S1X1_STG
 #define S1X1_STG 1    // conv1x1_stream_kernel: waves that share pixels take the operand from one LDS-DMA copy (A/B option)
 #endif
@@ -2802,6 +2805,28 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
     for (int j = 0; j < NS; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
     // lane's store column of channel-block pair (b, b + 1): even lg block b, odd lg block b + 1 (permlane16_swap)
     const int cst = c0w + 4 * lg + 12 * (lg & 1);
+    // S1X1_FULLROW: a lane's place in the whole-128-B-row layout of a 64-channel piece (pixel l16 & 7 of the first or
+    // second 8 of a 16-pixel block, channels fr_cw .. + 7 of the piece; see the stores in unit())
+    const bool fr_hi = l16 >= 8;
+    const int fr_cw = 32 * (l16 >> 3) + (cst & 31);
+    // the epilogue operands in that layout too where a wave holds one 64-channel piece (wider waves: their conversion
+    // temporaries spill)
+    // (not for the BN-backward-sum instances at K = 256, which then spill)
+    constexpr bool ST_FR = S1X1_FULLROW && !(MODE == 2 && K >= 256);
+    constexpr bool EPI_FR = ST_FR && NB == 4;
+    auto ror8 = [](const uint4& v) {
+        uint4 r;
+        r.x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x128, 0xf, 0xf, false);   // row_ror:8
+        r.y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x128, 0xf, 0xf, false);
+        r.z = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x128, 0xf, 0xf, false);
+        r.w = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x128, 0xf, 0xf, false);
+        return r;
+    };
+    auto sel4 = [](bool c, const uint4& a, const uint4& b) {
+        uint4 r;
+        r.x = c ? a.x : b.x; r.y = c ? a.y : b.y; r.z = c ? a.z : b.z; r.w = c ? a.w : b.w;
+        return r;
+    };
 
     auto pix0 = [&](int u) -> long { return chunk0 * 128 + (u * PXW + pw) * UP; };
     auto load_unit = [&](int u, bf16x8 (&xf)[UA][KS]) {
@@ -2816,10 +2841,21 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
         if constexpr (MODE != 0) {
             const char* src = MODE == 1 ? (const char*)p.y : p.bny;
 #pragma unroll
-            for (int a = 0; a < UA; ++a)
+            for (int a = 0; a < UA; ++a) {
+                if constexpr (EPI_FR) {
+                    // whole 128-B row pieces, in the stores' layout (turned into the fragment layout where used)
+                    const char* r0 = src + ((pix0(u) + 16 * a + (l16 & 7)) * ldy + cb + c0w + fr_cw) * 2;
 #pragma unroll
-                for (int pb = 0; pb < NB / 2; ++pb)
-                    ev[a][pb] = *(const uint4*)(src + ((pix0(u) + 16 * a + l16) * ldy + cb + 32 * pb + cst) * 2);
+                    for (int q = 0; q < NB / 4; ++q) {
+                        ev[a][2 * q] = *(const uint4*)(r0 + 128 * q);
+                        ev[a][2 * q + 1] = *(const uint4*)(r0 + 128 * q + 16 * ldy);
+                    }
+                } else {
+#pragma unroll
+                    for (int pb = 0; pb < NB / 2; ++pb)
+                        ev[a][pb] = *(const uint4*)(src + ((pix0(u) + 16 * a + l16) * ldy + cb + 32 * pb + cst) * 2);
+                }
+            }
         }
     };
     auto unit = [&](int u, const bf16x8 (&xf)[UA][KS], const uint4 (&ev)[UA][NB / 2]) {
@@ -2859,7 +2895,20 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
 #pragma unroll
         for (int a = 0; a < UA; ++a)
 #pragma unroll
-        for (int pb = 0; pb < NB / 2; ++pb) {
+        for (int q = 0; q < NB / 4; ++q) {
+        // one 64-channel piece (blocks 4q .. 4q + 3) at a time: the channel-block pairs 2q and 2q + 1
+        uint4 stv[2], evv[2];
+        if constexpr (MODE != 0 && EPI_FR) {                 // row-piece layout -> the fragment layout
+            const uint4 w0 = ev[a][2 * q], w1 = ev[a][2 * q + 1];
+            evv[0] = sel4(fr_hi, ror8(w1), w0);
+            evv[1] = sel4(fr_hi, w1, ror8(w0));
+        } else if constexpr (MODE != 0) {
+            evv[0] = ev[a][2 * q];
+            evv[1] = ev[a][2 * q + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int pb = 2 * q + j;
             const long m = pix0(u) + 16 * a + l16;
             hv4 h0, h1;
 #pragma unroll
@@ -2872,7 +2921,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
             if constexpr (MODE == 1) {
                 float a8[8], o8[8];
                 Vec16<T>::load(&st, a8);
-                Vec16<T>::load(&ev[a][pb], o8);
+                Vec16<T>::load(&evv[j], o8);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) a8[e] += o8[e];
                 Vec16<T>::store(&st, a8);
@@ -2880,7 +2929,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
             if constexpr (MODE == 2) {
                 float d8[8], y8[8], mu[8], is[8], sc[8], sh[8];
                 Vec16<T>::load(&st, d8);
-                Vec16<T>::load(&ev[a][pb], y8);
+                Vec16<T>::load(&evv[j], y8);
                 const int c0 = 32 * pb + cst;
 #pragma unroll
                 for (int e = 0; e < 8; e += 4) {
@@ -2898,7 +2947,17 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
                     ssq[8 * pb + e] += dz * (y8[e] - mu[e]) * is[e];
                 }
             }
-            *(uint4*)((T*)p.y + m * ldy + cb + 32 * pb + cst) = st;
+            if constexpr (ST_FR) stv[j] = st;
+            else *(uint4*)((T*)p.y + m * ldy + cb + 32 * pb + cst) = st;
+        }
+        if constexpr (ST_FR) {
+            // the piece as whole 128-B row pieces: the upper 8 lanes of each 16-lane row trade pair 2q + 1 of pixels
+            // 0-7 for pair 2q of pixels 8-15 (DPP rotate by 8 within the row), so each store writes 8 whole row pieces
+            // instead of 16 half ones
+            T* dst = (T*)p.y + (pix0(u) + 16 * a + (l16 & 7)) * ldy + cb + c0w + 64 * q + fr_cw;
+            *(uint4*)dst = sel4(fr_hi, ror8(stv[1]), stv[0]);
+            *(uint4*)(dst + 8 * ldy) = sel4(fr_hi, stv[1], ror8(stv[0]));
+        }
         }
     };
 
