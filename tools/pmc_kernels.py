@@ -1,13 +1,17 @@
 """Launch ONE dominant-kernel shape of a BASELINE config repeatedly, for rocprofv3 --pmc passes (HBM bytes per
 launch of exactly that kernel on exactly that shape; bench.py reads the summaries for its `traffic` fields).
 
-python tools/pmc_kernels.py --case {lastconv,cpool_add,heads_res50}[,...] [--reps 5]
+python tools/pmc_kernels.py --case {lastconv,cpool_add,heads_res50,s1x1_fwd,s1x1_bnbwd}[,...] [--reps 5]
 
   lastconv     cornerNetCPool (configs[3]) CornerPool lastConv: 3x3 256->256 conv + BN sums, B=32 at 128x128, bf16
                (conv_gemm_pp_kernel<256,false>, as _train_bn_conv launches it)
   cpool_add    its corner pool with the addend: (32,128,128,128) bf16 (cpool_fwd_kernel)
   heads_res50  centerOffsetRes50 1024^2 (configs[4]) fused heads GEMM, B=16 at 256x256, fp16, hidden channels of the
                size / offset heads kept at 30 random pixels per image (conv_gemm_heads384_kernel, as HeadsFn)
+  s1x1_fwd     its layer1 conv3 / downsample forward: 1x1 64 -> 256 + BN statistics, B=16 at 256x256, fp16
+               (conv1x1_stream_kernel<64,256,0,4,2,4>; algorithmic 2 x (64 + 256) B = 640 B per pixel, 671 MB)
+  s1x1_bnbwd   its layer1 conv3 input gradient with the bn2 backward sums: 1x1 256 -> 64, B=16 at 256x256, fp16
+               (conv1x1_stream_kernel<256,64,2,1,1,4>; 2 x (256 + 64 + 64) B = 768 B per pixel, 805 MB)
 """
 import argparse
 import os
@@ -22,7 +26,7 @@ from scdhip import ops  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--case", required=True, help="comma-separated: lastconv, cpool_add, heads_res50")
+    ap.add_argument("--case", required=True, help="comma-separated: lastconv, cpool_add, heads_res50, s1x1_fwd, s1x1_bnbwd")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     for case in a.case.split(","):
@@ -67,6 +71,34 @@ def run_case(case, reps):
 
         def run():
             ops.L.call("scd_conv_gemm_heads_keep", *args, ops.stream())
+    elif case in ("s1x1_fwd", "s1x1_bnbwd"):
+        N, H, W = 16, 256, 256
+        dt = torch.float16
+        K, C = 64, 256                       # conv3: 64 -> 256 (its input gradient: 256 -> 64)
+        w = torch.randn(C, K, 1, 1, device=dev, generator=g) / K ** 0.5
+        if case == "s1x1_fwd":
+            x = torch.randn(N, H, W, K, device=dev, generator=g).to(dt)
+            wp = ops.pack_weight(w, dt, 0)
+            stats = ops.new_stats(C, dev)
+
+            def run():
+                ops.conv_fwd(x, wp, C, 1, 1, 1, 0, stats=stats)
+        else:
+            dy = torch.randn(N, H, W, C, device=dev, generator=g).to(dt)
+            ybn = torch.randn(N, H, W, K, device=dev, generator=g).to(dt)
+            wt = ops.pack_weight(w, dt, 1)
+
+            class St:
+                pass
+            st = St()
+            st.mean = torch.randn(K, device=dev, generator=g) * 0.1
+            st.invstd = torch.rand(K, device=dev, generator=g) + 0.5
+            st.scale = torch.rand(K, device=dev, generator=g) + 0.5
+            st.shift = torch.randn(K, device=dev, generator=g) * 0.2
+            bst = ops.new_stats(K, dev)
+
+            def run():
+                ops.conv_dgrad(dy, wt, K, H, W, 1, 1, 1, 0, bn_bwd=(st, ybn, bst))
     else:
         raise SystemExit("unknown case %s" % case)
     for _ in range(reps):
