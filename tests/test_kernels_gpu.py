@@ -806,15 +806,17 @@ def test_conv_l1p_matches_register_staged(N, H, W, dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("K,C", [(64, 64), (128, 64), (256, 64), (64, 128), (256, 128), (64, 256), (128, 256),
-                                 (128, 512), (512, 128), (256, 256), (256, 1024), (1024, 256)])
-def test_conv1x1_stream_matches_tiled(K, C, dtype, monkeypatch):
+@pytest.mark.parametrize("K,C,N", [(64, 64, 2), (128, 64, 2), (256, 64, 2), (64, 128, 2), (256, 128, 2), (64, 256, 2),
+                                   (128, 256, 2), (128, 512, 2), (512, 128, 2), (256, 256, 2), (256, 1024, 2),
+                                   (1024, 256, 2), (64, 256, 3), (256, 256, 3)])
+def test_conv1x1_stream_matches_tiled(K, C, N, dtype, monkeypatch):
     """conv1x1_stream_kernel (HBM-bound stride-1 1x1 GEMMs: weights resident in LDS, operands streamed into the MFMA
     fragments; the Res50 layer1 1x1 convs, residuals.py:122-165) against the tiled kernels on the same shapes: the
     forward K -> C with its BN statistics, the input gradient C -> K, its += form and the BN-backward-sum form, each
     where the stream kernel is built for the GEMM shape (K_gemm, N_gemm).  Outputs are bit-identical (same MFMA chain
     per output); statistics and BN sums agree to fp32 summation-order noise.  SCD_GEMM_STREAM1X1=2 fails any GEMM the
-    stream kernel does not take, so the "2" results are its own."""
+    stream kernel does not take, so the "2" results are its own.  The pixel runs per workgroup follow the instance's
+    residency (launch_stream1x1 in conv_gemm.hip); N = 3 gives 1,536 chunks of 128 pixels."""
     from scdhip import ops
     # (K_gemm, N_gemm) built into the stream kernel; N = 1024 runs as four 256-channel slices
     sums = {(64, 64), (128, 64), (256, 64), (64, 128), (128, 128), (256, 128), (64, 256), (128, 256), (128, 512),
@@ -824,7 +826,8 @@ def test_conv1x1_stream_matches_tiled(K, C, dtype, monkeypatch):
              (256, 256), (256, 1024)}
     bnbwd = {(64, 64), (128, 64), (256, 64), (64, 128), (128, 128), (256, 128), (512, 128), (256, 256), (256, 1024)}
     g = torch.Generator().manual_seed(113)
-    N, H, W = 2, 256, 256                                    # M = 131,072 pixels
+    H, W = 256, 256                                          # M = 131,072 pixels (N = 3: 196,608, a grid that is no
+    #                                                          power of two of 128-pixel chunks)
     x = nhwc(torch.randn(N, K, H, W, generator=g), dtype)
     w = (torch.randn(C, K, 1, 1, generator=g) / K ** 0.5).to(DEV)
     dy = nhwc(torch.randn(N, C, H, W, generator=g), dtype)
