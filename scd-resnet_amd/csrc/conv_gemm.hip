@@ -22,6 +22,9 @@
 #ifndef SCD_ABLATE
 #define SCD_ABLATE 0
 #endif
+#ifndef L1P_SWAP
+#define L1P_SWAP 1      // conv_gemm_l1p_kernel, 256-pixel rows: 16-B stores of channel-block pairs (A/B option)
+#endif
 #ifndef S1X1_FULLROW
 #define S1X1_FULLROW 1  // conv1x1_stream_kernel: stores of whole 128-B row pieces (A/B option)
 #endif
@@ -703,7 +706,36 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
                                                                             af[a], acc[a][b], 0, 0, 0);
             }
         }
-        if constexpr (DIRECT) {
+        if constexpr (DIRECT && L1P_SWAP) {
+            // the tile is row r of image n: lane's pixel 64pw + 16a + l16 is its column.  The two channel blocks
+            // paired by v_permlane16_swap: the lane then holds 8 consecutive channels 32chh + 4lg + 12(lg & 1) ..,
+            // one 16-B store per pixel block (16 pixels x 64 B per instruction instead of 16 x 32 B)
+            const long base = ((long)(n * p.Ho + r) * p.Wo) * 64;
+            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+            const int cst = 32 * chh + 4 * lg + 12 * (lg & 1);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const long off = base + (long)(64 * pw + 16 * a + l16) * 64 + cst;
+                bf16x4 h0, h1;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { h0[q] = (__bf16)acc[a][0][q]; h1[q] = (__bf16)acc[a][1][q]; }
+                const u32x2 xv = __builtin_bit_cast(u32x2, h0), yv = __builtin_bit_cast(u32x2, h1);
+                const auto s0 = __builtin_amdgcn_permlane16_swap(xv[0], yv[0], false, false);
+                const auto s1 = __builtin_amdgcn_permlane16_swap(xv[1], yv[1], false, false);
+                uint4 v;
+                v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
+                if (p.accumulate) {
+                    float a8[8], o8[8];
+                    Vec16<T>::load(&v, a8);
+                    Vec16<T>::load((const T*)p.y + off, o8);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) a8[e] += o8[e];
+                    Vec16<T>::store(&v, a8);
+                }
+                *(uint4*)((T*)p.y + off) = v;
+            }
+        } else if constexpr (DIRECT) {
             // the tile is row r of image n: lane's pixel 64pw + 16a + l16 is its column; channels 32chh + 16b + 4lg
             const long base = ((long)(n * p.Ho + r) * p.Wo) * 64;
             typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
