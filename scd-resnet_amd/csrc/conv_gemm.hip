@@ -596,8 +596,9 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, const char* 
 // epilogue; BNB: the stored gradient against the BN input) are carried in registers across the run and added to
 // the fp64 replicas once per workgroup.
 // Rows of 256 pixels (Res50 layer1 at 1024^2 input, residuals.py:122-165, 357): a tile is one row, and the four ring
-// rows (132 KiB) leave no room for the staging buffer, so the tile is stored straight from the accumulators (8-B
-// stores of the lane's 4 channels; L2 merges a pixel's 128 B): outputs bit-identical.  The BN-backward-sum variant
+// rows (132 KiB) leave no room for the staging buffer, so the tile is stored straight from the accumulators (16-B
+// stores of 8 channels after v_permlane16_swap pairs the lane's two channel blocks; L2 merges a pixel's 128 B):
+// outputs bit-identical.  The BN-backward-sum variant
 // is not built for them (its operand loads in this layout spill registers): scd_conv_gemm_bnbwd then runs this
 // kernel's plain input gradient and the separate scd_bn_bwd_reduce.
 template <int WO, bool FLIP, bool BNB>
