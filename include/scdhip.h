@@ -416,16 +416,19 @@ int scd_adam_step(float* p, const float* g, float* m, float* v, long n, float lr
                   float eps, float bc1, float bc2, float gscale, void* stream);
 /* Same update with the step state in device memory: hyper = {lr, step} (fp64, step advanced by 1 on the stream
  * before the update), so a captured training-step graph (scdhip/graph.py) replays with the live learning rate and
- * bias corrections (networkFactory.py:228-234, :273-276). */
+ * bias corrections (networkFactory.py:228-234, :273-276).  skip (optional device word; the peer-memory SyncBN error
+ * word, scdhip/peer.py): non-zero = the gradients were formed from unreduced statistics -- nothing changes (step count,
+ * parameters, moments). */
 int scd_adam_step_dev(float* p, const float* g, float* m, float* v, long n, double* hyper, float beta1, float beta2,
-                      float eps, float gscale, void* stream);
+                      float eps, float gscale, const unsigned long long* skip, void* stream);
 /* ---- SGD (torch.optim.SGD, networkFactory.py:84-89: momentum 0.9, weight_decay 1e-4) over a flat fp32 buffer ----
  * hyper = {lr, step, initialised, scratch} (fp64, 4 values): step advanced on the stream as for scd_adam_step_dev;
  * the momentum buffer `buf` is initialised to this step's d = g*gscale + weight_decay*p (as torch clones it when the
  * parameter has no momentum_buffer yet) when hyper[2] == 0, and hyper[2] is set to 1 -- a per-buffer flag, so a
  * buffer rebuilt or reset mid-training starts like torch's, whatever the step.  buf may be NULL when momentum == 0. */
 int scd_sgd_step_dev(float* p, const float* g, float* buf, long n, double* hyper, float momentum, float dampening,
-                     float weight_decay, int nesterov, float gscale, void* stream);
+                     float weight_decay, int nesterov, float gscale,
+                     const unsigned long long* skip, void* stream);
 
 /* ---- corner pooling (cornerPooling/source/{top,bottom,left,right}Pool.cpp) ----
  * dir: 0 top (max over k>=h), 1 bottom (k<=h), 2 left (k>=w), 3 right (k<=w); NHWC dtype.
@@ -481,6 +484,17 @@ int scd_event_destroy(void* ev);
 int scd_event_record(void* ev, void* stream);
 int scd_event_elapsed_ms(void* start, void* end, float* ms);
 
+/* ---- calibration (diagnostics; SURVEY.md §8(d) C2: the achievable MFMA peak on the box) ----
+ * scd_calib_mfma_peak: grid workgroups of 4 waves, each running `iters` x 16 v_mfma_f32_16x16x32_bf16 on random bf16
+ * fragments read from `src` (>= 256 x 8 x 64 x 16 bytes); out: grid x 256 floats (keeps the accumulators live);
+ * stamps (optional): [grid x 4 waves][4] = {s_memtime at loop start, at loop end, s_memrealtime at start, at end}.
+ * scd_calib_set_stamps: the [workgroup][4] buffer the GEMM kernels of a stamped diagnostic build write their main-loop
+ * stamps to (scd_calib_stamped_build() == 1); the product build never writes it. */
+int scd_calib_mfma_peak(const void* src, int grid, int iters, float* out, unsigned long long* stamps, void* stream);
+int scd_calib_set_stamps(unsigned long long* stamps);
+int scd_calib_stamped_build(void);
+
+/* library identity: "libscdhip <abi> gfx950 <hash of the sources built>" */
 const char* scd_version(void);
 
 #ifdef __cplusplus

@@ -69,7 +69,7 @@ __device__ __forceinline__ void wave_collect(double* stats, int nrep, int C, int
 __device__ __forceinline__ void bn_finalize_channel(int c, double* stats, int nrep, int C, double count,
                                                     const float* gamma, const float* beta, float* rmean, float* rvar,
                                                     float momentum, float eps, float* mean_o, float* invstd_o,
-                                                    float* scale_o, float* shift_o) {
+                                                    float* scale_o, float* shift_o, int64_t* nbt) {
     double mean, var;
     if (stats) {
         double s, q;
@@ -91,7 +91,9 @@ __device__ __forceinline__ void bn_finalize_channel(int c, double* stats, int nr
     scale_o[c] = sc;
     shift_o[c] = b - (float)mean * sc;
     // (statistics that are NaN -- a failed peer-memory SyncBN all-reduce poisons its result, scdhip/peer.py -- leave the
-    // running statistics as they were, so a checkpoint written after the failure still carries the last good ones)
+    // running statistics AND num_batches_tracked as they were, so a checkpoint written after the failure still carries
+    // the last good, mutually consistent ones; channel 0's lane counts the batch)
+    if (c == 0 && nbt && stats && mean == mean && var == var) *nbt += 1;
     if (stats && rmean && mean == mean && var == var) {
         const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
         rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
@@ -103,10 +105,9 @@ __global__ void bn_finalize_kernel(double* stats, int nrep, int C, double count,
                                    const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum,
                                    float eps, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
     const int c = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt && stats) *nbt += 1;
     if (c >= C) return;
     bn_finalize_channel(c, stats, nrep, C, count, gamma, beta, rmean, rvar, momentum, eps, mean_o, invstd_o, scale_o,
-                        shift_o);
+                        shift_o, nbt);
 }
 
 // up to SCD_BN_FIN_MAX layers in one launch (scd_bn_finalize_n): layer i owns blocks [b0[i], b0[i + 1])
@@ -123,10 +124,9 @@ __global__ void bn_finalize_n_kernel(FinN f) {
     const scd_bn_fin_args& a = f.l[i];
     const int blk = blockIdx.x - f.b0[i];
     const int c = blk * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (blk == 0 && threadIdx.x == 0 && a.num_batches && a.stats) *a.num_batches += 1;
     if (c >= a.C) return;
     bn_finalize_channel(c, a.stats, a.nrep, a.C, a.count, a.gamma, a.beta, a.running_mean, a.running_var, a.momentum,
-                        a.eps, a.mean, a.invstd, a.scale, a.shift);
+                        a.eps, a.mean, a.invstd, a.scale, a.shift, a.num_batches);
 }
 
 // E consecutive per-channel floats (E = 4 or 8, 16-B aligned) as float4 loads

@@ -38,6 +38,8 @@
 #define WGRAD_OCC 2   // register-staged weight-gradient kernel: workgroups per CU the registers are budgeted for
 #endif
 
+extern unsigned long long* scd_calib_stamp_buffer;   // calib.hip (stamped diagnostic builds)
+
 namespace {
 SCD_KERNEL_NS_BEGIN
 
@@ -76,7 +78,30 @@ struct GemmParams {
     int shuf;
     // heads384: K-stage order reversed on every other round of 256 workgroups (kserp = 1; SCD_HEADS_SERP)
     int kserp;
+    // stamped diagnostic build only (SCD_STAMP, calib.hip): per-workgroup main-loop clock stamps
+    unsigned long long* stamps;
 };
+
+#ifndef SCD_STAMP
+#define SCD_STAMP 0
+#endif
+// SCD_STAMP builds: thread 0 of each workgroup records s_memtime / s_memrealtime at the start and the end of the
+// main loop into p.stamps[blockIdx.x][4] (tools/clock_probe.py; MI355X_MICROARCH.md "DVFS give-back" item 6)
+#define SCD_STAMP_BEGIN()                                                             \
+    unsigned long long stamp_t0 = 0, stamp_r0 = 0;                                    \
+    if constexpr (SCD_STAMP) {                                                        \
+        stamp_t0 = __builtin_amdgcn_s_memtime();                                      \
+        stamp_r0 = __builtin_amdgcn_s_memrealtime();                                  \
+    }
+#define SCD_STAMP_END()                                                               \
+    if constexpr (SCD_STAMP) {                                                        \
+        const unsigned long long stamp_t1 = __builtin_amdgcn_s_memtime();             \
+        const unsigned long long stamp_r1 = __builtin_amdgcn_s_memrealtime();         \
+        if (threadIdx.x == 0 && p.stamps) {                                           \
+            unsigned long long* sp = p.stamps + (long)blockIdx.x * 4;                 \
+            sp[0] = stamp_t0; sp[1] = stamp_t1; sp[2] = stamp_r0; sp[3] = stamp_r1;  \
+        }                                                                             \
+    }
 
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
 // chunk c ^ (r & 7).  ds_read_b128 fragment reads (16 consecutive rows, one chunk) and the
@@ -1185,6 +1210,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         __builtin_amdgcn_sched_barrier(0);
     };
 
+    SCD_STAMP_BEGIN();
     if (KT > 0) {
         {
             const StageArgs g0 = stage_args(0);
@@ -1236,6 +1262,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    SCD_STAMP_END();
     if constexpr (dbg == 61) {                 // ablation 61: no epilogue (the accumulators kept live by a test)
         float s = 0.f;
 #pragma unroll
@@ -1677,6 +1704,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
             __builtin_amdgcn_sched_barrier(0);
         };
 
+        SCD_STAMP_BEGIN();
         if (KT > 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
@@ -1714,6 +1742,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        SCD_STAMP_END();
         // ---- epilogue from the accumulators.  Lane (l16, lg) of block (a, b) holds hidden channels
         // 96wc + 16b + 4lg .. +3 of pixel 96grp + 16a + l16: after bias + ReLU those 4 bf16 are (1) an 8-B piece of
         // the pixel's NHWC row, stored at once, and (2) exactly the B operand of a 16x16x16 MFMA (B[k = 4lg + j][n =
@@ -3451,6 +3480,7 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.bnbwd = 0; p.bny = nullptr; p.bn_mean = p.bn_invstd = p.bn_rsc = p.bn_rsh = nullptr;
     p.hid_keep = nullptr; p.hid_cols = 1 << 30;
     p.shuf = 0;
+    p.stamps = scd_calib_stamp_buffer;
     {
         // read per call (tests switch them to compare the variants)
         const char* e = getenv("SCD_HEADS_SERP");

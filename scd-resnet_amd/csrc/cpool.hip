@@ -252,4 +252,3 @@ extern "C" int scd_cpool_bwd(int dtype, int dir, const void* x, const void* dy, 
     return SCD_ERR_ARG;
 }
 
-extern "C" const char* scd_version(void) { return "libscdhip 0.1 gfx950"; }

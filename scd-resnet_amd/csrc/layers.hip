@@ -758,12 +758,16 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long n
 // Device-resident step state (hyper = {lr, step}, fp64) so a captured step graph replays with the current learning
 // rate and bias corrections: the tick advances the step, the update kernel derives the corrections exactly as
 // the host path does (fp64 powers rounded to fp32, torch/optim/adam.py _single_tensor_adam).
-__global__ void adam_tick_kernel(double* hyper) {
+// skip (optional): a device word (the peer-memory SyncBN error word, scdhip/peer.py); non-zero = this step's gradients
+// were formed from unreduced (NaN-poisoned) statistics: neither the step count nor any parameter or moment changes.
+__global__ void adam_tick_kernel(double* hyper, const unsigned long long* skip) {
+    if (skip && *skip) return;
     if (threadIdx.x == 0) hyper[1] = hyper[1] + 1.0;
 }
 
 __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, long n, const double* hyper, float b1,
-                                float b2, float eps, float gscale) {
+                                float b2, float eps, float gscale, const unsigned long long* skip) {
+    if (skip && *skip) return;
     const double s = hyper[1];
     const float lr = (float)hyper[0];
     const float bc1 = (float)(1.0 - pow((double)b1, s));
@@ -788,7 +792,8 @@ __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, lo
 // buf.  hyper = {lr, step, initialised, snapshot} fp64 in device memory: the tick advances the step and moves the
 // buffer's "initialised" flag into the snapshot the update reads (set to 1 for the next step), so a buffer re-created
 // mid-training (flag cleared by the host) starts as torch's does, not from the global step count.
-__global__ void sgd_tick_kernel(double* hyper) {
+__global__ void sgd_tick_kernel(double* hyper, const unsigned long long* skip) {
+    if (skip && *skip) return;
     if (threadIdx.x == 0) {
         hyper[1] = hyper[1] + 1.0;
         hyper[3] = hyper[2];
@@ -797,7 +802,8 @@ __global__ void sgd_tick_kernel(double* hyper) {
 }
 
 __global__ void sgd_dev_kernel(float* p, const float* g, float* buf, long n, const double* hyper, float mom, float damp,
-                               float wd, int nesterov, float gscale) {
+                               float wd, int nesterov, float gscale, const unsigned long long* skip) {
+    if (skip && *skip) return;
     const float lr = (float)hyper[0];
     const bool first = hyper[3] == 0.0;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -1015,20 +1021,21 @@ extern "C" int scd_adam_step(float* p, const float* g, float* m, float* v, long 
 }
 
 extern "C" int scd_adam_step_dev(float* p, const float* g, float* m, float* v, long n, double* hyper, float beta1,
-                                 float beta2, float eps, float gscale, void* stream) {
+                                 float beta2, float eps, float gscale, const unsigned long long* skip, void* stream) {
     if (!hyper) return SCD_ERR_ARG;
-    hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
+    hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper, skip);
     hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
-                       (const double*)hyper, beta1, beta2, eps, gscale);
+                       (const double*)hyper, beta1, beta2, eps, gscale, skip);
     SCD_RETURN_LAUNCH();
 }
 
 extern "C" int scd_sgd_step_dev(float* p, const float* g, float* buf, long n, double* hyper, float momentum,
-                                float dampening, float weight_decay, int nesterov, float gscale, void* stream) {
+                                float dampening, float weight_decay, int nesterov, float gscale,
+                                const unsigned long long* skip, void* stream) {
     if (!hyper || (momentum != 0.f && !buf)) return SCD_ERR_ARG;
-    hipLaunchKernelGGL(sgd_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper);
+    hipLaunchKernelGGL(sgd_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper, skip);
     hipLaunchKernelGGL(sgd_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, p, g, buf, n,
-                       (const double*)hyper, momentum, dampening, weight_decay, nesterov, gscale);
+                       (const double*)hyper, momentum, dampening, weight_decay, nesterov, gscale, skip);
     SCD_RETURN_LAUNCH();
 }
 

@@ -177,7 +177,7 @@ class FlatAdam(_FlatOptimizer):
         from . import ops
         fp, g = self._begin_step()
         ops.adam_step_dev(fp.data, fp.grad, self._m, self._v, self._hyper, g["betas"][0], g["betas"][1], g["eps"],
-                          gscale=fp.grad_scale)
+                          gscale=fp.grad_scale, skip=ops.optimizer_skip_word())
         return None
 
     def state_dict(self):
@@ -217,7 +217,7 @@ class FlatSGD(_FlatOptimizer):
         from . import ops
         fp, g = self._begin_step()
         ops.sgd_step_dev(fp.data, fp.grad, self._buf, self._hyper, g["momentum"], g["dampening"], g["weight_decay"],
-                         g["nesterov"], gscale=fp.grad_scale)
+                         g["nesterov"], gscale=fp.grad_scale, skip=ops.optimizer_skip_word())
         return None
 
     def state_dict(self):

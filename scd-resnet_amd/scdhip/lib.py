@@ -126,8 +126,8 @@ SIGNATURES = {
     "scd_ceval_summary_workspace": (c_size_t, [L]),
     "scd_ceval_summary": (I, [PP, ctypes.POINTER(c_long), L, P, I, P, P, P]),
     "scd_adam_step": (I, [P, P, P, P, L, F, F, F, F, F, F, F, P]),
-    "scd_adam_step_dev": (I, [P, P, P, P, L, P, F, F, F, F, P]),
-    "scd_sgd_step_dev": (I, [P, P, P, L, P, F, F, F, I, F, P]),
+    "scd_adam_step_dev": (I, [P, P, P, P, L, P, F, F, F, F, P, P]),
+    "scd_sgd_step_dev": (I, [P, P, P, L, P, F, F, F, I, F, P, P]),
     "scd_render_center_targets": (I, [P, P, I, I, I, F, P, P, P, P, P]),
     "scd_cpool_fwd": (I, [I, I, P, P, P, I, I, I, I, P]),
     "scd_cpool_bwd": (I, [I, I, P, P, P, I, I, I, I, P]),
@@ -146,6 +146,9 @@ SIGNATURES = {
     "scd_event_destroy": (I, [P]),
     "scd_event_record": (I, [P, P]),
     "scd_event_elapsed_ms": (I, [P, P, ctypes.POINTER(c_float)]),
+    "scd_calib_mfma_peak": (I, [P, I, I, P, P, P]),
+    "scd_calib_set_stamps": (I, [P]),
+    "scd_calib_stamped_build": (I, []),
     "scd_version": (ctypes.c_char_p, []),
 }
 

@@ -240,22 +240,24 @@ def setup_syncbn(log=None):
     that FlatDDP's gradient buckets overlap the backward (networkFactory.py:126-136; BASELINE north_star: the
     all-reduce "overlapped with backward"):
 
-    * default: the statistics over peer memory when every rank can map every peer's mailbox -- checked collectively,
+    * default: through torch.distributed on ops.syncbn_group() -- WORLD, where RCCL serialises them with the buckets on
+      one communicator, so every bucket goes at the end of the backward (FlatDDP.overlap_buckets) -- or a communicator
+      of their own with SCD_SYNCBN_OWN_GROUP=1;
+    * SCD_SYNCBN_PEER=auto: over peer memory when every rank can map every peer's mailbox -- checked collectively,
       with a probe all-reduce (scdhip.peer.PeerAllReduce.try_create) -- so SyncBN issues no collective at all and
-      FlatDDP launches each bucket on WORLD from inside the backward as soon as its gradients are written;
-    * else (a rank cannot map its peers, no GPU, or SCD_SYNCBN_PEER=0): through torch.distributed on
-      ops.syncbn_group() -- WORLD, where RCCL serialises them with the buckets on one communicator, so every bucket
-      goes at the end of the backward (FlatDDP.overlap_buckets) -- or a communicator of their own with
-      SCD_SYNCBN_OWN_GROUP=1.  SCD_SYNCBN_PEER=1 requires the peer path (raises if it cannot be set up).
+      FlatDDP launches each bucket on WORLD from inside the backward as soon as its gradients are written; else (a
+      rank cannot map its peers, no GPU, more than one node's ranks) the default above, with the reason logged.
+      SCD_SYNCBN_PEER=1 requires the peer path (raises if it cannot be set up).  Opt-in until it has run on separate
+      GPUs over xGMI: every run so far had its ranks share one GPU.
 
     Collective: every rank calls it once, before FlatDDP is built.  Returns bn_sync_mode(); `log` (a callable) gets
     one line saying which transport runs and, for a fallback, why."""
-    want = os.environ.get("SCD_SYNCBN_PEER", "auto").lower()
+    want = os.environ.get("SCD_SYNCBN_PEER", "0").lower()
     if _BNSync.peer is not None:
         _BNSync.peer.close()
         _BNSync.peer = None
     _BNSync.why = None
-    if want not in ("0", "off") and torch.cuda.is_available() and dist.get_world_size() > 1:
+    if want in ("1", "auto", "on") and torch.cuda.is_available() and dist.get_world_size() > 1:
         from .peer import PeerAllReduce
         peer, why = PeerAllReduce.try_create(dist.group.WORLD)
         if peer is None and want == "1":
@@ -264,8 +266,8 @@ def setup_syncbn(log=None):
             _BNSync.group, _BNSync.world, _BNSync.peer = dist.group.WORLD, dist.get_world_size(), peer
         else:
             _BNSync.why = why
-    elif want in ("0", "off"):
-        _BNSync.why = "SCD_SYNCBN_PEER=0"
+    elif want not in ("1", "auto", "on"):
+        _BNSync.why = "opt-in (SCD_SYNCBN_PEER=auto)"
     else:
         _BNSync.why = "no GPU" if not torch.cuda.is_available() else "world 1"
     if _BNSync.peer is None:
@@ -1294,13 +1296,21 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, gscale=1.0):
            float(eps), float(bc1), float(bc2), float(gscale), stream())
 
 
-def adam_step_dev(p, g, m, v, hyper, beta1, beta2, eps, gscale=1.0):
-    """Adam with the step state on the device (hyper = {lr, step} fp64, step advanced on the stream)."""
+def optimizer_skip_word():
+    """The device word the optimizer kernels test before updating: the peer-memory SyncBN error word when
+    that path is on -- a failed call NaN-poisons its statistics, so that step's gradients must not reach the weights
+    -- else None (no test)."""
+    return _BNSync.peer.err if _BNSync.peer is not None else None
+
+
+def adam_step_dev(p, g, m, v, hyper, beta1, beta2, eps, gscale=1.0, skip=None):
+    """Adam with the step state on the device (hyper = {lr, step} fp64, step advanced on the stream); skip: a device
+    int64 word, non-zero = leave everything unchanged."""
     L.call("scd_adam_step_dev", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(hyper), float(beta1), float(beta2),
-           float(eps), float(gscale), stream())
+           float(eps), float(gscale), ptr(skip) if skip is not None else None, stream())
 
 
-def sgd_step_dev(p, g, buf, hyper, momentum, dampening, weight_decay, nesterov, gscale=1.0):
+def sgd_step_dev(p, g, buf, hyper, momentum, dampening, weight_decay, nesterov, gscale=1.0, skip=None):
     """torch.optim.SGD step over the flat buffer (networkFactory.py:84-89); hyper = {lr, step, initialised, snapshot}
     fp64 on the device (scd_sgd_step_dev reads and writes all four)."""
     if hyper.dtype != torch.float64 or hyper.numel() < 4 or not hyper.is_contiguous():
@@ -1308,7 +1318,8 @@ def sgd_step_dev(p, g, buf, hyper, momentum, dampening, weight_decay, nesterov, 
                            "{lr, step, initialised, snapshot}")
     _need_gpu(p)
     L.call("scd_sgd_step_dev", ptr(p), ptr(g), ptr(buf) if buf is not None else None, p.numel(), ptr(hyper),
-           float(momentum), float(dampening), float(weight_decay), int(bool(nesterov)), float(gscale), stream())
+           float(momentum), float(dampening), float(weight_decay), int(bool(nesterov)), float(gscale),
+           ptr(skip) if skip is not None else None, stream())
 
 
 def decode_topk(heat, offset, regr, K=100):

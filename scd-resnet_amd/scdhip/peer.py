@@ -3,10 +3,12 @@
 Every BN layer of a multi-GPU step all-reduces 2C fp64 sums twice (forward statistics, backward sums), each a small
 message on the critical path.  PeerAllReduce maps every rank's fine-grained mailbox into every process (hipIpc
 handles exchanged once through torch.distributed) and reduces with one kernel per call: write into every mailbox,
-flag, wait, sum in rank order.  The default SyncBN transport at world > 1 when every rank can map every peer's mailbox
-(``try_create``: checked collectively at set-up, with a probe all-reduce; ops.setup_syncbn), because it takes the SyncBN
-statistics off the RCCL communicator, so FlatDDP can all-reduce its gradient buckets on WORLD from inside the backward;
-SCD_SYNCBN_PEER=0 forces RCCL.  Single node, <= 8 ranks, eager steps (the epoch is a host counter).
+flag, wait, sum in rank order.  Opt-in (SCD_SYNCBN_PEER=auto: used when every rank can map every peer's mailbox,
+``try_create``: checked collectively at set-up, with a probe all-reduce, else RCCL; SCD_SYNCBN_PEER=1: required),
+because it takes the SyncBN statistics off the RCCL communicator, so FlatDDP can all-reduce its gradient buckets on
+WORLD from inside the backward.  RCCL stays the default until this path has run on separate GPUs over xGMI (every
+run so far had its ranks share one GPU).  Single node, <= MAX_RANKS ranks, eager steps (the epoch is a host
+counter).
 
 Late ranks: a rank whose host is seconds behind (a checkpoint write, validation, first-step allocation, a GC pause) is
 waited for on the device, up to SCD_PEER_TIMEOUT_S (120 s).  Only a peer that never arrives is an error: the kernel then
@@ -32,6 +34,8 @@ def _gather(obj, group):
 
 
 class PeerAllReduce:
+    MAX_RANKS = 8          # one node: every peer's mailbox mapped into every process
+
     @classmethod
     def try_create(cls, group=None, cap=4096, timeout_s=None, probe_timeout_s=10.0):
         """Collective and failure-tolerant: every rank returns a working PeerAllReduce, or every rank returns None, with
@@ -39,6 +43,10 @@ class PeerAllReduce:
         probe all-reduce (rank-ordered sum checked against its closed form, within probe_timeout_s) must succeed on
         every rank; the ranks agree on that through the group (all_gather_object) after each phase, so no rank is left
         waiting in a collective another rank has abandoned."""
+        R = dist.get_world_size(group)
+        if R > cls.MAX_RANKS:
+            # every rank sees the same world size: all of them return here, none is left in a collective
+            return None, "world %d > %d ranks (peer memory is single-node)" % (R, cls.MAX_RANKS)
         self = cls.__new__(cls)
         self._setup(group, cap, timeout_s)
         err = None
@@ -88,8 +96,8 @@ class PeerAllReduce:
         self.timeout_ms = max(1, min(int(timeout_s * 1000), 0xFFFFFFFF))
         self.R = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        if self.R > 8:
-            raise RuntimeError("PeerAllReduce: at most 8 ranks (one node)")
+        if self.R > self.MAX_RANKS:
+            raise RuntimeError("PeerAllReduce: at most %d ranks (one node)" % self.MAX_RANKS)
         self.cap = cap
         self.own = None
         self.mapped = []

@@ -163,20 +163,35 @@ def check_bn_group(rank, world):
     finally:
         os.environ.pop("SCD_SYNCBN_OWN_GROUP", None)
         ops.set_bn_sync(None)
-    # setup_syncbn (networkFactory / bench): without a GPU the peer-memory path is not tried, SyncBN falls back to
-    # WORLD (every rank agrees, the reason is logged) and the buckets wait for the end of the backward
+    # setup_syncbn (networkFactory / bench): by default SyncBN runs on WORLD over torch.distributed (the peer-memory
+    # path is opt-in) and the buckets wait for the end of the backward; with SCD_SYNCBN_PEER=auto and no GPU the peer
+    # path is not tried either (every rank agrees, the reason is logged)
     if not torch.cuda.is_available():
         logs = []
         try:
             assert ops.setup_syncbn(log=logs.append) == "rccl-world"
-            assert ops.bn_sync_mode() == "rccl-world" and ops._BNSync.why == "no GPU", ops._BNSync.why
-            assert len(logs) == 1 and "no GPU" in logs[0] and "end of the backward" in logs[0], logs
+            assert ops.bn_sync_mode() == "rccl-world" and "opt-in" in ops._BNSync.why, ops._BNSync.why
+            assert len(logs) == 1 and "opt-in" in logs[0] and "end of the backward" in logs[0], logs
+            os.environ["SCD_SYNCBN_PEER"] = "auto"
+            assert ops.setup_syncbn(log=logs.append) == "rccl-world"
+            assert ops._BNSync.why == "no GPU" and "no GPU" in logs[-1], (ops._BNSync.why, logs)
             os.environ["SCD_SYNCBN_OWN_GROUP"] = "1"
             assert ops.setup_syncbn() == "rccl-own"
         finally:
             os.environ.pop("SCD_SYNCBN_OWN_GROUP", None)
+            os.environ.pop("SCD_SYNCBN_PEER", None)
             ops.set_bn_sync(None)
         assert ops.bn_sync_mode() == "off"
+        # more ranks than one node's peer memory serves: try_create declines on every rank before any GPU call or
+        # collective (it raised), so setup_syncbn falls back instead of crashing
+        from scdhip.peer import PeerAllReduce
+        saved = PeerAllReduce.MAX_RANKS
+        PeerAllReduce.MAX_RANKS = world - 1
+        try:
+            peer, why = PeerAllReduce.try_create(dist.group.WORLD)
+            assert peer is None and "world %d > %d" % (world, world - 1) in why, why
+        finally:
+            PeerAllReduce.MAX_RANKS = saved
 
 
 def main():

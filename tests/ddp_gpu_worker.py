@@ -1,12 +1,14 @@
 """One rank of the GPU data-parallel parity test (F7 at W=2, F7b at W=4): the ranks share cuda:0 over gloo (RCCL cannot
 put two ranks on one device; the 8-GPU RCCL path is the same code with backend "nccl").
 Checks SyncBN statistics + FlatDDP gradient averaging against the reference's golden vectors with the SyncBN transport
-ops.setup_syncbn picks: by default the peer-memory path (the ranks map each other's mailboxes), so the gradient buckets
-are all-reduced from inside the backward; with SCD_SYNCBN_PEER=0 torch.distributed on WORLD beside the buckets (they
-then wait for the end of the backward) or, with SCD_SYNCBN_OWN_GROUP=1, on a group of its own.  EXPECT_SYNCBN names
+ops.setup_syncbn picks: by default torch.distributed on WORLD beside the buckets (they then wait for the end of the
+backward); with SCD_SYNCBN_PEER=auto the peer-memory path (the ranks map each other's mailboxes), so the gradient
+buckets are all-reduced from inside the backward; with SCD_SYNCBN_OWN_GROUP=1 a group of its own.  EXPECT_SYNCBN names
 the mode the test requires."""
 import os
 import sys
+
+import zlib
 
 import numpy as np
 import torch
@@ -71,6 +73,12 @@ def main():
     for k, p in m.named_parameters():
         np.testing.assert_allclose(p.grad.double().norm().item(), float(g["gnorm|" + k]), rtol=rtol, atol=1e-6,
                                    err_msg=k)
+    # sampled gradient ELEMENTS (gsamp|, make_golden.py:238 / make_golden_ddp4.py:51): |g - g_ref| <= rtol x max|g|
+    for k, p in m.named_parameters():
+        gr = p.grad.detach().double().cpu().reshape(-1)
+        pos = np.random.RandomState(zlib.crc32(k.encode()) & 0xFFFFFFFF).randint(0, gr.numel(), 16)
+        err = np.abs(gr[pos].numpy() - np.asarray(g["gsamp|" + k], dtype=np.float64)).max()
+        assert err <= rtol * max(gr.abs().max().item(), 1e-30), (rank, k, err)
     # a second backward on the same batch launches gradient buckets during backward (FlatDDP learned the
     # hook kinds on the first one): the averaged gradients must not change
     first = {k: p.grad.double().norm().item() for k, p in m.named_parameters()}
@@ -82,7 +90,7 @@ def main():
     for k, p in m.named_parameters():
         np.testing.assert_allclose(p.grad.double().norm().item(), first[k], rtol=1e-5, atol=1e-9, err_msg=k)
     # the head/deconv bucket is all-reduced from inside the backward pass, not from the end-of-backward callback --
-    # unless SyncBN shares FlatDDP's group (SCD_SYNCBN_PEER=0 on WORLD), where every bucket waits for the end of it
+    # unless SyncBN shares FlatDDP's group (the default, on WORLD), where every bucket waits for the end of it
     assert ddp.overlap_buckets() == (mode != "rccl-world")
     if ddp.overlap_buckets():
         assert ddp.early_launches >= 1, (ddp.early_launches, len(ddp._buckets))

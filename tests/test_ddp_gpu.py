@@ -38,17 +38,17 @@ def _run(worker, world, **extra):
     return outs
 
 
-@pytest.mark.parametrize("world,sync", [(2, "default"), (2, "world"), (2, "own"), (4, "default"), (4, "world"),
-                                        (8, "default")])
+@pytest.mark.parametrize("world,sync", [(2, "default"), (2, "peer"), (2, "own"), (4, "default"), (4, "peer"),
+                                        (8, "default"), (8, "peer")])
 def test_syncbn_ddp_matches_reference(world, sync):
     """F7 (W=2), F7b (W=4) and F7c (W=8: the driver's scaling world size; tests/golden/make_golden_ddp4.py) against
-    the reference's golden vectors, with the SyncBN
-    transport of the default set-up (ops.setup_syncbn: peer-memory statistics, scdhip/peer.py, so the gradient buckets
-    are all-reduced from inside the backward -- asserted) and the RCCL fallbacks: torch.distributed on WORLD beside
-    the buckets (all at the end of the backward) or on a group of their own (SCD_SYNCBN_PEER=0)."""
-    env = {"default": dict(EXPECT_SYNCBN="peer"),
-           "world": dict(SCD_SYNCBN_PEER="0", EXPECT_SYNCBN="rccl-world"),
-           "own": dict(SCD_SYNCBN_PEER="0", SCD_SYNCBN_OWN_GROUP="1", EXPECT_SYNCBN="rccl-own")}[sync]
+    the reference's golden vectors, with each SyncBN transport: the default set-up (ops.setup_syncbn: torch.distributed
+    on WORLD beside the gradient buckets, all at the end of the backward), the opt-in peer-memory statistics
+    (SCD_SYNCBN_PEER=auto, scdhip/peer.py: the gradient buckets are all-reduced from inside the backward -- asserted)
+    and a group of their own (SCD_SYNCBN_OWN_GROUP=1)."""
+    env = {"default": dict(EXPECT_SYNCBN="rccl-world"),
+           "peer": dict(SCD_SYNCBN_PEER="auto", EXPECT_SYNCBN="peer"),
+           "own": dict(SCD_SYNCBN_OWN_GROUP="1", EXPECT_SYNCBN="rccl-own")}[sync]
     outs = _run("ddp_gpu_worker.py", world, **env)
     for o in outs:
         assert "OK rank" in o, o

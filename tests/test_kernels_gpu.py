@@ -522,6 +522,47 @@ def test_adam_device_state_matches_torch():
     np.testing.assert_allclose(p.cpu().numpy(), pt.detach().numpy(), rtol=1e-6, atol=1e-7)
 
 
+def test_optimizer_skip_word_and_nan_bn_finalize():
+    """after a failed peer-memory SyncBN call (its error word set, statistics NaN) the Adam / SGD step
+    changes nothing (parameters, moments, step count) and the BN finalize keeps running_mean / running_var AND
+    num_batches_tracked; with the word clear, both update as usual."""
+    from scdhip import ops
+    p0 = torch.randn(5003, device=DEV)
+    gr = torch.randn(5003, device=DEV)
+    bad = torch.ones(1, dtype=torch.int64, device=DEV)
+    ok = torch.zeros(1, dtype=torch.int64, device=DEV)
+    p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+    hyper = torch.tensor([1e-3, 0.0], dtype=torch.float64, device=DEV)
+    ops.adam_step_dev(p, gr, m, v, hyper, 0.9, 0.999, 1e-8, skip=bad)
+    torch.cuda.synchronize()
+    assert torch.equal(p, p0) and not m.any() and not v.any() and hyper[1].item() == 0.0
+    ops.adam_step_dev(p, gr, m, v, hyper, 0.9, 0.999, 1e-8, skip=ok)
+    torch.cuda.synchronize()
+    assert not torch.equal(p, p0) and hyper[1].item() == 1.0
+    buf = torch.zeros_like(p0)
+    p = p0.clone()
+    sh = torch.tensor([0.1, 0.0, 0.0, 0.0], dtype=torch.float64, device=DEV)
+    ops.sgd_step_dev(p, gr, buf, sh, 0.9, 0.0, 1e-4, False, skip=bad)
+    torch.cuda.synchronize()
+    assert torch.equal(p, p0) and not buf.any() and sh[1].item() == 0.0
+    # BN finalize on NaN-poisoned (collapsed, nrep 1) statistics
+    C = 96
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    bn.running_mean.normal_()
+    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
+    nb = int(bn.num_batches_tracked.item())
+    stats = torch.full((2 * C,), float("nan"), dtype=torch.float64, device=DEV)
+    st = ops._bn_state(C, DEV)
+    ops._bn_finalize_launch(bn, st, stats, 1, C, 100.0)
+    torch.cuda.synchronize()
+    assert torch.equal(bn.running_mean, rm) and torch.equal(bn.running_var, rv)
+    assert int(bn.num_batches_tracked.item()) == nb
+    stats = torch.cat([torch.full((C,), 5.0), torch.full((C,), 100.0)]).double().to(DEV)
+    ops._bn_finalize_launch(bn, st, stats, 1, C, 100.0)
+    torch.cuda.synchronize()
+    assert int(bn.num_batches_tracked.item()) == nb + 1 and not torch.equal(bn.running_mean, rm)
+
+
 @pytest.mark.parametrize("nesterov,damp", [(False, 0.0), (True, 0.0), (False, 0.25)])
 def test_flat_sgd_matches_torch(nesterov, damp):
     """FlatSGD (scd_sgd_step_dev) against torch.optim.SGD with the reference's settings (networkFactory.py:84-89:

@@ -123,6 +123,22 @@ def _assert_gnorms(m, ref_of, tag, rtol):
     assert worst[0][1] < rtol, (tag, worst)
 
 
+def _assert_gsamp(grads, g, nsamp, tol, tag):
+    """Sampled gradient ELEMENTS against the reference's (`gsamp|<param>`, positions from the fixture's crc32 rule):
+    |g - g_ref| <= tol x max|g| of the tensor -- a wrong-permutation or wrong-tap gradient with the right norm fails
+    here.  Prints the worst four ratios first."""
+    worst = {}
+    for k, gr in grads.items():
+        gr = gr.detach().double().cpu().reshape(-1)
+        pos = _pos(k, gr.numel(), nsamp)
+        ref = np.asarray(g["gsamp|" + k], dtype=np.float64)
+        scale = max(gr.abs().max().item(), 1e-30)
+        worst[k] = float(np.abs(gr[pos].numpy() - ref).max() / scale)
+    top = sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+    print(tag, "worst sampled-gradient errors (/ max|g|):", top)
+    assert top[0][1] <= tol, (tag, top)
+
+
 def test_f3_train_step(golden):
     from scdhip.flat import FlatAdam
     g = golden("step")
@@ -149,6 +165,8 @@ def test_f3_train_step(golden):
     # fp32 parity mode against the reference's CPU step (summation order differs: MFMA tiles, split-K, fp64 BN
     # sums); was rtol 1e-2 through round 2
     assert worst[0][1] < 1e-3, worst
+    # elementwise: 16 sampled gradient elements per parameter (fixture gsamp|, make_golden.py:185)
+    _assert_gsamp(grads, g, 16, 1e-3, "F3")
 
 
 def test_bf16_forward_close_to_fp32(f1_outputs):
@@ -208,6 +226,8 @@ def test_f9_res50_bottleneck_step(dtype, golden):
         np.testing.assert_allclose(loss.item(), float(g["loss"]), rtol=1e-4)
         np.testing.assert_allclose([s.item() for s in stats], g["stats"], rtol=1e-4, atol=1e-6)
         _assert_gnorms(m, lambda k: float(g["gnorm|" + k]), "F9", 1e-2)
+        # 8 sampled gradient elements per parameter (make_golden_res50.py:56), at the norms' 1e-2
+        _assert_gsamp({k: p.grad for k, p in m.named_parameters()}, g, 8, 1e-2, "F9")
         sd = m.state_dict()
         for k in g.files:
             if k.startswith("rs|"):

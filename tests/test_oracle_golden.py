@@ -123,6 +123,9 @@ def test_f3_train_step(spec, golden):
         np.testing.assert_allclose(grads[k].double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7)
         np.testing.assert_allclose(pre[k].reshape(-1)[pos].numpy(), g["p0samp|" + k], rtol=0, atol=0)
         np.testing.assert_allclose(v.detach().reshape(-1)[pos].numpy(), g["psamp|" + k], rtol=1e-5, atol=2e-6)
+        gmax = max(grads[k].abs().max().item(), 1e-30)
+        np.testing.assert_allclose(grads[k].reshape(-1)[pos].numpy(), g["gsamp|" + k], rtol=0, atol=1e-4 * gmax,
+                                   err_msg=k)
 
 
 def test_f6_layer_stats(spec, golden):
@@ -160,6 +163,9 @@ def test_f7_ddp_syncbn(spec, golden, name, world, per, seeds):
         np.testing.assert_allclose(losses[r].item(), g["loss_r%d" % r], rtol=1e-4)
     for k, v in P.items():
         np.testing.assert_allclose(v.grad.double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7)
+        gmax = max(v.grad.abs().max().item(), 1e-30)
+        np.testing.assert_allclose(v.grad.reshape(-1)[_pos(k, v.numel(), 16)].numpy(), g["gsamp|" + k], rtol=0,
+                                   atol=1e-4 * gmax, err_msg=k)
     for k in g.files:
         if k.startswith("rs|"):
             np.testing.assert_allclose(Bf[k[3:]].numpy(), g[k], rtol=1e-4, atol=1e-5, err_msg=k)
@@ -236,6 +242,9 @@ def test_f9_res50_bottleneck_step(golden):
     np.testing.assert_allclose([s.item() for s in stats], g["stats"], rtol=1e-4, atol=1e-6)
     for k, v in st.P.items():
         np.testing.assert_allclose(v.grad.double().norm().item(), g["gnorm|" + k], rtol=2e-3, atol=1e-7, err_msg=k)
+        gmax = max(v.grad.abs().max().item(), 1e-30)
+        np.testing.assert_allclose(v.grad.reshape(-1)[_pos(k, v.numel(), 8)].numpy(), g["gsamp|" + k], rtol=0,
+                                   atol=1e-3 * gmax, err_msg=k)
     for k in g.files:
         if k.startswith("rs|"):
             np.testing.assert_allclose(st.B[k[3:]].numpy(), g[k], rtol=1e-4, atol=1e-6, err_msg=k)

@@ -10,12 +10,21 @@ python tools/pmc_kernels.py --case {lastconv,cpool_add,heads_res50,s1x1_fwd,s1x1
                size / offset heads kept at 30 random pixels per image (conv_gemm_heads384_kernel, as HeadsFn)
   s1x1_fwd     its layer1 conv3 / downsample forward: 1x1 64 -> 256 + BN statistics, B=16 at 256x256, fp16
                (conv1x1_stream_kernel<64,256,0,4,2,4>; algorithmic 2 x (64 + 256) B = 640 B per pixel, 671 MB)
+  heads_dgrad  centerOffsetRes10 B=32 (configs[1]) heatmap-head input gradient with the deconv3 BN's backward sums:
+               dhid (32,128,128,128) -> dfeat (32,128,128,256), 3x3 (conv_gemm_pp_kernel<256>, bnbwd epilogue)
+  deconv3_dgrad  its deconv3 input gradient with the deconv2 BN's backward sums: dy (32,128,128,256) -> (32,64,64,256),
+               ConvTranspose 4x4 / 2 (conv_gemm_pp_kernel<256>, bnbwd epilogue)
+  wgrad_hm     its heatmap-head weight gradient: dhid (32,128,128,128) x feat (32,128,128,256), 3x3
+               (conv_wgrad_pp2_kernel<2> + wgrad_reduce_kernel)
+  wgrad_d3     its deconv3 weight gradient: x (32,64,64,256) x dy (32,128,128,256), 4x4 / 2 taps
+               (conv_wgrad_pp2_kernel<4> + wgrad_reduce_kernel)
   s1x1_bnbwd   its layer1 conv3 input gradient with the bn2 backward sums: 1x1 256 -> 64, B=16 at 256x256, fp16
                (conv1x1_stream_kernel<256,64,2,1,1,4>; 2 x (256 + 64 + 64) B = 768 B per pixel, 805 MB)
 """
 import argparse
 import os
 import sys
+import types
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "scd-resnet_amd"))
@@ -26,7 +35,8 @@ from scdhip import ops  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--case", required=True, help="comma-separated: lastconv, cpool_add, heads_res50, s1x1_fwd, s1x1_bnbwd")
+    ap.add_argument("--case", required=True, help="comma-separated: lastconv, cpool_add, heads_res50, s1x1_fwd, s1x1_bnbwd, heads_dgrad, "
+                    "deconv3_dgrad, wgrad_hm, wgrad_d3")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     for case in a.case.split(","):
@@ -71,6 +81,45 @@ def run_case(case, reps):
 
         def run():
             ops.L.call("scd_conv_gemm_heads_keep", *args, ops.stream())
+    elif case in ("heads_dgrad", "deconv3_dgrad"):
+        bf = torch.bfloat16
+        st = types.SimpleNamespace(mean=torch.randn(256, device=dev, generator=g) * 0.1,
+                                   invstd=torch.rand(256, device=dev, generator=g) + 0.5,
+                                   scale=torch.rand(256, device=dev, generator=g) + 0.5,
+                                   shift=torch.randn(256, device=dev, generator=g) * 0.1)
+        stats = ops.new_stats(256, dev)
+        if case == "heads_dgrad":
+            dy = torch.randn(32, 128, 128, 128, device=dev, generator=g).to(bf)
+            wt = ops.pack_weight(torch.randn(128, 256, 3, 3, device=dev, generator=g) / 30, bf, 1)
+            y = torch.randn(32, 128, 128, 256, device=dev, generator=g).to(bf)
+            dx = torch.empty(32, 128, 128, 256, device=dev, dtype=bf)
+
+            def run():
+                ops.conv_dgrad(dy, wt, 256, 128, 128, 3, 3, 1, 1, out=dx, bn_bwd=(st, y, stats))
+        else:
+            dy = torch.randn(32, 128, 128, 256, device=dev, generator=g).to(bf)
+            wp = ops.pack_weight(torch.randn(256, 256, 4, 4, device=dev, generator=g) / 60, bf, 0)
+            y = torch.randn(32, 64, 64, 256, device=dev, generator=g).to(bf)
+            dx = torch.empty(32, 64, 64, 256, device=dev, dtype=bf)
+
+            def run():
+                ops.deconv_dgrad(dy, wp, 256, 4, 2, 1, out=dx, bn_bwd=(st, y, stats))
+    elif case in ("wgrad_hm", "wgrad_d3"):
+        bf = torch.bfloat16
+        if case == "wgrad_hm":
+            gy = torch.randn(32, 128, 128, 128, device=dev, generator=g).to(bf)
+            x = torch.randn(32, 128, 128, 256, device=dev, generator=g).to(bf)
+            dst = torch.zeros(128, 256, 3, 3, device=dev)
+            k, s, pd = 3, 1, 1
+        else:
+            gy = torch.randn(32, 64, 64, 256, device=dev, generator=g).to(bf)
+            x = torch.randn(32, 128, 128, 256, device=dev, generator=g).to(bf)
+            dst = torch.zeros(256, 256, 4, 4, device=dev)
+            k, s, pd = 4, 2, 1
+        T = k * k
+
+        def run():
+            ops._conv_wgrad(gy, x, k, k, s, pd, dst, (dst.shape[1] * T, T, 1))
     elif case in ("s1x1_fwd", "s1x1_bnbwd"):
         N, H, W = 16, 256, 256
         dt = torch.float16
