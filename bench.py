@@ -43,6 +43,12 @@ def parse():
                          "random sparse targets of the same layout (e.g. BASELINE configs[4]: Res50 at 1024)")
     ap.add_argument("--cpu-baseline-steps", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--class-rooflines", type=int, default=None,
+                    help="extra steps after the timed region with HIP events around every GEMM / weight-gradient / BN "
+                         "launch (scdhip.ops.ClassTimer): per-class time and roofline (default: 5 for models other "
+                         "than the Res10 headline, 0 for it)")
+    ap.add_argument("--no-calib", action="store_true",
+                    help="skip the achievable-peak calibration (scdhip.calib.mfma_peak, ~4 s after the timed steps)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a captured HIP graph (scdhip/graph.py; single process).  Off by default: "
                          "on ROCm 7 the replayed two-stream step measured 7.85 ms against 7.63 ms eager")
@@ -124,13 +130,17 @@ def pmc_traffic(kernel, batch, dtype, model="centerOffsetRes10", S=512):
     """HBM bytes per launch of `kernel` (a key of the summary, or a substring of one) from the newest committed
     rocprofv3 PMC summary for this workload (profiles/r<N>_pmc_*.json, written by tools/pmc_summary.py from separate
     FETCH_SIZE and WRITE_SIZE passes: of this same bench command for Res10, of tools/pmc_kernels.py -- the same kernel
-    on the same shape -- for the other BASELINE configs), or None when none matches."""
+    on the same shape -- for the other BASELINE configs).  Only a summary stamped with THIS library's build identity
+    (scd_version(): a hash of the sources built) is used; (None, reason) when none matches."""
     import glob
     import re
+    from scdhip import lib as L
+    mine = L.lib().dll.scd_version().decode()
     # (round-numbered summaries only: r<N>_pmc_*.json, newest round first; any other name is skipped)
     files = [f for f in glob.glob(os.path.join(REPO, "profiles", "r*_pmc_*.json"))
              if re.match(r"r\d+_pmc_", os.path.basename(f))]
     files.sort(key=lambda f: int(re.match(r"r(\d+)_", os.path.basename(f)).group(1)))
+    other = None
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
@@ -139,9 +149,14 @@ def pmc_traffic(kernel, batch, dtype, model="centerOffsetRes10", S=512):
             continue
         ks = d.get("kernels", {})
         hit = kernel if kernel in ks else next((k for k in sorted(ks) if kernel in k), None)
-        if hit is not None:
-            return ks[hit]["hbm_bytes"], os.path.relpath(f, REPO)
-    return None, None
+        if hit is None:
+            continue
+        if d.get("scd_version") != mine:
+            other = other or "%s was taken with %s, not this build (%s)" % (
+                os.path.relpath(f, REPO), d.get("scd_version", "an unstamped library"), mine)
+            continue
+        return ks[hit]["hbm_bytes"], os.path.relpath(f, REPO)
+    return None, other
 
 
 def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2), kept_px=None, model="centerOffsetRes10"):
@@ -169,7 +184,8 @@ def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2), ke
         traffic, src = pmc_traffic("heads384", B, dtype_name, model=model, S=S)
     return {"bound": "mfma", "kernel": kernel, "achieved": round(achieved, 1), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-            "traffic": None if traffic is None else round(traffic), "traffic_source": src,
+            "traffic": None if traffic is None else round(traffic), "traffic_source": src if traffic is not None else None,
+            "traffic_note": None if traffic is not None else src,
             "algorithmic_bytes": algo_bytes, "flop_per_launch": flops, "avg_launch_ms": round(ms, 4),
             "launches_timed": n}
 
@@ -405,6 +421,18 @@ def main():
         dist.all_reduce(tl, op=dist.ReduceOp.MAX)
         local_ms = 1e3 * tl.item() / args.steps
 
+    ncls = args.class_rooflines if args.class_rooflines is not None else (
+        0 if (args.model == "centerOffsetRes10" and S == 512) else 5)
+    classes = None
+    if ncls > 0 and world == 1:
+        # after the timed region: per-class kernel time and algorithmic work over ncls more steps (events around every
+        # launch of a class, on its stream; classes on the two streams overlap, so their times do not add up to the step)
+        ops.ClassTimer.on = True
+        for _ in range(ncls):
+            step()
+        ops.ClassTimer.on = False
+        classes = ops.ClassTimer.collect(ncls)
+
     if rank == 0:
         imgs = B * world * args.steps
         value = imgs / elapsed
@@ -453,6 +481,27 @@ def main():
             "step_mfma_frac_dense_equiv": round(value * gflop / 1e3 / peak, 4),
             "final_loss": round(final_loss, 5),
         }
+        if classes:
+            mfma_peak = PEAK_F32_TFLOPS if dtype == torch.float32 else PEAK_BF16_TFLOPS
+            cr = {}
+            for name, d in sorted(classes.items(), key=lambda kv: -kv[1]["ms_per_step"]):
+                rate = d["work_per_step"] / (d["ms_per_step"] * 1e-3)
+                if name == "bn":
+                    ach, peak, unit, bound = rate / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+                else:
+                    ach, peak, unit, bound = rate / 1e12, mfma_peak, "TFLOP/s", "mfma"
+                cr[name] = {"bound": bound, "kernel_ms_per_step": round(d["ms_per_step"], 3),
+                            "share_of_step": round(d["ms_per_step"] / line["ms_per_step"], 4),
+                            "launches_per_step": round(d["launches_per_step"], 1),
+                            ("gflop_per_step" if bound == "mfma" else "mb_per_step"):
+                                round(d["work_per_step"] / (1e9 if bound == "mfma" else 1e6), 1),
+                            "achieved": round(ach, 1), "peak": peak, "unit": unit, "frac": round(ach / peak, 4)}
+            line["class_rooflines"] = {
+                "method": "HIP events around every launch of a class over %d steps after the timed region "
+                          "(scdhip.ops.ClassTimer); gemm = forward / input-gradient gather-GEMMs (all kernels), "
+                          "wgrad = weight-gradient GEMM + split reduce, bn = BatchNorm apply / backward passes "
+                          "(algorithmic bytes); the side-stream weight gradients overlap the rest" % ncls,
+                **cr}
         if local_ms is not None:
             # in-run split of the N-rank step: the same per-rank work without any collective (not the driver's
             # cross-run scaling efficiency, which it computes from the per-N values itself)
@@ -465,6 +514,21 @@ def main():
                                 "peer_fallback_reason": ops._BNSync.why,
                                 "buckets_overlap_backward": bool(model.overlap_buckets()),
                                 "early_bucket_launches": int(model.early_launches)}
+        if world == 1 and not args.no_calib and dtype != torch.float32:
+            # the bf16 MFMA rate this box sustains (bare 16x16x32 loops on random operands, 2 waves per SIMD, after
+            # 2.5 s of back-to-back launches: MI355X_MICROARCH.md "DVFS give-back"), beside the 2.5 PF/s nameplate
+            from scdhip import calib
+            cal = calib.mfma_peak(waves_per_simd=2)
+            pa = cal["tflops"]
+            for r in ([line.get("roofline")] + [v for v in extra.values() if isinstance(v, dict)] +
+                      [v for v in line.get("class_rooflines", {}).values() if isinstance(v, dict)]):
+                if r and r.get("unit") == "TFLOP/s":
+                    r["peak_achievable"] = pa
+                    r["frac_achievable"] = round(r["achieved"] / pa, 4)
+            line["peak_achievable"] = {"tflops": pa, "clock_ghz": cal["clock_ghz"],
+                                       "source": "scd_calib_mfma_peak: 16x16x32 bf16 MFMA loops on random operands, "
+                                                 "2 waves/SIMD, in-kernel clock from s_memtime / s_memrealtime"}
+            line["step_mfma_frac_achievable"] = round(value * executed / 1e3 / (world * pa), 4)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_baseline_steps)
         print(json.dumps(line), flush=True)

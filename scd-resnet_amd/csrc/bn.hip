@@ -678,9 +678,9 @@ extern "C" int scd_bn_apply(int dtype, const void* y, void* out, int C, long tot
     if (dtype == SCD_DT_BF16) {
         if (C % 8 || !ew_rows_ok(C / 8)) return SCD_ERR_ARG;
         long nvec = total / 8;
-        static const int g = resident_grid((const void*)bn_apply_kernel<__bf16>, 256);
-        hipLaunchKernelGGL((bn_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 0, st, (const __bf16*)y,
-                           (__bf16*)out, C, (unsigned)nvec, scale, shift, (const __bf16*)res, rscale, rshift, relu);
+        static const int g = resident_grid((const void*)bn_apply_kernel<h16>, 256);
+        hipLaunchKernelGGL((bn_apply_kernel<h16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), 0, st, (const h16*)y,
+                           (h16*)out, C, (unsigned)nvec, scale, shift, (const h16*)res, rscale, rshift, relu);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4 || !ew_rows_ok(C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;
@@ -707,7 +707,7 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
     const int scpr = std::min(cpr, 256), sC = scpr * E;
     // one round of resident blocks (at most), at least 8 rows per row lane
     const size_t lds = (size_t)4 * sC * sizeof(float);
-    const long nb = dtype == SCD_DT_BF16 ? ew_resident<4>((const void*)bn_bwd_reduce_kernel<__bf16>, lds)
+    const long nb = dtype == SCD_DT_BF16 ? ew_resident<4>((const void*)bn_bwd_reduce_kernel<h16>, lds)
                                          : ew_resident<5>((const void*)bn_bwd_reduce_kernel<float>, lds);
     const long rpi = 256 / scpr;
     const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
@@ -720,8 +720,8 @@ extern "C" int scd_bn_bwd_reduce(int dtype, const void* dout, const void* mask, 
         const float* rs = relu_scale ? relu_scale + c0 : nullptr;
         const float* rh = relu_shift ? relu_shift + c0 : nullptr;
         if (dtype == SCD_DT_BF16)
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)dz,
-                               (const __bf16*)mk, (const __bf16*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<h16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const h16*)dz,
+                               (const h16*)mk, (const h16*)yy, rs, rh, mean + c0, invstd + c0, sC, C,
                                (unsigned)rows, (unsigned)rpb, stats + c0);
         else if (dtype == SCD_DT_F32)
             hipLaunchKernelGGL((bn_bwd_reduce_kernel<float>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const float*)dz,
@@ -750,7 +750,7 @@ extern "C" int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask,
     const int scpr = std::min(cpr, 256), sC = scpr * E;
     // the same row partition as scd_bn_bwd_reduce (per-thread partial sums identical to two separate passes)
     const size_t lds = (size_t)4 * sC * sizeof(float);
-    const long nb = dtype == SCD_DT_BF16 ? ew_resident<4>((const void*)bn_bwd_reduce_kernel<__bf16>, lds)
+    const long nb = dtype == SCD_DT_BF16 ? ew_resident<4>((const void*)bn_bwd_reduce_kernel<h16>, lds)
                                          : ew_resident<5>((const void*)bn_bwd_reduce_kernel<float>, lds);
     const long rpi = 256 / scpr;
     const long rpb = std::max<long>(8 * rpi, (rows + nb - 1) / nb + rpi - 1) / rpi * rpi;
@@ -761,8 +761,8 @@ extern "C" int scd_bn_bwd_reduce2(int dtype, const void* dout, const void* mask,
         const char *d = (const char*)dout + o, *m = (const char*)mask + o, *a = (const char*)ya + o,
                    *b = (const char*)yb + o;
         if (dtype == SCD_DT_BF16)
-            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<__bf16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const __bf16*)d,
-                               (const __bf16*)m, (const __bf16*)a, (const __bf16*)b, mean_a + c0, invstd_a + c0,
+            hipLaunchKernelGGL((bn_bwd_reduce2_kernel<h16>), dim3(blocks), dim3(256), 4 * sC * 4, st, (const h16*)d,
+                               (const h16*)m, (const h16*)a, (const h16*)b, mean_a + c0, invstd_a + c0,
                                mean_b + c0, invstd_b + c0, sC, C, (unsigned)rows, (unsigned)rpb, stats_a + c0,
                                stats_b + c0);
         else if (dtype == SCD_DT_F32)
@@ -790,10 +790,10 @@ extern "C" int scd_bn_bwd_apply2(int dtype, const void* dout, const void* mask, 
     if (dtype == SCD_DT_BF16) {
         const size_t lds = ew_param_lds(6, C, 8);
         if (lds > EW_LDS_MAX) return SCD_ERR_ARG;
-        const int g = ew_resident<0>((const void*)bn_bwd_apply2_kernel<__bf16>, lds);
-        hipLaunchKernelGGL((bn_bwd_apply2_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), lds, st,
-                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)ya, (const __bf16*)yb, coef_a,
-                           coef_b, C, (unsigned)nvec, (__bf16*)dya, (__bf16*)dyb);
+        const int g = ew_resident<0>((const void*)bn_bwd_apply2_kernel<h16>, lds);
+        hipLaunchKernelGGL((bn_bwd_apply2_kernel<h16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), lds, st,
+                           (const h16*)dout, (const h16*)mask, (const h16*)ya, (const h16*)yb, coef_a,
+                           coef_b, C, (unsigned)nvec, (h16*)dya, (h16*)dyb);
     } else if (dtype == SCD_DT_F32) {
         const size_t lds = ew_param_lds(6, C, 4);
         if (lds > EW_LDS_MAX) return SCD_ERR_ARG;
@@ -825,10 +825,10 @@ extern "C" int scd_bn_bwd_apply(int dtype, const void* dout, const void* mask, c
         long nvec = total / 8;
         const size_t lds = ew_param_lds(5, C, 8);
         if (lds > EW_LDS_MAX) return SCD_ERR_ARG;
-        const int g = ew_resident<2>((const void*)bn_bwd_apply_kernel<__bf16>, lds);
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<__bf16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), lds, st,
-                           (const __bf16*)dout, (const __bf16*)mask, (const __bf16*)y, relu_scale, relu_shift, coef, C,
-                           (unsigned)nvec, (__bf16*)dy, (__bf16*)dz);
+        const int g = ew_resident<2>((const void*)bn_bwd_apply_kernel<h16>, lds);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<h16>), dim3(ew_grid(g, nvec, C / 8)), dim3(256), lds, st,
+                           (const h16*)dout, (const h16*)mask, (const h16*)y, relu_scale, relu_shift, coef, C,
+                           (unsigned)nvec, (h16*)dy, (h16*)dz);
     } else if (dtype == SCD_DT_F32) {
         if (C % 4 || !ew_rows_ok(C / 4)) return SCD_ERR_ARG;
         long nvec = total / 4;

@@ -80,6 +80,8 @@ struct GemmParams {
     int kserp;
     // stamped diagnostic build only (SCD_STAMP, calib.hip): per-workgroup main-loop clock stamps
     unsigned long long* stamps;
+    // duo kernel: workgroups [duo_ncu, 2 duo_ncu) sleep duo_delay x 8K cycles before their first tile
+    int duo_ncu, duo_delay;
 };
 
 #ifndef SCD_STAMP
@@ -106,8 +108,8 @@ struct GemmParams {
 // LDS image of one operand stage: rows of 128 B (BK elements), 16-B chunk c of row r stored at
 // chunk c ^ (r & 7).  ds_read_b128 fragment reads (16 consecutive rows, one chunk) and the
 // ds_write_b128 staging stores (8 chunks of one row) are then bank-conflict free.
-// 16x16x16 MFMA on 4-element 16-bit vectors (the 16-bit type is __bf16, or _Float16 in the SCD_F16_BUILD pass)
-typedef __attribute__((ext_vector_type(4))) __bf16 hx4;
+// 16x16x16 MFMA on 4-element 16-bit vectors (the 16-bit type is h16, or _Float16 in the SCD_F16_BUILD pass)
+typedef __attribute__((ext_vector_type(4))) h16 hx4;
 __device__ __forceinline__ f32x4 mfma_16x16x16(hx4 a, hx4 b, f32x4 c) {
 #ifdef SCD_F16_BUILD
     return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
@@ -253,8 +255,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[
             }
             char* dst = ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * ESZ;
             if constexpr (ESZ == 2) {
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-                bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
+                bf16x4 o = {(h16)v[0], (h16)v[1], (h16)v[2], (h16)v[3]};
                 *(bf16x4*)dst = o;
             } else {
                 *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
@@ -488,17 +490,17 @@ __global__ __launch_bounds__(256 * KS, 2 / KS) void conv_gemm_kernel(GemmParams 
         if constexpr (ESZ == 2) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                bf16x8 af[4], bfr[4];
+                h16x8 af[4], bfr[4];
                 const int co = ((s * 4 + lg) ^ l7) << 4;
 #pragma unroll
-                for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(As + (wm * 64 + a * 16 + l16) * 128 + co);
+                for (int a = 0; a < 4; ++a) af[a] = *(const h16x8*)(As + (wm * 64 + a * 16 + l16) * 128 + co);
 #pragma unroll
-                for (int b = 0; b < 4; ++b) bfr[b] = *(const bf16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
+                for (int b = 0; b < 4; ++b) bfr[b] = *(const h16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+                        acc[a][b] = mfma_16x16x32_h16(bfr[b], af[a], acc[a][b]);
             }
         } else {
             // exact-f32 MFMA: lane group lg owns K elements [8lg, 8lg+8) of the 32-wide stage;
@@ -628,7 +630,7 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, const char* 
 // kernel's plain input gradient and the separate scd_bn_bwd_reduce.
 template <int WO, bool FLIP, bool BNB>
 __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int run) {
-    typedef __bf16 T;
+    typedef h16 T;
     constexpr int TR = WO >= 256 ? 1 : 256 / WO;  // output rows per tile
     constexpr bool DIRECT = WO == 256;            // no staging buffer: stores from the accumulators
     static_assert(!(DIRECT && BNB), "256-pixel rows: BN-backward sums by the separate reduction");
@@ -721,15 +723,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
             const int dhi = FLIP ? 2 - kr : kr, dwi = FLIP ? 2 - kc : kc;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                bf16x8 af[4];
+                h16x8 af[4];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(smem + rowoff[dhi] + abase[dwi][s] + a * 16 * 128);
+                for (int a = 0; a < 4; ++a) af[a] = *(const h16x8*)(smem + rowoff[dhi] + abase[dwi][s] + a * 16 * 128);
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 2; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wreg[t][s][b]),
-                                                                            af[a], acc[a][b], 0, 0, 0);
+                        acc[a][b] = mfma_16x16x32_h16(__builtin_bit_cast(h16x8, wreg[t][s][b]),
+                                                                            af[a], acc[a][b]);
             }
         }
         if constexpr (DIRECT && L1P_SWAP) {
@@ -737,7 +739,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
             // paired by v_permlane16_swap: the lane then holds 8 consecutive channels 32chh + 4lg + 12(lg & 1) ..,
             // one 16-B store per pixel block (16 pixels x 64 B per instruction instead of 16 x 32 B)
             const long base = ((long)(n * p.Ho + r) * p.Wo) * 64;
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
             typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
             const int cst = 32 * chh + 4 * lg + 12 * (lg & 1);
 #pragma unroll
@@ -745,7 +747,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
                 const long off = base + (long)(64 * pw + 16 * a + l16) * 64 + cst;
                 bf16x4 h0, h1;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { h0[q] = (__bf16)acc[a][0][q]; h1[q] = (__bf16)acc[a][1][q]; }
+                for (int q = 0; q < 4; ++q) { h0[q] = (h16)acc[a][0][q]; h1[q] = (h16)acc[a][1][q]; }
                 const u32x2 xv = __builtin_bit_cast(u32x2, h0), yv = __builtin_bit_cast(u32x2, h1);
                 const auto s0 = __builtin_amdgcn_permlane16_swap(xv[0], yv[0], false, false);
                 const auto s1 = __builtin_amdgcn_permlane16_swap(xv[1], yv[1], false, false);
@@ -764,7 +766,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
         } else if constexpr (DIRECT) {
             // the tile is row r of image n: lane's pixel 64pw + 16a + l16 is its column; channels 32chh + 16b + 4lg
             const long base = ((long)(n * p.Ho + r) * p.Wo) * 64;
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
 #pragma unroll
             for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -772,11 +774,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
                     const long off = base + (long)(64 * pw + 16 * a + l16) * 64 + 32 * chh + 16 * b + 4 * lg;
                     bf16x4 o;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) o[q] = (__bf16)acc[a][b][q];
+                    for (int q = 0; q < 4; ++q) o[q] = (h16)acc[a][b][q];
                     if (p.accumulate) {
                         const bf16x4 old4 = *(const bf16x4*)((const T*)p.y + off);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) o[q] = (__bf16)((float)o[q] + (float)old4[q]);
+                        for (int q = 0; q < 4; ++q) o[q] = (h16)((float)o[q] + (float)old4[q]);
                     }
                     *(bf16x4*)((T*)p.y + off) = o;
                 }
@@ -786,10 +788,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
-                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
                 bf16x4 o;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] = (__bf16)acc[a][b][q];
+                for (int q = 0; q < 4; ++q) o[q] = (h16)acc[a][b][q];
                 *(bf16x4*)(stg + (64 * pw + 16 * a + l16) * SROW + (32 * chh + 16 * b + 4 * lg) * 2) = o;
             }
         }
@@ -891,7 +893,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_l1p_kernel(GemmParams p, int
 
 template <bool HEADS, bool BNB = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
-    typedef __bf16 T;
+    typedef h16 T;
     constexpr int BM = 256, BN = 128, WN = 2, BK = 64, EPC = 8;
     constexpr int STAGE = (BM + BN) * 128;          // 48 KiB
     constexpr int NSLOT = 3;
@@ -999,14 +1001,14 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
         else issue(nxt, slot == 0 ? 2 : slot - 1);
         const char* As = smem + slot * STAGE;
         const char* Bs = As + BM * 128;
-        bf16x8 af[2][4], bfr[2][4];
+        h16x8 af[2][4], bfr[2][4];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int co = ((s * 4 + lg) ^ l7) << 4;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) af[s][a] = *(const bf16x8*)(As + (wm * 64 + a * 16 + l16) * 128 + co);
+            for (int a = 0; a < 4; ++a) af[s][a] = *(const h16x8*)(As + (wm * 64 + a * 16 + l16) * 128 + co);
 #pragma unroll
-            for (int b = 0; b < 4; ++b) bfr[s][b] = *(const bf16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
+            for (int b = 0; b < 4; ++b) bfr[s][b] = *(const h16x8*)(Bs + (wn * 64 + b * 16 + l16) * 128 + co);
         }
         if constexpr (SCD_ABLATE == 1) {
 #pragma unroll
@@ -1021,7 +1023,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][b], af[s][a], acc[a][b], 0, 0, 0);
+                        acc[a][b] = mfma_16x16x32_h16(bfr[s][b], af[s][a], acc[a][b]);
             __builtin_amdgcn_s_setprio(0);
         }
         slot = slot == 2 ? 0 : slot + 1;
@@ -1046,7 +1048,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
 // 64..127 of stage t).  Every region is rewritten >= 3 phases after its last fragment read.
 template <int BN, bool HEADS>
 __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
-    typedef __bf16 T;
+    typedef h16 T;
     constexpr int BM = 256, BK = 64, EPC = 8;
     constexpr int NB = BN / 64;                 // 16-channel blocks per wave
     constexpr int WCOLS = BN / 4;               // channels per wave
@@ -1157,26 +1159,26 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     for (int a = 0; a < 8; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 bfr[NB][2], afx[2][2], afy[2][2];
+    h16x8 bfr[NB][2], afx[2][2], afy[2][2];
 
     auto read_b = [&](const char* buf) {
         const char* Bs = buf + BM * 128;
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             const char* row = Bs + (wc * WCOLS + b * 16 + l16) * 128;
-            bfr[b][0] = *(const bf16x8*)(row + co0);
-            bfr[b][1] = *(const bf16x8*)(row + co1);
+            bfr[b][0] = *(const h16x8*)(row + co0);
+            bfr[b][1] = *(const h16x8*)(row + co1);
         }
     };
-    auto read_a = [&](const char* buf, int q, bf16x8 (&af)[2][2]) {
+    auto read_a = [&](const char* buf, int q, h16x8 (&af)[2][2]) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
             const char* row = buf + (128 * grp + 32 * q + 16 * a + l16) * 128;
-            af[a][0] = *(const bf16x8*)(row + co0);
-            af[a][1] = *(const bf16x8*)(row + co1);
+            af[a][0] = *(const h16x8*)(row + co0);
+            af[a][1] = *(const h16x8*)(row + co1);
         }
     };
-    auto mfma_q = [&](int q, const bf16x8 (&af)[2][2]) {
+    auto mfma_q = [&](int q, const h16x8 (&af)[2][2]) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (SCD_ABLATE == 1) {       // ablation: fragments read, no MFMA
@@ -1196,7 +1198,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
-                    acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b][s], af[a][s], acc[2 * q + a][b], 0, 0, 0);
+                    acc[2 * q + a][b] = mfma_16x16x32_h16(bfr[b][s], af[a][s], acc[2 * q + a][b]);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -1334,8 +1336,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
                     csq[b][r] += t * t;
                 }
             }
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-            bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+            typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
+            bf16x4 o = {(h16)v[0], (h16)v[1], (h16)v[2], (h16)v[3]};
             *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
         }
     }
@@ -1544,6 +1546,409 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
 }
 
 // -------------------------------------------------------------------------------------
+// Two-workgroups-per-CU bf16 gather-GEMM ("duo", round 6).  The ping-pong kernel above holds a CU
+// alone (two 64-KiB stages, 8 waves x ~206 VGPRs), so nothing runs while its tile epilogue stores 128 KiB and (BN
+// backward) reads another 128 KiB: stamped in the step's shapes, the main loops take 53 % of the heatmap-head input
+// gradient and 76 % of the deconv3 one (profiles/r6_clock.txt), the rest is per-tile epilogue and prologue with the
+// matrix pipe idle.  Here a 256 x 128 tile belongs to a 4-wave workgroup (waves 2 x 2, 128 x 64 each: the
+// ping-pong kernel's per-wave tile, fragment reads per MFMA and epilogue), its LDS is a 3-slot ring of BK = 32
+// stages (rows of 64 B, 24 KiB per stage) that the epilogue reuses as its staging buffer, and its registers fit
+// 2 waves per SIMD -- so TWO workgroups share each CU, and one's epilogue runs beside the other's MFMAs.  The
+// workgroups of the first round's second slot (blockIdx in [CUs, 2 CUs)) start half a tile late (s_sleep), so the two
+// slots of a CU stay half a tile apart for the whole launch.
+// K order: (64-channel chunk, tap, 32-channel half), so both halves of a pixel's 128-B line are fetched in
+// consecutive K-steps, and every output sees the same MFMA sequence as the ping-pong kernel's (chunk, tap, s = half):
+// bit-identical results.
+// LDS row r (64 B, 4 chunks of 16 B): chunk c in slot c ^ F[(r >> 2) & 3], F = {0, 2, 3, 1}: the 16 lanes of every
+// ds_read_b128 lane group (rows l16, chunk lg) then hit 16 distinct 16-B units of the 256-B bank window; the DMA
+// writes a wave-instruction's 1 KiB lane-linearly (16 rows), so the swizzle is applied to the source chunk.
+// One barrier per K-step: wait for this wave's DMAs of stage k (vmcnt(6): stage k+1's 6 stay in flight), barrier,
+// issue stage k+2 into the slot stage k-1 used, read the fragments of stage k, 32 MFMAs.
+#ifndef DUO_PRIO
+#define DUO_PRIO 1    // duo kernel: s_setprio 1 around a K-step's MFMAs (A/B build option)
+#endif
+#ifndef DUO_ILV
+#define DUO_ILV 1     // duo kernel: DMA issues and fragment reads interleaved with the MFMAs (A/B build option)
+#endif
+__device__ __forceinline__ int duo_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
+__global__ __launch_bounds__(256, 2) void conv_gemm_duo_kernel(GemmParams p) {
+    typedef h16 T;
+    constexpr int BM = 256, BN = 128, BK = 32, EPC = 8;
+    constexpr int NB = 4, WCOLS = 64;            // per wave: 8 x 4 blocks of 16 x 16 (128 pixels x 64 channels)
+    constexpr int ROWB = BK * 2;                 // 64-B LDS rows
+    constexpr int STAGE = (BM + BN) * ROWB;      // 24 KiB
+    constexpr int NSLOT = 3;
+    constexpr int EROW = WCOLS * 2 + 16;         // epilogue staging row (144 B)
+    constexpr int EPI = 4 * 128 * EROW;          // 72 KiB = the ring
+    constexpr int RING = NSLOT * STAGE;
+    constexpr int SMEM = (RING > EPI ? RING : EPI) + 2 * BN * 2 * 4;    // + the BN partial sums [2][BN][2]
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    int bid;
+    {
+        const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = blockIdx.x & 7;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+    }
+    // the first round's second workgroup per CU starts about half a tile late (host-sized, p.duo_delay x 8K cycles)
+    if ((int)blockIdx.x >= p.duo_ncu && (int)blockIdx.x < 2 * p.duo_ncu) {
+        for (int i = 0; i < p.duo_delay; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+    int phase = 0;
+#pragma unroll
+    for (int i = 1; i < SCD_MAX_PHASES; ++i)
+        if (i < p.nphase && bid >= p.tile_start[i]) phase = i;
+    const scd_gemm_phase& ph = p.ph[phase];
+    const int local = bid - p.tile_start[phase];
+    const int mt = local / p.ntn;
+    const int nt = local - mt * p.ntn;
+    const int QQ = ph.Qh * ph.Qw;
+    const int M = p.N * QQ;
+
+    // DMA: lane -> row lr = lane / 4 of a 16-row piece, LDS slot lane & 3, source chunk (lane & 3) ^ F[lane / 16]
+    const int lr = lane >> 2;
+    const int cch = (lane & 3) ^ duo_swz(lr);
+    // A rows 64 * wave + 16 i + lr (i < 4): byte offset at tap (0, 0) of channel 0 + in-image tap mask
+    int a_base[4];
+    unsigned a_mask[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = mt * BM + 64 * wave + 16 * i + lr;
+        const bool ok = m < M;
+        const int mm = ok ? m : 0;
+        const int n = mm / QQ;
+        const int rem = mm - n * QQ;
+        const int qh = rem / ph.Qw;
+        const int qw = rem - qh * ph.Qw;
+        const int ih0 = p.is * qh, iw0 = p.is * qw;
+        a_base[i] = ((n * p.Hi + ih0) * p.Wi + iw0) * p.Ci * 2 + cch * 16;
+        unsigned msk = 0;
+        for (int t = 0; t < ph.ntaps; ++t) {
+            const int ih = ih0 + ph.dh[t], iw = iw0 + ph.dw[t];
+            if (ok && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) msk |= 1u << t;
+        }
+        a_mask[i] = msk;
+    }
+    // B rows 32 * wave + 16 j + lr (j < 2)
+    int b_base[2];
+    bool b_ok[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int nn = nt * BN + 32 * wave + 16 * j + lr;
+        b_ok[j] = nn < p.Co;
+        b_base[j] = (b_ok[j] ? nn : 0) * p.wrow * 2 + cch * 16;
+    }
+    const int KT = ph.ntaps * (p.Ci / 64) * 2;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.wbytes, 0x00020000);
+
+    struct StageArgs { int live, tap, adelta, bdelta; };
+    auto stage_args = [&](int kt_req) {
+        StageArgs a;
+        a.live = kt_req < KT;
+        const int kt = min(kt_req, KT - 1);
+        const int h = kt & 1, k2 = kt >> 1;
+        const int chunk = k2 / ph.ntaps, tap = k2 - chunk * ph.ntaps;   // 64-channel chunk outer, tap, half inner
+        a.tap = tap;
+        a.adelta = ((ph.dh[tap] * p.Wi + ph.dw[tap]) * p.Ci + chunk * 64 + h * 32) * 2;
+        a.bdelta = (ph.wt[tap] * p.Ci + chunk * 64 + h * 32) * 2;
+        return a;
+    };
+    // the 6 DMA instructions of one K-step (always 6: the vmcnt counts are static)
+    auto issue = [&](const StageArgs& g, char* buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool ok = g.live && ((a_mask[i] >> g.tap) & 1u);
+            dma16(xrs, buf + (64 * wave + 16 * i) * ROWB, sel_off(ok, a_base[i] + g.adelta));
+        }
+        char* Bs = buf + BM * ROWB;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            dma16(wrs, Bs + (32 * wave + 16 * j) * ROWB, sel_off(g.live && b_ok[j], b_base[j] + g.bdelta));
+    };
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int fo = (lg ^ duo_swz(l16)) << 4;     // this lane's chunk lg in any 16-row block
+    f32x4 acc[8][NB];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    SCD_STAMP_BEGIN();
+    // fragments of stage k are read in iteration k and used by the MFMAs of iteration k + 1 (two register sets, X / Y):
+    // the reads' latency hides behind the previous stage's MFMAs, and the next stage's DMA issues sit between them
+    h16x8 bx[NB], ax[8], by[NB], ay[8];
+    auto read_frags = [&](const char* As, h16x8 (&bf)[NB], h16x8 (&af)[8]) {
+        const char* Bs = As + BM * ROWB;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) bf[b] = *(const h16x8*)(Bs + (64 * wn + 16 * b + l16) * ROWB + fo);
+#pragma unroll
+        for (int a = 0; a < 8; ++a) af[a] = *(const h16x8*)(As + (128 * wm + 16 * a + l16) * ROWB + fo);
+    };
+    auto mfmas = [&](const h16x8 (&bf)[NB], const h16x8 (&af)[8]) {
+        if constexpr (DUO_PRIO && !DUO_ILV) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+                acc[a][b] = mfma_16x16x32_h16(bf[b], af[a], acc[a][b]);
+        if constexpr (DUO_PRIO && !DUO_ILV) __builtin_amdgcn_s_setprio(0);
+    };
+    // one K-step k >= 1: stage k landed everywhere (this wave: vmcnt(6) leaves stage k + 1's 6 in flight; its reads
+    // of stage k - 1 drained: lgkmcnt(0), long done by now) -> barrier -> stage k + 2 into stage k - 1's slot ->
+    // read stage k into (bn, an) -> MFMAs of stage k - 1 from (bo, ao)
+    auto step = [&](int kt, int& cur, h16x8 (&bn)[NB], h16x8 (&an)[8], const h16x8 (&bo)[NB],
+                    const h16x8 (&ao)[8]) {
+        const StageArgs g = stage_args(kt + 2);
+        asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const int nxs = cur == 0 ? 2 : cur - 1;
+        if constexpr (!DUO_ILV) {
+            issue(g, smem + nxs * STAGE);
+            read_frags(smem + cur * STAGE, bn, an);
+            mfmas(bo, ao);
+        } else {
+            // written in the interleaved order (the LDS-DMA builtin is a scheduling boundary, so the source order is
+            // the issue order): per group one DMA issue, two fragment reads, four MFMAs of the previous stage
+            if constexpr (DUO_PRIO) __builtin_amdgcn_s_setprio(1);
+            char* nb = smem + nxs * STAGE;
+            const char* As = smem + cur * STAGE;
+            const char* Bs = As + BM * ROWB;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (q < 4) {
+                    const bool ok = g.live && ((a_mask[q] >> g.tap) & 1u);
+                    dma16(xrs, nb + (64 * wave + 16 * q) * ROWB, sel_off(ok, a_base[q] + g.adelta));
+                } else if (q < 6) {
+                    const int j = q - 4;
+                    dma16(wrs, nb + BM * ROWB + (32 * wave + 16 * j) * ROWB,
+                          sel_off(g.live && b_ok[j], b_base[j] + g.bdelta));
+                }
+                if (q < 2) {
+                    bn[2 * q] = *(const h16x8*)(Bs + (64 * wn + 16 * (2 * q) + l16) * ROWB + fo);
+                    bn[2 * q + 1] = *(const h16x8*)(Bs + (64 * wn + 16 * (2 * q + 1) + l16) * ROWB + fo);
+                } else if (q < 6) {
+                    const int a0 = 2 * (q - 2);
+                    an[a0] = *(const h16x8*)(As + (128 * wm + 16 * a0 + l16) * ROWB + fo);
+                    an[a0 + 1] = *(const h16x8*)(As + (128 * wm + 16 * (a0 + 1) + l16) * ROWB + fo);
+                }
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    acc[q][b] = mfma_16x16x32_h16(bo[b], ao[q], acc[q][b]);
+            }
+            if constexpr (DUO_PRIO) __builtin_amdgcn_s_setprio(0);
+        }
+        cur = cur == 2 ? 0 : cur + 1;
+    };
+    issue(stage_args(0), smem);
+    issue(stage_args(1), smem + STAGE);
+    {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(stage_args(2), smem + 2 * STAGE);
+        read_frags(smem, by, ay);
+    }
+    int cur = 1;                                  // ring slot of stage kt
+    int kt = 1;
+    for (; kt + 1 < KT; kt += 2) {                // KT is even: pairs of steps 1..KT-2, then step KT-1
+        step(kt, cur, bx, ax, by, ay);
+        step(kt + 1, cur, by, ay, bx, ax);
+    }
+    step(kt, cur, bx, ax, by, ay);
+    mfmas(bx, ax);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    SCD_STAMP_END();
+
+    // ---- epilogue (the ping-pong kernel's, per wave 128 x 64): bias / relu, BN partial sums, the wave's tile staged in
+    // the ring, coalesced 16-B NHWC stores (+= when accumulating; the BN-backward sums from the stored gradient)
+    const int grp = wm, wc = wn;
+    char* ep = smem + wave * 128 * EROW;
+    float csum[NB][4], csq[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { csum[b][r] = 0.f; csq[b][r] = 0.f; }
+    constexpr int CPR = WCOLS * 2 / 16;                      // 8 chunks per staged row
+    struct PixPos { int n, qh, qw; };
+    auto pix_of = [&](int m) -> PixPos {
+        PixPos q;
+        q.n = m / QQ;
+        const int rem = m - q.n * QQ;
+        q.qh = rem / ph.Qw;
+        q.qw = rem - q.qh * ph.Qw;
+        return q;
+    };
+    auto pix_advance = [&](PixPos& q, int step) {
+        q.qw += step;
+        while (q.qw >= ph.Qw) {
+            q.qw -= ph.Qw;
+            if (++q.qh == ph.Qh) { q.qh = 0; ++q.n; }
+        }
+    };
+    auto out_off = [&](const PixPos& q, int col) -> long {
+        const int oh = p.os * q.qh + ph.rho_h, ow = p.os * q.qw + ph.rho_w;
+        if (p.shuf) {
+            const int c4 = p.Co >> 2, sp = col / c4;
+            return ((long)(q.n * 2 * p.Ho + 2 * oh + (sp >> 1)) * (2 * p.Wo) + 2 * ow + (sp & 1)) * c4 + (col - sp * c4);
+        }
+        return ((long)(q.n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
+    };
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
+        float bias[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+            const int m = mt * BM + 128 * grp + a * 16 + l16;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[a][b][r] + bias[r];
+                if (p.relu) v[r] = fmaxf(v[r], 0.f);
+            }
+            if (!p.bnbwd) {
+                const bool mok = m < M;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float t = mok ? v[r] : 0.f;
+                    csum[b][r] += t;
+                    csq[b][r] += t * t;
+                }
+            }
+            typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
+            bf16x4 o = {(h16)v[0], (h16)v[1], (h16)v[2], (h16)v[3]};
+            *(bf16x4*)(ep + (a * 16 + l16) * EROW + (b * 16 + lg * 4) * 2) = o;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the staged tile is wave-private
+    constexpr int RPI = 64 / CPR;                            // 8 rows per pass
+    constexpr int NIT = 128 / RPI;
+    const int rsub = lane / CPR, chx = lane - (lane / CPR) * CPR;
+    float bs8[EPC], bq8[EPC];
+    if (p.bnbwd) {
+        const int colb = nt * BN + wc * WCOLS + chx * EPC;
+        const bool cok = colb < p.Co;
+        const int cl = cok ? colb : 0;
+        float mu[EPC], is[EPC], sc[EPC], sh[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; e += 4) {
+            const float4 f0 = *(const float4*)(p.bn_mean + cl + e), f1 = *(const float4*)(p.bn_invstd + cl + e);
+            const float4 f2 = *(const float4*)(p.bn_rsc + cl + e), f3 = *(const float4*)(p.bn_rsh + cl + e);
+            mu[e] = f0.x; mu[e + 1] = f0.y; mu[e + 2] = f0.z; mu[e + 3] = f0.w;
+            is[e] = f1.x; is[e + 1] = f1.y; is[e + 2] = f1.z; is[e + 3] = f1.w;
+            sc[e] = f2.x; sc[e + 1] = f2.y; sc[e + 2] = f2.z; sc[e + 3] = f2.w;
+            sh[e] = f3.x; sh[e + 1] = f3.y; sh[e + 2] = f3.z; sh[e + 3] = f3.w;
+        }
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) { bs8[e] = 0.f; bq8[e] = 0.f; }
+        PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
+#pragma unroll 4
+        for (int it = 0; it < NIT; ++it) {
+            const int row = it * RPI + rsub;
+            const int m = mt * BM + 128 * grp + row;
+            const bool ok = cok && m < M;
+            const long off = ok ? out_off(pq, cl) : 0;
+            pix_advance(pq, RPI);
+            uint4 v = *(const uint4*)(ep + row * EROW + chx * 16);
+            T* dst = (T*)(p.y) + off;
+            if (p.accumulate) {
+                float a8[EPC], o8[EPC];
+                Vec16<T>::load(&v, a8);
+                Vec16<T>::load(dst, o8);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) a8[e] += o8[e];
+                Vec16<T>::store(&v, a8);
+            }
+            float d8[EPC], y8[EPC];
+            Vec16<T>::load(&v, d8);
+            Vec16<T>::load((const T*)p.bny + off, y8);
+            if (ok) {
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) {
+                    const float dz = y8[e] * sc[e] + sh[e] > 0.f ? d8[e] : 0.f;
+                    bs8[e] += dz;
+                    bq8[e] += dz * (y8[e] - mu[e]) * is[e];
+                }
+                *(uint4*)dst = v;
+            }
+        }
+    } else {
+        const int col = nt * BN + wc * WCOLS + chx * EPC;
+        PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
+#pragma unroll 4
+        for (int it = 0; it < NIT; ++it) {
+            const int row = it * RPI + rsub;
+            const int m = mt * BM + 128 * grp + row;
+            const bool ok = m < M && col < p.Co;
+            T* dst = (T*)(p.y) + (ok ? out_off(pq, col) : 0);
+            pix_advance(pq, RPI);
+            uint4 v = *(const uint4*)(ep + row * EROW + chx * 16);
+            if (p.accumulate) {
+                float a[EPC], o[EPC];
+                Vec16<T>::load(&v, a);
+                Vec16<T>::load(dst, o);
+#pragma unroll
+                for (int e = 0; e < EPC; ++e) a[e] += o[e];
+                Vec16<T>::store(&v, a);
+            }
+            if (ok) *(uint4*)dst = v;
+        }
+    }
+    if (p.stats) {
+        float* red = (float*)(smem + (RING > EPI ? RING : EPI));    // [2 groups][BN][2]
+        if (p.bnbwd) {
+            float* part = (float*)ep;                        // [64 lanes][2 * EPC]
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) { part[lane * 2 * EPC + e] = bs8[e]; part[lane * 2 * EPC + EPC + e] = bq8[e]; }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane < WCOLS) {
+                const int cx = lane / EPC, e = lane - (lane / EPC) * EPC;
+                float s = 0.f, q = 0.f;
+                for (int r = 0; r < RPI; ++r) {
+                    s += part[(r * CPR + cx) * 2 * EPC + e];
+                    q += part[(r * CPR + cx) * 2 * EPC + EPC + e];
+                }
+                red[(grp * BN + wc * WCOLS + lane) * 2 + 0] = s;
+                red[(grp * BN + wc * WCOLS + lane) * 2 + 1] = q;
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float s = row16_sum(csum[b][r]), q = row16_sum(csq[b][r]);
+                    if (l16 == 0) {
+                        const int c = wc * WCOLS + b * 16 + lg * 4 + r;
+                        red[(grp * BN + c) * 2 + 0] = s;
+                        red[(grp * BN + c) * 2 + 1] = q;
+                    }
+                }
+        }
+        __syncthreads();
+        if (tid < BN) {
+            const int col = nt * BN + tid;
+            if (col < p.Co) {
+                const double s = (double)red[tid * 2] + (double)red[(BN + tid) * 2];
+                const double q = (double)red[tid * 2 + 1] + (double)red[(BN + tid) * 2 + 1];
+                const int rep = bid % SCD_STAT_REPLICAS;
+                atomic_add_f64(p.stats + ((long)rep * 2 + 0) * p.Co + col, s);
+                atomic_add_f64(p.stats + ((long)rep * 2 + 1) * p.Co + col, q);
+            }
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------
 // CenterNet head convolution (centerNetOffset.py:106-110) for the three 128-wide heads: ONE 192 x 384 tile
 // covers every hidden channel of 192 pixels, so the input (A) panel is read once (the 256 x 192 ping-pong
 // tiles above read it twice, through L2) and each head's 1x1 tail sees its whole hidden vector in the same
@@ -1561,7 +1966,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
 // stores of the hidden activation, then the 1x1 tails: one thread per (pixel, head) with the head
 // wave-uniform, so its 1x1 weights come through the scalar cache; outputs NCHW fp32.
 __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p) {
-    typedef __bf16 T;
+    typedef h16 T;
     constexpr int BM = 192, BN = 384, BK = 64, EPC = 8;
     constexpr int NA = 6, NB = 6;                     // 16-row / 16-column blocks per wave
     constexpr int STAGE = (BM + BN) * 128;
@@ -1665,23 +2070,23 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         for (int a = 0; a < NA; ++a)
     #pragma unroll
             for (int b = 0; b < NB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        bf16x8 bfr[NB][2], af[2][2];
+        h16x8 bfr[NB][2], af[2][2];
 
         auto read_b = [&](const char* buf) {
             const char* Bs = buf + BM * 128;
     #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 const char* row = Bs + (96 * wc + 16 * b + l16) * 128;
-                bfr[b][0] = *(const bf16x8*)(row + co0);
-                bfr[b][1] = *(const bf16x8*)(row + co1);
+                bfr[b][0] = *(const h16x8*)(row + co0);
+                bfr[b][1] = *(const h16x8*)(row + co1);
             }
         };
         auto read_a = [&](const char* buf, int q) {
     #pragma unroll
             for (int a = 0; a < 2; ++a) {
                 const char* row = buf + (96 * grp + 32 * q + 16 * a + l16) * 128;
-                af[a][0] = *(const bf16x8*)(row + co0);
-                af[a][1] = *(const bf16x8*)(row + co1);
+                af[a][0] = *(const h16x8*)(row + co0);
+                af[a][1] = *(const h16x8*)(row + co1);
             }
         };
         auto mfma_q = [&](int q) {
@@ -1694,7 +2099,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                 for (int a = 0; a < 2; ++a)
     #pragma unroll
                     for (int b = 0; b < NB; ++b)
-                        acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b][s], af[a][s], acc[2 * q + a][b], 0, 0, 0);
+                        acc[2 * q + a][b] = mfma_16x16x32_h16(bfr[b][s], af[a][s], acc[2 * q + a][b]);
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
         };
@@ -1751,7 +2156,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         // ~2^-17), 12 MFMAs per 16-pixel block.  The four channel waves of a group meet in LDS (48 KiB of fp32
         // partials), then one pass adds them, the bias, and writes the NCHW fp32 outputs.
         {
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
             const int od0 = p.head_od[0], od1 = p.head_od[1], od2 = p.head_od[2];
             const int odsum = od0 + od1 + od2;
             const int o = l16;                                       // tail output row of this lane's W1 fragment
@@ -1787,8 +2192,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                     const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
     #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        whi[e][j] = (__bf16)w4[j];
-                        wlo[e][j] = (__bf16)(w4[j] - (float)whi[e][j]);
+                        whi[e][j] = (h16)w4[j];
+                        wlo[e][j] = (h16)(w4[j] - (float)whi[e][j]);
                     }
                 }
                 const int colst = 96 * wc + 16 * b + ((lg & 1) ? 16 + 4 * (lg - 1) : 4 * lg);
@@ -1798,7 +2203,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     #pragma unroll
                     for (int e = 0; e < 2; ++e)
     #pragma unroll
-                        for (int r = 0; r < 4; ++r) hv[e][r] = (__bf16)fmaxf(acc[a][b + e][r] + bias[e][r], 0.f);
+                        for (int r = 0; r < 4; ++r) hv[e][r] = (h16)fmaxf(acc[a][b + e][r] + bias[e][r], 0.f);
     #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         tl[a] = mfma_16x16x16(whi[e], hv[e], tl[a]);
@@ -2075,14 +2480,14 @@ __global__ __launch_bounds__(256, WGRAD_OCC) void conv_wgrad_kernel(WgradParams 
 #pragma unroll
             for (int s = 0; s < KP / 32; ++s) {
                 const int r0 = 32 * s + 8 * lg + q;
-                bf16x8 af[4], bfr[4];
+                h16x8 af[4], bfr[4];
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
                     const int cb = (wm * 64 + a * 16 + 4 * pp) * 2;
                     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + wswz(r0, cb, GROW)));
                     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Gs + wswz(r0 + 4, cb, GROW)));
                     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    af[a] = __builtin_bit_cast(bf16x8, v);
+                    af[a] = __builtin_bit_cast(h16x8, v);
                 }
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
@@ -2090,7 +2495,7 @@ __global__ __launch_bounds__(256, WGRAD_OCC) void conv_wgrad_kernel(WgradParams 
                     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + wswz(r0, cb, XROW)));
                     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Xs + wswz(r0 + 4, cb, XROW)));
                     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    bfr[b] = __builtin_bit_cast(bf16x8, v);
+                    bfr[b] = __builtin_bit_cast(h16x8, v);
                 }
                 if constexpr (SCD_ABLATE == 21) {
 #pragma unroll
@@ -2100,7 +2505,7 @@ __global__ __launch_bounds__(256, WGRAD_OCC) void conv_wgrad_kernel(WgradParams 
                 for (int a = 0; a < 4; ++a)
 #pragma unroll
                     for (int b = 0; b < 4; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+                        acc[a][b] = mfma_16x16x32_h16(af[a], bfr[b], acc[a][b]);
                 }
                 // FASTX frees the address registers the hoisted fragment reads of the next k-step would take:
                 // keep one k-step of fragments live at a time (256-VGPR budget at two workgroups per CU)
@@ -2282,14 +2687,14 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo_addr);
         s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)hi_addr);
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        return __builtin_bit_cast(bf16x8, v);
+        return __builtin_bit_cast(h16x8, v);
     };
     f32x4 acc[2 * NQ][4];
 #pragma unroll
     for (int a = 0; a < 2 * NQ; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 xf[4][2], gfx[2][2], gfy[2][2];
+    h16x8 xf[4][2], gfx[2][2], gfy[2][2];
     auto read_x = [&](const char* stg) {
         const char* X = stg + GBYTES;
 #pragma unroll
@@ -2304,7 +2709,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
             }
         }
     };
-    auto read_g = [&](const char* stg, int q, bf16x8 (&gf)[2][2]) {
+    auto read_g = [&](const char* stg, int q, h16x8 (&gf)[2][2]) {
         const char* G = stg + (grp * NQ + q) * QIMG;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -2316,7 +2721,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
             }
         }
     };
-    auto mfma_q = [&](int q, const bf16x8 (&gf)[2][2]) {
+    auto mfma_q = [&](int q, const h16x8 (&gf)[2][2]) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
@@ -2326,7 +2731,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
-                    acc[2 * q + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[b][s], gf[a][s], acc[2 * q + a][b], 0, 0, 0);
+                    acc[2 * q + a][b] = mfma_16x16x32_h16(xf[b][s], gf[a][s], acc[2 * q + a][b]);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -2377,7 +2782,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
             const int k1 = pix0 + (t + NBUF - 1) * KP;      // >= pix1 near the end: the DMAs read nothing
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                bf16x8 (&gf)[2][2] = (q & 1) ? gfy : gfx;
+                h16x8 (&gf)[2][2] = (q & 1) ? gfy : gfx;
                 if (q == 0) read_x(cur);
                 read_g(cur, q, gf);
                 if constexpr (NQ == 2) {
@@ -2540,7 +2945,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
         s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo_addr);
         s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)hi_addr);
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        return __builtin_bit_cast(bf16x8, v);
+        return __builtin_bit_cast(h16x8, v);
     };
     // per-lane byte offsets: halo (tap column dw, lo/hi rows) and output gradient (block a; hi = lo + 4 rows)
     int xo[3][2], go[4];
@@ -2556,7 +2961,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[a][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    bf16x8 gf[4], xf[9];
+    h16x8 gf[4], xf[9];
     auto reads = [&](const char* cur, int s2) {
 #pragma unroll
         for (int a = 0; a < 4; ++a) gf[a] = trf(cur + go[a] + 4096 * s2, cur + go[a] + 4096 * s2 + 512);
@@ -2574,7 +2979,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_l1_kernel(WgradParams p) {
                 if constexpr (SCD_ABLATE == 42) {          // ablation: fragment reads kept, no MFMA
                     asm volatile("" ::"v"(xf[t]), "v"(gf[a]));
                 } else {
-                    acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[t], gf[a], acc[a][t], 0, 0, 0);
+                    acc[a][t] = mfma_16x16x32_h16(xf[t], gf[a], acc[a][t]);
                 }
             }
     };
@@ -2820,8 +3225,8 @@ struct S1x1Plan {
 template <int K, int N, int MODE, int SPL, int UA, int WV>
 __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmParams p, int cpw) {
     typedef S1x1Plan<K, N, MODE, SPL, UA, WV> Plan;
-    typedef __bf16 T;
-    typedef __attribute__((ext_vector_type(4))) __bf16 hv4;
+    typedef h16 T;
+    typedef __attribute__((ext_vector_type(4))) h16 hv4;
     typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
     constexpr int KS = K / 32;                              // MFMA k-steps
     constexpr int NH = N / SPL;                             // channels per wave
@@ -2891,12 +3296,12 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
     };
 
     auto pix0 = [&](int u) -> long { return chunk0 * 128 + (u * PXW + pw) * UP; };
-    auto load_unit = [&](int u, bf16x8 (&xf)[UA][KS]) {
+    auto load_unit = [&](int u, h16x8 (&xf)[UA][KS]) {
 #pragma unroll
         for (int a = 0; a < UA; ++a) {
             const char* row = p.x + ((pix0(u) + 16 * a + l16) * K + 8 * lg) * 2;
 #pragma unroll
-            for (int s = 0; s < KS; ++s) xf[a][s] = *(const bf16x8*)(row + s * 64);
+            for (int s = 0; s < KS; ++s) xf[a][s] = *(const h16x8*)(row + s * 64);
         }
     };
     auto load_epi = [&](int u, uint4 (&ev)[UA][NB / 2]) {
@@ -2920,7 +3325,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
             }
         }
     };
-    auto unit = [&](int u, const bf16x8 (&xf)[UA][KS], const uint4 (&ev)[UA][NB / 2]) {
+    auto unit = [&](int u, const h16x8 (&xf)[UA][KS], const uint4 (&ev)[UA][NB / 2]) {
         f32x4 acc[UA][NB];
 #pragma unroll
         for (int a = 0; a < UA; ++a)
@@ -2935,10 +3340,10 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 const int r = c0w + 16 * b + l16;
-                const bf16x8 wf = *(const bf16x8*)(smem + wo + 16 * b * K * 2 + (((4 * s + lg) ^ (r & XM)) << 4));
+                const h16x8 wf = *(const h16x8*)(smem + wo + 16 * b * K * 2 + (((4 * s + lg) ^ (r & XM)) << 4));
 #pragma unroll
                 for (int a = 0; a < UA; ++a)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[a][s], acc[a][b], 0, 0, 0);
+                    acc[a][b] = mfma_16x16x32_h16(wf, xf[a][s], acc[a][b]);
             }
         if constexpr (MODE == 0 && SUMS) {
             if (stats_on) {
@@ -3023,7 +3428,7 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
         }
     };
 
-    bf16x8 xa[UA][KS], xb[UA][KS];
+    h16x8 xa[UA][KS], xb[UA][KS];
     uint4 ea[UA][NB / 2], eb[UA][NB / 2];
     // an even number of units per wave; the prefetch past the run re-reads its last unit (clamped: every load from a
     // valid address)
@@ -3045,13 +3450,13 @@ __global__ __launch_bounds__(64 * WV, 8 / WV) void conv1x1_stream_kernel(GemmPar
                 dma16(xrs, dst + q0 * 16, ((px + r) * K + c * 8) * 2);
             }
         };
-        auto read_unit = [&](int b, bf16x8 (&xf)[UA][KS]) {
+        auto read_unit = [&](int b, h16x8 (&xf)[UA][KS]) {
             const char* src = xs + (b * PXW + pw) * XU;
 #pragma unroll
             for (int a = 0; a < UA; ++a) {
                 const int r = 16 * a + l16;
 #pragma unroll
-                for (int s = 0; s < KS; ++s) xf[a][s] = *(const bf16x8*)(src + r * K * 2 + (((4 * s + lg) ^ (r & XM)) << 4));
+                for (int s = 0; s < KS; ++s) xf[a][s] = *(const h16x8*)(src + r * K * 2 + (((4 * s + lg) ^ (r & XM)) << 4));
             }
         };
         // unit u sits in buffer u & 1; before a wave reads it, every wave's DMAs of it have landed (counted vmcnt: the
@@ -3257,6 +3662,20 @@ static int pp_mode() {
     return mode;
 }
 
+static int duo_mode() {
+    // SCD_GEMM_DUO (read per call: tests compare the kernels): 0 = off, 1 = the ping-pong shapes (Co % 256 / 192 == 0)
+    // on the two-workgroups-per-CU kernel, 2 = also the 256 x 128 ring shapes (Co % 128 == 0), 3 = only the ping-pong
+    // shapes with the BN-backward-sum epilogue and >= 8 rounds of duo tiles (where the epilogue is what the two
+    // workgroups per CU overlap: the heatmap-head input gradient; tools/duo_probe.py)
+    const char* e = getenv("SCD_GEMM_DUO");
+    return e ? atoi(e) : 0;
+}
+
+static int duo_delay_pct() {
+    const char* e = getenv("SCD_DUO_DELAY");
+    return e ? atoi(e) : 100;
+}
+
 static int heads384_mode() {
     static int mode = -2;
     if (mode == -2) {
@@ -3347,6 +3766,38 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         const int tiles = cdiv(Mtot, 192);
         hipLaunchKernelGGL(conv_gemm_heads384_kernel, dim3(tiles), dim3(512), 0, (hipStream_t)stream, p);
         SCD_RETURN_LAUNCH();
+    }
+    {
+        // two 256 x 128 workgroups per CU (conv_gemm_duo_kernel) where the grid gives each CU >= 2 tiles
+        const int dm = duo_mode();
+        const bool shape = dtype == SCD_DT_BF16 && !p.head_on && p.Co % 128 == 0 &&
+                           (pp_bn(dtype, p.Co) || dm >= 2);
+        const long dtiles = (long)cdiv(Mtot, 256) * (p.Co / 128);
+        const bool take = dm == 3 ? (p.bnbwd && dtiles >= 16L * num_cus()) : dtiles >= 2L * num_cus();
+        if (dm && shape && take) {
+            p.ntn = p.Co / 128;
+            int tiles = 0;
+            int ktmax = 0;
+            for (int i = 0; i < SCD_MAX_PHASES; ++i) {
+                p.tile_start[i] = tiles;
+                if (i < nphase) {
+                    p.ph[i] = phases[i];
+                    tiles += cdiv((long)p.N * phases[i].Qh * phases[i].Qw, 256) * p.ntn;
+                    ktmax = std::max(ktmax, phases[i].ntaps * (p.Ci / 64) * 2);
+                }
+            }
+            p.tile_start[SCD_MAX_PHASES] = tiles;
+            const long wb = (long)p.Co * p.wrow * esz;
+            if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
+            p.xbytes = (int)xb;
+            p.wbytes = (int)wb;
+            // half a tile: ~KT x 32 MFMAs x 16 cycles x 2 workgroups sharing the matrix pipe / 2, at ~75 % of it, in
+            // s_sleep(127) quanta of 8,128 cycles
+            p.duo_ncu = num_cus();
+            p.duo_delay = (int)((long)ktmax * 680 * duo_delay_pct() / 100 / 8128);
+            hipLaunchKernelGGL(conv_gemm_duo_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, p);
+            SCD_RETURN_LAUNCH();
+        }
     }
     {
         // ping-pong 256 x BN kernel when the grid fills the chip (fused head tails are run as a separate pass)
@@ -3455,7 +3906,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         SCD_RETURN_LAUNCH();
     }
     if (dtype == SCD_DT_BF16) {
-        if (narrow) return launch_gemm<__bf16, 256, 64>(p, tiles, st);
+        if (narrow) return launch_gemm<h16, 256, 64>(p, tiles, st);
         int ks = 1;
         const int km = ksplit_mode();
         if (km && !p.head_on) {
@@ -3463,7 +3914,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
             for (int i = 0; i < nphase; ++i) kt = std::max(kt, phases[i].ntaps * (p.Ci / 64));
             if (km == 2 || (kt >= 16 && 2 * (long)tiles <= 3L * num_cus())) ks = 2;
         }
-        return launch_gemm<__bf16, 128, 128>(p, tiles, st, ks);
+        return launch_gemm<h16, 128, 128>(p, tiles, st, ks);
     }
     if (dtype == SCD_DT_F32)
         return narrow ? launch_gemm<float, 256, 64>(p, tiles, st) : launch_gemm<float, 128, 128>(p, tiles, st);
@@ -3481,6 +3932,7 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.hid_keep = nullptr; p.hid_cols = 1 << 30;
     p.shuf = 0;
     p.stamps = scd_calib_stamp_buffer;
+    p.duo_ncu = 0; p.duo_delay = 0;
     {
         // read per call (tests switch them to compare the variants)
         const char* e = getenv("SCD_HEADS_SERP");
@@ -3765,12 +4217,12 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
         const int fx = !(wgrad_fastx() && ((long)Ho * Wo) % 64 == 0) ? 0 : (Wo % 64 == 0 ? 1 : 2);
         dim3 grid(p.ntm * p.ntn * n8);
         if (BM == 64) {
-            if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
-            else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), 0, st, p);
-            else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), 0, st, p);
+            if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<h16, 64, 256, 1>), grid, dim3(256), 0, st, p);
+            else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<h16, 64, 256, 2>), grid, dim3(256), 0, st, p);
+            else hipLaunchKernelGGL((conv_wgrad_kernel<h16, 64, 256, 0>), grid, dim3(256), 0, st, p);
         } else {
-            if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
-            else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), 0, st, p);
+            if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<h16, 128, 128, 1>), grid, dim3(256), 0, st, p);
+            else hipLaunchKernelGGL((conv_wgrad_kernel<h16, 128, 128, 0>), grid, dim3(256), 0, st, p);
         }
         SCD_RETURN_LAUNCH();
     }
@@ -3789,12 +4241,12 @@ extern "C" int scd_conv_wgrad(int dtype, const void* g, const void* x, float* ws
         // (the 128 x 128 tile has registers for FASTX 1 only)
         if (dtype == SCD_DT_BF16) {
             if (Cg <= 64) {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 1>), grid, dim3(256), 0, st, p);
-                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 2>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 64, 256, 0>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<h16, 64, 256, 1>), grid, dim3(256), 0, st, p);
+                else if (fx == 2) hipLaunchKernelGGL((conv_wgrad_kernel<h16, 64, 256, 2>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<h16, 64, 256, 0>), grid, dim3(256), 0, st, p);
             } else {
-                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 1>), grid, dim3(256), 0, st, p);
-                else hipLaunchKernelGGL((conv_wgrad_kernel<__bf16, 128, 128, 0>), grid, dim3(256), 0, st, p);
+                if (fx == 1) hipLaunchKernelGGL((conv_wgrad_kernel<h16, 128, 128, 1>), grid, dim3(256), 0, st, p);
+                else hipLaunchKernelGGL((conv_wgrad_kernel<h16, 128, 128, 0>), grid, dim3(256), 0, st, p);
             }
         } else {
             if (Cg <= 64) {

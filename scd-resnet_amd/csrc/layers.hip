@@ -88,12 +88,12 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
             for (int i = threadIdx.x; i < na8 * rowl; i += 256) {
                 const int bt = i / na8, a = (i - bt * na8) * 8;
                 const int b = bt / T, t = bt - b * T;
-                typedef __attribute__((ext_vector_type(8))) __bf16 bf8;
+                typedef __attribute__((ext_vector_type(8))) h16 bf8;
                 bf8 v;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = (__bf16)tile[(a + e) * pitch + b * T + t];
+                for (int e = 0; e < 8; ++e) v[e] = (h16)tile[(a + e) * pitch + b * T + t];
                 const unsigned o = (unsigned)(b0 + b) * q.ldp + t * q.a_tot + q.a_off + a0 + a;
-                *(bf8*)((__bf16*)q.out + o) = v;
+                *(bf8*)((h16*)q.out + o) = v;
             }
             return;
         }
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
             const int b = bt / T, t = bt - b * T;
             const float v = tile[a * pitch + b * T + t];
             const unsigned o = (unsigned)(b0 + b) * q.ldp + t * q.a_tot + q.a_off + a0 + a;
-            if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
+            if (bf16) ((h16*)q.out)[o] = (h16)v;
             else ((float*)q.out)[o] = v;
         }
         return;
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
             const unsigned r = i / (unsigned)q.ldp, k = i - r * (unsigned)q.ldp;
             const float v = s2_phase_weight(q.w, q.A, q.B, r, k);
             const unsigned o = (q.row_off + r) * (unsigned)q.ldp + k;
-            if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
+            if (bf16) ((h16*)q.out)[o] = (h16)v;
             else ((float*)q.out)[o] = v;
         }
         return;
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
     if (q.mode == 0 && bf16 && ldp % 8 == 0 && B % 8 == 0 && q.row_off >= 0) {
         // 8 consecutive k of one row share their tap (B % 8 == 0): one 16-B store per thread and chunk (staging the
         // source rows through LDS for coalesced reads measured slower: 62 vs 48 us per step)
-        typedef __attribute__((ext_vector_type(8))) __bf16 bf8;
+        typedef __attribute__((ext_vector_type(8))) h16 bf8;
 #pragma unroll
         for (int j = 0; j < PACK_UNIT / 256 / 8; ++j) {
             const unsigned i = base + 8 * (threadIdx.x + 256 * j);
@@ -142,9 +142,9 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const float x = src[e * Tt];
-                v[e] = (__bf16)(t < Tt ? x : 0.f);
+                v[e] = (h16)(t < Tt ? x : 0.f);
             }
-            *(bf8*)((__bf16*)q.out + (q.row_off + r) * ldp + k) = v;
+            *(bf8*)((h16*)q.out + (q.row_off + r) * ldp + k) = v;
         }
         return;
     }
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void pack_weights_batched_kernel(const scd_pac
             v = q.w[(a * B + b) * Tt + t];
             o = (t * B + b) * ldp + q.a_off + a;
         }
-        if (bf16) ((__bf16*)q.out)[o] = (__bf16)v;
+        if (bf16) ((h16*)q.out)[o] = (h16)v;
         else ((float*)q.out)[o] = v;
     }
 }
@@ -831,7 +831,7 @@ extern "C" int scd_pack_weight(int dtype, const float* w, void* out, int A, int 
     const long total = (long)(mode == 0 ? A : mode == 3 ? 4 * B : B) * ldp;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((pack_weight_kernel<__bf16>), dim3(ew_blocks(total)), dim3(256), 0, st, w, (__bf16*)out, A, B,
+        hipLaunchKernelGGL((pack_weight_kernel<h16>), dim3(ew_blocks(total)), dim3(256), 0, st, w, (h16*)out, A, B,
                            T, mode, ldp, row_off);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((pack_weight_kernel<float>), dim3(ew_blocks(total)), dim3(256), 0, st, w, (float*)out, A, B, T,
@@ -848,7 +848,7 @@ extern "C" int scd_im2col_stem(int dtype, const float* x, void* cols, int N, int
     if (Kpad % 8 || Kpad < kh * kw) return SCD_ERR_ARG;
     const long total = (long)N * Ho * Wo * (Kpad / (dtype == SCD_DT_BF16 ? 8 : 4));
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((im2col_stem_kernel<__bf16>), dim3(ew_blocks(total)), dim3(256), 0, st, x, (__bf16*)cols, N, H,
+        hipLaunchKernelGGL((im2col_stem_kernel<h16>), dim3(ew_blocks(total)), dim3(256), 0, st, x, (h16*)cols, N, H,
                            W, Ho, Wo, kh, kw, stride, pad, Kpad);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((im2col_stem_kernel<float>), dim3(ew_blocks(total)), dim3(256), 0, st, x, (float*)cols, N, H,
@@ -867,8 +867,8 @@ extern "C" int scd_stem_pool_fwd(int dtype, const void* y, const float* scale, c
     const long total = (long)N * ((Ho + SPR - 1) / SPR) * Wo * (C / E);
     if (total >= (1L << 32)) return SCD_ERR_ARG;
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((stem_pool_fwd_kernel<__bf16>), dim3(ew_blocks(total)), dim3(256), 0, st, (const __bf16*)y,
-                           scale, shift, (__bf16*)out, argmax, N, H, W, C, Ho, Wo);
+        hipLaunchKernelGGL((stem_pool_fwd_kernel<h16>), dim3(ew_blocks(total)), dim3(256), 0, st, (const h16*)y,
+                           scale, shift, (h16*)out, argmax, N, H, W, C, Ho, Wo);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((stem_pool_fwd_kernel<float>), dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)y,
                            scale, shift, (float*)out, argmax, N, H, W, C, Ho, Wo);
@@ -885,8 +885,8 @@ extern "C" int scd_stem_pool_bwd(int dtype, const void* dout, const uint8_t* arg
     if (C % E) return SCD_ERR_ARG;
     const long total = (long)N * H * W * (C / E);
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((stem_pool_bwd_kernel<__bf16>), dim3(ew_blocks(total)), dim3(256), 0, st,
-                           (const __bf16*)dout, argmax, (const __bf16*)y, scale, shift, (__bf16*)dz, N, H, W, C, Ho, Wo);
+        hipLaunchKernelGGL((stem_pool_bwd_kernel<h16>), dim3(ew_blocks(total)), dim3(256), 0, st,
+                           (const h16*)dout, argmax, (const h16*)y, scale, shift, (h16*)dz, N, H, W, C, Ho, Wo);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((stem_pool_bwd_kernel<float>), dim3(ew_blocks(total)), dim3(256), 0, st, (const float*)dout,
                            argmax, (const float*)y, scale, shift, (float*)dz, N, H, W, C, Ho, Wo);
@@ -906,13 +906,13 @@ extern "C" int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* 
     static int mode = -1;
     if (mode < 0) { const char* e = getenv("SCD_POOL_2X2"); mode = e ? atoi(e) : 1; }
     if (mode && H == 2 * Ho && W == 2 * Wo && (long)N * H * W * C < (1L << 31)) {
-        static const int g2b = resident_grid((const void*)stem_pool_bwd_bn_2x2_kernel<__bf16>, 256);
+        static const int g2b = resident_grid((const void*)stem_pool_bwd_bn_2x2_kernel<h16>, 256);
         static const int g2f = resident_grid((const void*)stem_pool_bwd_bn_2x2_kernel<float>, 256);
         const long blocks2 = (long)N * Ho * Wo * (C / E);
         const int grid = (int)std::min<long>(dtype == SCD_DT_BF16 ? g2b : g2f, (blocks2 + 255) / 256);
         if (dtype == SCD_DT_BF16)
-            hipLaunchKernelGGL((stem_pool_bwd_bn_2x2_kernel<__bf16>), dim3(grid), dim3(256), 0, st, (const __bf16*)dout,
-                               argmax, (const __bf16*)y, scale, shift, mean, invstd, (__bf16*)dz, stats, N, C, Ho, Wo);
+            hipLaunchKernelGGL((stem_pool_bwd_bn_2x2_kernel<h16>), dim3(grid), dim3(256), 0, st, (const h16*)dout,
+                               argmax, (const h16*)y, scale, shift, mean, invstd, (h16*)dz, stats, N, C, Ho, Wo);
         else if (dtype == SCD_DT_F32)
             hipLaunchKernelGGL((stem_pool_bwd_bn_2x2_kernel<float>), dim3(grid), dim3(256), 0, st, (const float*)dout,
                                argmax, (const float*)y, scale, shift, mean, invstd, (float*)dz, stats, N, C, Ho, Wo);
@@ -920,12 +920,12 @@ extern "C" int scd_stem_pool_bwd_bn(int dtype, const void* dout, const uint8_t* 
             return SCD_ERR_ARG;
         SCD_RETURN_LAUNCH();
     }
-    static const int gb = resident_grid((const void*)stem_pool_bwd_bn_kernel<__bf16>, 256);
+    static const int gb = resident_grid((const void*)stem_pool_bwd_bn_kernel<h16>, 256);
     static const int gf = resident_grid((const void*)stem_pool_bwd_bn_kernel<float>, 256);
     const int blocks = (int)std::min<long>(dtype == SCD_DT_BF16 ? gb : gf, (total + 255) / 256);
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((stem_pool_bwd_bn_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)dout, argmax,
-                           (const __bf16*)y, scale, shift, mean, invstd, (__bf16*)dz, stats, N, H, W, C, Ho, Wo);
+        hipLaunchKernelGGL((stem_pool_bwd_bn_kernel<h16>), dim3(blocks), dim3(256), 0, st, (const h16*)dout, argmax,
+                           (const h16*)y, scale, shift, mean, invstd, (h16*)dz, stats, N, H, W, C, Ho, Wo);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((stem_pool_bwd_bn_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)dout, argmax,
                            (const float*)y, scale, shift, mean, invstd, (float*)dz, stats, N, H, W, C, Ho, Wo);
@@ -947,7 +947,7 @@ extern "C" int scd_heads_fwd(int dtype, const void* hid, int N, int HW, int nh, 
     const long total = (long)N * HW * nh * cph;
     const int blocks = (int)std::min<long>(16384, (total + 255) / 256);
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((heads_fwd_kernel<__bf16>), dim3(blocks), dim3(256), 0, st, (const __bf16*)hid, N, HW, d);
+        hipLaunchKernelGGL((heads_fwd_kernel<h16>), dim3(blocks), dim3(256), 0, st, (const h16*)hid, N, HW, d);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((heads_fwd_kernel<float>), dim3(blocks), dim3(256), 0, st, (const float*)hid, N, HW, d);
     else
@@ -984,11 +984,11 @@ extern "C" int scd_heads_bwd(int dtype, const void* hid, int N, int HW, int nh, 
     static int u_env = -1;
     if (u_env < 0) { const char* e = getenv("SCD_HEADS_U"); u_env = e ? atoi(e) : 8; }
     if (dtype == SCD_DT_BF16 && u_env == 8)
-        hipLaunchKernelGGL((heads_bwd_kernel<__bf16, 8>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid, N,
-                           HW, d, (__bf16*)dhid, acc, accsz, PXB);
+        hipLaunchKernelGGL((heads_bwd_kernel<h16, 8>), dim3(blocks), dim3(threads), 0, st, (const h16*)hid, N,
+                           HW, d, (h16*)dhid, acc, accsz, PXB);
     else if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((heads_bwd_kernel<__bf16, 4>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid, N,
-                           HW, d, (__bf16*)dhid, acc, accsz, PXB);
+        hipLaunchKernelGGL((heads_bwd_kernel<h16, 4>), dim3(blocks), dim3(threads), 0, st, (const h16*)hid, N,
+                           HW, d, (h16*)dhid, acc, accsz, PXB);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((heads_bwd_kernel<float, 4>), dim3(blocks), dim3(threads), 0, st, (const float*)hid, N, HW,
                            d, (float*)dhid, acc, accsz, PXB);
@@ -1072,8 +1072,8 @@ extern "C" int scd_heads_bwd_packed_split(int dtype, const void* hid, int N, int
     const int PXB = pxb_env > 0 ? pxb_env : 2048;
     const int blocks = cdiv(P, PXB);
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL((heads_bwd_kernel<__bf16, 8, true>), dim3(blocks), dim3(threads), 0, st, (const __bf16*)hid,
-                           N, HW, d, (__bf16*)dhid, acc, accsz, PXB);
+        hipLaunchKernelGGL((heads_bwd_kernel<h16, 8, true>), dim3(blocks), dim3(threads), 0, st, (const h16*)hid,
+                           N, HW, d, (h16*)dhid, acc, accsz, PXB);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL((heads_bwd_kernel<float, 4, true>), dim3(blocks), dim3(threads), 0, st, (const float*)hid,
                            N, HW, d, (float*)dhid, acc, accsz, PXB);
@@ -1275,8 +1275,8 @@ extern "C" int scd_heads_sparse_bwd(int dtype, const void* hid, const void* feat
     const int blocks = cdiv((long)N * K, SP_SPB);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL(heads_sparse_bwd_kernel<__bf16>, dim3(blocks), dim3(256), 0, st, (const __bf16*)hid,
-                           (const __bf16*)feat, N, H, W, Cin, d, dscale, inds, K, (__bf16*)dhid_s, (__bf16*)xcol, acc,
+        hipLaunchKernelGGL(heads_sparse_bwd_kernel<h16>, dim3(blocks), dim3(256), 0, st, (const h16*)hid,
+                           (const h16*)feat, N, H, W, Cin, d, dscale, inds, K, (h16*)dhid_s, (h16*)xcol, acc,
                            accsz, slotmap, ownermap);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL(heads_sparse_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)hid,
@@ -1298,8 +1298,8 @@ extern "C" int scd_heads_sparse_fixup(int dtype, void* dx, const void* cols, int
     const int S = N * K;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == SCD_DT_BF16)
-        hipLaunchKernelGGL(heads_sparse_fixup_kernel<__bf16>, dim3(S), dim3(256), 0, st, (__bf16*)dx,
-                           (const __bf16*)cols, N, H, W, Cin, inds, K, slotmap, ownermap, (const __bf16*)bn_y, mean,
+        hipLaunchKernelGGL(heads_sparse_fixup_kernel<h16>, dim3(S), dim3(256), 0, st, (h16*)dx,
+                           (const h16*)cols, N, H, W, Cin, inds, K, slotmap, ownermap, (const h16*)bn_y, mean,
                            invstd, relu_scale, relu_shift, bn_stats);
     else if (dtype == SCD_DT_F32)
         hipLaunchKernelGGL(heads_sparse_fixup_kernel<float>, dim3(S), dim3(256), 0, st, (float*)dx, (const float*)cols,

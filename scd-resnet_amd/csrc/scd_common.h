@@ -5,8 +5,10 @@
 #include <string.h>
 
 // fp16 compute mode (SCD_DT_F16).  The type-generic sources (conv_gemm, bn, layers, stem, pad) are compiled twice:
-// once as written (16-bit type __bf16, v_mfma_f32_16x16x32_bf16) and once with SCD_F16_BUILD, where the 16-bit type
-// is _Float16, the MFMA is v_mfma_f32_16x16x32_f16 and every entry point gets the suffix __f16.  A call with
+// once as written (16-bit storage type h16 = __bf16, v_mfma_f32_16x16x32_bf16) and once with SCD_F16_BUILD, where h16
+// is _Float16, the MFMA is v_mfma_f32_16x16x32_f16 and every entry point gets the suffix __f16.  Those sources name
+// the 16-bit type h16 (and h16x8 / mfma_16x16x32_h16) wherever it is the build's type; __bf16 in them is always a real
+// bf16, whichever build.  A call with
 // dtype SCD_DT_F16 is forwarded by the first build to the second with dtype SCD_DT_BF16 ("the 16-bit type"), so
 // every kernel, tile shape and dispatch rule is shared and the C-ABI takes SCD_DT_F16 like any other dtype.
 #ifdef SCD_F16_BUILD
@@ -56,8 +58,6 @@
 #define scd_stem_bwd_fused scd_stem_bwd_fused__f16
 #define scd_stem_bwd_combine scd_stem_bwd_combine__f16
 #define scd_pad_channels scd_pad_channels__f16
-#define __bf16 _Float16
-#define __builtin_amdgcn_mfma_f32_16x16x32_bf16 __builtin_amdgcn_mfma_f32_16x16x32_f16
 #endif
 
 #include "../../include/scdhip.h"
@@ -121,7 +121,22 @@ __device__ __forceinline__ float h16_word_half(unsigned w, int hi) {
 }
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;     // a real bf16 vector in either build
+#ifdef SCD_F16_BUILD
+typedef _Float16 h16;                                           // the build's 16-bit compute type
+#else
+typedef __bf16 h16;
+#endif
+typedef __attribute__((ext_vector_type(8))) h16 h16x8;
+typedef __attribute__((ext_vector_type(4))) h16 h16x4;
+// v_mfma_f32_16x16x32_{bf16,f16} on the build's 16-bit type
+__device__ __forceinline__ f32x4 mfma_16x16x32_h16(h16x8 a, h16x8 b, f32x4 c) {
+#ifdef SCD_F16_BUILD
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -129,11 +144,11 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 template <typename T> __device__ __forceinline__ float to_f(T v);
 template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
-template <> __device__ __forceinline__ float to_f<__bf16>(__bf16 v) { return (float)v; }
+template <> __device__ __forceinline__ float to_f<h16>(h16 v) { return (float)v; }
 
 template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
-template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
+template <> __device__ __forceinline__ h16 from_f<h16>(float v) { return (h16)v; }
 
 // 16-byte vector of T <-> floats
 template <typename T> struct Vec16;
@@ -147,18 +162,18 @@ template <> struct Vec16<float> {
         *(float4*)p = make_float4(f[0], f[1], f[2], f[3]);
     }
 };
-template <> struct Vec16<__bf16> {
+template <> struct Vec16<h16> {
     static constexpr int N = 8;
     __device__ static void load(const void* p, float* f) {
-        bf16x8 v = *(const bf16x8*)p;
+        h16x8 v = *(const h16x8*)p;
 #pragma unroll
         for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
     }
     __device__ static void store(void* p, const float* f) {
-        bf16x8 v;
+        h16x8 v;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (__bf16)f[i];
-        *(bf16x8*)p = v;
+        for (int i = 0; i < 8; ++i) v[i] = (h16)f[i];
+        *(h16x8*)p = v;
     }
 };
 

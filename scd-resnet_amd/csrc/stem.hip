@@ -41,8 +41,8 @@ constexpr int PCOLS = SP * (FTW - 1) + KS + 1;      // 262 -> padded to an even 
 constexpr int FPAR = 132;                            // >= 131 columns per parity
 constexpr int FROW = 2 * FPAR;
 
-__global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const float* __restrict__ x, const __bf16* __restrict__ wpk,
-                                                            __bf16* __restrict__ y, double* __restrict__ stats,
+__global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const float* __restrict__ x, const h16* __restrict__ wpk,
+                                                            h16* __restrict__ y, double* __restrict__ stats,
                                                             int H, int W, int Ho, int Wo) {
     constexpr int AT = FTH * FTW * 128;             // A tile [256 px][64 taps] bf16, 128-B rows
     constexpr int BT = CO * 128;                    // B tile [64 co][64 taps]
@@ -94,13 +94,13 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
         const float* pp = patch + (SP * pr) * FROW + pc;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            bf16x8 v;
+            h16x8 v;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int k = c * 8 + e;
-                v[e] = (__bf16)(k < KK ? pp[(k / KS) * FROW + ((k % KS) & 1) * FPAR + ((k % KS) >> 1)] : 0.f);
+                v[e] = (h16)(k < KK ? pp[(k / KS) * FROW + ((k % KS) & 1) * FPAR + ((k % KS) >> 1)] : 0.f);
             }
-            *(bf16x8*)(As + swz128(tid, c)) = v;
+            *(h16x8*)(As + swz128(tid, c)) = v;
         }
     }
     __syncthreads();
@@ -116,16 +116,16 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const int co = ((s * 4 + lg) ^ l7) << 4;
-        bf16x8 af[4], bfr[4];
+        h16x8 af[4], bfr[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) af[a] = *(const bf16x8*)(As + (wave * 64 + a * 16 + l16) * 128 + co);
+        for (int a = 0; a < 4; ++a) af[a] = *(const h16x8*)(As + (wave * 64 + a * 16 + l16) * 128 + co);
 #pragma unroll
-        for (int b = 0; b < 4; ++b) bfr[b] = *(const bf16x8*)(Bs + (b * 16 + l16) * 128 + co);
+        for (int b = 0; b < 4; ++b) bfr[b] = *(const h16x8*)(Bs + (b * 16 + l16) * 128 + co);
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = 0; b < 4; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+                acc[a][b] = mfma_16x16x32_h16(bfr[b], af[a], acc[a][b]);
     }
     __syncthreads();          // A tile no longer read: reuse it for the output staging
 
@@ -140,12 +140,12 @@ __global__ __launch_bounds__(256, STEM_FWD_OCC) void stem_conv_fwd_kernel(const 
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+            typedef __attribute__((ext_vector_type(4))) h16 bf16x4;
             bf16x4 o;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float v = acc[a][b][r];
-                o[r] = (__bf16)v;
+                o[r] = (h16)v;
                 csum[b][r] += v;
                 csq[b][r] += v * v;
             }
@@ -196,7 +196,7 @@ constexpr int DROW = 288;                           // dy stage row stride (128 
 
 __device__ __forceinline__ int dswz(int row, int byte) { return row * DROW + (byte ^ (((row >> 3) & 1) << 7)); }
 
-__global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ ybn,
+__global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const h16* __restrict__ dy, const h16* __restrict__ ybn,
                                                               const float* __restrict__ coef, const float* __restrict__ x,
                                                               float* __restrict__ ws, int H, int W, int Ho, int Wo,
                                                               long M, int chunk) {
@@ -240,12 +240,12 @@ __global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __re
             uint4 v = *(const uint4*)(dy + (ps + r) * CO + c * 8);
             if (coef) {
                 const uint4 yv = *(const uint4*)(ybn + (ps + r) * CO + c * 8);
-                const bf16x8 d8 = __builtin_bit_cast(bf16x8, v), y8 = __builtin_bit_cast(bf16x8, yv);
-                bf16x8 o8;
+                const h16x8 d8 = __builtin_bit_cast(h16x8, v), y8 = __builtin_bit_cast(h16x8, yv);
+                h16x8 o8;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const int ch = c * 8 + e;
-                    o8[e] = (__bf16)(coef[ch] * (float)d8[e] + coef[CO + ch] * (float)y8[e] + coef[2 * CO + ch]);
+                    o8[e] = (h16)(coef[ch] * (float)d8[e] + coef[CO + ch] * (float)y8[e] + coef[2 * CO + ch]);
                 }
                 v = __builtin_bit_cast(uint4, o8);
             }
@@ -263,13 +263,13 @@ __global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __re
             const int kh = k / KS, kw = k - (k / KS) * KS;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                bf16x8 v;
+                h16x8 v;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const int px = pq * 16 + h * 8 + e;
-                    v[e] = (__bf16)(k < KK ? patch[kh * WPCOLS + SP * px + kw] : 0.f);
+                    v[e] = (h16)(k < KK ? patch[kh * WPCOLS + SP * px + kw] : 0.f);
                 }
-                *(bf16x8*)(Cs + swz128(k, pq * 2 + h)) = v;
+                *(h16x8*)(Cs + swz128(k, pq * 2 + h)) = v;
             }
         }
         __syncthreads();
@@ -277,23 +277,23 @@ __global__ __launch_bounds__(256) void stem_conv_wgrad_kernel(const __bf16* __re
         for (int s = 0; s < 2; ++s) {
             // A (taps, 8 consecutive pixels) from the [tap][px] tile; B (channels, 8 consecutive pixels) by tr reads
             const int r0 = 32 * s + 8 * lg + q4;
-            bf16x8 tf[2], df[2];
+            h16x8 tf[2], df[2];
 #pragma unroll
             for (int b = 0; b < 2; ++b)
-                tf[b] = *(const bf16x8*)(Cs + swz128(wn * 32 + b * 16 + l16, s * 4 + lg));
+                tf[b] = *(const h16x8*)(Cs + swz128(wn * 32 + b * 16 + l16, s * 4 + lg));
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
                 const int cb = (wm * 32 + a * 16 + 4 * pp) * 2;
                 s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + dswz(r0, cb)));
                 s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ds + dswz(r0 + 4, cb)));
                 s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                df[a] = __builtin_bit_cast(bf16x8, v);
+                df[a] = __builtin_bit_cast(h16x8, v);
             }
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[b], df[a], acc[a][b], 0, 0, 0);
+                    acc[a][b] = mfma_16x16x32_h16(tf[b], df[a], acc[a][b]);
         }
     }
     // lane holds taps wn*32 + b*16 + 4lg .. +3 of channel wm*32 + a*16 + l16
@@ -329,7 +329,7 @@ constexpr int BPROWS = 9;                            // input rows of a tile: co
 constexpr int ONE_TAP = KK;                          // col tap 49 = 1
 
 __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
-    const __bf16* __restrict__ dout, const uint8_t* __restrict__ argmax, const __bf16* __restrict__ y,
+    const h16* __restrict__ dout, const uint8_t* __restrict__ argmax, const h16* __restrict__ y,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ x, double* __restrict__ stats, float* __restrict__ ws,
     int H, int W, int Ho, int Wo, int ntiles, int chunk) {
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                         if (oi > a || oj > b) continue;
                         const unsigned sel = (a - 2 * oi + 1) * 3 + (b - 2 * oj + 1);
                         float d[8];
-                        Vec16<__bf16>::load(&rd[oi][oj], d);
+                        Vec16<h16>::load(&rd[oi][oj], d);
                         const unsigned aw[2] = {ra[oi][oj].x, ra[oi][oj].y};
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                             g[e] += hit ? d[e] : 0.f;
                         }
                     }
-                Vec16<__bf16>::load(&yb, v);
+                Vec16<h16>::load(&yb, v);
                 float sc[8], sh[8], mu[8], is[8];
                 *(float4*)sc = *(const float4*)(prm + ch * 8); *(float4*)(sc + 4) = *(const float4*)(prm + ch * 8 + 4);
                 *(float4*)sh = *(const float4*)(prm + CO + ch * 8);
@@ -451,15 +451,15 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
                 *(float4*)(mu + 4) = *(const float4*)(prm + 2 * CO + ch * 8 + 4);
                 *(float4*)is = *(const float4*)(prm + 3 * CO + ch * 8);
                 *(float4*)(is + 4) = *(const float4*)(prm + 3 * CO + ch * 8 + 4);
-                bf16x8 o8;
+                h16x8 o8;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    o8[e] = (__bf16)(v[e] * sc[e] + sh[e] > 0.f ? g[e] : 0.f);
+                    o8[e] = (h16)(v[e] * sc[e] + sh[e] > 0.f ? g[e] : 0.f);
                     const float r = (float)o8[e];
                     s1[e] += r;
                     s2[e] += r * (v[e] - mu[e]) * is[e];
                 }
-                *(bf16x8*)(Ds + a * DT + dswz(2 * bl + b, ch * 16)) = o8;
+                *(h16x8*)(Ds + a * DT + dswz(2 * bl + b, ch * 16)) = o8;
             }
 #pragma unroll
         for (int q = 0; q < (BPROWS * WPCOLS + 255) / 256; ++q) {
@@ -483,14 +483,14 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    bf16x8 v;
+                    h16x8 v;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         const int px = pq * 16 + h * 8 + e;
                         const float pv = patch[(2 * a + kh) * PROW + (kw & 1) * PPAR + px + (kw >> 1)];
-                        v[e] = (__bf16)(k < KK ? pv : kfill);
+                        v[e] = (h16)(k < KK ? pv : kfill);
                     }
-                    *(bf16x8*)(Cs + a * CT + swz128(k, pq * 2 + h)) = v;
+                    *(h16x8*)(Cs + a * CT + swz128(k, pq * 2 + h)) = v;
                 }
         }
         __syncthreads();
@@ -501,24 +501,24 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_fused_kernel(
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const int r0 = 32 * s + 8 * lg + q4;
-                bf16x8 tf[2], df[2], gf[2];
+                h16x8 tf[2], df[2], gf[2];
 #pragma unroll
-                for (int b = 0; b < 2; ++b) tf[b] = *(const bf16x8*)(C + swz128(wn * 32 + b * 16 + l16, s * 4 + lg));
+                for (int b = 0; b < 2; ++b) tf[b] = *(const h16x8*)(C + swz128(wn * 32 + b * 16 + l16, s * 4 + lg));
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    gf[i] = *(const bf16x8*)(C + swz128(wm * 32 + i * 16 + l16, s * 4 + lg));
+                    gf[i] = *(const h16x8*)(C + swz128(wm * 32 + i * 16 + l16, s * 4 + lg));
                     const int cb = (wm * 32 + i * 16 + 4 * pp) * 2;
                     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(D + dswz(r0, cb)));
                     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(D + dswz(r0 + 4, cb)));
                     s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    df[i] = __builtin_bit_cast(bf16x8, v8);
+                    df[i] = __builtin_bit_cast(h16x8, v8);
                 }
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
                     for (int b = 0; b < 2; ++b) {
-                        acc1[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[b], df[i], acc1[i][b], 0, 0, 0);
-                        acc2[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[b], gf[i], acc2[i][b], 0, 0, 0);
+                        acc1[i][b] = mfma_16x16x32_h16(tf[b], df[i], acc1[i][b]);
+                        acc2[i][b] = mfma_16x16x32_h16(tf[b], gf[i], acc2[i][b]);
                     }
             }
         }
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(256) void stem_bwd_reduce_kernel(const float* __res
 
 // dst[co][k] (+)= alpha (a[co] T1[co][k] + b[co] (W G)[co][k] + c[co] G[k][49]) for the 49 taps, W = the conv's bf16
 // weights (wpk rows [co][64], taps >= 49 zero); one workgroup per output channel
-__global__ __launch_bounds__(64) void stem_bwd_combine_kernel(const float* __restrict__ tg, const __bf16* __restrict__ wpk,
+__global__ __launch_bounds__(64) void stem_bwd_combine_kernel(const float* __restrict__ tg, const h16* __restrict__ wpk,
                                                               const float* __restrict__ coef, float* __restrict__ dst,
                                                               int accumulate, float alpha) {
     const int co = blockIdx.x, k = threadIdx.x;
@@ -606,8 +606,8 @@ extern "C" int scd_stem_conv_fwd(int dtype, const float* x, const void* wpk, voi
     // one workgroup per tile (a resident-grid walk with the next tile's patch in flight and the weights in registers
     // measured slower, 121 vs 106 us: the kernel is bound by its LDS / VALU tile build, not by load latency)
     const int blocks = N * (Ho / FTH) * (Wo / FTW);
-    hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (const __bf16*)wpk,
-                       (__bf16*)y, stats, H, W, Ho, Wo);
+    hipLaunchKernelGGL(stem_conv_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (const h16*)wpk,
+                       (h16*)y, stats, H, W, Ho, Wo);
     SCD_RETURN_LAUNCH();
 }
 
@@ -628,8 +628,8 @@ extern "C" int scd_stem_conv_wgrad(int dtype, const void* dy, const void* ybn, c
     chunk = (chunk + WPX - 1) / WPX * WPX;
     if (chunk >= (1L << 31)) return SCD_ERR_ARG;
     if (coef && !ybn) return SCD_ERR_ARG;
-    hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(nsplit), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dy,
-                       (const __bf16*)ybn, coef, x, ws, H, W, Ho, Wo, M, (int)chunk);
+    hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(nsplit), dim3(256), 0, (hipStream_t)stream, (const h16*)dy,
+                       (const h16*)ybn, coef, x, ws, H, W, Ho, Wo, M, (int)chunk);
     SCD_RETURN_LAUNCH();
 }
 
@@ -653,8 +653,8 @@ extern "C" int scd_stem_bwd_fused(int dtype, const void* dout, const uint8_t* ar
     const int chunk = (ntiles + nsplit - 1) / nsplit;
     const int grid = (ntiles + chunk - 1) / chunk;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(stem_bwd_fused_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)dout, argmax,
-                       (const __bf16*)y, scale, shift, mean, invstd, x, stats, ws, H, W, Ho, Wo, ntiles, chunk);
+    hipLaunchKernelGGL(stem_bwd_fused_kernel, dim3(grid), dim3(256), 0, st, (const h16*)dout, argmax,
+                       (const h16*)y, scale, shift, mean, invstd, x, stats, ws, H, W, Ho, Wo, ntiles, chunk);
     hipLaunchKernelGGL(stem_bwd_reduce_kernel, dim3(2 * CO * 64 / 32), dim3(256), 0, st, (const float*)ws, grid, tg);
     SCD_RETURN_LAUNCH();
 }
@@ -664,7 +664,7 @@ extern "C" int scd_stem_bwd_combine(int dtype, const float* tg, const void* wpk,
                                     int accumulate, float alpha, void* stream) {
     SCD_F16_FWD(scd_stem_bwd_combine, tg, wpk, coef, dst, accumulate, alpha, stream);
     if (dtype != SCD_DT_BF16) return SCD_ERR_ARG;
-    hipLaunchKernelGGL(stem_bwd_combine_kernel, dim3(CO), dim3(64), 0, (hipStream_t)stream, tg, (const __bf16*)wpk,
+    hipLaunchKernelGGL(stem_bwd_combine_kernel, dim3(CO), dim3(64), 0, (hipStream_t)stream, tg, (const h16*)wpk,
                        coef, dst, accumulate, alpha);
     SCD_RETURN_LAUNCH();
 }

@@ -175,6 +175,49 @@ class LaunchTimer:
         return sum(ts) / len(ts), len(ts)
 
 
+class ClassTimer:
+    """Per-class kernel time and algorithmic work (bench.py: the class rooflines of BASELINE configs[3] / [4], taken
+    over extra steps after the timed region): HIP-event pairs around every launch of a class on the stream it is
+    issued on -- "gemm" (forward / input-gradient gather-GEMMs, FLOPs), "wgrad" (weight-gradient GEMM + split reduce,
+    FLOPs), "bn" (BatchNorm apply / backward passes, HBM bytes).  Off unless enabled; eager steps only."""
+    on = False
+    recs = []
+
+    @classmethod
+    def begin(cls):
+        if not cls.on or capturing():
+            return None
+        e = _Event()
+        e.record()
+        return e
+
+    @classmethod
+    def end(cls, name, start, work):
+        if start is None:
+            return
+        e = _Event()
+        e.record()
+        cls.recs.append((name, start, e, float(work)))
+
+    @classmethod
+    def collect(cls, steps):
+        """{class: {ms_per_step, work_per_step, launches_per_step}} over `steps` steps (synchronises)."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, a, b, work in cls.recs:
+            d = out.setdefault(name, {"ms_per_step": 0.0, "work_per_step": 0.0, "launches_per_step": 0.0})
+            d["ms_per_step"] += a.elapsed_ms(b) / steps
+            d["work_per_step"] += work / steps
+            d["launches_per_step"] += 1.0 / steps
+        cls.recs = []
+        return out
+
+
+def _gemm_flops(Ci, Co, N, phases):
+    arr = phases.arr
+    return 2.0 * Co * Ci * sum(N * arr[i].Qh * arr[i].Qw * arr[i].ntaps for i in range(phases.n))
+
+
 # ------------------------------------------------------------------ SyncBN / process group
 
 class _BNSync:
@@ -624,6 +667,7 @@ def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, sta
         wpack = pad_channels(wpack, Ci, Cp, wpack.shape[0] * T).view(wpack.shape[0], T * Cp)
         Ci = Cp
     arr, nph = phases.arr, phases.n
+    t0 = ClassTimer.begin()
     if bn_bwd is not None:
         # bn_bwd = (st, y_pre_bn, stats): the next BN+ReLU layer's backward sums from the GEMM epilogue
         st, ybn, bstats = bn_bwd
@@ -631,9 +675,11 @@ def _gemm(x, wpack, y, Co, Ho, Wo, in_stride, out_stride, phases, bias=None, sta
         L.call("scd_conv_gemm_bnbwd", dt(x), ptr(x), ptr(wpack), ptr(y), N, Hi, Wi, Ci, Ho, Wo, Co, in_stride,
                out_stride, wpack.shape[1], nph, arr, ptr(ybn), ptr(st.mean), ptr(st.invstd), ptr(st.scale),
                ptr(st.shift), ptr(bstats), stream())
-        return y
-    L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
-           in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), nph, arr, stream())
+    else:
+        L.call("scd_conv_gemm", dt(x), ptr(x), ptr(wpack), ptr(y), ptr(bias), ptr(stats), N, Hi, Wi, Ci, Ho, Wo, Co,
+               in_stride, out_stride, wpack.shape[1], int(relu), int(accumulate), nph, arr, stream())
+    if t0 is not None:
+        ClassTimer.end("gemm", t0, _gemm_flops(Ci, Co, N, phases))
     return y
 
 
@@ -1017,6 +1063,7 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
         plan = _WGRAD_PLANS[key] = (dh, dw, ns, L.lib().scd_conv_wgrad_workspace(Cg, T, Ci, ns) // 4)
     dh, dw, ns, wsn = plan
     ws = torch.empty(wsn, dtype=torch.float32, device=g.device)
+    t0 = ClassTimer.begin()
     L.call("scd_conv_wgrad", d, ptr(g), ptr(x), ptr(ws), ns, N, Ho, Wo, Cg, Hi, Wi, Ci, stride, T, dh, dw, stream())
     if rows is None:
         rows = [(0, Cg, dst, ld)]
@@ -1037,6 +1084,8 @@ def _conv_wgrad(g, x, kh, kw, stride, pad, dst, ld, cvalid=None, accumulate=True
                 L.long_array([r[3][2] for r in part]), L.ptr_array([ptr(r[2]) for r in part]))
         L.call("scd_wgrad_reduce_rows", ptr(ws), ns, Cg, Tr, Cr, len(part), *arrs, cv, int(accumulate), grad_alpha(g),
                stream())
+    if t0 is not None:
+        ClassTimer.end("wgrad", t0, 2.0 * N * Ho * Wo * Cg * T * Ci)
 
 
 # geometry -> (dh, dw, split count, workspace floats); (row slices) -> the reduce's argument arrays (keyed by the
@@ -1102,8 +1151,11 @@ def bn_apply(y, st, relu, res=None, rst=None, out=None):
     C = y.shape[-1]
     if out is None:
         out = torch.empty_like(y)
+    t0 = ClassTimer.begin()
     L.call("scd_bn_apply", dt(y), ptr(y), ptr(out), C, y.numel(), ptr(st.scale), ptr(st.shift), ptr(res),
            ptr(rst.scale) if rst is not None else 0, ptr(rst.shift) if rst is not None else 0, int(relu), stream())
+    if t0 is not None:
+        ClassTimer.end("bn", t0, y.numel() * y.element_size() * (3 if res is not None else 2))
     return out
 
 
@@ -1114,14 +1166,21 @@ def bn_backward(bn, st, dout, y, mask=None, dz_out=None, relu=False, stats=None)
     stats: the backward sums already accumulated by the producing GEMM (take_bn_bwd_fused)."""
     C = y.shape[-1]
     rsc, rsh = (ptr(st.scale), ptr(st.shift)) if (relu and mask is None) else (0, 0)
+    E = y.numel() * y.element_size()
     if stats is None:
         stats = bn_stats(bn, "bwd")
+        t0 = ClassTimer.begin()
         L.call("scd_bn_bwd_reduce", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(st.mean), ptr(st.invstd),
                C, y.numel(), ptr(stats), stream())
+        if t0 is not None:
+            ClassTimer.end("bn", t0, E * (3 if mask is not None else 2))
     coef = bn_backward_coef(bn, st, stats, C, grad_alpha(y))
     dy = torch.empty_like(y)
+    t0 = ClassTimer.begin()
     L.call("scd_bn_bwd_apply", dt(y), ptr(dout), ptr(mask), ptr(y), rsc, rsh, ptr(coef), C, y.numel(), ptr(dy),
            ptr(dz_out), stream())
+    if t0 is not None:
+        ClassTimer.end("bn", t0, E * (3 + (mask is not None) + (dz_out is not None)))
     return dy
 
 
@@ -1139,8 +1198,12 @@ def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
     C = y_a.shape[-1]
     sa, sb = bn_stats(bn_a, "bwd"), bn_stats(bn_b, "bwd")
     alpha = grad_alpha(y_a)
+    E = y_a.numel() * y_a.element_size()
+    t0 = ClassTimer.begin()
     L.call("scd_bn_bwd_reduce2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(st_a.mean),
            ptr(st_a.invstd), ptr(st_b.mean), ptr(st_b.invstd), C, y_a.numel(), ptr(sa), ptr(sb), stream())
+    if t0 is not None:
+        ClassTimer.end("bn", t0, 4 * E)
     sa, sb, nrep = _allreduce_stats_pair(sa, C, sb, C)
     # both backward finalizes in one launch (scd_bn_bwd_finalize_n)
     ca, cb = torch.empty(2, 3 * C, device=sa.device).unbind(0)
@@ -1150,8 +1213,11 @@ def bn_backward_pair(bn_a, st_a, y_a, bn_b, st_b, y_b, dout, mask):
                                  ptr(grad_of(bn.weight)), ptr(grad_of(bn.bias)), alpha / bn_sync_world(), ptr(coef))
     L.call("scd_bn_bwd_finalize_n", args, 2, stream())
     dya, dyb = torch.empty_like(y_a), torch.empty_like(y_b)
+    t0 = ClassTimer.begin()
     L.call("scd_bn_bwd_apply2", dt(y_a), ptr(dout), ptr(mask), ptr(y_a), ptr(y_b), ptr(ca), ptr(cb), C, y_a.numel(),
            ptr(dya), ptr(dyb), stream())
+    if t0 is not None:
+        ClassTimer.end("bn", t0, 6 * E)
     return dya, dyb
 
 

@@ -299,3 +299,14 @@ def test_sgd_step_dev_checks_hyper():
     for hyper in (torch.zeros(2, dtype=torch.float64), torch.zeros(4, dtype=torch.float32)):
         with pytest.raises(RuntimeError, match="hyper"):
             ops.sgd_step_dev(p, p, p, hyper, 0.9, 0.0, 0.0, False)
+
+
+def test_no_type_macros_in_the_f16_build():
+    """VERDICT r5 hygiene: the fp16 build names its 16-bit type through the h16 typedef and mfma_16x16x32_h16, not by
+    macro-redefining the compiler type __bf16 or an MFMA builtin (code that needs a real bf16 inside an fp16
+    translation unit would silently become fp16)."""
+    import re
+    src = open(os.path.join(REPO, "scd-resnet_amd", "csrc", "scd_common.h")).read()
+    assert not re.search(r"#\s*define\s+__bf16\b", src)
+    assert not re.search(r"#\s*define\s+__builtin_amdgcn_mfma", src)
+    assert "typedef _Float16 h16;" in src and "typedef __bf16 h16;" in src

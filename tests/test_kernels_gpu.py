@@ -1094,3 +1094,93 @@ def test_raw_stream_handle_follows_torch_current_stream():
     with torch.cuda.stream(s):
         assert ops.stream() == s.cuda_stream == torch.cuda.current_stream().cuda_stream
     assert ops.stream() == torch.cuda.current_stream().cuda_stream
+
+
+def _bnst(C, g):
+    class St:
+        pass
+    st = St()
+    st.mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    st.invstd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    st.scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    st.shift = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    return st
+
+
+@pytest.mark.parametrize("case", ["fwd_stats", "fwd_bias_relu_384", "fwd_ragged", "heads_dgrad_bnbwd", "dgrad_accum",
+                                  "deconv_fwd_stats", "deconv_dgrad_bnbwd", "dgrad_s2"])
+def test_duo_matches_pingpong(case, monkeypatch):
+    """conv_gemm_duo_kernel (two 4-wave 256 x 128 workgroups per CU, BK = 32 K-steps in a 3-slot ring, round 6) against
+    the ping-pong kernel on the shapes it replaces: its K order (64-channel chunk, tap, 32-channel half) gives every
+    output the ping-pong kernel's MFMA sequence, so outputs are bit-identical; BN statistics / backward sums agree to
+    fp64 summation-order noise (the tiles' fp32 partials are the same, their replica slots differ).  SCD_GEMM_DUO=1
+    routes the ping-pong shapes to it (read per call)."""
+    from scdhip import ops
+    g = torch.Generator().manual_seed(29)
+    bf = torch.bfloat16
+    st = _bnst(256, g)
+
+    def run():
+        r = {}
+        if case == "fwd_stats":               # 3x3 256 -> 256 with BN statistics (layer4-like, 4 x 128^2 pixels)
+            x = nhwc(torch.randn(4, 256, 128, 128, generator=g), bf)
+            w = (torch.randn(256, 256, 3, 3, generator=g) / 48).to(DEV)
+            stats = torch.zeros(64 * 2 * 256, dtype=torch.float64, device=DEV)
+            r["y"] = ops.conv_fwd(x, ops.pack_weight(w, bf, 0), 256, 3, 3, 1, 1, stats=stats)
+            r["stats"] = stats.view(64, 2, 256).sum(0)
+        elif case == "fwd_bias_relu_384":      # the heads' N = 384 without tails, bias + ReLU
+            x = nhwc(torch.randn(4, 256, 128, 128, generator=g), bf)
+            w = (torch.randn(384, 256, 3, 3, generator=g) / 48).to(DEV)
+            b = torch.randn(384, generator=g).to(DEV)
+            r["y"] = ops.conv_fwd(x, ops.pack_weight(w, bf, 0), 384, 3, 3, 1, 1, bias=b, relu=True)
+        elif case == "fwd_ragged":             # M = 5 x 127^2 (not a multiple of 256), stride 2 input
+            x = nhwc(torch.randn(5, 128, 254, 254, generator=g), bf)
+            w = (torch.randn(256, 128, 3, 3, generator=g) / 34).to(DEV)
+            stats = torch.zeros(64 * 2 * 256, dtype=torch.float64, device=DEV)
+            r["y"] = ops.conv_fwd(x, ops.pack_weight(w, bf, 0), 256, 3, 3, 2, 1, stats=stats)
+            r["stats"] = stats.view(64, 2, 256).sum(0)
+        elif case == "heads_dgrad_bnbwd":      # dhid (128 ch) -> dfeat (256 ch), 3x3, with the next BN's backward sums
+            dy = nhwc(torch.randn(4, 128, 128, 128, generator=g), bf)
+            w = (torch.randn(128, 256, 3, 3, generator=g) / 30).to(DEV)
+            y = nhwc(torch.randn(4, 256, 128, 128, generator=g), bf)
+            bst = torch.zeros(64 * 2 * 256, dtype=torch.float64, device=DEV)
+            r["dx"] = ops.conv_dgrad(dy, ops.pack_weight(w, bf, 1), 256, 128, 128, 3, 3, 1, 1, bn_bwd=(st, y, bst))
+            r["bsums"] = bst.view(64, 2, 256).sum(0)
+        elif case == "dgrad_accum":
+            dy = nhwc(torch.randn(4, 256, 128, 128, generator=g), bf)
+            w = (torch.randn(256, 256, 3, 3, generator=g) / 48).to(DEV)
+            base = nhwc(torch.randn(4, 256, 128, 128, generator=g), bf)
+            r["dx+"] = base.clone()
+            ops.conv_dgrad(dy, ops.pack_weight(w, bf, 1), 256, 128, 128, 3, 3, 1, 1, out=r["dx+"], accumulate=True)
+        elif case == "deconv_fwd_stats":       # ConvTranspose2d(256, 256, 4, 2, 1): 4 sub-pixel phases
+            x = nhwc(torch.randn(4, 256, 64, 64, generator=g), bf)
+            w = (torch.randn(256, 256, 4, 4, generator=g) / 60).to(DEV)
+            stats = torch.zeros(64 * 2 * 256, dtype=torch.float64, device=DEV)
+            r["y"] = ops.deconv_fwd(x, ops.pack_weight(w, bf, 1), 256, stats=stats)
+            r["stats"] = stats.view(64, 2, 256).sum(0)
+        elif case == "deconv_dgrad_bnbwd":     # its input gradient (16 taps, stride 2) with the BN-backward sums
+            dy = nhwc(torch.randn(16, 256, 128, 128, generator=g), bf)
+            w = (torch.randn(256, 256, 4, 4, generator=g) / 60).to(DEV)
+            y = nhwc(torch.randn(16, 256, 64, 64, generator=g), bf)
+            bst = torch.zeros(64 * 2 * 256, dtype=torch.float64, device=DEV)
+            r["dx"] = ops.deconv_dgrad(dy, ops.pack_weight(w, bf, 0), 256, 4, 2, 1, bn_bwd=(st, y, bst))
+            r["bsums"] = bst.view(64, 2, 256).sum(0)
+        else:                                  # 3x3 / stride 2 input gradient as one GEMM with phase columns (shuf)
+            dy = nhwc(torch.randn(32, 256, 32, 32, generator=g), bf)
+            w = torch.randn(256, 128, 3, 3, generator=g).to(DEV) / 34
+            r["dx"] = ops.conv_dgrad_w(dy, w, 64, 64, 2, 1)
+        torch.cuda.synchronize()
+        return r
+
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SCD_GEMM_DUO", mode)
+        g.manual_seed(29)
+        st = _bnst(256, g)
+        outs[mode] = run()
+    for k, v in outs["0"].items():
+        if k in ("stats", "bsums"):
+            d = (outs["1"][k] - v).abs().max().item()
+            assert d <= 1e-9 * max(v.abs().max().item(), 1.0), (k, d)
+        else:
+            assert torch.equal(outs["1"][k], v), (k, (outs["1"][k].float() - v.float()).abs().max().item())

@@ -18,6 +18,25 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from prof_summary import short  # noqa: E402
 
 
+def library_version():
+    """scd_version() of the library the profiled command loaded (SCDHIP_LIB or the in-tree build), read from the
+    .so's bytes (no GPU, no torch): bench.py attributes a summary only to the build it was taken with."""
+    import re
+    path = os.environ.get("SCDHIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "scd-resnet_amd", "scdhip", "libscdhip.so"))
+    m = re.search(rb"libscdhip [0-9.]+ gfx950 [0-9a-z+_]+", open(path, "rb").read())
+    return m.group(0).decode() if m else None
+
+
+def git_head():
+    import subprocess
+    try:
+        return subprocess.check_output(["git", "rev-parse", "--short=12", "HEAD"], stderr=subprocess.DEVNULL,
+                                       cwd=os.path.dirname(os.path.abspath(__file__))).decode().strip()
+    except Exception:
+        return os.environ.get("SCD_HEAD")
+
+
 def per_kernel(path, counter):
     acc = defaultdict(lambda: defaultdict(float))     # kernel -> dispatch -> value (summed over dims)
     with open(path) as f:
@@ -32,7 +51,7 @@ def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
     out = {"units": "bytes per launch (FETCH_SIZE KiB x1024 x2 gfx950 correction; WRITE_SIZE KiB x1024)",
-           "kernels": {}}
+           "kernels": {}, "scd_version": library_version(), "head": git_head()}
     if len(sys.argv) > 5:
         out.update({"batch": int(sys.argv[4]), "dtype": sys.argv[5]})
     if len(sys.argv) > 6:
