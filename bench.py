@@ -190,6 +190,48 @@ def heads_gemm_roofline(B, dtype_name, S=512, cin=256, hd=128, ods=(1, 4, 2), ke
             "launches_timed": n}
 
 
+def exchange_probe(model, dev, reps=50):
+    """Before the warm-up: the measured cost of the two exchange steps on this run's transports (DESIGN §6 cost model):
+    one SyncBN statistics all-reduce (2 x 512 fp64 = the widest layer's sums; ops._allreduce_stats path: peer memory
+    or RCCL on the SyncBN group), mean over `reps` back-to-back calls, and one all-reduce of the whole flat fp32
+    gradient (FlatDDP's buckets, AVG) on WORLD.  Max over ranks."""
+    from scdhip import ops
+    out = {}
+    stats = torch.zeros(2 * 512, dtype=torch.float64, device=dev)
+    peer = ops.bn_sync_peer()
+    group = ops.bn_sync_group()
+
+    def one():
+        if peer is not None:
+            peer.all_reduce(stats)
+        else:
+            dist.all_reduce(stats, group=group)
+    for _ in range(5):
+        one()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one()
+    torch.cuda.synchronize()
+    out["syncbn_call_us"] = (time.perf_counter() - t0) / reps * 1e6
+    g = model.flat.grad
+    dist.all_reduce(g)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        dist.all_reduce(g)
+    torch.cuda.synchronize()
+    out["grad_allreduce_ms"] = (time.perf_counter() - t0) / 3 * 1e3
+    out["grad_bytes"] = g.numel() * g.element_size()
+    g.zero_()
+    t = torch.tensor([out["syncbn_call_us"], out["grad_allreduce_ms"]], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"syncbn_call_us": round(t[0].item(), 1), "grad_allreduce_ms": round(t[1].item(), 3),
+            "grad_bytes": out["grad_bytes"], "syncbn_calls_per_step": None}
+
+
 def launch_ranks(n):
     """`--gpus N` without a torch.distributed launcher: start N child processes of this script, one per
     GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as torch.distributed.run would --
@@ -374,6 +416,10 @@ def main():
     else:
         step = train_step
 
+    probe = None
+    if world > 1:
+        probe = exchange_probe(model, dev)
+
     # with the graph: 2 eager steps, the capture step and the first replay of the second copy are warm-up
     nwarm = max(args.warmup, 4) if graph is not None else args.warmup
     # the step runs on a high-priority stream (SCD_STEP_PRIORITY=0: the default stream): the weight-gradient side
@@ -390,6 +436,7 @@ def main():
     if graph is not None:
         graph.finish()
     ops.LaunchTimer.reset()
+    ops.SyncCounter.calls = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -404,6 +451,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
     final_loss = loss.item()
+    ops.SyncCounter.per_step = ops.SyncCounter.calls / args.steps
     local_ms = None
     if world > 1:
         # after the timed region: the same steps with every collective off (FlatDDP.local_only), max over ranks --
@@ -514,6 +562,11 @@ def main():
                                 "peer_fallback_reason": ops._BNSync.why,
                                 "buckets_overlap_backward": bool(model.overlap_buckets()),
                                 "early_bucket_launches": int(model.early_launches)}
+            if probe is not None:
+                # measured inputs of DESIGN §6's cost model: per-call SyncBN latency x the step's calls, plus the
+                # flat-gradient all-reduce when the buckets do not overlap the backward
+                probe["syncbn_calls_per_step"] = ops.SyncCounter.per_step
+                line["exchange"]["probe"] = probe
         if world == 1 and not args.no_calib and dtype != torch.float32:
             # the bf16 MFMA rate this box sustains (bare 16x16x32 loops on random operands, 2 waves per SIMD, after
             # 2.5 s of back-to-back launches: MI355X_MICROARCH.md "DVFS give-back"), beside the 2.5 PF/s nameplate

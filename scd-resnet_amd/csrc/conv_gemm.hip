@@ -4116,7 +4116,10 @@ static int wgrad_pp2_nsplit(long M, int Cg, int KK) {
         const double stage_us = 2.0 * win * 256 * 64 / 4.3e6;
         const double epi_us = 4.0 * win * 256 / (5.0e6 / 256);
         // many tiles: splits need not come in XCD groups of 8 (wgrad_block's linear map), so one round can be filled
-        const long ns = wgrad_ns_model(M, tiles, 256, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem),
+        // slots: the CUs the model fills (SCD_WGRAD_SLOTS, read once; A/B of leaving CUs to the compute stream)
+        static int slots = -1;
+        if (slots < 0) { const char* e = getenv("SCD_WGRAD_SLOTS"); slots = e ? std::max(8, atoi(e)) : 256; }
+        const long ns = wgrad_ns_model(M, tiles, slots, 64, stage_us, epi_us, 4.0 * Cg * KK, std::min(cap_px, cap_mem),
                                        tiles >= 24);
         return (int)ns;
     }

@@ -364,10 +364,17 @@ def bn_sync_world():
     return _BNSync.world if _BNSync.group is not None else 1
 
 
+class SyncCounter:
+    """SyncBN all-reduce calls issued (bench.py: calls per step, for the exchange cost model)."""
+    calls = 0
+    per_step = None
+
+
 def _allreduce_stats(stats, C):
     """collapse replicas and all-reduce [2][C] fp64 over the BN group; returns nrep."""
     if _BNSync.group is None:
         return L.STAT_REPLICAS
+    SyncCounter.calls += 1
     L.call("scd_stats_collapse", ptr(stats), L.STAT_REPLICAS, C, stream())
     if _BNSync.peer is not None:
         _BNSync.peer.all_reduce(stats[:2 * C])
@@ -387,6 +394,7 @@ def _allreduce_stats_pair(sa, Ca, sb, Cb):
         _allreduce_stats(sa, Ca)
         _allreduce_stats(sb, Cb)
         return sa, sb, 1
+    SyncCounter.calls += 1
     stage = torch.empty(n, dtype=torch.float64, device=sa.device)
     L.call("scd_stats_collapse_to", ptr(sa), L.STAT_REPLICAS, Ca, ptr(stage), stream())
     L.call("scd_stats_collapse_to", ptr(sb), L.STAT_REPLICAS, Cb, ptr(stage[2 * Ca:]), stream())

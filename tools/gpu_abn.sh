@@ -14,14 +14,14 @@ for i in 1 2; do
   k=0
   for c in "$@"; do
     k=$((k+1))
-    env $(envof "$c") timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 30 --warmup 5} --no-cpu-baseline > $O/abn_${TAG}_${k}_$i.json 2>> $O/abn_${TAG}.err || exit 1
+    env $(envof "$c") timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 30 --warmup 5} --no-cpu-baseline --no-calib > $O/abn_${TAG}_${k}_$i.json 2>> $O/abn_${TAG}.err || exit 1
     python -c "import json; d=json.load(open('$O/abn_${TAG}_${k}_$i.json')); print('$k [$c]', d['value'], d['ms_per_step'])"
   done
 done
 k=0
 for c in "$@"; do
   k=$((k+1))
-  env $(envof "$c") timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/abn_${TAG}_${k}_prof -o run -- python3 bench.py ${BENCH_ARGS:---steps 10 --warmup 3} --no-cpu-baseline > /dev/null 2>> $O/abn_${TAG}.err || exit 1
+  env $(envof "$c") timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/abn_${TAG}_${k}_prof -o run -- python3 bench.py ${BENCH_ARGS:---steps 10 --warmup 3} --no-cpu-baseline --no-calib > /dev/null 2>> $O/abn_${TAG}.err || exit 1
   python tools/prof_summary.py $O/abn_${TAG}_${k}_prof/run_kernel_trace.csv $O/abn_${TAG}_${k}_kernel_stats.csv > $O/abn_${TAG}_${k}_kernel_summary.txt 2>&1
   python tools/step_timeline.py $O/abn_${TAG}_${k}_prof/run_kernel_trace.csv > $O/abn_${TAG}_${k}_step_timeline.txt 2>&1
   rm -rf $O/abn_${TAG}_${k}_prof

@@ -10,7 +10,7 @@ mkdir -p $O
 for k in A B; do
   if [ $k = A ]; then E="$A"; else E="$B"; fi
   for c in FETCH_SIZE WRITE_SIZE; do
-    env $E timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmcab_${TAG}_${k}_$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmcab_${TAG}_${k}_$c.log 2>&1 || exit 1
+    env $E timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmcab_${TAG}_${k}_$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-calib > $O/pmcab_${TAG}_${k}_$c.log 2>&1 || exit 1
   done
   f=$(find $O/pmcab_${TAG}_${k}_FETCH_SIZE -name "*counter_collection.csv" | head -1)
   w=$(find $O/pmcab_${TAG}_${k}_WRITE_SIZE -name "*counter_collection.csv" | head -1)

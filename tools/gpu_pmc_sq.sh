@@ -12,7 +12,7 @@ P2="SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_I
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "$K" --output-format csv -d $O/sq_${T}_$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/sq_${T}_$i.log 2>&1 || { tail -5 $O/sq_${T}_$i.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "$K" --output-format csv -d $O/sq_${T}_$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-calib > $O/sq_${T}_$i.log 2>&1 || { tail -5 $O/sq_${T}_$i.log; exit 1; }
 done
 python3 tools/sq_summary.py $O/sq_${T}_1 $O/sq_${T}_2 > $O/sq_${T}.txt || exit 1
 cat $O/sq_${T}.txt

@@ -34,7 +34,7 @@ done
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "conv_gemm_pp|conv_wgrad_pp2|heads384" --output-format csv -d $O/r6c_step_sq$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/r6c_step_sq$i.log 2>&1 || { tail -5 $O/r6c_step_sq$i.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-include-regex "conv_gemm_pp|conv_wgrad_pp2|heads384" --output-format csv -d $O/r6c_step_sq$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-calib > $O/r6c_step_sq$i.log 2>&1 || { tail -5 $O/r6c_step_sq$i.log; exit 1; }
 done
 python3 tools/sq_summary.py --by-grid $O/r6c_step_sq1 $O/r6c_step_sq2 > $O/r6c_step_sq.txt || exit 1
 rm -rf $O/r6c_step_sq1 $O/r6c_step_sq2
