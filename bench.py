@@ -294,7 +294,9 @@ def cornernet_rooflines(B, dtype_name, S=512, C=256, Cp=128):
         out["roofline"] = {"bound": "mfma", "kernel": "conv_gemm_pp_kernel<bf16,256,256> (CornerPool lastConv)"
                            if dtype_name == "bf16" else "conv_gemm_kernel<f32,128,128>", "achieved": round(achieved, 1),
                            "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                           "traffic": None if traffic is None else round(traffic), "traffic_source": src,
+                           "traffic": None if traffic is None else round(traffic),
+                           "traffic_source": src if traffic is not None else None,
+                           "traffic_note": None if traffic is not None else src,
                            "algorithmic_bytes": 2 * M * C * esz + 9 * C * C * esz, "flop_per_launch": flops,
                            "avg_launch_ms": round(ms, 4), "launches_timed": n}
     r = ops.LaunchTimer.mean_ms("cpool_fwd_add")
@@ -305,7 +307,9 @@ def cornernet_rooflines(B, dtype_name, S=512, C=256, Cp=128):
         traffic, src = pmc_traffic("cpool_fwd", B, dtype_name, model="cornerNetCPool", S=S)
         out["pool_roofline"] = {"bound": "hbm", "kernel": "cpool_fwd_kernel (with addend)", "achieved": round(gbs, 1),
                                 "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
-                                "traffic": None if traffic is None else round(traffic), "traffic_source": src,
+                                "traffic": None if traffic is None else round(traffic),
+                                "traffic_source": src if traffic is not None else None,
+                                "traffic_note": None if traffic is not None else src,
                                 "algorithmic_bytes": nbytes, "avg_launch_ms": round(ms, 4),
                                 "launches_timed": n}
     return out
