@@ -118,6 +118,12 @@ __device__ __forceinline__ f32x4 mfma_16x16x16(hx4 a, hx4 b, f32x4 c) {
 #endif
 }
 
+#ifndef PP_PRIO
+// ping-pong kernels (conv_gemm_pp, heads384, wgrad_pp2): 1 = s_setprio 1 around every MFMA segment (the round-1
+// form), 2 = static priority for the second-dispatched group for the whole main loop, no per-segment flips
+// (MI355X_MICROARCH.md "Two waves per SIMD" item 4), 0 = none (A/B build option)
+#define PP_PRIO 1
+#endif
 #ifndef PP_DPP
 #define PP_DPP 1      // ping-pong epilogue: BN sums over the 16 pixel lanes with DPP row ops instead of ds_bpermute
 #endif
@@ -1191,7 +1197,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             }
             return;
         }
-        __builtin_amdgcn_s_setprio(1);
+        if constexpr (PP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1199,7 +1205,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b)
                     acc[2 * q + a][b] = mfma_16x16x32_h16(bfr[b][s], af[a][s], acc[2 * q + a][b]);
-        __builtin_amdgcn_s_setprio(0);
+        if constexpr (PP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
     // ablations (SCD_GEMM_DEBUG): 3 = no DMA instructions in the loop, 4 = no fragment reads in the loop,
@@ -1225,6 +1231,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         bar();
         if constexpr (dbg == 4) { read_b(smem); read_a(smem, 0, afx); read_a(smem, 1, afy); }
         if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
+        if constexpr (PP_PRIO == 2) { if (grp == 1) __builtin_amdgcn_s_setprio(1); }
         for (int t = 0; t < KT; ++t) {
             char* cur = smem + (t & 1) * STAGE;
             char* nxt = smem + ((t & 1) ^ 1) * STAGE;
@@ -1261,6 +1268,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
             bar();
         }
         if (grp == 0) bar();
+        if constexpr (PP_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -2092,7 +2100,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
         auto mfma_q = [&](int q) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
+            if constexpr (PP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     #pragma unroll
             for (int s = 0; s < 2; ++s)
     #pragma unroll
@@ -2100,7 +2108,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     #pragma unroll
                     for (int b = 0; b < NB; ++b)
                         acc[2 * q + a][b] = mfma_16x16x32_h16(bfr[b][s], af[a][s], acc[2 * q + a][b]);
-            __builtin_amdgcn_s_setprio(0);
+            if constexpr (PP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
         };
         auto bar = [&]() {
@@ -2114,6 +2122,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             bar();
             if (grp == 1) bar();                 // stagger: group 1 runs one barrier behind
+            if constexpr (PP_PRIO == 2) { if (grp == 1) __builtin_amdgcn_s_setprio(1); }
             for (int t = 0; t < KT; ++t) {
                 char* cur = smem + (t & 1) * STAGE;
                 char* nxt = smem + ((t & 1) ^ 1) * STAGE;
@@ -2144,6 +2153,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
                 bar();
             }
             if (grp == 0) bar();
+            if constexpr (PP_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -2724,7 +2734,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
     auto mfma_q = [&](int q, const h16x8 (&gf)[2][2]) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
+        if constexpr (PP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -2732,7 +2742,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
                     acc[2 * q + a][b] = mfma_16x16x32_h16(xf[b][s], gf[a][s], acc[2 * q + a][b]);
-        __builtin_amdgcn_s_setprio(0);
+        if constexpr (PP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
     auto bar = [&]() {
@@ -2761,6 +2771,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
         }
         bar();
         if (grp == 1) bar();
+        if constexpr (PP_PRIO == 2) { if (grp == 1) __builtin_amdgcn_s_setprio(1); }
         // schedule (stage t fetches stage t+1 into the other buffer): phase 1: X half 0, phase 2: X half 1,
         // phases 3(-4): the G quarters.  NQ 4: C2 vmcnt(4), L4 vmcnt(4), C4 vmcnt(2);
         // NQ 3: C1 vmcnt(3), C2 vmcnt(4), L3 vmcnt(3), C3 vmcnt(2);
@@ -2825,6 +2836,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pp2_kernel(WgradParams p) {
             }
         }
         if (grp == 0) bar();
+        if constexpr (PP_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     // fp32 slab: lane holds columns kk..kk+3 of channel row cg for every (m, b) block
@@ -3666,7 +3678,8 @@ static int duo_mode() {
     // SCD_GEMM_DUO (read per call: tests compare the kernels): 0 = off, 1 = the ping-pong shapes (Co % 256 / 192 == 0)
     // on the two-workgroups-per-CU kernel, 2 = also the 256 x 128 ring shapes (Co % 128 == 0), 3 = only the ping-pong
     // shapes with the BN-backward-sum epilogue and >= 8 rounds of duo tiles (where the epilogue is what the two
-    // workgroups per CU overlap: the heatmap-head input gradient; tools/duo_probe.py)
+    // workgroups per CU overlap: the heatmap-head input gradient; tools/duo_probe.py), 4 = only the ring shapes
+    // (Co % 128 == 0, not a ping-pong width: the layer2 convs at 128 channels)
     const char* e = getenv("SCD_GEMM_DUO");
     return e ? atoi(e) : 0;
 }
@@ -3771,7 +3784,7 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
         // two 256 x 128 workgroups per CU (conv_gemm_duo_kernel) where the grid gives each CU >= 2 tiles
         const int dm = duo_mode();
         const bool shape = dtype == SCD_DT_BF16 && !p.head_on && p.Co % 128 == 0 &&
-                           (pp_bn(dtype, p.Co) || dm >= 2);
+                           (dm == 4 ? !pp_bn(dtype, p.Co) : (pp_bn(dtype, p.Co) || dm >= 2));
         const long dtiles = (long)cdiv(Mtot, 256) * (p.Co / 128);
         const bool take = dm == 3 ? (p.bnbwd && dtiles >= 16L * num_cus()) : dtiles >= 2L * num_cus();
         if (dm && shape && take) {
