@@ -11,6 +11,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "scd_common.h"
 
@@ -52,6 +53,7 @@ struct GemmParams {
     int N, Hi, Wi, Ci, Ho, Wo, Co;
     int is, os, wrow, relu, accumulate, nphase, ntn;
     int xbytes, wbytes;
+    int ybytes;        // ping-pong BN-backward epilogue: bytes of the pre-BN activation (bny), its buffer range
     int tile_start[SCD_MAX_PHASES + 1];
     scd_gemm_phase ph[SCD_MAX_PHASES];
     // optional fused CenterNet head tails (n-tile t == head t, BN == head hidden width)
@@ -123,6 +125,9 @@ __device__ __forceinline__ f32x4 mfma_16x16x16(hx4 a, hx4 b, f32x4 c) {
 // form), 2 = static priority for the second-dispatched group for the whole main loop, no per-segment flips
 // (MI355X_MICROARCH.md "Two waves per SIMD" item 4), 0 = none (A/B build option)
 #define PP_PRIO 1
+#endif
+#ifndef PP_YPF
+#define PP_YPF 1      // ping-pong BN-backward epilogue: the pre-BN rows loaded before the accumulators are staged
 #endif
 #ifndef PP_DPP
 #define PP_DPP 1      // ping-pong epilogue: BN sums over the 16 pixel lanes with DPP row ops instead of ds_bpermute
@@ -1052,7 +1057,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_ring_kernel(GemmParams p) {
 // 2 (NB2), P3 own A rows 0..63 (2), P4 own A rows 64..127 (2); counted waits: end of L4 vmcnt(4)
 // (both B parts of t+1 landed), end of C4 vmcnt(2) (A rows 0..63), end of C2 vmcnt(2+NB2) (A rows
 // 64..127 of stage t).  Every region is rewritten >= 3 phases after its last fragment read.
-template <int BN, bool HEADS>
+template <int BN, bool HEADS, bool BNB = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     typedef h16 T;
     constexpr int BM = 256, BK = 64, EPC = 8;
@@ -1318,22 +1323,49 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         }
         return ((long)(q.n * p.Ho + oh) * p.Wo + ow) * p.Co + col;
     };
+    // BN-backward mode (below): the lane's rows of the pre-BN activation are loaded now, in flight while the
+    // accumulators are staged (the fragment registers are free after the main loop); PP_YPF=0 loads them in the
+    // store loop
+    float bias[NB][4];                                       // before the row loads (in-order returns)
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const int col0 = nt * BN + wc * WCOLS + b * 16 + lg * 4;
-        float bias[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bias[r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+        for (int r = 0; r < 4; ++r) bias[b][r] = (p.bias && col0 + r < p.Co) ? p.bias[col0 + r] : 0.f;
+    }
+    constexpr int RPI = 64 / CPR;                            // rows per pass (8, or 10 with 4 lanes idle)
+    constexpr int NIT = (128 + RPI - 1) / RPI;
+    const int rsub = lane / CPR, chx = lane - (lane / CPR) * CPR;
+    // Buffer loads on every launch (a zero-sized range without BN-backward: they return zeros and fetch nothing), so
+    // no branch around them: the bias loads' wait above them stays a counted one
+    uint4 ypf[PP_YPF && BNB ? NIT : 1];
+    if constexpr (PP_YPF && BNB) {
+        const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.bny, (short)0, p.ybytes, 0x00020000);
+        const int colb = nt * BN + wc * WCOLS + chx * EPC;
+        const bool cok = rsub < RPI && colb < p.Co;
+        const int cl = cok ? colb : 0;
+        PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int row = it * RPI + rsub;
+            const bool ok = cok && row < 128 && mt * BM + 128 * grp + row < M;
+            const int off = (int)out_off(pq, cl) * (int)sizeof(T);
+            pix_advance(pq, RPI);
+            ypf[it] = bload(yrs, sel_off(ok, off));
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
             const int m = mt * BM + 128 * grp + a * 16 + l16;
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                v[r] = acc[a][b][r] + bias[r];
+                v[r] = acc[a][b][r] + bias[b][r];
                 if (p.relu) v[r] = fmaxf(v[r], 0.f);
             }
-            if (!p.bnbwd) {
+            if constexpr (!BNB) {
                 // a select per element, not a branch region per fragment (the sums never hold -0, so adding +0 for
                 // rows past M leaves them unchanged)
                 const bool mok = m < M;
@@ -1353,10 +1385,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     // BN-backward mode (scd_conv_gemm_bnbwd: the output is the gradient of a following BN+ReLU layer): its backward
     // sums come from the stored gradient and the pre-BN activation, read in the store phase as whole 128-B row pieces
     // (lane: fixed 16-B channel chunk, RPI rows per pass) -- not as 8-B pieces per accumulator fragment
-    constexpr int RPI = 64 / CPR;                            // rows per pass (8, or 10 with 4 lanes idle)
-    const int rsub = lane / CPR, chx = lane - (lane / CPR) * CPR;
     float bs8[EPC], bq8[EPC];
-    if (p.bnbwd) {
+    if constexpr (BNB) {
         const int colb = nt * BN + wc * WCOLS + chx * EPC;
         const bool cok = rsub < RPI && colb < p.Co;
         const int cl = cok ? colb : 0;
@@ -1372,70 +1402,83 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
         }
 #pragma unroll
         for (int e = 0; e < EPC; ++e) { bs8[e] = 0.f; bq8[e] = 0.f; }
-        constexpr int NIT = (128 + RPI - 1) / RPI;
-        PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
-#pragma unroll 4
-        for (int it = 0; it < NIT; ++it) {
-            const int row = it * RPI + rsub;
-            const int m = mt * BM + 128 * grp + row;
-            const bool ok = cok && row < 128 && m < M;
-            // every load from a valid address (row 0 / pixel 0 when masked off): no branch around the loads
-            const long off = ok ? out_off(pq, cl) : 0;
-            pix_advance(pq, RPI);
-            uint4 v = *(const uint4*)(ep + (ok ? row : 0) * EROW + chx * 16);
-            T* dst = (T*)(p.y) + off;
-            if (p.accumulate) {
-                float a8[EPC], o8[EPC];
-                Vec16<T>::load(&v, a8);
-                Vec16<T>::load(dst, o8);
+        // the accumulate branch outside the row loop: a load under a branch inside it makes the compiler's waitcnt
+        // pass drain every outstanding access (the previous rows' stores included) at each row
+        auto rows = [&](auto acc_c) {
+            constexpr bool ACC = decltype(acc_c)::value;
+            PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
 #pragma unroll
-                for (int e = 0; e < EPC; ++e) a8[e] += o8[e];
-                Vec16<T>::store(&v, a8);
-            }
-            float d8[EPC], y8[EPC];
-            Vec16<T>::load(&v, d8);
-            Vec16<T>::load((const T*)p.bny + off, y8);
-            if (ok) {
+            for (int it = 0; it < NIT; ++it) {
+                const int row = it * RPI + rsub;
+                const int m = mt * BM + 128 * grp + row;
+                const bool ok = cok && row < 128 && m < M;
+                // every load from a valid address (row 0 / pixel 0 when masked off): no branch around the loads
+                const long off = ok ? out_off(pq, cl) : 0;
+                pix_advance(pq, RPI);
+                uint4 v = *(const uint4*)(ep + (ok ? row : 0) * EROW + chx * 16);
+                T* dst = (T*)(p.y) + off;
+                if constexpr (ACC) {
+                    float a8[EPC], o8[EPC];
+                    Vec16<T>::load(&v, a8);
+                    Vec16<T>::load(dst, o8);
+#pragma unroll
+                    for (int e = 0; e < EPC; ++e) a8[e] += o8[e];
+                    Vec16<T>::store(&v, a8);
+                }
+                float d8[EPC], y8[EPC];
+                Vec16<T>::load(&v, d8);
+                if constexpr (PP_YPF && BNB) Vec16<T>::load(&ypf[it], y8);
+                else Vec16<T>::load((const T*)p.bny + off, y8);
+                // the sums on every row (+0 for rows masked off; they never hold -0) and only the store under the
+                // branch: the BN parameters are then waited for once, not on every row behind the previous store
 #pragma unroll
                 for (int e = 0; e < EPC; ++e) {
-                    const float dz = y8[e] * sc[e] + sh[e] > 0.f ? d8[e] : 0.f;
+                    const float dz = ok && y8[e] * sc[e] + sh[e] > 0.f ? d8[e] : 0.f;
                     bs8[e] += dz;
                     bq8[e] += dz * (y8[e] - mu[e]) * is[e];
                 }
-                if constexpr (dbg == 60) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-                else *(uint4*)dst = v;
+                if (ok) {
+                    if constexpr (dbg == 60) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+                    else *(uint4*)dst = v;
+                }
             }
-        }
+        };
+        if (p.accumulate) rows(std::true_type{});
+        else rows(std::false_type{});
     } else {
         // lane: 16-B channel chunk chx of rows rsub, rsub + RPI, ... (RPI = 64 / CPR rows per pass; 4 lanes idle when
         // CPR = 6).  Rows past M / columns past Co compute on a valid address (pixel 0, channel 0) and skip only the
         // store: no branch around the accumulate load
-        constexpr int NIT = (128 + RPI - 1) / RPI;
         const int col = nt * BN + wc * WCOLS + chx * EPC;
-        PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
+        auto rows = [&](auto acc_c) {
+            constexpr bool ACC = decltype(acc_c)::value;
+            PixPos pq = pix_of(mt * BM + 128 * grp + rsub);
 #pragma unroll 4
-        for (int it = 0; it < NIT; ++it) {
-            const int row = it * RPI + rsub;
-            const int m = mt * BM + 128 * grp + row;
-            const bool ok = rsub < RPI && row < 128 && m < M && col < p.Co;
-            T* dst = (T*)(p.y) + (ok ? out_off(pq, col) : 0);
-            pix_advance(pq, RPI);
-            uint4 v = *(const uint4*)(ep + (ok ? row : 0) * EROW + chx * 16);
-            if (p.accumulate) {
-                float a[EPC], o[EPC];
-                Vec16<T>::load(&v, a);
-                Vec16<T>::load(dst, o);
+            for (int it = 0; it < NIT; ++it) {
+                const int row = it * RPI + rsub;
+                const int m = mt * BM + 128 * grp + row;
+                const bool ok = rsub < RPI && row < 128 && m < M && col < p.Co;
+                T* dst = (T*)(p.y) + (ok ? out_off(pq, col) : 0);
+                pix_advance(pq, RPI);
+                uint4 v = *(const uint4*)(ep + (ok ? row : 0) * EROW + chx * 16);
+                if constexpr (ACC) {
+                    float a[EPC], o[EPC];
+                    Vec16<T>::load(&v, a);
+                    Vec16<T>::load(dst, o);
 #pragma unroll
-                for (int e = 0; e < EPC; ++e) a[e] += o[e];
-                Vec16<T>::store(&v, a);
+                    for (int e = 0; e < EPC; ++e) a[e] += o[e];
+                    Vec16<T>::store(&v, a);
+                }
+                if constexpr (dbg == 60) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));   // ablation 60: no stores
+                else if (ok) *(uint4*)dst = v;
             }
-            if constexpr (dbg == 60) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));   // ablation 60: no stores
-            else if (ok) *(uint4*)dst = v;
-        }
+        };
+        if (p.accumulate) rows(std::true_type{});
+        else rows(std::false_type{});
     }
     if (p.stats) {
         float* red = (float*)(smem + EPI);    // [2 groups][BN][2]
-        if (p.bnbwd) {
+        if constexpr (BNB) {
             // the lanes' partials into the wave's own staging rows (read above, wave-private), then channel c of the
             // wave summed over its RPI row lanes in a fixed order
             float* part = (float*)ep;                        // [64 lanes][2 * EPC]
@@ -2181,31 +2224,47 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
             // channels 16b + 4lg .., odd rows 16(b+1) + 4(lg-1) ..; 64 contiguous bytes per pixel and instruction)
             // hidden channels >= hid_cols are stored only at the pixels the keep map names (the size / offset heads'
             // sparse backward reads them there only; HeadsFn recomputes the whole tensor for any other backward)
-            unsigned keep = 0;
+            unsigned keep = (1u << NA) - 1;
+            if (p.hid_keep) {                                        // the NA loads together, one wait
+                unsigned char kv[NA];
     #pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                const int m = mt * BM + 96 * grp + 16 * a + l16;
-                if (!p.hid_keep || (m < M && p.hid_keep[m])) keep |= 1u << a;
+                for (int a = 0; a < NA; ++a) {
+                    const int m = mt * BM + 96 * grp + 16 * a + l16;
+                    kv[a] = p.hid_keep[m < M ? m : 0];
+                }
+                keep = 0;
+    #pragma unroll
+                for (int a = 0; a < NA; ++a)
+                    if (mt * BM + 96 * grp + 16 * a + l16 < M && kv[a]) keep |= 1u << a;
             }
+            // the bias and W1 slices of all NB blocks loaded up front, unconditionally (from a valid address, the
+            // value selected after): a load inside the block loop, or under a branch, makes the compiler wait for
+            // every access before it -- the previous blocks' hidden-row stores included
+            hx4 whi[NB], wlo[NB];
+            float bias[NB][4];
+    #pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int col0 = 96 * wc + 16 * b + 4 * lg;
+                const float4 bb = *(const float4*)(p.bias + col0);
+                bias[b][0] = bb.x; bias[b][1] = bb.y; bias[b][2] = bb.z; bias[b][3] = bb.w;
+                // W1[o][col0 .. col0 + 3] when those channels belong to output o's head, else 0
+                const bool wok = hh >= 0 && (col0 >> 7) == hh;
+                const float4 wl = *(const float4*)((hh >= 0 ? wsel : p.head_w[0]) + (wok ? oo * 128 + (col0 & 127) : 0));
+                const float4 wv = wok ? wl : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+    #pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    whi[b][j] = (h16)w4[j];
+                    wlo[b][j] = (h16)(w4[j] - (float)whi[b][j]);
+                }
+            }
+            // consumed here, before the first store (else the compiler's wait for the last ones lands after stores)
+    #pragma unroll
+            for (int b = 0; b < NB; ++b)
+                asm volatile("" : "+v"(whi[b]), "+v"(wlo[b]), "+v"(bias[b][0]), "+v"(bias[b][1]), "+v"(bias[b][2]),
+                             "+v"(bias[b][3]));
     #pragma unroll
             for (int b = 0; b < NB; b += 2) {
-                hx4 whi[2], wlo[2];
-                float bias[2][4];
-    #pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int col0 = 96 * wc + 16 * (b + e) + 4 * lg;
-                    const float4 bb = *(const float4*)(p.bias + col0);
-                    bias[e][0] = bb.x; bias[e][1] = bb.y; bias[e][2] = bb.z; bias[e][3] = bb.w;
-                    // W1[o][col0 .. col0 + 3] when those channels belong to output o's head, else 0
-                    float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (hh >= 0 && (col0 >> 7) == hh) wv = *(const float4*)(wsel + oo * 128 + (col0 & 127));
-                    const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
-    #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        whi[e][j] = (h16)w4[j];
-                        wlo[e][j] = (h16)(w4[j] - (float)whi[e][j]);
-                    }
-                }
                 const int colst = 96 * wc + 16 * b + ((lg & 1) ? 16 + 4 * (lg - 1) : 4 * lg);
     #pragma unroll
                 for (int a = 0; a < NA; ++a) {
@@ -2213,11 +2272,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_heads384_kernel(GemmParams p
     #pragma unroll
                     for (int e = 0; e < 2; ++e)
     #pragma unroll
-                        for (int r = 0; r < 4; ++r) hv[e][r] = (h16)fmaxf(acc[a][b + e][r] + bias[e][r], 0.f);
+                        for (int r = 0; r < 4; ++r) hv[e][r] = (h16)fmaxf(acc[a][b + e][r] + bias[b + e][r], 0.f);
     #pragma unroll
                     for (int e = 0; e < 2; ++e) {
-                        tl[a] = mfma_16x16x16(whi[e], hv[e], tl[a]);
-                        tl[a] = mfma_16x16x16(wlo[e], hv[e], tl[a]);
+                        tl[a] = mfma_16x16x16(whi[b + e], hv[e], tl[a]);
+                        tl[a] = mfma_16x16x16(wlo[b + e], hv[e], tl[a]);
                     }
                     typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
                     const u32x2 x = __builtin_bit_cast(u32x2, hv[0]), y = __builtin_bit_cast(u32x2, hv[1]);
@@ -3830,6 +3889,9 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
             if (xb >= (1L << 31) - 64 || wb >= (1L << 31) - 64) return SCD_ERR_ARG;
             p.xbytes = (int)xb;
             p.wbytes = (int)wb;
+            const long yb = p.bnbwd ? (long)p.N * p.Ho * p.Wo * p.Co * esz : 0;
+            if (yb >= (1L << 31) - 64) return SCD_ERR_ARG;
+            p.ybytes = (int)yb;
             hipStream_t st = (hipStream_t)stream;
             if (p.head_on) {
                 // heads split between two column tiles accumulate two partial sums: zero them first
@@ -3840,6 +3902,9 @@ static int conv_gemm_launch(int dtype, GemmParams& p, int nphase, const scd_gemm
                     }
                 if (bn == 256) hipLaunchKernelGGL((conv_gemm_pp_kernel<256, true>), dim3(tiles), dim3(512), 0, st, p);
                 else hipLaunchKernelGGL((conv_gemm_pp_kernel<192, true>), dim3(tiles), dim3(512), 0, st, p);
+            } else if (p.bnbwd) {
+                if (bn == 256) hipLaunchKernelGGL((conv_gemm_pp_kernel<256, false, true>), dim3(tiles), dim3(512), 0, st, p);
+                else hipLaunchKernelGGL((conv_gemm_pp_kernel<192, false, true>), dim3(tiles), dim3(512), 0, st, p);
             } else {
                 if (bn == 256) hipLaunchKernelGGL((conv_gemm_pp_kernel<256, false>), dim3(tiles), dim3(512), 0, st, p);
                 else hipLaunchKernelGGL((conv_gemm_pp_kernel<192, false>), dim3(tiles), dim3(512), 0, st, p);
@@ -3940,6 +4005,7 @@ static void fill_params(GemmParams& p, const void* x, const void* w, void* y, co
     p.x = (const char*)x; p.w = (const char*)w; p.y = (char*)y; p.bias = bias; p.stats = stats;
     p.N = N; p.Hi = Hi; p.Wi = Wi; p.Ci = Ci; p.Ho = Ho; p.Wo = Wo; p.Co = Co;
     p.is = in_stride; p.os = out_stride; p.wrow = wrow; p.relu = relu; p.accumulate = accumulate;
+    p.ybytes = 0;
     p.head_on = 0;
     p.bnbwd = 0; p.bny = nullptr; p.bn_mean = p.bn_invstd = p.bn_rsc = p.bn_rsh = nullptr;
     p.hid_keep = nullptr; p.hid_cols = 1 << 30;
