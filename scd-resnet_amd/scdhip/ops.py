@@ -437,30 +437,18 @@ class PackPlan:
     packed views.  Only nn.Parameter arguments are cached (keyed by the Parameter object); the plan is active
     from the model's forward until the next optimizer step (``pack_end``)."""
 
-    split = int(os.environ.get("SCD_PACK_SPLIT", "0"))     # 0 one launch; 1 split, pack stream at the compute
-                                                            # stream's priority; 2 split, lowest priority
-
     def __init__(self):
         self.entries = {}           # key -> [out tensor, parts, dtype, used]
         self._sig = None
-        self._dev = {}              # (group, dtype) -> (device descriptor tensor, n, total)
+        self._dev = {}              # dtype -> (device descriptor tensor, n, total)
         self.frozen = False         # a captured step graph uses the operands / descriptors: never free them
         self._retired = []
-        self._late = set()          # keys of the operands the pack stream writes this step
-        self._late_event = None     # recorded on the pack stream after them; each stream waits at its first lookup
-        self._late_waited = set()
-        self._stream = None
 
     def lookup(self, key):
         e = self.entries.get(key)
         if e is None:
             return None
         e[3] = True
-        if self._late_event is not None and key in self._late:
-            cur = torch.cuda.current_stream(e[0].device)
-            if cur.cuda_stream not in self._late_waited:
-                cur.wait_event(self._late_event)
-                self._late_waited.add(cur.cuda_stream)
         return e[0]
 
     def add(self, key, out, parts, dtype):
@@ -484,16 +472,10 @@ class PackPlan:
             if self.frozen:
                 self._retired.append(self._dev)
             self._dev = {}
-            # group 0: the first operand the forward asks for (the stem's), packed on the compute stream; group 1:
-            # every other one, packed on a second stream while the stem runs (waited for at its first lookup)
             per = {}
-            self._late = set()
-            for i, (k, e) in enumerate(self.entries.items()):
-                g = 1 if (i > 0 and self.split) else 0
-                if g:
-                    self._late.add(k)
-                per.setdefault((g, e[2]), []).append(e)
-            for (g, dtype), es in per.items():
+            for e in self.entries.values():
+                per.setdefault(e[2], []).append(e)
+            for dtype, es in per.items():
                 descs, start = [], 0
                 for out, parts, _, _ in es:
                     for (w, mode, ldp, row_off, a_off, a_tot) in parts:
@@ -512,24 +494,9 @@ class PackPlan:
                             start += ((A + 63) // 64) * ((B + bb - 1) // bb) * 4096
                 arr = (L.PackDesc * len(descs))(*descs)
                 host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-                self._dev[(g, dtype)] = (host.to(es[0][0].device), len(descs), start)
-        late = [(dtype, v) for (g, dtype), v in self._dev.items() if g == 1]
-        for (g, dtype), (dev, n, total) in self._dev.items():
-            if g == 0 or capturing():
-                L.call("scd_pack_weights_batched", _DT[dtype], dev.data_ptr(), n, total, stream())
-        self._late_event = None
-        self._late_waited = set()
-        if late and not capturing():
-            cur = torch.cuda.current_stream(late[0][1][0].device)
-            if self._stream is None:
-                self._stream = torch.cuda.Stream(device=cur.device,
-                                                 priority=cur.priority if self.split == 1 else _Side.priority)
-            self._stream.wait_stream(cur)          # after the previous step's optimizer and every reader of them
-            with torch.cuda.stream(self._stream):
-                for dtype, (dev, n, total) in late:
-                    L.call("scd_pack_weights_batched", _DT[dtype], dev.data_ptr(), n, total, stream())
-                self._late_event = torch.cuda.Event()
-                self._late_event.record(self._stream)
+                self._dev[dtype] = (host.to(es[0][0].device), len(descs), start)
+        for dtype, (dev, n, total) in self._dev.items():
+            L.call("scd_pack_weights_batched", _DT[dtype], dev.data_ptr(), n, total, stream())
         for e in self.entries.values():
             e[3] = False
 
