@@ -32,9 +32,10 @@ def short(name):
     if m:
         return "%s<%s>" % (m.group(1), _TY[m.group(2)])
     n = n.replace("(anonymous namespace)::", "").replace("f16::", "")
-    m = re.search(r"conv_gemm_pp_kernel<(\d+)(, (true|false))?>", n)
+    m = re.search(r"conv_gemm_pp_kernel<(\d+)(, (true|false))?(, (true|false))?>", n)
     if m:
-        return "conv_gemm_pp_kernel<%s,256,%s%s>" % (half, m.group(1), ",heads" if m.group(3) == "true" else "")
+        return "conv_gemm_pp_kernel<%s,256,%s%s%s>" % (half, m.group(1), ",heads" if m.group(3) == "true" else "",
+                                                      ",bnbwd" if m.group(5) == "true" else "")
     m = re.search(r"(conv_gemm_halo_kernel|conv_wgrad_pp_kernel)<([\d, ]+)>", n)
     if m:
         return "%s<%s>" % (m.group(1), m.group(2).replace(" ", ""))
