@@ -77,3 +77,13 @@ def test_peer_syncbn_late_rank_and_sticky_error():
     outs = _run("peer_gpu_worker.py", 2)
     for o in outs:
         assert "OK rank" in o, o
+
+
+def test_bf16_ddp_replicas_stay_identical():
+    """bf16 performance mode at world size 2 (nothing checked bf16 at world > 1): three training steps
+    with SyncBN + FlatDDP + FlatAdam; every rank ends each step with bit-identical averaged gradients, parameters,
+    Adam moments and BN running statistics, all finite (tests/ddp_bf16_gpu_worker.py)."""
+    outs = _run("ddp_bf16_gpu_worker.py", 2, EXPECT_SYNCBN="rccl-world")
+    for o in outs:
+        assert "OK rank" in o, o
+    print([line for o in outs for line in o.splitlines() if "losses" in line])
