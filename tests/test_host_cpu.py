@@ -310,3 +310,25 @@ def test_no_type_macros_in_the_f16_build():
     assert not re.search(r"#\s*define\s+__bf16\b", src)
     assert not re.search(r"#\s*define\s+__builtin_amdgcn_mfma", src)
     assert "typedef _Float16 h16;" in src and "typedef __bf16 h16;" in src
+
+
+def test_profile_kernel_names():
+    """tools/prof_summary.short: the names the kernel summaries, PMC summaries and bench.py's traffic lookups key on
+    (bench.py reads `conv_gemm_pp_kernel<bf16,256,256>` for the CornerPool lastConv and `heads384` for the heads)."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from prof_summary import short
+    cases = {
+        "void (anonymous namespace)::conv_gemm_pp_kernel<256, false, false>((anonymous namespace)::GemmParams)":
+            "conv_gemm_pp_kernel<bf16,256,256>",
+        "void conv_gemm_pp_kernel<256, false, true>": "conv_gemm_pp_kernel<bf16,256,256,bnbwd>",
+        "void (anonymous namespace)::f16::conv_gemm_pp_kernel<192, true, false>(GemmParams)":
+            "conv_gemm_pp_kernel<f16,256,192,heads>",
+        "void conv_gemm_pp_kernel<256, true>": "conv_gemm_pp_kernel<bf16,256,256,heads>",
+        "void (anonymous namespace)::conv_gemm_ring_kernel<false, true>(GemmParams)":
+            "conv_gemm_ring_kernel<bf16,256,128,bnbwd>",
+        "void (anonymous namespace)::conv_gemm_l1p_kernel<128, true, true>(GemmParams, int)":
+            "conv_gemm_l1p_kernel<bf16,128,dgrad,bnbwd>",
+        "_ZN12_GLOBAL__N_125conv_gemm_heads384_kernelENS_10GemmParamsE": "conv_gemm_heads384_kernel",
+    }
+    for name, want in cases.items():
+        assert short(name) == want, (name, short(name))
