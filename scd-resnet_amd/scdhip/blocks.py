@@ -158,15 +158,18 @@ class BasicBlockFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         C = blk.conv1.weight.shape[0]
         dx = dyd = None
+        w2 = blk.conv2.weight
         if blk.downsample is not None:
             dy2, dyd = ops.bn_backward_pair(blk.bn2, st2, y2, blk.downsample[1], std, yd, dout, out)
             wd = blk.downsample[0].weight
-            ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
+            gd, g2 = ops.grad_of(wd), ops.grad_of(w2)      # (before the ordering: may zero-fill on this stream)
+            with ops.side_batch():          # both weight gradients behind one side-stream ordering
+                ops.conv_wgrad(dyd, x, 1, 1, s, 0, gd, _conv_ld(wd))
+                ops.conv_wgrad(dy2, a1, 3, 3, 1, 1, g2, _conv_ld(w2))
         else:
             dx = torch.empty_like(x)
             dy2 = ops.bn_backward(blk.bn2, st2, dout, y2, mask=out, dz_out=dx)
-        w2 = blk.conv2.weight
-        ops.conv_wgrad(dy2, a1, 3, 3, 1, 1, ops.grad_of(w2), _conv_ld(w2))
+            ops.conv_wgrad(dy2, a1, 3, 3, 1, 1, ops.grad_of(w2), _conv_ld(w2))
         dy1 = _dgrad_bn_relu_bwd(dy2, ops.pack_weight(w2, x.dtype, 1), C, a1.shape[1], a1.shape[2], 3, 3, 1, 1,
                                  blk.bn1, st1, y1)
         w1 = blk.conv1.weight
@@ -215,15 +218,18 @@ class BottleneckFn(torch.autograd.Function):
         N, H, W, Cin = x.shape
         P = blk.conv1.weight.shape[0]
         dx = dyd = None
+        w3 = blk.conv3.weight
         if blk.downsample is not None:
             dy3, dyd = ops.bn_backward_pair(blk.bn3, st3, y3, blk.downsample[1], std, yd, dout, out)
             wd = blk.downsample[0].weight
-            ops.conv_wgrad(dyd, x, 1, 1, s, 0, ops.grad_of(wd), _conv_ld(wd))
+            gd, g3 = ops.grad_of(wd), ops.grad_of(w3)      # (before the ordering: may zero-fill on this stream)
+            with ops.side_batch():          # both weight gradients behind one side-stream ordering
+                ops.conv_wgrad(dyd, x, 1, 1, s, 0, gd, _conv_ld(wd))
+                ops.conv_wgrad(dy3, a2, 1, 1, 1, 0, g3, _conv_ld(w3))
         else:
             dx = torch.empty_like(x)
             dy3 = ops.bn_backward(blk.bn3, st3, dout, y3, mask=out, dz_out=dx)
-        w3 = blk.conv3.weight
-        ops.conv_wgrad(dy3, a2, 1, 1, 1, 0, ops.grad_of(w3), _conv_ld(w3))
+            ops.conv_wgrad(dy3, a2, 1, 1, 1, 0, ops.grad_of(w3), _conv_ld(w3))
         dy2 = _dgrad_bn_relu_bwd(dy3, ops.pack_weight(w3, x.dtype, 1), P, a2.shape[1], a2.shape[2], 1, 1, 1, 0,
                                  blk.bn2, st2, y2)
         w2 = blk.conv2.weight
@@ -461,12 +467,15 @@ class HeadsFn(torch.autograd.Function):
         ld = (Cin * 9, 9, 1)
 
         def wgrads():
-            ops.conv_wgrad(dh_dense, feat, 3, 3, 1, 1, None, None,
-                           rows=[(i * Hd, (i + 1) * Hd, ops.grad_of(heads[i][0].weight), ld) for i in range(nd)])
-            # (a 1x1 GEMM over the slots; its 9*Cin columns are reduced as 9 taps x Cin into the OIHW rows)
-            ops.conv_wgrad(dhid_s.view(1, 1, Sl, Cs), xcol.view(1, 1, Sl, 9 * Cin), 1, 1, 1, 0, None, None,
-                           rows=[((i - nd) * Hd, (i - nd + 1) * Hd, ops.grad_of(heads[i][0].weight), ld)
-                                 for i in range(nd, nh)], red_taps=9)
+            # (the gradient views first -- they may zero-fill on this stream -- then both GEMMs behind one
+            # side-stream ordering)
+            rd = [(i * Hd, (i + 1) * Hd, ops.grad_of(heads[i][0].weight), ld) for i in range(nd)]
+            rs = [((i - nd) * Hd, (i - nd + 1) * Hd, ops.grad_of(heads[i][0].weight), ld) for i in range(nd, nh)]
+            with ops.side_batch():
+                ops.conv_wgrad(dh_dense, feat, 3, 3, 1, 1, None, None, rows=rd)
+                # (a 1x1 GEMM over the slots; its 9*Cin columns are reduced as 9 taps x Cin into the OIHW rows)
+                ops.conv_wgrad(dhid_s.view(1, 1, Sl, Cs), xcol.view(1, 1, Sl, 9 * Cin), 1, 1, 1, 0, None, None,
+                               rows=rs, red_taps=9)
         # input gradient: dense heads' GEMM (+ the deconv BN's backward sums), then the sparse heads' part
         fuse = ctx.prod is not None and dt in ops.HALF
         bn_args = ops.fused_bn_bwd_args(ctx.prod) if fuse else None
