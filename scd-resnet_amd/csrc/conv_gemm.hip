@@ -1336,8 +1336,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_pp_kernel(GemmParams p) {
     constexpr int RPI = 64 / CPR;                            // rows per pass (8, or 10 with 4 lanes idle)
     constexpr int NIT = (128 + RPI - 1) / RPI;
     const int rsub = lane / CPR, chx = lane - (lane / CPR) * CPR;
-    // Buffer loads on every launch (a zero-sized range without BN-backward: they return zeros and fetch nothing), so
-    // no branch around them: the bias loads' wait above them stays a counted one
+    // Buffer loads with no branch around them (rows past M / columns past Co take an out-of-range offset and read
+    // zeros), so the compiler's wait for the bias loads above them stays a counted one
     uint4 ypf[PP_YPF && BNB ? NIT : 1];
     if constexpr (PP_YPF && BNB) {
         const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.bny, (short)0, p.ybytes, 0x00020000);
